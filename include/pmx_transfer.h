@@ -1,0 +1,186 @@
+/*
+ * pmx_transfer.h -- C ABI of the MI355X-native ParMmg transfer path.
+ *
+ * Replaces, behind ParMmg's own seams, the reference interface:
+ *   PMMG_interpMetricsAndFields(PMMG_pParMesh, int *permNodGlob)
+ *       reference src/parmmg.h:472, def src/interpmesh_pmmg.c:663-741,
+ *       sole caller src/libparmmg1.c:829  -> PMX_interpMetricsAndFields
+ *   PMMG_copyMetricsAndFields_point(...)
+ *       reference src/parmmg.h:473, def src/interpmesh_pmmg.c:432-446,
+ *       caller src/libparmmg1.c:792       -> PMX_copyMetricsAndFields_point
+ *   PMMG_locatePointVol / PMMG_locatePointBdy (src/locate_pmmg.h:63-68) and
+ *   PMMG_interp{4,3,2}bar_{iso,ani} selected by PMMG_setfunc
+ *       (src/parmmgexterns.c:4-6, src/libparmmg_tools.c:595-612)
+ *                                          -> pmx_run (batched, on device)
+ *   PMMG_tetraQual / PMMG_qualhisto / PMMG_prilen (src/parmmg.h:564-566,
+ *       def src/quality_pmmg.c:156-346,591-733)
+ *                                          -> pmx_tetra_qual / pmx_qualhisto /
+ *                                             pmx_prilen
+ *
+ * Rules (ParMmg conventions): plain C, pointers + sizes, no torch types.
+ * Host memory is caller owned; device buffers are owned by the context.
+ * Functions return 1 on success and 0 on failure (pmx_last_error() says why).
+ * One host thread per context, one context per GPU (rank -> device by
+ * rank % ndev).  Mesh arrays are 1-based exactly as in Mmg: slot 0 unused,
+ * adja[4*(k-1)+1+f] = 4*k'+f', adjt[3*(k-1)+1+e] = 3*k'+e'.
+ */
+#ifndef PMX_TRANSFER_H
+#define PMX_TRANSFER_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PMX_TAG_REQ   4        /* MG_REQ */
+#define PMX_TAG_BDY   16       /* MG_BDY */
+#define PMX_TAG_NUL   16384    /* MG_NUL */
+#define PMX_MAX_SOLS  8        /* metric + fields per group */
+
+typedef struct pmx_ctx pmx_ctx;
+
+/* Strided view of an Mmg-style AoS mesh.  Pass e.g.
+ *   point_c = &mesh->point[0].c[0], point_stride = sizeof(MMG5_Point),
+ *   tetra_v = &mesh->tetra[0].v[0], tetra_stride = sizeof(MMG5_Tetra).
+ * Strides are in BYTES.  Entries 1..n are read. */
+typedef struct {
+  int64_t       np, ne, nt;
+  const double *point_c;  int64_t point_stride;
+  const int    *tetra_v;  int64_t tetra_stride;
+  const int    *adja;                       /* 4*ne+5 ints, may be NULL */
+  const int    *tria_v;   int64_t tria_stride;
+  const int    *adjt;                       /* 3*nt+4 ints, may be NULL  */
+  double        hausd;                      /* mesh->info.hausd          */
+} pmx_mesh_view;
+
+/* A solution on the mesh vertices: m[size*ip + j], ip = 1..np (Mmg layout). */
+typedef struct {
+  int           size;     /* 1 scalar/iso metric, 3 vector, 6 tensor/ani metric */
+  double       *m;
+} pmx_sol_view;
+
+/* New points to transfer onto: c[ip] at (const char*)c + ip*stride, ip=first..last;
+ * tag as uint16_t at (const char*)tag + ip*tag_stride (MMG5_Point.tag). */
+typedef struct {
+  int64_t         first, last;
+  const double   *c;    int64_t stride;
+  const uint16_t *tag;  int64_t tag_stride;
+} pmx_points_view;
+
+/* Localisation statistics (reference PMMG_locateStats, src/locate_pmmg.h:45-50) */
+typedef struct {
+  int64_t nvol, nbdy;        /* located points by path            */
+  int64_t nexhaust;          /* exhaustive searches               */
+  int64_t nclosest;          /* not found -> closest element      */
+  int64_t stepmin, stepmax;  /* walk steps                        */
+  double  stepav;
+} pmx_locate_stats;
+
+/* ---- context ---------------------------------------------------------- */
+pmx_ctx    *pmx_create(int device);
+void        pmx_destroy(pmx_ctx *ctx);
+const char *pmx_last_error(pmx_ctx *ctx);
+/* Run on an external HIP stream (hipStream_t passed as void*); NULL = own. */
+int         pmx_set_stream(pmx_ctx *ctx, void *hip_stream);
+int         pmx_synchronize(pmx_ctx *ctx);
+/* Device and build identification. */
+int         pmx_device_info(pmx_ctx *ctx, char *buf, int buflen);
+
+/* ---- background (old) group -------------------------------------------- */
+/* AoS -> SoA conversion on the host, then upload.  imet = index of the
+ * metric in sols[] (or -1).  If adja is NULL it is rebuilt from tetra_v. */
+int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *old_mesh,
+                          int nsol, const pmx_sol_view *old_sols, int imet);
+
+/* ---- new points -------------------------------------------------------- */
+int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pts);
+
+/* ---- the hot path (device resident) ------------------------------------ */
+typedef struct {
+  int    hint_cells_per_tet_log2;  /* hint grid density, default 0 -> auto   */
+  int    max_walk;                 /* walk step cap before exhaustive, 0=auto */
+  double hsiz;                     /* >0: constant-size metric shortcut
+                                      (src/interpmesh_pmmg.c:497-512)        */
+  int    timing;                   /* record per-kernel HIP events           */
+} pmx_run_opts;
+
+/* Locate every uploaded new point in the background group and interpolate all
+ * background solutions onto it.  Results stay on the device. */
+int pmx_run(pmx_ctx *ctx, const pmx_run_opts *opts);
+
+/* Copy results to the host.  new_sols[s].m receives size*(npts) doubles in
+ * point-list order (entries of REQ points and of failed tensor inversions are
+ * left untouched).  elem/status/steps may be NULL. */
+int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem,
+                 int *status, int *steps);
+/* Per-point start element used by the device walk (debug/parity). */
+int pmx_download_starts(pmx_ctx *ctx, int *start);
+/* Per-point reference-style extras for boundary points: edge/vertex (-1 unset). */
+int pmx_download_border(pmx_ctx *ctx, int *edge, int *vertex);
+int pmx_locate_stats_get(pmx_ctx *ctx, pmx_locate_stats *st);
+
+/* Device pointers of the resident result buffers (for collectives / chaining):
+ * which = 0 packed solutions [npts][S], 1 elem, 2 status. */
+void *pmx_device_buffer(pmx_ctx *ctx, int which);
+
+/* Kernel timing of the last pmx_run with opts.timing != 0, in ms:
+ * which = 0 hint build, 1 volume locate+interp, 2 surface locate+interp,
+ * 3 exhaustive fallback, 4 total. */
+double pmx_kernel_ms(pmx_ctx *ctx, int which);
+/* Forget recorded kernel timings. */
+int    pmx_timing_reset(pmx_ctx *ctx);
+
+/* ---- drop-in mirrors of the reference seams ------------------------------ */
+typedef struct {
+  pmx_mesh_view    mesh;        /* new mesh (only points are read)            */
+  pmx_points_view  points;      /* its vertices (first=1,last=np typically)   */
+  pmx_sol_view    *met;         /* new metric (written), or NULL              */
+  pmx_sol_view    *fields;      /* new fields (written), nsols entries        */
+  int              nsols;
+  double           hsiz;        /* mesh->info.hsiz                            */
+  pmx_mesh_view    old_mesh;    /* background snapshot (old_listgrp)          */
+  pmx_sol_view    *old_met;
+  pmx_sol_view    *old_fields;
+} pmx_group;
+
+/* PMMG_interpMetricsAndFields (src/interpmesh_pmmg.c:663-741): loop on
+ * groups; inputMet = parmesh->info.inputMet.  Returns 1 ok / 0 fail. */
+int PMX_interpMetricsAndFields(pmx_ctx *ctx, int ngrp, pmx_group *grps,
+                               const int *permNodGlob, int inputMet);
+
+/* PMMG_copyMetricsAndFields_point (src/interpmesh_pmmg.c:432-446). Old-point
+ * tags are read through old_tag (uint16_t, stride bytes). */
+int PMX_copyMetricsAndFields_point(pmx_ctx *ctx, pmx_group *grp,
+                                   const uint16_t *old_tag, int64_t old_tag_stride,
+                                   const int *permNodGlob, int renum, int inputMet);
+
+/* ---- statistics ---------------------------------------------------------- */
+typedef struct {
+  int64_t ne, np;
+  double  max, min, avg;       /* alpha*q, avg is the SUM (reference avg_cur) */
+  int64_t iel;                 /* element realising min (1-based)            */
+  int64_t good, med;
+  int64_t his[5];
+} pmx_qual_stats;
+
+typedef struct {
+  int64_t ned, nullEdge;
+  double  avlen, lmin, lmax;   /* avlen is the SUM over edges                */
+  int64_t amin, bmin, amax, bmax;
+  int64_t hl[9];
+} pmx_len_stats;
+
+/* Quality of every background tet in the uploaded metric (MMG3D_tetraQual).
+ * Result stays on the device; qual (ne+1 doubles) may be NULL. */
+int pmx_tetra_qual(pmx_ctx *ctx, double *qual);
+/* PMMG_qualhisto on the uploaded group (per-group part, before the reduce). */
+int pmx_qualhisto(pmx_ctx *ctx, pmx_qual_stats *st);
+/* PMMG_prilen / MMG3D_computePrilen on the uploaded group.  point_tag may be
+ * NULL (no ridges).  metRidTyp as in the reference. */
+int pmx_prilen(pmx_ctx *ctx, const uint16_t *point_tag, int64_t tag_stride,
+               int metRidTyp, pmx_len_stats *st);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

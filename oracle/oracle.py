@@ -1,0 +1,153 @@
+"""ctypes wrapper of oracle/liboracle.so -- the CPU restatement of the reference
+transfer path.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, always as the checker.  PARITY UNPINNED (see
+pmx_oracle.h and DESIGN.md).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+vp, i64 = C.c_void_p, C.c_int64
+
+
+class QualStats(C.Structure):
+    _fields_ = [("ne", i64), ("max", C.c_double), ("min", C.c_double), ("avg", C.c_double),
+                ("iel", i64), ("good", i64), ("med", i64), ("his", i64 * 5)]
+
+
+class LenStats(C.Structure):
+    _fields_ = [("ned", i64), ("nullEdge", i64), ("avlen", C.c_double), ("lmin", C.c_double),
+                ("lmax", C.c_double), ("amin", i64), ("bmin", i64), ("amax", i64), ("bmax", i64),
+                ("hl", i64 * 9)]
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            import sys
+            sys.path.insert(0, os.path.dirname(_HERE))
+            from parmmg_amd import build
+            build.build_oracle()
+        lib = C.CDLL(LIB)
+        lib.orc_create.restype = vp
+        lib.orc_create.argtypes = [i64, i64, i64, vp, vp, vp, vp, vp, C.c_double]
+        lib.orc_destroy.argtypes = [vp]
+        lib.orc_reset.argtypes = [vp]
+        lib.orc_locate_vol.argtypes = [vp, vp, vp, vp, vp]
+        lib.orc_locate_bdy.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp]
+        lib.orc_tet_contains.argtypes = [vp, C.c_int, vp, vp]
+        lib.orc_tria_contains.argtypes = [vp, C.c_int, vp]
+        lib.orc_invmat.argtypes = [vp, vp]
+        lib.orc_interp_points.argtypes = [vp, i64, vp, vp, vp, C.c_int, vp, vp, vp, C.c_int,
+                                          vp, vp, C.c_int, vp, vp, vp, vp, vp]
+        lib.orc_constant_size.argtypes = [i64, C.c_int, C.c_double, vp]
+        lib.orc_tetra_qual.argtypes = [i64, vp, vp, vp, C.c_int, vp]
+        lib.orc_qualhisto.argtypes = [i64, vp, vp, C.POINTER(QualStats)]
+        lib.orc_prilen.restype = C.c_int
+        lib.orc_prilen.argtypes = [i64, i64, vp, vp, vp, C.c_int, C.POINTER(LenStats)]
+        _lib = lib
+    return _lib
+
+
+def _p(a):
+    return C.c_void_p(a.ctypes.data) if a is not None else None
+
+
+class Oracle:
+    """Reference-semantics CPU transfer on one background group."""
+
+    def __init__(self, mesh):
+        self.lib = load()
+        self.m = mesh
+        self.ctx = self.lib.orc_create(mesh.np, mesh.ne, mesh.nt, _p(mesh.xyz), _p(mesh.tet),
+                                       _p(mesh.adja), _p(mesh.tria) if mesh.nt else None,
+                                       _p(mesh.adjt) if mesh.nt else None, mesh.hausd)
+
+    def __del__(self):
+        if getattr(self, "ctx", None):
+            self.lib.orc_destroy(self.ctx)
+            self.ctx = None
+
+    def tet_contains(self, k: int, p) -> tuple[bool, float]:
+        p = np.ascontiguousarray(p, np.float64)
+        lm = np.zeros(1)
+        r = self.lib.orc_tet_contains(self.ctx, int(k), _p(p), _p(lm))
+        return bool(r), float(lm[0])
+
+    def tria_contains(self, k: int, p) -> bool:
+        p = np.ascontiguousarray(p, np.float64)
+        return bool(self.lib.orc_tria_contains(self.ctx, int(k), _p(p)))
+
+    def interp(self, xyz, tags, sols, imet=0, order=None, start_vol=None, start_bdy=None,
+               fresh=False, init=None):
+        """Returns (outs, elem, status, steps, edge, vertex); outs[s] is (npts, size)."""
+        xyz = np.ascontiguousarray(xyz, np.float64)
+        n = xyz.shape[0]
+        tags = np.ascontiguousarray(tags if tags is not None else np.zeros(n), np.int32)
+        sols = [np.ascontiguousarray(s, np.float64) for s in sols]
+        sizes = np.array([s.shape[1] for s in sols], np.int32)
+        outs = []
+        for i, s in enumerate(sols):
+            a = (np.array(init[i], np.float64, copy=True).reshape(n, s.shape[1]) if init is not None
+                 else np.full((n, s.shape[1]), np.nan))
+            outs.append(a)
+        oldp = (C.c_void_p * max(len(sols), 1))(*[s.ctypes.data for s in sols])
+        newp = (C.c_void_p * max(len(sols), 1))(*[a.ctypes.data for a in outs])
+        elem = np.zeros(n, np.int32)
+        status = np.zeros(n, np.int32)
+        steps = np.zeros(n, np.int32)
+        edge = np.full(n, -1, np.int32)
+        vertex = np.full(n, -1, np.int32)
+        od = np.ascontiguousarray(order, np.int64) if order is not None else None
+        sv = np.ascontiguousarray(start_vol, np.int32) if start_vol is not None else None
+        sb = np.ascontiguousarray(start_bdy, np.int32) if start_bdy is not None else None
+        self.lib.orc_interp_points(self.ctx, n, _p(xyz), _p(tags), _p(od), len(sols), _p(sizes),
+                                   oldp, newp, imet if sols else -1, _p(sv), _p(sb), int(fresh),
+                                   _p(elem), _p(status), _p(steps), _p(edge), _p(vertex))
+        return outs, elem, status, steps, edge, vertex
+
+
+def invmat(m):
+    lib = load()
+    m = np.ascontiguousarray(m, np.float64)
+    mi = np.full(6, np.nan)
+    ok = lib.orc_invmat(_p(m), _p(mi))
+    return bool(ok), mi
+
+
+def tetra_qual(mesh, met=None):
+    lib = load()
+    q = np.zeros(mesh.ne + 1)
+    msize = met.shape[1] if met is not None else 0
+    m = np.ascontiguousarray(met, np.float64) if met is not None else None
+    lib.orc_tetra_qual(mesh.ne, _p(mesh.xyz), _p(mesh.tet), _p(m), msize, _p(q))
+    return q
+
+
+def qualhisto(mesh, qual):
+    lib = load()
+    st = QualStats()
+    lib.orc_qualhisto(mesh.ne, _p(mesh.tet), _p(np.ascontiguousarray(qual)), C.byref(st))
+    d = {f: getattr(st, f) for f, _ in QualStats._fields_}
+    d["his"] = list(st.his)
+    return d
+
+
+def prilen(mesh, met):
+    lib = load()
+    st = LenStats()
+    m = np.ascontiguousarray(met, np.float64)
+    lib.orc_prilen(mesh.np, mesh.ne, _p(mesh.xyz), _p(mesh.tet), _p(m), m.shape[1], C.byref(st))
+    d = {f: getattr(st, f) for f, _ in LenStats._fields_}
+    d["hl"] = list(st.hl)
+    return d

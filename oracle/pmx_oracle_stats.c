@@ -1,0 +1,194 @@
+/*
+ * pmx_oracle_stats.c -- CPU restatement of the quality / edge-length
+ * statistics (TEST INFRASTRUCTURE ONLY, PARITY UNPINNED: the per-element
+ * arithmetic is Mmg's and Mmg is absent from the container).
+ *
+ *   orc_tetra_qual  MMG3D_tetraQual -> MMG5_caltet_iso / MMG5_caltet33_ani
+ *                   (called from reference src/quality_pmmg.c:720-733)
+ *   orc_qualhisto   MMG3D_computeInqua statistics as aggregated by
+ *                   PMMG_qualhisto (src/quality_pmmg.c:156-261)
+ *   orc_prilen      MMG3D_computePrilen (centralized branch of PMMG_prilen,
+ *                   src/quality_pmmg.c:646-651; same loop as the distributed
+ *                   one at :506-564): hash every tet edge, then pop them in
+ *                   (k ascending, ia ascending) order.
+ */
+#include "pmx_oracle.h"
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ALPHAD 20.7846097   /* MMG3D_ALPHAD */
+#define EPS    1.e-6
+#define EPSD2  1.e-200
+#define TAG_GEO 2
+#define TAG_REQ 4
+#define TAG_NOM 8
+#define TAG_CRN 32
+
+static const int IARE[6][2] = {{0,1},{0,2},{0,3},{1,2},{1,3},{2,3}};
+
+static double caltet_iso(const double *a, const double *b, const double *c, const double *d) {
+  double abx = b[0]-a[0], aby = b[1]-a[1], abz = b[2]-a[2];
+  double acx = c[0]-a[0], acy = c[1]-a[1], acz = c[2]-a[2];
+  double adx = d[0]-a[0], ady = d[1]-a[1], adz = d[2]-a[2];
+  double v1 = acy*adz - acz*ady, v2 = acz*adx - acx*adz, v3 = acx*ady - acy*adx;
+  double vol = abx*v1 + aby*v2 + abz*v3, rap;
+  double bcx, bcy, bcz, bdx, bdy, bdz, cdx, cdy, cdz;
+  if (vol <= 0.) return 0.0;
+  bcx = c[0]-b[0]; bcy = c[1]-b[1]; bcz = c[2]-b[2];
+  bdx = d[0]-b[0]; bdy = d[1]-b[1]; bdz = d[2]-b[2];
+  cdx = d[0]-c[0]; cdy = d[1]-c[1]; cdz = d[2]-c[2];
+  rap  = abx*abx + aby*aby + abz*abz;
+  rap += acx*acx + acy*acy + acz*acz;
+  rap += adx*adx + ady*ady + adz*adz;
+  rap += bcx*bcx + bcy*bcy + bcz*bcz;
+  rap += bdx*bdx + bdy*bdy + bdz*bdz;
+  rap += cdx*cdx + cdy*cdy + cdz*cdz;
+  if (rap < EPSD2) return 0.0;
+  rap = rap * sqrt(rap);
+  return vol / rap;
+}
+
+static double mlen2(const double *m, double x, double y, double z) {
+  return m[0]*x*x + m[3]*y*y + m[5]*z*z + 2.0*(m[1]*x*y + m[2]*x*z + m[4]*y*z);
+}
+
+static double caltet_ani(const double *a, const double *b, const double *c, const double *d,
+                         const double *ma, const double *mb, const double *mc, const double *md) {
+  double mm[6], det, rap, num, vol;
+  double abx = b[0]-a[0], aby = b[1]-a[1], abz = b[2]-a[2];
+  double acx = c[0]-a[0], acy = c[1]-a[1], acz = c[2]-a[2];
+  double adx = d[0]-a[0], ady = d[1]-a[1], adz = d[2]-a[2];
+  double bcx, bcy, bcz, bdx, bdy, bdz, cdx, cdy, cdz;
+  int i;
+  for (i = 0; i < 6; i++) mm[i] = 0.25 * (ma[i] + mb[i] + mc[i] + md[i]);
+  vol = abx*(acy*adz - acz*ady) + aby*(acz*adx - acx*adz) + abz*(acx*ady - acy*adx);
+  if (vol <= 0.) return 0.0;
+  det = mm[0]*(mm[3]*mm[5] - mm[4]*mm[4]) - mm[1]*(mm[1]*mm[5] - mm[2]*mm[4])
+      + mm[2]*(mm[1]*mm[4] - mm[2]*mm[3]);
+  if (det < EPSD2) return 0.0;
+  det = sqrt(det) * vol;
+  bcx = c[0]-b[0]; bcy = c[1]-b[1]; bcz = c[2]-b[2];
+  bdx = d[0]-b[0]; bdy = d[1]-b[1]; bdz = d[2]-b[2];
+  cdx = d[0]-c[0]; cdy = d[1]-c[1]; cdz = d[2]-c[2];
+  rap  = mlen2(mm, abx, aby, abz);
+  rap += mlen2(mm, acx, acy, acz);
+  rap += mlen2(mm, adx, ady, adz);
+  rap += mlen2(mm, bcx, bcy, bcz);
+  rap += mlen2(mm, bdx, bdy, bdz);
+  rap += mlen2(mm, cdx, cdy, cdz);
+  if (rap < EPSD2) return 0.0;
+  num = sqrt(rap) * rap;
+  return det / num;
+}
+
+void orc_tetra_qual(int64_t ne, const double *xyz, const int *tet, const double *met, int msize,
+                    double *qual) {
+  int64_t k;
+  qual[0] = 0.0;
+  for (k = 1; k <= ne; k++) {
+    const int *v = &tet[4*k];
+    if (v[0] <= 0) { qual[k] = 0.0; continue; }
+    if (met && msize == 6)
+      qual[k] = caltet_ani(&xyz[3*v[0]], &xyz[3*v[1]], &xyz[3*v[2]], &xyz[3*v[3]],
+                           &met[6*v[0]], &met[6*v[1]], &met[6*v[2]], &met[6*v[3]]);
+    else
+      qual[k] = caltet_iso(&xyz[3*v[0]], &xyz[3*v[1]], &xyz[3*v[2]], &xyz[3*v[3]]);
+  }
+}
+
+void orc_qualhisto(int64_t ne, const int *tet, const double *qual, orc_qualstats *st) {
+  int64_t k;
+  int i;
+  memset(st, 0, sizeof *st);
+  st->min = 2.0;
+  st->max = 0.0;
+  for (k = 1; k <= ne; k++) {
+    double rap;
+    int ir;
+    if (tet[4*k] <= 0) continue;
+    st->ne++;
+    rap = ALPHAD * qual[k];
+    if (rap < st->min) { st->min = rap; st->iel = k; }
+    if (rap > 0.5) st->med++;
+    if (rap > 0.12) st->good++;
+    st->avg += rap;
+    if (rap > st->max) st->max = rap;
+    ir = (int)(5.0 * rap);
+    if (ir > 4) ir = 4;
+    st->his[ir] += 1;
+  }
+  (void)i;
+}
+
+/* ---- edge lengths -------------------------------------------------------- */
+
+typedef struct { int a, b; int used; } hedge;
+
+static uint64_t hkey(int a, int b) { return ((uint64_t)(uint32_t)a << 32) | (uint32_t)b; }
+
+static double len_iso(const double *xyz, const double *met, int p1, int p2) {
+  const double *c1 = &xyz[3*p1], *c2 = &xyz[3*p2];
+  double h1 = met[p1], h2 = met[p2], l, r;
+  l = (c2[0]-c1[0])*(c2[0]-c1[0]) + (c2[1]-c1[1])*(c2[1]-c1[1]) + (c2[2]-c1[2])*(c2[2]-c1[2]);
+  l = sqrt(l);
+  r = h2 / h1 - 1.0;
+  return (fabs(r) < EPS) ? (l / h1) : (l / (h2 - h1) * log1p(r));
+}
+
+static double len_ani(const double *xyz, const double *met, int p1, int p2) {
+  const double *c1 = &xyz[3*p1], *c2 = &xyz[3*p2];
+  double ux = c2[0]-c1[0], uy = c2[1]-c1[1], uz = c2[2]-c1[2];
+  double dd1 = mlen2(&met[6*p1], ux, uy, uz), dd2 = mlen2(&met[6*p2], ux, uy, uz);
+  if (dd1 <= 0.0) dd1 = 0.0;
+  if (dd2 <= 0.0) dd2 = 0.0;
+  return (sqrt(dd1) + sqrt(dd2) + 4.0*sqrt(0.5*(dd1 + dd2))) / 6.0;
+}
+
+int orc_prilen(int64_t np, int64_t ne, const double *xyz, const int *tet, const double *met,
+               int msize, orc_lenstats *st) {
+  static const double bd[9] = {0.0, 0.3, 0.6, 0.7071, 0.9, 1.3, 1.4142, 2.0, 5.0};
+  /* open-addressing set of unordered edges */
+  uint64_t cap = 1, mask, *tab;
+  uint8_t *popped;
+  int64_t k;
+  (void)np;
+  while (cap < (uint64_t)(16 * ne + 16)) cap <<= 1;
+  mask = cap - 1;
+  tab = (uint64_t *)calloc(cap, sizeof(uint64_t));
+  popped = (uint8_t *)calloc(cap, 1);
+  if (!tab || !popped) { free(tab); free(popped); return 0; }
+  memset(st, 0, sizeof *st);
+  st->lmin = 1.e30;
+  st->lmax = 0.0;
+  /* the admissibility filter needs point tags; the oracle takes none (all
+   * tets admissible), matching pmx_prilen with point_tag == NULL */
+  for (k = 1; k <= ne; k++) {
+    const int *v = &tet[4*k];
+    int ia;
+    if (v[0] <= 0) continue;
+    for (ia = 0; ia < 6; ia++) {
+      int np_ = v[IARE[ia][0]], nq_ = v[IARE[ia][1]];
+      int a = np_ < nq_ ? np_ : nq_, b = np_ < nq_ ? nq_ : np_;
+      uint64_t key = hkey(a, b), h = (key * 0x9e3779b97f4a7c15ULL) >> 20;
+      double len;
+      int i;
+      while (tab[h & mask] && tab[h & mask] != key) h++;
+      if (!tab[h & mask]) tab[h & mask] = key;
+      if (popped[h & mask]) continue;          /* MMG5_hashPop returned 0 */
+      popped[h & mask] = 1;
+      len = (msize == 6) ? len_ani(xyz, met, np_, nq_) : len_iso(xyz, met, np_, nq_);
+      if (!len) { st->nullEdge++; continue; }
+      st->avlen += len;
+      st->ned++;
+      if (len < st->lmin) { st->lmin = len; st->amin = np_; st->bmin = nq_; }
+      if (len > st->lmax) { st->lmax = len; st->amax = np_; st->bmax = nq_; }
+      for (i = 0; i < 8; i++)
+        if (bd[i] <= len && len < bd[i+1]) { st->hl[i]++; break; }
+      if (i == 8) st->hl[8]++;
+    }
+  }
+  free(tab);
+  free(popped);
+  return 1;
+}

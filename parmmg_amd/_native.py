@@ -1,0 +1,124 @@
+"""ctypes binding of ``libpmx_transfer.so`` (the C ABI in include/pmx_transfer.h).
+
+Loading fails loudly: there is no Python or CPU fallback for the transfer path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpmx_transfer.so")
+
+i64 = C.c_int64
+dptr = C.POINTER(C.c_double)
+iptr = C.POINTER(C.c_int)
+u16ptr = C.POINTER(C.c_uint16)
+
+
+class MeshView(C.Structure):
+    _fields_ = [
+        ("np", i64), ("ne", i64), ("nt", i64),
+        ("point_c", dptr), ("point_stride", i64),
+        ("tetra_v", iptr), ("tetra_stride", i64),
+        ("adja", iptr),
+        ("tria_v", iptr), ("tria_stride", i64),
+        ("adjt", iptr),
+        ("hausd", C.c_double),
+    ]
+
+
+class SolView(C.Structure):
+    _fields_ = [("size", C.c_int), ("m", dptr)]
+
+
+class PointsView(C.Structure):
+    _fields_ = [
+        ("first", i64), ("last", i64),
+        ("c", dptr), ("stride", i64),
+        ("tag", u16ptr), ("tag_stride", i64),
+    ]
+
+
+class LocateStats(C.Structure):
+    _fields_ = [
+        ("nvol", i64), ("nbdy", i64), ("nexhaust", i64), ("nclosest", i64),
+        ("stepmin", i64), ("stepmax", i64), ("stepav", C.c_double),
+    ]
+
+
+class RunOpts(C.Structure):
+    _fields_ = [
+        ("hint_cells_per_tet_log2", C.c_int), ("max_walk", C.c_int),
+        ("hsiz", C.c_double), ("timing", C.c_int),
+    ]
+
+
+class Group(C.Structure):
+    _fields_ = [
+        ("mesh", MeshView), ("points", PointsView),
+        ("met", C.POINTER(SolView)), ("fields", C.POINTER(SolView)), ("nsols", C.c_int),
+        ("hsiz", C.c_double),
+        ("old_mesh", MeshView), ("old_met", C.POINTER(SolView)), ("old_fields", C.POINTER(SolView)),
+    ]
+
+
+class QualStats(C.Structure):
+    _fields_ = [
+        ("ne", i64), ("np", i64), ("max", C.c_double), ("min", C.c_double), ("avg", C.c_double),
+        ("iel", i64), ("good", i64), ("med", i64), ("his", i64 * 5),
+    ]
+
+
+class LenStats(C.Structure):
+    _fields_ = [
+        ("ned", i64), ("nullEdge", i64), ("avlen", C.c_double), ("lmin", C.c_double),
+        ("lmax", C.c_double), ("amin", i64), ("bmin", i64), ("amax", i64), ("bmax", i64),
+        ("hl", i64 * 9),
+    ]
+
+
+# symbol -> (restype, argtypes); every function declared in include/pmx_transfer.h
+SIGNATURES = {
+    "pmx_create": (C.c_void_p, [C.c_int]),
+    "pmx_destroy": (None, [C.c_void_p]),
+    "pmx_last_error": (C.c_char_p, [C.c_void_p]),
+    "pmx_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "pmx_synchronize": (C.c_int, [C.c_void_p]),
+    "pmx_device_info": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
+    "pmx_upload_background": (C.c_int, [C.c_void_p, C.POINTER(MeshView), C.c_int, C.POINTER(SolView), C.c_int]),
+    "pmx_upload_points": (C.c_int, [C.c_void_p, C.POINTER(PointsView)]),
+    "pmx_run": (C.c_int, [C.c_void_p, C.POINTER(RunOpts)]),
+    "pmx_download": (C.c_int, [C.c_void_p, C.POINTER(SolView), iptr, iptr, iptr]),
+    "pmx_download_starts": (C.c_int, [C.c_void_p, iptr]),
+    "pmx_download_border": (C.c_int, [C.c_void_p, iptr, iptr]),
+    "pmx_locate_stats_get": (C.c_int, [C.c_void_p, C.POINTER(LocateStats)]),
+    "pmx_device_buffer": (C.c_void_p, [C.c_void_p, C.c_int]),
+    "pmx_kernel_ms": (C.c_double, [C.c_void_p, C.c_int]),
+    "pmx_timing_reset": (C.c_int, [C.c_void_p]),
+    "PMX_interpMetricsAndFields": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(Group), iptr, C.c_int]),
+    "PMX_copyMetricsAndFields_point": (C.c_int, [C.c_void_p, C.POINTER(Group), u16ptr, i64, iptr, C.c_int, C.c_int]),
+    "pmx_tetra_qual": (C.c_int, [C.c_void_p, dptr]),
+    "pmx_qualhisto": (C.c_int, [C.c_void_p, C.POINTER(QualStats)]),
+    "pmx_prilen": (C.c_int, [C.c_void_p, u16ptr, i64, C.c_int, C.POINTER(LenStats)]),
+}
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load the HIP extension; raise if it is missing (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: build it with `python -m parmmg_amd.build` "
+            "(the transfer path has no CPU fallback)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib

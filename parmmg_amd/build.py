@@ -1,0 +1,97 @@
+"""Build recipes for the native parts of parmmg_amd (in-tree, no JIT cache).
+
+* ``libpmx_transfer.so`` -- the product: HIP kernels for gfx950 + the C ABI of
+  ``include/pmx_transfer.h``.  Built with ``-ffp-contract=off`` so that no
+  multiply-add is fused and results match the x86-64 oracle bit for bit.
+* ``libpmx_meshgen.so`` -- synthetic Kuhn-cube meshes / new points for tests and
+  the bench (plain C + OpenMP, not on the product path).
+* ``oracle/liboracle.so`` -- the CPU restatement used only as the checker
+  (tests, smoke, bench cpu_baseline).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "parmmg_amd")
+CSRC = os.path.join(PKG, "csrc")
+INC = os.path.join(ROOT, "include")
+ORACLE = os.path.join(ROOT, "oracle")
+
+TRANSFER_SO = os.path.join(PKG, "libpmx_transfer.so")
+MESHGEN_SO = os.path.join(PKG, "libpmx_meshgen.so")
+ORACLE_SO = os.path.join(ORACLE, "liboracle.so")
+
+HIP_SOURCES = ["pmx_capi.hip", "pmx_kernels.hip", "pmx_bdy.hip", "pmx_stats.hip", "pmx_groups.hip"]
+HIPCC_FLAGS = [
+    "-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-shared",
+    "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
+]
+
+
+def _hipcc() -> str:
+    for c in ("/opt/rocm/bin/hipcc", shutil.which("hipcc") or ""):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found: the HIP extension cannot be built")
+
+
+def _stale(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError("build failed: " + " ".join(cmd))
+
+
+def build_transfer(force: bool = False) -> str:
+    srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES]
+    deps = srcs + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
+    deps.append(os.path.join(INC, "pmx_transfer.h"))
+    if force or _stale(TRANSFER_SO, deps):
+        tmp = TRANSFER_SO + ".tmp"
+        _run([_hipcc(), *HIPCC_FLAGS, "-I", INC, "-I", CSRC, *srcs, "-o", tmp])
+        os.replace(tmp, TRANSFER_SO)
+    return TRANSFER_SO
+
+
+def build_meshgen(force: bool = False) -> str:
+    src = os.path.join(CSRC, "meshgen.c")
+    if force or _stale(MESHGEN_SO, [src]):
+        tmp = MESHGEN_SO + ".tmp"
+        _run(["gcc", "-O2", "-std=c99", "-fPIC", "-shared", "-fopenmp", src, "-o", tmp, "-lm"])
+        os.replace(tmp, MESHGEN_SO)
+    return MESHGEN_SO
+
+
+def build_oracle(force: bool = False) -> str:
+    srcs = [os.path.join(ORACLE, f) for f in sorted(os.listdir(ORACLE)) if f.endswith(".c")]
+    deps = srcs + [os.path.join(ORACLE, "pmx_oracle.h")]
+    if force or _stale(ORACLE_SO, deps):
+        tmp = ORACLE_SO + ".tmp"
+        # x86-64 baseline (SSE2, no FMA), no contraction: the reference's
+        # Release arithmetic (CMakeLists.txt:100-116) without -ffast-math
+        _run(["gcc", "-O2", "-std=c99", "-fPIC", "-shared", "-ffp-contract=off",
+              "-fno-fast-math", *srcs, "-o", tmp, "-lm"])
+        os.replace(tmp, ORACLE_SO)
+    return ORACLE_SO
+
+
+def build_all(force: bool = False) -> None:
+    build_meshgen(force)
+    build_oracle(force)
+    build_transfer(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)
+    print("built:", TRANSFER_SO, MESHGEN_SO, ORACLE_SO)

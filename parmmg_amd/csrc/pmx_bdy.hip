@@ -1,0 +1,625 @@
+// pmx_bdy.hip -- surface (MG_BDY) part of the transfer path on gfx950.
+//
+// One thread per boundary vertex runs PMMG_locatePointBdy (reference
+// src/locate_pmmg.c:587-723) with its shadow-wedge / shadow-cone tests
+// (:209-334) and the PMMG_interp{3,2}bar / PMMG_copyMetrics dispatch of
+// src/interpmesh_pmmg.c:550-599.
+//
+// Device semantics (documented in DESIGN.md): each query starts from the hint
+// triangle instead of the previous query's result, and sees the old-mesh point
+// flags in the state PMMG_precompute_nodeTrias leaves them (number of incident
+// trias), with mesh->base = query ordinal + 1.  The flags a query writes
+// (visited trias, wedge/cone marks) are kept in thread-private lists.
+#include "pmx_device.h"
+#include "pmx_kernels.h"
+#include "pmx_internal.h"
+#include <algorithm>
+#include <cmath>
+
+#define UNSET (-1)
+
+__device__ __constant__ int NXT2d[6] = {1, 2, 0, 1, 2, 0};
+
+struct BdyArgs {
+  const Pt4 *pts;
+  const TriRec *tris;
+  const Pt4 *trn;
+  const int *ntoff, *ntlist;
+  const double *sol;
+  SolDesc sd;
+  const Pt4 *q;
+  const int8_t *kind;
+  int64_t nq, nt;
+  double hausd;
+  const int *grid;     // tria hint grid (shares GridDesc with the tet grid)
+  GridDesc g;
+  double *out;
+  uint8_t *wmask;
+  int *elem, *status, *steps, *start, *edge, *vertex;
+  int *stuck_list;     // bdy exhaustive list
+  unsigned *stuck_count;
+  int *ovf_list;       // private-list overflow
+  unsigned *ovf_count;
+  unsigned long long *lstats;
+};
+
+// thread-private query state: visited trias + point-flag overrides
+template <int CAP> struct RegState {
+  int vis[CAP];
+  int ovp[CAP], ovf[CAP];
+  int nv = 0, no = 0;
+  bool over = false;
+  __device__ void init(int *, int) {}
+  __device__ int &V(int i) { return vis[i]; }
+  __device__ int &OP(int i) { return ovp[i]; }
+  __device__ int &OF(int i) { return ovf[i]; }
+  static constexpr int cap() { return CAP; }
+};
+struct GlobState {
+  int *vis, *ovp, *ovf;
+  int nv = 0, no = 0, capv = 0;
+  bool over = false;
+  __device__ void init(int *ws, int cap) {
+    vis = ws; ovp = ws + cap; ovf = ws + 2 * cap; capv = cap;
+  }
+  __device__ int &V(int i) { return vis[i]; }
+  __device__ int &OP(int i) { return ovp[i]; }
+  __device__ int &OF(int i) { return ovf[i]; }
+};
+template <class St> __device__ __forceinline__ int st_cap(const St &s);
+template <int C> __device__ __forceinline__ int st_cap(const RegState<C> &) { return C; }
+template <> __device__ __forceinline__ int st_cap(const GlobState &s) { return s.capv; }
+
+template <class St> __device__ bool visited(St &s, int t) {
+  for (int i = 0; i < s.nv; i++)
+    if (s.V(i) == t) return true;
+  return false;
+}
+template <class St> __device__ void mark_visited(St &s, int t) {
+  if (visited(s, t)) return;
+  if (s.nv >= st_cap(s)) { s.over = true; return; }
+  s.V(s.nv++) = t;
+}
+template <class St> __device__ int get_flag(St &s, const BdyArgs &A, int p) {
+  for (int i = s.no - 1; i >= 0; i--)
+    if (s.OP(i) == p) return s.OF(i);
+  return A.ntoff[p + 1] - A.ntoff[p];
+}
+template <class St> __device__ void set_flag(St &s, int p, int f) {
+  for (int i = 0; i < s.no; i++)
+    if (s.OP(i) == p) { s.OF(i) = f; return; }
+  if (s.no >= st_cap(s)) { s.over = true; return; }
+  s.OP(s.no) = p;
+  s.OF(s.no) = f;
+  s.no++;
+}
+
+// PMMG_quickarea (src/barycoord_pmmg.c:41-59)
+__device__ __forceinline__ double qarea(D3 a, D3 b, D3 c, D3 n) {
+  double abx = b.x - a.x, aby = b.y - a.y, abz = b.z - a.z;
+  double acx = c.x - a.x, acy = c.y - a.y, acz = c.z - a.z;
+  double a0 = aby * acz - abz * acy, a1 = abz * acx - abx * acz, a2 = abx * acy - aby * acx;
+  return a0 * n.x + a1 * n.y + a2 * n.z;
+}
+
+struct Bary { double val[4]; int idx[4]; };
+
+// PMMG_barycoord2d_compute + sort + isInside (src/barycoord_pmmg.c:191-223,
+// :274-284) on the geometry of tria g with the normal of tria kn
+__device__ bool tria_eval(const BdyArgs &A, int g, int kn, D3 p, Bary &b) {
+  TriRec t = A.tris[g];
+  Pt4 nn = A.trn[kn];
+  D3 n{nn.x, nn.y, nn.z};
+  D3 c = ld3(A.pts, t.v[0]);
+  double h = 0.0;
+  h += (p.x - c.x) * n.x;
+  h += (p.y - c.y) * n.y;
+  h += (p.z - c.z) * n.z;
+  D3 q{p.x - h * n.x, p.y - h * n.y, p.z - h * n.z};
+  double area = A.trn[g].w;
+  D3 P[3] = {ld3(A.pts, t.v[0]), ld3(A.pts, t.v[1]), ld3(A.pts, t.v[2])};
+  b.val[0] = qarea(q, P[1], P[2], n) / area;
+  b.val[1] = qarea(q, P[2], P[0], n) / area;
+  b.val[2] = qarea(q, P[0], P[1], n) / area;
+  b.idx[0] = 0; b.idx[1] = 1; b.idx[2] = 2;
+  b.val[3] = h; b.idx[3] = 3;
+  sort3(b.val, b.idx);
+  return b.val[0] > -PMX_EPS;
+}
+
+__device__ __forceinline__ double norm3(double a, double b, double c) {
+  double r = 0.0;
+  r += a * a;
+  r += b * b;
+  r += c * c;
+  return sqrt(r);
+}
+
+// centroid distance of tria g (closest tracking, src/locate_pmmg.c:398-416)
+__device__ __forceinline__ double centroid_dist(const BdyArgs &A, int g, D3 p) {
+  TriRec t = A.tris[g];
+  double d0 = p.x, d1 = p.y, d2 = p.z;
+  for (int j = 0; j < 3; j++) {
+    D3 c = ld3(A.pts, t.v[j]);
+    d0 -= c.x / 3.0;
+    d1 -= c.y / 3.0;
+    d2 -= c.z / 3.0;
+  }
+  return norm3(d0, d1, d2);
+}
+
+// PMMG_locateChkDistTria (src/locate_pmmg.c:347-366)
+__device__ __forceinline__ bool chk_dist(const BdyArgs &A, int g, int kn, D3 p) {
+  TriRec t = A.tris[g];
+  Pt4 nn = A.trn[kn];
+  D3 c = ld3(A.pts, t.v[0]);
+  double h = 0.0;
+  h += (p.x - c.x) * nn.x;
+  h += (p.y - c.y) * nn.y;
+  h += (p.z - c.z) * nn.z;
+  return !(fabs(h) > A.hausd);
+}
+
+// PMMG_locatePointInTria (src/locate_pmmg.c:385-423), geometry g, normal kn
+template <class St>
+__device__ bool in_tria(const BdyArgs &A, St &s, int g, int kn, D3 p, Bary &b, double &cdist,
+                        int &ctria) {
+  mark_visited(s, g);
+  bool found = tria_eval(A, g, kn, p, b);
+  double nrm = centroid_dist(A, g, p);
+  if (nrm < cdist) { cdist = nrm; ctria = kn; }
+  if (!chk_dist(A, g, kn, p)) return false;
+  return found;
+}
+
+// PMMG_locatePointInWedge (src/locate_pmmg.c:286-334)
+template <class St>
+__device__ int in_wedge(const BdyArgs &A, St &s, int k, int l, D3 p, int base, Bary &b) {
+  int i0 = NXT2d[l], i1 = NXT2d[l + 1];   // inxt2[l], iprv2[l]
+  TriRec t = A.tris[k];
+  int q0 = t.v[i0], q1 = t.v[i1];
+  D3 c0 = ld3(A.pts, q0), c1 = ld3(A.pts, q1);
+  double pv[3] = {p.x - c0.x, p.y - c0.y, p.z - c0.z};
+  double a[3] = {c1.x - c0.x, c1.y - c0.y, c1.z - c0.z};
+  double n2 = 0.0, alpha = 0.0, dist = 0.0;
+  for (int d = 0; d < 3; d++) n2 += a[d] * a[d];
+  for (int d = 0; d < 3; d++) alpha += a[d] * pv[d];
+  for (int d = 0; d < 3; d++) pv[d] -= (alpha / n2) * a[d];
+  for (int d = 0; d < 3; d++) dist += pv[d] * pv[d];
+  dist = sqrt(dist);
+  if (dist > A.hausd) return UNSET;
+  if (alpha < 0.0) { set_flag(s, q1, base); return i0; }
+  if (alpha > n2) { set_flag(s, q0, base); return i1; }
+  b.idx[0] = 0; b.idx[1] = 1; b.idx[2] = 2;
+  b.val[l] = 0.0;
+  b.val[i0] = 1.0 - alpha / n2;
+  b.val[i1] = alpha / n2;
+  return 4;
+}
+
+// PMMG_locatePointInCone (src/locate_pmmg.c:209-270)
+template <class St>
+__device__ bool in_cone(const BdyArgs &A, St &s, int k, int iloc, D3 p, int base) {
+  int ip = A.tris[k].v[iloc];
+  D3 c0 = ld3(A.pts, ip);
+  set_flag(s, ip, base);
+  double pv[3] = {p.x - c0.x, p.y - c0.y, p.z - c0.z};
+  double dist = 0.0;
+  for (int d = 0; d < 3; d++) dist += pv[d] * pv[d];
+  dist = sqrt(dist);
+  int f0 = A.ntoff[ip], f1 = A.ntoff[ip + 1];
+  for (int f = f0; f < f1; f++) {
+    TriRec t = A.tris[A.ntlist[f]];
+    for (int j = 0; j < 3; j++) {
+      int jp = t.v[j];
+      if (jp == ip) continue;
+      if (get_flag(s, A, jp) == ip) continue;
+      set_flag(s, jp, ip);
+      D3 cj = ld3(A.pts, jp);
+      double a[3] = {cj.x - c0.x, cj.y - c0.y, cj.z - c0.z};
+      if (dist > A.hausd) return false;
+      double alpha = 0.0;
+      for (int d = 0; d < 3; d++) alpha += a[d] * pv[d];
+      if (alpha > 0.0) return false;
+    }
+  }
+  return true;
+}
+
+// ---- interpolation on a boundary triangle --------------------------------
+
+__device__ void interp_tria(const BdyArgs &A, int k, const Bary &b, int edge, int vtx,
+                            double *out, unsigned &wm) {
+  TriRec t = A.tris[k];
+  int v[3] = {t.v[0], t.v[1], t.v[2]};
+  double phi[3];
+  // PMMG_barycoord_get(phi, barycoord, 3)
+  for (int i = 0; i < 3; i++) {
+    int id = b.idx[i];
+    double val = b.val[i];
+    if (id == 0) phi[0] = val;
+    if (id == 1) phi[1] = val;
+    if (id == 2) phi[2] = val;
+  }
+  const SolDesc &sd = A.sd;
+  for (int s = 0; s < sd.nsol; ++s) {
+    if (s == sd.imet && sd.metric_const) continue;
+    const int sz = sd.size[s], off = sd.off[s];
+    const bool met = (s == sd.imet);
+    if (met && vtx != UNSET) {                       // PMMG_copyMetrics
+      int src = v[0];
+      if (vtx == 1) src = v[1];
+      if (vtx == 2) src = v[2];
+      for (int j = 0; j < sz; j++) out[off + j] = A.sol[(int64_t)src * sd.S + off + j];
+      wm |= 1u << s;
+    } else if (met && edge != UNSET) {               // PMMG_interp2bar_{iso,ani}
+      int i0 = NXT2d[edge], i1 = NXT2d[edge + 1];
+      int va = v[0], vb = v[0];
+      double pa = phi[0], pb = phi[0];
+      if (i0 == 1) { va = v[1]; pa = phi[1]; }
+      if (i0 == 2) { va = v[2]; pa = phi[2]; }
+      if (i1 == 1) { vb = v[1]; pb = phi[1]; }
+      if (i1 == 2) { vb = v[2]; pb = phi[2]; }
+      if (sz == 1) {
+        out[off] = pa * A.sol[(int64_t)va * sd.S + off] + pb * A.sol[(int64_t)vb * sd.S + off];
+        wm |= 1u << s;
+      } else {
+        double m0[6], m1[6], mi0[6], mi1[6], mint[6], r[6];
+        for (int j = 0; j < 6; j++) {
+          m0[j] = A.sol[(int64_t)va * sd.S + off + j];
+          m1[j] = A.sol[(int64_t)vb * sd.S + off + j];
+        }
+        if (!invmat(m0, mi0)) continue;
+        if (!invmat(m1, mi1)) continue;
+        for (int j = 0; j < 6; j++) mint[j] = pa * mi0[j] + pb * mi1[j];
+        if (!invmat(mint, r)) continue;
+        for (int j = 0; j < 6; j++) out[off + j] = r[j];
+        wm |= 1u << s;
+      }
+    } else if (sz == 6) {                             // PMMG_interp3bar_ani
+      double mi[3][6], mint[6], r[6];
+      bool okk = true;
+      for (int i = 0; i < 3 && okk; i++) {
+        double m[6];
+        for (int j = 0; j < 6; j++) m[j] = A.sol[(int64_t)v[i] * sd.S + off + j];
+        okk = invmat(m, mi[i]);
+      }
+      if (!okk) continue;
+      for (int j = 0; j < 6; j++) mint[j] = phi[0] * mi[0][j] + phi[1] * mi[1][j] + phi[2] * mi[2][j];
+      if (!invmat(mint, r)) continue;
+      for (int j = 0; j < 6; j++) out[off + j] = r[j];
+      wm |= 1u << s;
+    } else {                                          // PMMG_interp3bar_iso
+      for (int j = 0; j < sz; j++) {
+        double acc = 0.0;
+        for (int i = 0; i < 3; i++) acc += phi[i] * A.sol[(int64_t)v[i] * sd.S + off + j];
+        out[off + j] = acc;
+      }
+      wm |= 1u << s;
+    }
+  }
+}
+
+// ---- the walk ----------------------------------------------------------------
+
+// returns 1 found, 2 stuck (needs exhaustive), 3 private-state overflow
+template <class St>
+__device__ int walk_bdy(const BdyArgs &A, St &s, D3 p, int start, int base, int &k, Bary &b,
+                        int &edge, int &vtx, int &step) {
+  double cdist = 1.0e10;
+  int ctria = 0;
+  k = start;
+  step = 0;
+  edge = UNSET;
+  vtx = UNSET;
+  bool stuck = false;
+  while (step <= A.nt && !stuck) {
+    step++;
+    TriRec t = A.tris[k];
+    if (t.v[0] <= 0) { stuck = true; break; }
+    if (in_tria(A, s, k, k, p, b, cdist, ctria)) {
+      if (b.val[0] < PMX_EPS) {                        // PMMG_barycoord_isBorder
+        if (b.val[1] < PMX_EPS) vtx = b.idx[2];
+        else edge = b.idx[0];
+      }
+      return s.over ? 3 : 1;
+    }
+    if (s.over) return 3;
+    int j;
+    for (j = 0; j < 3; j++) {
+      int i = b.idx[j];
+      int nb = t.nb[0];
+      if (i == 1) nb = t.nb[1];
+      if (i == 2) nb = t.nb[2];
+      if (!nb) continue;
+      if (visited(s, nb)) {
+        int il = in_wedge(A, s, k, i, p, base, b);
+        if (s.over) return 3;
+        if (il == UNSET) continue;
+        if (il == 4) { edge = i; return 1; }
+        bool c = in_cone(A, s, k, il, p, base);
+        if (s.over) return 3;
+        if (c) { vtx = il; return 1; }
+        continue;
+      }
+      k = nb;
+      break;
+    }
+    if (j == 3) stuck = true;
+  }
+  return 2;
+}
+
+__device__ void finish_bdy(const BdyArgs &A, int64_t i, int k, const Bary &b, int edge, int vtx,
+                           int status, int step) {
+  A.elem[i] = k;
+  A.status[i] = status;
+  A.steps[i] = step;
+  A.edge[i] = edge;
+  A.vertex[i] = vtx;
+  unsigned wm = 0;
+  interp_tria(A, k, b, edge, vtx, A.out + i * A.sd.S, wm);
+  A.wmask[i] = (uint8_t)(A.wmask[i] | wm);
+}
+
+__device__ int tria_hint(const BdyArgs &A, D3 p);
+
+template <int CAP>
+__global__ __launch_bounds__(256) void k_locate_bdy(BdyArgs A) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.nq || A.kind[i] != KIND_BDY) return;
+  Pt4 qq = A.q[i];
+  D3 p{qq.x, qq.y, qq.z};
+  int start = tria_hint(A, p);
+  A.start[i] = start;
+  RegState<CAP> s;
+  Bary b;
+  int k, edge, vtx, step;
+  int r = walk_bdy(A, s, p, start, (int)(i + 1), k, b, edge, vtx, step);
+  if (r == 1) {
+    finish_bdy(A, i, k, b, edge, vtx, 1, step);
+    atomicAdd(&A.lstats[4], 1ull);
+    atomicAdd(&A.lstats[5], (unsigned long long)step);
+    atomicMax(&A.lstats[6], (unsigned long long)step);
+    atomicMin(&A.lstats[7], (unsigned long long)step);
+  } else if (r == 2) {
+    unsigned slot = atomicAdd(A.stuck_count, 1u);
+    A.stuck_list[slot] = (int)i;
+    A.steps[i] = -step;
+  } else {
+    unsigned slot = atomicAdd(A.ovf_count, 1u);
+    A.ovf_list[slot] = (int)i;
+  }
+}
+
+// overflow pass: same walk with large lists in a global workspace
+__global__ __launch_bounds__(64) void k_locate_bdy_ovf(BdyArgs A, int *ws, int cap) {
+  const unsigned n = *A.ovf_count;
+  const unsigned nthr = gridDim.x * blockDim.x;
+  const unsigned tid = blockIdx.x * blockDim.x + threadIdx.x;
+  for (unsigned j = tid; j < n; j += nthr) {
+    int64_t i = A.ovf_list[j];
+    Pt4 qq = A.q[i];
+    D3 p{qq.x, qq.y, qq.z};
+    GlobState s;
+    s.init(ws + (size_t)tid * 3 * cap, cap);
+    Bary b;
+    int k, edge, vtx, step;
+    int r = walk_bdy(A, s, p, A.start[i], (int)(i + 1), k, b, edge, vtx, step);
+    if (r == 1) {
+      finish_bdy(A, i, k, b, edge, vtx, 1, step);
+    } else {
+      unsigned slot = atomicAdd(A.stuck_count, 1u);
+      A.stuck_list[slot] = (int)i;
+      A.steps[i] = -step;
+    }
+  }
+}
+
+// Exhaustive surface search (PMMG_locatePoint_exhaustTria, :477-515):
+// one workgroup per stuck point.  First containing tria in index order, else
+// the closest tria by centroid distance (lowest index on ties) and the
+// reference's re-evaluation with the last tria's geometry.
+__global__ __launch_bounds__(256) void k_exh_bdy(BdyArgs A) {
+  __shared__ int s_min;
+  __shared__ double s_d[256];
+  __shared__ int s_k[256];
+  const unsigned n = *A.stuck_count;
+  for (unsigned j = blockIdx.x; j < n; j += gridDim.x) {
+    int64_t i = A.stuck_list[j];
+    Pt4 qq = A.q[i];
+    D3 p{qq.x, qq.y, qq.z};
+    if (threadIdx.x == 0) s_min = 0x7fffffff;
+    __syncthreads();
+    RegState<1> dummy;
+    for (int64_t t = 1 + threadIdx.x; t <= A.nt; t += blockDim.x) {
+      if (A.tris[t].v[0] <= 0) continue;
+      Bary b;
+      double cd = 1e300;
+      int ct = 0;
+      dummy.nv = 0;
+      dummy.over = false;
+      if (in_tria(A, dummy, (int)t, (int)t, p, b, cd, ct)) {
+        atomicMin(&s_min, (int)t);
+        break;   // later t of this thread are larger
+      }
+    }
+    __syncthreads();
+    int kf = s_min;
+    if (kf != 0x7fffffff) {
+      if (threadIdx.x == 0) {
+        Bary b;
+        tria_eval(A, kf, kf, p, b);
+        finish_bdy(A, i, kf, b, UNSET, UNSET, -1, A.steps[i] - 1);
+      }
+    } else {
+      double best = 1.0e10;
+      int bk = 0x7fffffff;
+      for (int64_t t = 1 + threadIdx.x; t <= A.nt; t += blockDim.x) {
+        if (A.tris[t].v[0] <= 0) continue;
+        double d = centroid_dist(A, (int)t, p);
+        if (d < best || (d == best && (int)t < bk)) { best = d; bk = (int)t; }
+      }
+      s_d[threadIdx.x] = best;
+      s_k[threadIdx.x] = bk;
+      __syncthreads();
+      for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+          double d2 = s_d[threadIdx.x + o];
+          int k2 = s_k[threadIdx.x + o];
+          if (d2 < s_d[threadIdx.x] || (d2 == s_d[threadIdx.x] && k2 < s_k[threadIdx.x])) {
+            s_d[threadIdx.x] = d2;
+            s_k[threadIdx.x] = k2;
+          }
+        }
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) {
+        int ct = s_k[0];
+        Bary b;
+        RegState<1> d1;
+        double cd = 1e300;
+        int cc = 0;
+        if (!in_tria(A, d1, (int)A.nt, ct, p, b, cd, cc)) {
+          // PMMG_barycoord2d_getClosest (src/barycoord_pmmg.c:324-357)
+          TriRec t = A.tris[ct];
+          double bd = 0.0;
+          int it = 0;
+          for (int l = 0; l < 3; l++) {
+            D3 c = ld3(A.pts, t.v[l]);
+            double d = norm3(p.x - c.x, p.y - c.y, p.z - c.z);
+            if (l == 0 || d < bd) { bd = d; it = l; }
+          }
+          for (int l = 0; l < 3; l++) { b.idx[l] = l; b.val[l] = (l == it) ? 1.0 : 0.0; }
+        }
+        finish_bdy(A, i, ct, b, UNSET, UNSET, 0, A.steps[i] - 1);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// tria hint grid: cell -> largest tria index whose centroid falls in it
+__global__ __launch_bounds__(256) void k_tria_hint_build(const TriRec *tris, const Pt4 *pts,
+                                                         int64_t nt, int *grid, GridDesc g) {
+  for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= nt;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    TriRec t = tris[k];
+    if (t.v[0] <= 0) continue;
+    D3 a = ld3(pts, t.v[0]), b = ld3(pts, t.v[1]), c = ld3(pts, t.v[2]);
+    D3 m{(a.x + b.x + c.x) / 3.0, (a.y + b.y + c.y) / 3.0, (a.z + b.z + c.z) / 3.0};
+    int cx = (int)fmin(fmax((m.x - g.lo[0]) * g.inv[0], 0.0), (double)(g.dim[0] - 1));
+    int cy = (int)fmin(fmax((m.y - g.lo[1]) * g.inv[1], 0.0), (double)(g.dim[1] - 1));
+    int cz = (int)fmin(fmax((m.z - g.lo[2]) * g.inv[2], 0.0), (double)(g.dim[2] - 1));
+    atomicMax(&grid[(int64_t)cx + (int64_t)g.dim[0] * ((int64_t)cy + (int64_t)g.dim[1] * cz)], (int)k);
+  }
+}
+
+__device__ int tria_hint(const BdyArgs &A, D3 p) {
+  const GridDesc &g = A.g;
+  int c[3];
+  c[0] = (int)fmin(fmax((p.x - g.lo[0]) * g.inv[0], 0.0), (double)(g.dim[0] - 1));
+  c[1] = (int)fmin(fmax((p.y - g.lo[1]) * g.inv[1], 0.0), (double)(g.dim[1] - 1));
+  c[2] = (int)fmin(fmax((p.z - g.lo[2]) * g.inv[2], 0.0), (double)(g.dim[2] - 1));
+  int k = A.grid[(int64_t)c[0] + (int64_t)g.dim[0] * ((int64_t)c[1] + (int64_t)g.dim[1] * c[2])];
+  if (k) return k;
+  for (int r = 1; r <= 4; r++)
+    for (int dz = -r; dz <= r; dz++)
+      for (int dy = -r; dy <= r; dy++)
+        for (int dx = -r; dx <= r; dx++) {
+          if (max(abs(dx), max(abs(dy), abs(dz))) != r) continue;
+          int x = c[0] + dx, y = c[1] + dy, z = c[2] + dz;
+          if (x < 0 || y < 0 || z < 0 || x >= g.dim[0] || y >= g.dim[1] || z >= g.dim[2]) continue;
+          int kk = A.grid[(int64_t)x + (int64_t)g.dim[0] * ((int64_t)y + (int64_t)g.dim[1] * z)];
+          if (kk) return kk;
+        }
+  return 1;
+}
+
+// PMMG_precompute_triaNormals (src/locate_pmmg.c:68-90): unit normal + |n|
+__global__ __launch_bounds__(256) void k_tria_normals(const TriRec *tris, const Pt4 *pts,
+                                                      int64_t nt, Pt4 *trn) {
+  for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= nt;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    TriRec t = tris[k];
+    if (t.v[0] <= 0) { trn[k] = Pt4{0, 0, 0, 0}; continue; }
+    D3 n = nonunit_normal(ld3(pts, t.v[0]), ld3(pts, t.v[1]), ld3(pts, t.v[2]));
+    double q = sqrt(n.x * n.x + n.y * n.y + n.z * n.z);
+    double dd = 1.0 / q;
+    trn[k] = Pt4{n.x * dd, n.y * dd, n.z * dd, q};
+  }
+}
+
+void launch_tria_normals(const TriRec *tris, const Pt4 *pts, int64_t nt, Pt4 *trn, hipStream_t s) {
+  int64_t nb = (nt + 255) / 256;
+  if (nb > 4096) nb = 4096;
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(k_tria_normals, dim3((unsigned)nb), dim3(256), 0, s, tris, pts, nt, trn);
+}
+
+#define BDY_CAP 32
+#define OVF_CAP 2048
+#define OVF_THREADS (64 * 64)
+
+bool pmx_ctx::launch_bdy(const VolArgs &a, const pmx_run_opts &o, hipStream_t s) {
+  if (nt < 1) { err = "surface points present but the background has no boundary trias"; return false; }
+  // tria hint grid: a coarser grid over the same bbox (about 2 trias / cell
+  // in each direction of the surface)
+  if (!d_blist.p || d_blist.cap < (size_t)nq) {
+    if (d_blist.p) hipFree(d_blist.p);
+    if (hipMalloc((void **)&d_blist.p, sizeof(int) * (size_t)std::max<int64_t>(nq, 1)) != hipSuccess) { err = "hipMalloc blist"; return false; }
+    d_blist.cap = (size_t)nq;
+    if (d_olist.p) hipFree(d_olist.p);
+    if (hipMalloc((void **)&d_olist.p, sizeof(int) * (size_t)std::max<int64_t>(nq, 1)) != hipSuccess) { err = "hipMalloc olist"; return false; }
+    d_olist.cap = (size_t)nq;
+  }
+  if (!d_ows.p) {
+    if (hipMalloc((void **)&d_ows.p, sizeof(int) * (size_t)OVF_THREADS * 3 * OVF_CAP) != hipSuccess) { err = "hipMalloc ows"; return false; }
+    d_ows.cap = (size_t)OVF_THREADS * 3 * OVF_CAP;
+  }
+  // tria grid: reuse d_found as storage is not possible (stuck slots); use a
+  // dedicated coarse grid stored past the tet grid cells
+  GridDesc tg;
+  double ext[3];
+  int64_t cells = 1;
+  double area = 0.0;
+  for (int ax = 0; ax < 3; ax++) ext[ax] = std::max(bbhi[ax] - bblo[ax], 1e-300);
+  area = 2.0 * (ext[0] * ext[1] + ext[1] * ext[2] + ext[0] * ext[2]);
+  double h = std::sqrt(area / std::max(1.0, (double)nt / 2.0));
+  for (int ax = 0; ax < 3; ax++) {
+    int d = (int)std::ceil(ext[ax] / h);
+    d = std::max(1, std::min(d, 1024));
+    tg.dim[ax] = d;
+    tg.lo[ax] = bblo[ax];
+    tg.inv[ax] = (double)d / ext[ax];
+    cells *= d;
+  }
+  if (d_tgrid_cap < (size_t)cells) {
+    if (d_tgrid) hipFree(d_tgrid);
+    d_tgrid = nullptr;
+    if (hipMalloc((void **)&d_tgrid, sizeof(int) * (size_t)cells) != hipSuccess) { err = "hipMalloc tgrid"; return false; }
+    d_tgrid_cap = (size_t)cells;
+  }
+  hipMemsetAsync(d_tgrid, 0, sizeof(int) * (size_t)cells, s);
+  {
+    int64_t nb = (nt + 255) / 256;
+    if (nb > 4096) nb = 4096;
+    hipLaunchKernelGGL(k_tria_hint_build, dim3((unsigned)std::max<int64_t>(nb, 1)), dim3(256), 0, s,
+                       d_tris.p, d_pts.p, nt, d_tgrid, tg);
+  }
+  BdyArgs B{};
+  B.pts = d_pts.p; B.tris = d_tris.p; B.trn = d_trn.p; B.ntoff = d_ntoff.p; B.ntlist = d_ntlist.p;
+  B.sol = d_sol.p; B.sd = a.sd; B.q = d_q.p; B.kind = d_kind.p; B.nq = nq; B.nt = nt;
+  B.hausd = hausd; B.grid = d_tgrid; B.g = tg;
+  B.out = d_out.p; B.wmask = d_wmask.p; B.elem = d_elem.p; B.status = d_status.p;
+  B.steps = d_steps.p; B.start = d_start.p; B.edge = d_edge.p; B.vertex = d_vertex.p;
+  B.stuck_list = d_blist.p; B.stuck_count = d_counts.p + 1;
+  B.ovf_list = d_olist.p; B.ovf_count = d_counts.p + 2;
+  B.lstats = d_lstats.p;
+  int64_t nb = (nq + 255) / 256;
+  hipLaunchKernelGGL(k_locate_bdy<BDY_CAP>, dim3((unsigned)nb), dim3(256), 0, s, B);
+  hipLaunchKernelGGL(k_locate_bdy_ovf, dim3(OVF_THREADS / 64), dim3(64), 0, s, B, d_ows.p, OVF_CAP);
+  hipLaunchKernelGGL(k_exh_bdy, dim3(256), dim3(256), 0, s, B);
+  (void)o;
+  return hipGetLastError() == hipSuccess;
+}

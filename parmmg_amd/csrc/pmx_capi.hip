@@ -1,0 +1,479 @@
+// pmx_capi.hip -- host side of the C ABI declared in include/pmx_transfer.h.
+//
+// Converts Mmg-style AoS (strided) meshes and solutions into the SoA device
+// layout of pmx_device.h, owns the device buffers of one GPU, and sequences
+// the kernels of one transfer step on one HIP stream.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pmx_transfer.h"
+#include "pmx_kernels.h"
+#include "pmx_internal.h"
+
+static bool ok(pmx_ctx *c, hipError_t e, const char *what) {
+  if (e == hipSuccess) return true;
+  c->err = std::string(what) + ": " + hipGetErrorString(e);
+  return false;
+}
+#define CK(x) do { if (!ok(ctx, (x), #x)) return 0; } while (0)
+
+template <class T>
+static bool dgrow(pmx_ctx *ctx, DevBuf<T> &b, size_t n) {
+  if (n <= b.cap && b.p) return true;
+  if (b.p) hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+  if (!ok(ctx, hipMalloc((void **)&b.p, bytes), "hipMalloc")) return false;
+  b.cap = n;
+  return true;
+}
+template <class T> static void dfree(DevBuf<T> &b) {
+  if (b.p) hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+}
+
+extern "C" {
+
+pmx_ctx *pmx_create(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return nullptr;
+  if (device < 0) device = 0;
+  device %= n;
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  pmx_ctx *ctx = new pmx_ctx();
+  ctx->device = device;
+  if (hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return nullptr;
+  }
+  ctx->stream = ctx->own;
+  return ctx;
+}
+
+void pmx_destroy(pmx_ctx *ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  hipStreamSynchronize(ctx->stream);
+  ctx->free_all();
+  for (auto &e : ctx->events) hipEventDestroy(e);
+  if (ctx->own) hipStreamDestroy(ctx->own);
+  delete ctx;
+}
+
+const char *pmx_last_error(pmx_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int pmx_set_stream(pmx_ctx *ctx, void *s) {
+  if (!ctx) return 0;
+  ctx->stream = s ? (hipStream_t)s : ctx->own;
+  return 1;
+}
+
+int pmx_synchronize(pmx_ctx *ctx) {
+  if (!ctx) return 0;
+  CK(hipStreamSynchronize(ctx->stream));
+  return 1;
+}
+
+int pmx_device_info(pmx_ctx *ctx, char *buf, int buflen) {
+  if (!ctx) return 0;
+  hipDeviceProp_t p;
+  CK(hipGetDeviceProperties(&p, ctx->device));
+  snprintf(buf, (size_t)buflen, "%s %s CUs=%d HBM=%.1fGB", p.name, p.gcnArchName,
+           p.multiProcessorCount, (double)p.totalGlobalMem / 1e9);
+  return 1;
+}
+
+// ---- background upload ------------------------------------------------------
+
+int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
+                          const pmx_sol_view *sols, int imet) {
+  if (!ctx || !m) return 0;
+  hipSetDevice(ctx->device);
+  if (m->np < 1 || m->ne < 1 || m->np >= (1LL << 31) || 4 * m->ne >= (1LL << 31)) {
+    ctx->err = "pmx_upload_background: mesh sizes out of range";
+    return 0;
+  }
+  if (!m->point_c || !m->tetra_v || !m->adja) {
+    ctx->err = "pmx_upload_background: point_c, tetra_v and adja are required";
+    return 0;
+  }
+  if (nsol < 0 || nsol > PMX_MAX_SOLS || imet >= nsol) {
+    ctx->err = "pmx_upload_background: bad solution list";
+    return 0;
+  }
+  const int64_t np = m->np, ne = m->ne, nt = m->nt;
+  ctx->np = np; ctx->ne = ne; ctx->nt = nt; ctx->hausd = m->hausd;
+
+  // points -> Pt4, bbox
+  std::vector<Pt4> hp((size_t)(np + 1));
+  double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+  hp[0] = Pt4{0, 0, 0, 0};
+  const char *pc = (const char *)m->point_c;
+  for (int64_t i = 1; i <= np; i++) {
+    const double *c = (const double *)(pc + i * m->point_stride);
+    hp[i] = Pt4{c[0], c[1], c[2], 0.0};
+    for (int a = 0; a < 3; a++) {
+      lo[a] = std::min(lo[a], c[a]);
+      hi[a] = std::max(hi[a], c[a]);
+    }
+  }
+  // tets -> TetRec with neighbour tet index
+  std::vector<TetRec> ht((size_t)(ne + 1));
+  memset(&ht[0], 0, sizeof(TetRec));
+  const char *tc = (const char *)m->tetra_v;
+  for (int64_t k = 1; k <= ne; k++) {
+    const int *v = (const int *)(tc + k * m->tetra_stride);
+    TetRec &r = ht[(size_t)k];
+    for (int l = 0; l < 4; l++) {
+      r.v[l] = v[l];
+      r.nb[l] = m->adja[4 * (k - 1) + 1 + l] / 4;
+    }
+  }
+  // solutions -> interleaved [np+1][S]
+  SolDesc sd{};
+  sd.nsol = nsol;
+  sd.imet = imet;
+  int S = 0;
+  for (int s = 0; s < nsol; s++) {
+    if (sols[s].size != 1 && sols[s].size != 3 && sols[s].size != 6) {
+      ctx->err = "pmx_upload_background: solution size must be 1, 3 or 6";
+      return 0;
+    }
+    sd.size[s] = sols[s].size;
+    sd.off[s] = S;
+    S += sols[s].size;
+  }
+  sd.S = S;
+  ctx->sd = sd;
+  std::vector<double> hs((size_t)(np + 1) * std::max(S, 1), 0.0);
+  for (int s = 0; s < nsol; s++) {
+    const int sz = sols[s].size;
+    if (!sols[s].m) { ctx->err = "pmx_upload_background: null solution"; return 0; }
+    for (int64_t i = 1; i <= np; i++)
+      for (int j = 0; j < sz; j++) hs[(size_t)i * S + sd.off[s] + j] = sols[s].m[i * sz + j];
+  }
+  // boundary triangles
+  std::vector<TriRec> htr((size_t)(nt + 1));
+  memset(&htr[0], 0, sizeof(TriRec));
+  if (nt > 0) {
+    if (!m->tria_v || !m->adjt) {
+      ctx->err = "pmx_upload_background: nt > 0 requires tria_v and adjt";
+      return 0;
+    }
+    const char *rc = (const char *)m->tria_v;
+    for (int64_t k = 1; k <= nt; k++) {
+      const int *v = (const int *)(rc + k * m->tria_stride);
+      TriRec &r = htr[(size_t)k];
+      for (int l = 0; l < 3; l++) {
+        r.v[l] = v[l];
+        r.nb[l] = m->adjt[3 * (k - 1) + 1 + l] / 3;
+      }
+    }
+  }
+  ctx->host_build_node_trias(htr);
+
+  // hint grid over the background bbox: about one cell per 6 tets
+  double ext[3], vol = 1.0;
+  for (int a = 0; a < 3; a++) {
+    ext[a] = std::max(hi[a] - lo[a], 1e-300);
+    vol *= ext[a];
+  }
+  double target = std::max(1.0, (double)ne / 6.0);
+  double h = std::cbrt(vol / target);
+  GridDesc g;
+  int64_t cells = 1;
+  for (int a = 0; a < 3; a++) {
+    int d = (int)std::ceil(ext[a] / h);
+    d = std::max(1, std::min(d, 4096));
+    g.dim[a] = d;
+    g.lo[a] = lo[a];
+    g.inv[a] = (double)d / ext[a];
+    cells *= d;
+  }
+  ctx->grid = g;
+  ctx->gcells = cells;
+  for (int a = 0; a < 3; a++) { ctx->bblo[a] = lo[a]; ctx->bbhi[a] = hi[a]; }
+
+  if (!dgrow(ctx, ctx->d_pts, (size_t)(np + 1))) return 0;
+  if (!dgrow(ctx, ctx->d_tets, (size_t)(ne + 1))) return 0;
+  if (!dgrow(ctx, ctx->d_sol, hs.size())) return 0;
+  if (!dgrow(ctx, ctx->d_tris, (size_t)(nt + 1))) return 0;
+  if (!dgrow(ctx, ctx->d_grid, (size_t)cells)) return 0;
+  if (!dgrow(ctx, ctx->d_ntoff, ctx->h_ntoff.size())) return 0;
+  if (!dgrow(ctx, ctx->d_ntlist, std::max<size_t>(ctx->h_ntlist.size(), 1))) return 0;
+  if (!dgrow(ctx, ctx->d_trn, (size_t)(nt + 1))) return 0;
+  CK(hipMemcpyAsync(ctx->d_pts.p, hp.data(), hp.size() * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemcpyAsync(ctx->d_tets.p, ht.data(), ht.size() * sizeof(TetRec), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemcpyAsync(ctx->d_sol.p, hs.data(), hs.size() * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemcpyAsync(ctx->d_tris.p, htr.data(), htr.size() * sizeof(TriRec), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemcpyAsync(ctx->d_ntoff.p, ctx->h_ntoff.data(), ctx->h_ntoff.size() * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+  if (!ctx->h_ntlist.empty())
+    CK(hipMemcpyAsync(ctx->d_ntlist.p, ctx->h_ntlist.data(), ctx->h_ntlist.size() * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+  if (nt > 0) launch_tria_normals(ctx->d_tris.p, ctx->d_pts.p, nt, ctx->d_trn.p, ctx->stream);
+  CK(hipGetLastError());
+  CK(hipStreamSynchronize(ctx->stream));   // host staging vectors die here
+  ctx->have_bg = true;
+  return 1;
+}
+
+int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
+  if (!ctx || !pv) return 0;
+  hipSetDevice(ctx->device);
+  const int64_t n = pv->last - pv->first + 1;
+  if (n < 0 || n >= (1LL << 31)) { ctx->err = "pmx_upload_points: bad range"; return 0; }
+  std::vector<Pt4> hq((size_t)std::max<int64_t>(n, 1));
+  std::vector<int8_t> hk((size_t)std::max<int64_t>(n, 1));
+  const char *pc = (const char *)pv->c;
+  const char *tg = (const char *)pv->tag;
+  int64_t nv = 0, nb = 0;
+  for (int64_t j = 0; j < n; j++) {
+    const double *c = (const double *)(pc + (pv->first + j) * pv->stride);
+    hq[(size_t)j] = Pt4{c[0], c[1], c[2], 0.0};
+    unsigned tag = tg ? *(const uint16_t *)(tg + (pv->first + j) * pv->tag_stride) : 0u;
+    int8_t kd;
+    if (tag >= PMX_TAG_NUL) kd = KIND_NUL;
+    else if (tag & PMX_TAG_REQ) kd = KIND_SKIP;
+    else if (tag & PMX_TAG_BDY) { kd = KIND_BDY; nb++; }
+    else { kd = KIND_VOL; nv++; }
+    hk[(size_t)j] = kd;
+  }
+  ctx->nq = n;
+  ctx->nq_vol = nv;
+  ctx->nq_bdy = nb;
+  const size_t nn = (size_t)std::max<int64_t>(n, 1);
+  if (!dgrow(ctx, ctx->d_q, nn)) return 0;
+  if (!dgrow(ctx, ctx->d_kind, nn)) return 0;
+  if (!dgrow(ctx, ctx->d_wmask, nn)) return 0;
+  if (!dgrow(ctx, ctx->d_elem, nn)) return 0;
+  if (!dgrow(ctx, ctx->d_status, nn)) return 0;
+  if (!dgrow(ctx, ctx->d_steps, nn)) return 0;
+  if (!dgrow(ctx, ctx->d_start, nn)) return 0;
+  if (!dgrow(ctx, ctx->d_edge, nn)) return 0;
+  if (!dgrow(ctx, ctx->d_vertex, nn)) return 0;
+  if (!dgrow(ctx, ctx->d_list, nn)) return 0;
+  if (!dgrow(ctx, ctx->d_found, nn)) return 0;
+  if (!dgrow(ctx, ctx->d_bestk, nn)) return 0;
+  if (!dgrow(ctx, ctx->d_best, nn)) return 0;
+  if (!dgrow(ctx, ctx->d_counts, 8)) return 0;
+  if (!dgrow(ctx, ctx->d_lstats, 16)) return 0;
+  CK(hipMemcpyAsync(ctx->d_q.p, hq.data(), (size_t)n * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemcpyAsync(ctx->d_kind.p, hk.data(), (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  ctx->have_pts = true;
+  ctx->out_S = -1;
+  return 1;
+}
+
+// ---- the step ---------------------------------------------------------------
+
+int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
+  if (!ctx) return 0;
+  if (!ctx->have_bg || !ctx->have_pts) { ctx->err = "pmx_run: upload background and points first"; return 0; }
+  hipSetDevice(ctx->device);
+  pmx_run_opts opts{};
+  if (o) opts = *o;
+  const int64_t n = ctx->nq;
+  const int S = ctx->sd.S;
+  if (!dgrow(ctx, ctx->d_out, (size_t)std::max<int64_t>(n * S, 1))) return 0;
+  ctx->out_S = S;
+  SolDesc sd = ctx->sd;
+  sd.metric_const = (opts.hsiz > 0.0 && sd.imet >= 0) ? 1 : 0;
+
+  hipEvent_t *ev = nullptr;
+  if (opts.timing) ev = ctx->next_event_slot();
+
+  hipStream_t st = ctx->stream;
+  if (ev) CK(hipEventRecord(ev[0], st));
+  CK(hipMemsetAsync(ctx->d_wmask.p, 0, (size_t)std::max<int64_t>(n, 1), st));
+  launch_run_init(ctx->d_counts.p, ctx->d_lstats.p, st);
+  if (sd.metric_const)
+    launch_const_metric(ctx->d_kind.p, n, ctx->d_out.p, S, sd.off[sd.imet], sd.size[sd.imet],
+                        opts.hsiz, ctx->d_wmask.p, sd.imet, st);
+  bool any_interp = false;
+  for (int s = 0; s < sd.nsol; s++)
+    if (!(s == sd.imet && sd.metric_const)) any_interp = true;
+  // reference early exit (src/interpmesh_pmmg.c:509-512): nothing to locate
+  if (any_interp) {
+    CK(hipMemsetAsync(ctx->d_grid.p, 0, (size_t)ctx->gcells * sizeof(int), st));
+    launch_hint_build(ctx->d_tets.p, ctx->d_pts.p, ctx->ne, 1, ctx->d_grid.p, ctx->grid, st);
+    if (ev) CK(hipEventRecord(ev[1], st));
+    VolArgs A{};
+    A.pts = ctx->d_pts.p; A.tets = ctx->d_tets.p; A.sol = ctx->d_sol.p; A.sd = sd;
+    A.q = ctx->d_q.p; A.kind = ctx->d_kind.p; A.nq = n; A.ne = ctx->ne;
+    A.grid = ctx->d_grid.p; A.g = ctx->grid;
+    A.out = ctx->d_out.p; A.wmask = ctx->d_wmask.p;
+    A.elem = ctx->d_elem.p; A.status = ctx->d_status.p; A.steps = ctx->d_steps.p;
+    A.start = ctx->d_start.p;
+    A.stuck_list = ctx->d_list.p; A.stuck_count = ctx->d_counts.p;
+    A.found = ctx->d_found.p; A.bestk = ctx->d_bestk.p; A.best = ctx->d_best.p;
+    A.lstats = ctx->d_lstats.p;
+    A.max_walk = opts.max_walk > 0 ? opts.max_walk : 512;
+    A.xcd_swizzle = 1;
+    if (ctx->nq_vol) launch_locate_vol(A, st);
+    if (ev) CK(hipEventRecord(ev[2], st));
+    if (ctx->nq_bdy) {
+      if (!ctx->launch_bdy(A, opts, st)) return 0;
+    }
+    if (ev) CK(hipEventRecord(ev[3], st));
+    ExhArgs E{};
+    E.pts = ctx->d_pts.p; E.tets = ctx->d_tets.p; E.ne = ctx->ne; E.q = ctx->d_q.p;
+    E.list = ctx->d_list.p; E.count = ctx->d_counts.p; E.found = ctx->d_found.p;
+    E.best = ctx->d_best.p; E.bestk = ctx->d_bestk.p;
+    if (ctx->nq_vol) launch_exhaustive(E, A, st);
+    if (ev) CK(hipEventRecord(ev[4], st));
+  } else if (ev) {
+    for (int k = 1; k < 5; k++) CK(hipEventRecord(ev[k], st));
+  }
+  CK(hipGetLastError());
+  ctx->ran = true;
+  return 1;
+}
+
+int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem, int *status, int *steps) {
+  if (!ctx || !ctx->ran) { if (ctx) ctx->err = "pmx_download: nothing ran"; return 0; }
+  hipSetDevice(ctx->device);
+  const int64_t n = ctx->nq;
+  const int S = ctx->sd.S;
+  CK(hipStreamSynchronize(ctx->stream));
+  if (new_sols && S > 0) {
+    std::vector<double> h((size_t)(n * S));
+    std::vector<uint8_t> wm((size_t)std::max<int64_t>(n, 1));
+    CK(hipMemcpy(h.data(), ctx->d_out.p, (size_t)(n * S) * sizeof(double), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(wm.data(), ctx->d_wmask.p, (size_t)n, hipMemcpyDeviceToHost));
+    for (int s = 0; s < ctx->sd.nsol; s++) {
+      double *dst = new_sols[s].m;
+      const int sz = ctx->sd.size[s], off = ctx->sd.off[s];
+      if (!dst) continue;
+      for (int64_t i = 0; i < n; i++) {
+        if (!(wm[(size_t)i] & (1u << s))) continue;
+        for (int j = 0; j < sz; j++) dst[i * sz + j] = h[(size_t)(i * S + off + j)];
+      }
+    }
+  }
+  if (elem) CK(hipMemcpy(elem, ctx->d_elem.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
+  if (status) CK(hipMemcpy(status, ctx->d_status.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
+  if (steps) CK(hipMemcpy(steps, ctx->d_steps.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
+  return 1;
+}
+
+int pmx_download_starts(pmx_ctx *ctx, int *start) {
+  if (!ctx || !ctx->ran) return 0;
+  CK(hipStreamSynchronize(ctx->stream));
+  CK(hipMemcpy(start, ctx->d_start.p, (size_t)ctx->nq * sizeof(int), hipMemcpyDeviceToHost));
+  return 1;
+}
+
+int pmx_download_border(pmx_ctx *ctx, int *edge, int *vertex) {
+  if (!ctx || !ctx->ran) return 0;
+  CK(hipStreamSynchronize(ctx->stream));
+  if (edge) CK(hipMemcpy(edge, ctx->d_edge.p, (size_t)ctx->nq * sizeof(int), hipMemcpyDeviceToHost));
+  if (vertex) CK(hipMemcpy(vertex, ctx->d_vertex.p, (size_t)ctx->nq * sizeof(int), hipMemcpyDeviceToHost));
+  return 1;
+}
+
+int pmx_locate_stats_get(pmx_ctx *ctx, pmx_locate_stats *st) {
+  if (!ctx || !ctx->ran || !st) return 0;
+  unsigned long long h[16];
+  unsigned cnt[8];
+  CK(hipStreamSynchronize(ctx->stream));
+  CK(hipMemcpy(h, ctx->d_lstats.p, sizeof h, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(cnt, ctx->d_counts.p, sizeof cnt, hipMemcpyDeviceToHost));
+  memset(st, 0, sizeof *st);
+  st->nvol = ctx->nq_vol;
+  st->nbdy = ctx->nq_bdy;
+  st->nexhaust = cnt[0] + cnt[1];
+  unsigned long long located = h[0] + h[4];
+  st->stepmax = (int64_t)std::max(h[2], h[6]);
+  unsigned long long mn = std::min(h[3], h[7]);
+  st->stepmin = located ? (int64_t)mn : 0;
+  st->stepav = located ? (double)(h[1] + h[5]) / (double)located : 0.0;
+  // points resolved by the exhaustive scans and still not contained anywhere
+  std::vector<int> status((size_t)std::max<int64_t>(ctx->nq, 1));
+  if (ctx->nq) CK(hipMemcpy(status.data(), ctx->d_status.p, (size_t)ctx->nq * sizeof(int), hipMemcpyDeviceToHost));
+  std::vector<int8_t> kind((size_t)std::max<int64_t>(ctx->nq, 1));
+  if (ctx->nq) CK(hipMemcpy(kind.data(), ctx->d_kind.p, (size_t)ctx->nq, hipMemcpyDeviceToHost));
+  int64_t nc = 0;
+  for (int64_t i = 0; i < ctx->nq; i++)
+    if ((kind[(size_t)i] == KIND_VOL || kind[(size_t)i] == KIND_BDY) && status[(size_t)i] == 0) nc++;
+  st->nclosest = nc;
+  return 1;
+}
+
+void *pmx_device_buffer(pmx_ctx *ctx, int which) {
+  if (!ctx) return nullptr;
+  switch (which) {
+    case 0: return ctx->d_out.p;
+    case 1: return ctx->d_elem.p;
+    case 2: return ctx->d_status.p;
+    default: return nullptr;
+  }
+}
+
+int pmx_timing_reset(pmx_ctx *ctx) {
+  if (!ctx) return 0;
+  ctx->ev_used = 0;
+  return 1;
+}
+
+double pmx_kernel_ms(pmx_ctx *ctx, int which) {
+  if (!ctx || ctx->ev_used == 0 || which < 0 || which > 4) return -1.0;
+  hipStreamSynchronize(ctx->stream);
+  double tot = 0.0;
+  for (int r = 0; r < ctx->ev_used; r++) {
+    hipEvent_t *e = &ctx->events[(size_t)r * 5];
+    float ms = 0.f;
+    if (which == 4) hipEventElapsedTime(&ms, e[0], e[4]);
+    else hipEventElapsedTime(&ms, e[which], e[which + 1]);
+    tot += ms;
+  }
+  return tot / ctx->ev_used;
+}
+
+}  // extern "C"
+
+// ---- pmx_ctx members ----------------------------------------------------------
+
+hipEvent_t *pmx_ctx::next_event_slot() {
+  size_t need = (size_t)(ev_used + 1) * 5;
+  while (events.size() < need) {
+    hipEvent_t e;
+    hipEventCreate(&e);
+    events.push_back(e);
+  }
+  hipEvent_t *r = &events[(size_t)ev_used * 5];
+  ev_used++;
+  return r;
+}
+
+void pmx_ctx::free_all() {
+  dfree(d_pts); dfree(d_tets); dfree(d_sol); dfree(d_tris); dfree(d_trn); dfree(d_grid);
+  dfree(d_ntoff); dfree(d_ntlist);
+  dfree(d_q); dfree(d_kind); dfree(d_wmask); dfree(d_out); dfree(d_elem); dfree(d_status);
+  dfree(d_steps); dfree(d_start); dfree(d_edge); dfree(d_vertex); dfree(d_list); dfree(d_found);
+  dfree(d_bestk); dfree(d_best); dfree(d_counts); dfree(d_lstats);
+  dfree(d_qual); dfree(d_red); dfree(d_blist); dfree(d_olist); dfree(d_ows);
+  if (d_tgrid) hipFree(d_tgrid);
+  d_tgrid = nullptr;
+  d_tgrid_cap = 0;
+}
+
+// node -> trias graph: offsets[np+2] (0-based CSR) + list of incident trias
+// (the content of PMMG_precompute_nodeTrias, src/locate_pmmg.c:134-195, in
+// CSR form; fan order = increasing tria index, as in the reference)
+void pmx_ctx::host_build_node_trias(const std::vector<TriRec> &tr) {
+  h_ntoff.assign((size_t)(np + 2), 0);
+  for (int64_t k = 1; k <= nt; k++)
+    for (int l = 0; l < 3; l++) h_ntoff[(size_t)tr[(size_t)k].v[l] + 1]++;
+  for (int64_t i = 1; i <= np + 1; i++) h_ntoff[(size_t)i] += h_ntoff[(size_t)i - 1];
+  h_ntlist.assign((size_t)h_ntoff[(size_t)np + 1], 0);
+  std::vector<int> fill(h_ntoff.begin(), h_ntoff.end() - 1);
+  for (int64_t k = 1; k <= nt; k++)
+    for (int l = 0; l < 3; l++) h_ntlist[(size_t)fill[(size_t)tr[(size_t)k].v[l]]++] = (int)k;
+}

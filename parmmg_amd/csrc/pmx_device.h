@@ -1,0 +1,145 @@
+// pmx_device.h -- device-side data layout and geometry for the gfx950 kernels.
+//
+// HBM layout (all 1-based like Mmg, slot 0 unused):
+//   Pt4     pts[np+1]     32 B  {x,y,z,0}          one aligned 32-B gather / vertex
+//   TetRec  tets[ne+1]    32 B  {v[4], nb[4]}      nb[f] = adja/4 (0 = boundary face)
+//   double  sol[(np+1)*S]        all background solutions interleaved per vertex
+//   TriRec  tris[nt+1]    32 B  {v[3], -, nb[3], -} nb[e] = adjt/3
+//   Pt4     trn[nt+1]     32 B  unit normal + |n| (PMMG_precompute_triaNormals)
+// New points: Pt4 q[npts] (0-based list), int8 kind[npts].
+//
+// Floating point: every expression below follows the operation order of the
+// reference / restated Mmg helper it cites, and the library is built with
+// -ffp-contract=off so that no a*b+c is fused: results are bit-identical to
+// the x86-64 oracle (oracle/pmx_oracle.c) on the same inputs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PMX_EPS   1.e-6     // MMG5_EPS
+#define PMX_EPSD2 1.e-200   // MMG5_EPSD2
+
+struct __align__(32) Pt4 { double x, y, z, w; };
+struct __align__(32) TetRec { int v[4]; int nb[4]; };
+struct __align__(32) TriRec { int v[3]; int pad0; int nb[3]; int pad1; };
+
+struct D3 { double x, y, z; };
+
+enum : int8_t { KIND_VOL = 0, KIND_BDY = 1, KIND_SKIP = 2, KIND_NUL = 3 };
+
+struct SolDesc {
+  int nsol;
+  int S;              // total doubles per vertex
+  int imet;           // index of the metric, -1 none
+  int metric_const;   // 1: metric set by constant size (not interpolated)
+  int size[8];
+  int off[8];
+};
+
+__device__ __forceinline__ D3 ld3(const Pt4 *p, int i) {
+  Pt4 t = p[i];
+  return D3{t.x, t.y, t.z};
+}
+
+// MMG5_nonUnitNorPts (restated): (b-a) x (c-a)
+__device__ __forceinline__ D3 nonunit_normal(D3 a, D3 b, D3 c) {
+  double abx = b.x - a.x, aby = b.y - a.y, abz = b.z - a.z;
+  double acx = c.x - a.x, acy = c.y - a.y, acz = c.z - a.z;
+  D3 n;
+  n.x = aby * acz - abz * acy;
+  n.y = abz * acx - abx * acz;
+  n.z = abx * acy - aby * acx;
+  return n;
+}
+
+// MMG5_orvol -> MMG5_det4pt -> MMG5_det3pt1vec (restated)
+__device__ __forceinline__ double orvol(D3 c0, D3 c1, D3 c2, D3 c3) {
+  double w0 = c3.x - c0.x, w1 = c3.y - c0.y, w2 = c3.z - c0.z;
+  double m00 = c1.x - c0.x, m01 = c2.x - c0.x, m02 = w0;
+  double m10 = c1.y - c0.y, m11 = c2.y - c0.y, m12 = w1;
+  double m20 = c1.z - c0.z, m21 = c2.z - c0.z, m22 = w2;
+  return m00 * (m11 * m22 - m21 * m12) - m10 * (m01 * m22 - m21 * m02) +
+         m20 * (m01 * m12 - m11 * m02);
+}
+
+// lambda_f = -((p - c_f) . n_f) / vol, c_f = first vertex of face f in
+// MMG5_idir order (reference src/barycoord_pmmg.c:238-257 with the normals
+// of src/locate_pmmg.c:101-122 recomputed in registers instead of stored).
+__device__ __forceinline__ void tet_lambda(const D3 P[4], D3 p, double lam[4], double *volp) {
+  double vol = orvol(P[0], P[1], P[2], P[3]);
+  D3 n0 = nonunit_normal(P[1], P[2], P[3]);
+  D3 n1 = nonunit_normal(P[0], P[3], P[2]);
+  D3 n2 = nonunit_normal(P[0], P[1], P[3]);
+  D3 n3 = nonunit_normal(P[0], P[2], P[1]);
+  lam[0] = -((p.x - P[1].x) * n0.x + (p.y - P[1].y) * n0.y + (p.z - P[1].z) * n0.z) / vol;
+  lam[1] = -((p.x - P[0].x) * n1.x + (p.y - P[0].y) * n1.y + (p.z - P[0].z) * n1.z) / vol;
+  lam[2] = -((p.x - P[0].x) * n2.x + (p.y - P[0].y) * n2.y + (p.z - P[0].z) * n2.z) / vol;
+  lam[3] = -((p.x - P[0].x) * n3.x + (p.y - P[0].y) * n3.y + (p.z - P[0].z) * n3.z) / vol;
+  *volp = vol;
+}
+
+// Stable ascending order of 4 (value, index) pairs: adjacent compare-exchange
+// (bubble) network == glibc's stable qsort of src/barycoord_pmmg.c:306.
+__device__ __forceinline__ void cswap(double &a, double &b, int &ia, int &ib) {
+  bool s = a > b;
+  double ta = s ? b : a, tb = s ? a : b;
+  int tia = s ? ib : ia, tib = s ? ia : ib;
+  a = ta; b = tb; ia = tia; ib = tib;
+}
+__device__ __forceinline__ void sort4(double v[4], int id[4]) {
+  cswap(v[0], v[1], id[0], id[1]);
+  cswap(v[1], v[2], id[1], id[2]);
+  cswap(v[2], v[3], id[2], id[3]);
+  cswap(v[0], v[1], id[0], id[1]);
+  cswap(v[1], v[2], id[1], id[2]);
+  cswap(v[0], v[1], id[0], id[1]);
+}
+__device__ __forceinline__ void sort3(double v[3], int id[3]) {
+  cswap(v[0], v[1], id[0], id[1]);
+  cswap(v[1], v[2], id[1], id[2]);
+  cswap(v[0], v[1], id[0], id[1]);
+}
+
+__device__ __forceinline__ int sel4(const int a[4], int i) {
+  int r = a[0];
+  r = (i == 1) ? a[1] : r;
+  r = (i == 2) ? a[2] : r;
+  r = (i == 3) ? a[3] : r;
+  return r;
+}
+
+// MMG5_invmat (restated from Mmg @889d408; unpinned)
+__device__ __forceinline__ bool invmat(const double m[6], double mi[6]) {
+  double vmax = fabs(m[1]), t;
+  t = fabs(m[2]); if (t > vmax) vmax = t;
+  t = fabs(m[4]); if (t > vmax) vmax = t;
+  if (vmax < PMX_EPS) {
+    mi[0] = 1. / m[0];
+    mi[3] = 1. / m[3];
+    mi[5] = 1. / m[5];
+    mi[1] = mi[2] = mi[4] = 0.0;
+    return true;
+  }
+  double vmin = fabs(m[0]);
+  vmax = vmin;
+#pragma unroll
+  for (int k = 1; k < 6; k++) {
+    t = fabs(m[k]);
+    if (t < vmin) vmin = t;
+    else if (t > vmax) vmax = t;
+  }
+  if (vmax == 0.0) return false;
+  double aa = m[3] * m[5] - m[4] * m[4];
+  double bb = m[4] * m[2] - m[1] * m[5];
+  double cc = m[1] * m[4] - m[2] * m[3];
+  double det = m[0] * aa + m[1] * bb + m[2] * cc;
+  if (fabs(det) < PMX_EPSD2) return false;
+  det = 1.0 / det;
+  mi[0] = aa * det;
+  mi[1] = bb * det;
+  mi[2] = cc * det;
+  mi[3] = (m[0] * m[5] - m[2] * m[2]) * det;
+  mi[4] = (m[1] * m[2] - m[0] * m[4]) * det;
+  mi[5] = (m[0] * m[3] - m[1] * m[1]) * det;
+  return true;
+}

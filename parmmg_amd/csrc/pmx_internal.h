@@ -1,0 +1,69 @@
+// pmx_internal.h -- the context object behind the C ABI (host only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <string>
+#include <vector>
+#include "pmx_transfer.h"
+#include "pmx_kernels.h"
+
+template <class T> struct DevBuf {
+  T *p = nullptr;
+  size_t cap = 0;
+};
+
+struct pmx_ctx {
+  int device = 0;
+  hipStream_t own = nullptr, stream = nullptr;
+  std::string err;
+
+  // background group
+  bool have_bg = false;
+  int64_t np = 0, ne = 0, nt = 0;
+  double hausd = 0.0;
+  SolDesc sd{};
+  GridDesc grid{};
+  int64_t gcells = 0;
+  double bblo[3]{}, bbhi[3]{};
+  DevBuf<Pt4> d_pts;
+  DevBuf<TetRec> d_tets;
+  DevBuf<double> d_sol;
+  DevBuf<TriRec> d_tris;
+  DevBuf<Pt4> d_trn;
+  DevBuf<int> d_grid;
+  DevBuf<int> d_ntoff, d_ntlist;
+  std::vector<int> h_ntoff, h_ntlist;
+
+  // new points and results
+  bool have_pts = false, ran = false;
+  int64_t nq = 0, nq_vol = 0, nq_bdy = 0;
+  int out_S = -1;
+  DevBuf<Pt4> d_q;
+  DevBuf<int8_t> d_kind;
+  DevBuf<uint8_t> d_wmask;
+  DevBuf<double> d_out;
+  DevBuf<int> d_elem, d_status, d_steps, d_start, d_edge, d_vertex;
+  DevBuf<int> d_list, d_found, d_bestk;
+  DevBuf<unsigned long long> d_best;
+  DevBuf<unsigned> d_counts;            // [0] vol stuck, [1] bdy stuck, [2] bdy overflow
+  DevBuf<unsigned long long> d_lstats;  // [0..3] vol, [4..7] bdy
+  DevBuf<int> d_blist, d_olist, d_ows;
+  int *d_tgrid = nullptr;
+  size_t d_tgrid_cap = 0;
+
+  // statistics
+  DevBuf<double> d_qual;
+  DevBuf<unsigned long long> d_red;
+  bool have_qual = false;
+
+  // timing
+  std::vector<hipEvent_t> events;
+  int ev_used = 0;
+
+  hipEvent_t *next_event_slot();
+  void free_all();
+  void host_build_node_trias(const std::vector<TriRec> &tr);
+  bool launch_bdy(const VolArgs &a, const pmx_run_opts &o, hipStream_t s);
+};
+
+void launch_tria_normals(const TriRec *tris, const Pt4 *pts, int64_t nt, Pt4 *trn, hipStream_t s);
+extern "C" int pmx_timing_reset(pmx_ctx *ctx);

@@ -1,0 +1,60 @@
+// pmx_kernels.h -- kernel argument blocks and launchers (host <-> device).
+#pragma once
+#include "pmx_device.h"
+
+struct GridDesc {
+  int dim[3];
+  double lo[3];
+  double inv[3];
+};
+
+struct VolArgs {
+  const Pt4 *pts;
+  const TetRec *tets;
+  const double *sol;
+  SolDesc sd;
+  const Pt4 *q;
+  const int8_t *kind;
+  int64_t nq, ne;
+  const int *grid;
+  GridDesc g;
+  double *out;
+  uint8_t *wmask;
+  int *elem, *status, *steps, *start;
+  int *stuck_list;
+  unsigned *stuck_count;
+  int *found, *bestk;
+  unsigned long long *best;
+  unsigned long long *lstats;   // [0] located, [1] sum steps, [2] max, [3] min
+  int max_walk;
+  int xcd_swizzle;
+};
+
+struct ExhArgs {
+  const Pt4 *pts;
+  const TetRec *tets;
+  int64_t ne;
+  const Pt4 *q;
+  const int *list;
+  const unsigned *count;
+  int *found;
+  unsigned long long *best;
+  int *bestk;
+};
+
+void launch_hint_build(const TetRec *tets, const Pt4 *pts, int64_t ne, int stride, int *grid,
+                       GridDesc g, hipStream_t s);
+void launch_locate_vol(const VolArgs &a, hipStream_t s);
+void launch_exhaustive(const ExhArgs &e, const VolArgs &v, hipStream_t s);
+void launch_const_metric(const int8_t *kind, int64_t nq, double *out, int S, int off, int size,
+                         double hsiz, uint8_t *wmask, int imet, hipStream_t s);
+void launch_run_init(unsigned *stuck_count, unsigned long long *lstats, hipStream_t s);
+
+struct StatArgs {
+  const Pt4 *pts;
+  const TetRec *tets;
+  int64_t ne;
+  const double *sol;
+  int S, msize, moff;
+  const uint16_t *ptag;
+};

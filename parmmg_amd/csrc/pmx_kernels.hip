@@ -1,0 +1,397 @@
+// pmx_kernels.hip -- gfx950 kernels of the transfer path (volume part).
+//
+// k_hint_build       uniform grid over the background bbox, cell -> largest
+//                    tet index whose centroid falls in it (deterministic)
+// k_locate_vol       one thread per new vertex: adjacency walk from the hint
+//                    (PMMG_locatePointVol, reference src/locate_pmmg.c:786-883)
+//                    fused with PMMG_interp4bar_{iso,ani}
+//                    (src/interpmesh_pmmg.c:206-270); stuck lanes are
+//                    compacted into a list (wave-aggregated atomic)
+// k_exh_find         LDS-staged exhaustive scan for the stuck list: smallest
+//                    containing tet index == the reference's first hit in
+//                    index order (src/locate_pmmg.c:737-770)
+// k_exh_closest[_idx] argmin of |lambda_min|*vol over all tets for points
+//                    contained nowhere, then the reference's closest-vertex
+//                    barycentrics (src/barycoord_pmmg.c:371-404)
+// k_exh_finish       interpolation for the stuck list
+#include "pmx_device.h"
+#include "pmx_kernels.h"
+
+#define WALK_RING 8
+
+__device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nb) {
+  // blocks b and b+8 share an XCD (round-robin dispatch): give each XCD a
+  // contiguous range of the Morton-ordered queries so its L2 sees neighbours.
+  int64_t xcd = b & 7, r = b >> 3, q = nb >> 3, rem = nb & 7;
+  return (xcd < rem) ? xcd * (q + 1) + r : rem * (q + 1) + (xcd - rem) * q + r;
+}
+
+__device__ __forceinline__ int clampi(double t, int n) {
+  if (!(t > 0.0)) return 0;                 // also catches NaN
+  if (t >= (double)(n - 1)) return n - 1;
+  return (int)t;
+}
+
+__device__ __forceinline__ int64_t cell_of(const GridDesc &g, D3 p, int *c) {
+  c[0] = clampi((p.x - g.lo[0]) * g.inv[0], g.dim[0]);
+  c[1] = clampi((p.y - g.lo[1]) * g.inv[1], g.dim[1]);
+  c[2] = clampi((p.z - g.lo[2]) * g.inv[2], g.dim[2]);
+  return (int64_t)c[0] + (int64_t)g.dim[0] * ((int64_t)c[1] + (int64_t)g.dim[1] * c[2]);
+}
+
+__device__ int hint_lookup(const int *grid, const GridDesc &g, D3 p) {
+  int c[3];
+  int k = grid[cell_of(g, p, c)];
+  if (k) return k;
+  for (int r = 1; r <= 3; r++) {
+    for (int dz = -r; dz <= r; dz++)
+      for (int dy = -r; dy <= r; dy++)
+        for (int dx = -r; dx <= r; dx++) {
+          if (max(abs(dx), max(abs(dy), abs(dz))) != r) continue;
+          int x = c[0] + dx, y = c[1] + dy, z = c[2] + dz;
+          if (x < 0 || y < 0 || z < 0 || x >= g.dim[0] || y >= g.dim[1] || z >= g.dim[2]) continue;
+          int kk = grid[(int64_t)x + (int64_t)g.dim[0] * ((int64_t)y + (int64_t)g.dim[1] * z)];
+          if (kk) return kk;
+        }
+  }
+  return 1;
+}
+
+__global__ __launch_bounds__(256) void k_hint_build(const TetRec *__restrict__ tets,
+                                                    const Pt4 *__restrict__ pts, int64_t ne,
+                                                    int stride, int *__restrict__ grid,
+                                                    GridDesc g) {
+  int64_t n = (ne + stride - 1) / stride;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t k = 1 + t * stride;
+    int4 v = *reinterpret_cast<const int4 *>(&tets[k]);
+    if (v.x <= 0) continue;
+    D3 a = ld3(pts, v.x), b = ld3(pts, v.y), c = ld3(pts, v.z), d = ld3(pts, v.w);
+    D3 m{(a.x + b.x + c.x + d.x) * 0.25, (a.y + b.y + c.y + d.y) * 0.25,
+         (a.z + b.z + c.z + d.z) * 0.25};
+    int cc[3];
+    atomicMax(&grid[cell_of(g, m, cc)], (int)k);
+  }
+}
+
+// ---- interpolation --------------------------------------------------------
+
+// PMMG_interp4bar_iso / PMMG_interp3bar_iso (src/interpmesh_pmmg.c:125-149,
+// :206-230): out = 0, then += phi_i * old_i in vertex order.
+// PMMG_interp4bar_ani / 3bar_ani (:166-190, :247-270): invert, interpolate,
+// invert; a failed inversion leaves the output untouched (bit s of wmask).
+template <int NV>
+__device__ __forceinline__ unsigned interp_bar(const double *__restrict__ sol, const SolDesc &sd,
+                                               const int *v, const double *phi,
+                                               double *__restrict__ out) {
+  unsigned wm = 0;
+  for (int s = 0; s < sd.nsol; ++s) {
+    if (s == sd.imet && sd.metric_const) continue;
+    const int sz = sd.size[s], off = sd.off[s];
+    if (sz == 6) {
+      double mi[NV][6];
+      bool ok = true;
+#pragma unroll
+      for (int i = 0; i < NV; i++) {
+        const double *m = sol + (int64_t)v[i] * sd.S + off;
+        double mm[6] = {m[0], m[1], m[2], m[3], m[4], m[5]};
+        if (ok) ok = invmat(mm, mi[i]);
+      }
+      if (!ok) continue;
+      double mint[6], r[6];
+#pragma unroll
+      for (int j = 0; j < 6; j++) {
+        if (NV == 4)
+          mint[j] = phi[0] * mi[0][j] + phi[1] * mi[1][j] + phi[2] * mi[2][j] + phi[3] * mi[NV - 1][j];
+        else
+          mint[j] = phi[0] * mi[0][j] + phi[1] * mi[1][j] + phi[2] * mi[2][j];
+      }
+      if (!invmat(mint, r)) continue;
+#pragma unroll
+      for (int j = 0; j < 6; j++) out[off + j] = r[j];
+      wm |= 1u << s;
+    } else {
+      for (int j = 0; j < sz; j++) {
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < NV; i++) acc += phi[i] * sol[(int64_t)v[i] * sd.S + off + j];
+        out[off + j] = acc;
+      }
+      wm |= 1u << s;
+    }
+  }
+  return wm;
+}
+
+// ---- volume locate + interpolate ------------------------------------------
+
+__device__ __forceinline__ bool in_ring(const int r[WALK_RING], int k) {
+  bool h = false;
+#pragma unroll
+  for (int i = 0; i < WALK_RING; i++) h |= (r[i] == k);
+  return h;
+}
+
+__device__ __forceinline__ void wave_stats(unsigned long long *st, unsigned long long cnt,
+                                           unsigned long long sum, unsigned long long mx,
+                                           unsigned long long mn) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += __shfl_xor(cnt, o, 64);
+    sum += __shfl_xor(sum, o, 64);
+    unsigned long long a = __shfl_xor(mx, o, 64), b = __shfl_xor(mn, o, 64);
+    mx = a > mx ? a : mx;
+    mn = b < mn ? b : mn;
+  }
+  if ((threadIdx.x & 63) == 0 && cnt) {
+    atomicAdd(&st[0], cnt);
+    atomicAdd(&st[1], sum);
+    atomicMax(&st[2], mx);
+    atomicMin(&st[3], mn);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_locate_vol(VolArgs A) {
+  int64_t b = A.xcd_swizzle ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  int64_t i = b * blockDim.x + threadIdx.x;
+  unsigned long long s_cnt = 0, s_sum = 0, s_max = 0, s_min = ~0ull;
+
+  if (i < A.nq && A.kind[i] == KIND_VOL) {
+    Pt4 qq = A.q[i];
+    D3 p{qq.x, qq.y, qq.z};
+    int cur = hint_lookup(A.grid, A.g, p);
+    if (A.start) A.start[i] = cur;
+    int ring[WALK_RING];
+#pragma unroll
+    for (int r = 0; r < WALK_RING; r++) ring[r] = 0;
+    int step = 0;
+    bool found = false;
+    int v[4];
+    double lam[4];
+    for (;;) {
+      step++;
+      TetRec t = A.tets[cur];
+      if (t.v[0] <= 0) break;                       // !MG_EOK: let the scan decide
+      v[0] = t.v[0]; v[1] = t.v[1]; v[2] = t.v[2]; v[3] = t.v[3];
+      D3 P[4] = {ld3(A.pts, v[0]), ld3(A.pts, v[1]), ld3(A.pts, v[2]), ld3(A.pts, v[3])};
+      double vol;
+      tet_lambda(P, p, lam, &vol);
+      double sv[4] = {lam[0], lam[1], lam[2], lam[3]};
+      int si[4] = {0, 1, 2, 3};
+      sort4(sv, si);
+      if (sv[0] > -PMX_EPS) { found = true; break; }   // src/barycoord_pmmg.c:102-107
+      if (step >= A.max_walk) break;
+#pragma unroll
+      for (int r = WALK_RING - 1; r > 0; r--) ring[r] = ring[r - 1];
+      ring[0] = cur;
+      // first interior, not recently visited neighbour in ascending-lambda
+      // order (src/locate_pmmg.c:819-833)
+      int next = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        int nb = sel4(t.nb, si[j]);
+        if (!next && nb && !in_ring(ring, nb)) next = nb;
+      }
+      if (!next) break;
+      cur = next;
+    }
+    if (found) {
+      A.elem[i] = cur;
+      A.status[i] = 1;
+      A.steps[i] = step;
+      double *out = A.out + i * A.sd.S;
+      unsigned wm = interp_bar<4>(A.sol, A.sd, v, lam, out);
+      A.wmask[i] = (uint8_t)(A.wmask[i] | wm);
+      s_cnt = 1; s_sum = step; s_max = step; s_min = step;
+    } else {
+      unsigned slot = atomicAdd(A.stuck_count, 1u);
+      A.stuck_list[slot] = (int)i;
+      A.found[slot] = 0x7fffffff;
+      A.bestk[slot] = 0x7fffffff;
+      A.best[slot] = ~0ull;
+      A.steps[i] = -step;
+    }
+  }
+  wave_stats(A.lstats, s_cnt, s_sum, s_max, s_min);
+}
+
+// ---- exhaustive fallback ---------------------------------------------------
+
+#define EXH_CHUNK 256
+
+// smallest tet index containing each stuck point (bbox prefilter, exact test)
+__global__ __launch_bounds__(256) void k_exh_find(ExhArgs A) {
+  __shared__ D3 sp[EXH_CHUNK];
+  const unsigned n = *A.count;
+  for (unsigned c0 = 0; c0 < n; c0 += EXH_CHUNK) {
+    unsigned m = min((unsigned)EXH_CHUNK, n - c0);
+    __syncthreads();
+    for (unsigned j = threadIdx.x; j < m; j += blockDim.x) {
+      Pt4 qq = A.q[A.list[c0 + j]];
+      sp[j] = D3{qq.x, qq.y, qq.z};
+    }
+    __syncthreads();
+    for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= A.ne;
+         k += (int64_t)gridDim.x * blockDim.x) {
+      TetRec t = A.tets[k];
+      if (t.v[0] <= 0) continue;
+      D3 P[4] = {ld3(A.pts, t.v[0]), ld3(A.pts, t.v[1]), ld3(A.pts, t.v[2]), ld3(A.pts, t.v[3])};
+      double lo[3] = {P[0].x, P[0].y, P[0].z}, hi[3] = {P[0].x, P[0].y, P[0].z};
+#pragma unroll
+      for (int l = 1; l < 4; l++) {
+        lo[0] = fmin(lo[0], P[l].x); hi[0] = fmax(hi[0], P[l].x);
+        lo[1] = fmin(lo[1], P[l].y); hi[1] = fmax(hi[1], P[l].y);
+        lo[2] = fmin(lo[2], P[l].z); hi[2] = fmax(hi[2], P[l].z);
+      }
+      // lambda_i >= -1e-6 for all i keeps the point within 3e-6 * extent of
+      // the bbox; 1e-5 * max extent is a safe margin
+      double ext = fmax(hi[0] - lo[0], fmax(hi[1] - lo[1], hi[2] - lo[2]));
+      double mg = 1.e-5 * ext;
+      for (unsigned j = 0; j < m; j++) {
+        D3 p = sp[j];
+        if (p.x < lo[0] - mg || p.x > hi[0] + mg || p.y < lo[1] - mg || p.y > hi[1] + mg ||
+            p.z < lo[2] - mg || p.z > hi[2] + mg)
+          continue;
+        double lam[4], vol;
+        tet_lambda(P, p, lam, &vol);
+        double mn = fmin(fmin(lam[0], lam[1]), fmin(lam[2], lam[3]));
+        if (mn > -PMX_EPS) atomicMin(&A.found[c0 + j], (int)k);
+      }
+    }
+  }
+}
+
+// argmin over all tets of |lambda_min| * vol for points found nowhere
+__global__ __launch_bounds__(256) void k_exh_closest(ExhArgs A, int pass) {
+  __shared__ D3 sp[EXH_CHUNK];
+  __shared__ int act[EXH_CHUNK];
+  const unsigned n = *A.count;
+  for (unsigned c0 = 0; c0 < n; c0 += EXH_CHUNK) {
+    unsigned m = min((unsigned)EXH_CHUNK, n - c0);
+    __syncthreads();
+    for (unsigned j = threadIdx.x; j < m; j += blockDim.x) {
+      Pt4 qq = A.q[A.list[c0 + j]];
+      sp[j] = D3{qq.x, qq.y, qq.z};
+      act[j] = (A.found[c0 + j] == 0x7fffffff);
+    }
+    __syncthreads();
+    for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= A.ne;
+         k += (int64_t)gridDim.x * blockDim.x) {
+      TetRec t = A.tets[k];
+      if (t.v[0] <= 0) continue;
+      D3 P[4] = {ld3(A.pts, t.v[0]), ld3(A.pts, t.v[1]), ld3(A.pts, t.v[2]), ld3(A.pts, t.v[3])};
+      for (unsigned j = 0; j < m; j++) {
+        if (!act[j]) continue;
+        double lam[4], vol;
+        tet_lambda(P, sp[j], lam, &vol);
+        double mn = fmin(fmin(lam[0], lam[1]), fmin(lam[2], lam[3]));
+        double d = fabs(mn) * vol;                 // src/locate_pmmg.c:455-458
+        unsigned long long bits = (unsigned long long)__double_as_longlong(d);
+        if (pass == 0) atomicMin(&A.best[c0 + j], bits);
+        else if (bits == A.best[c0 + j]) atomicMin(&A.bestk[c0 + j], (int)k);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_exh_finish(ExhArgs A, VolArgs V) {
+  const unsigned n = *A.count;
+  for (unsigned j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    int64_t i = A.list[j];
+    Pt4 qq = A.q[i];
+    D3 p{qq.x, qq.y, qq.z};
+    int k = A.found[j];
+    int st = 1;
+    double phi[4];
+    if (k == 0x7fffffff) {
+      k = A.bestk[j];
+      st = 0;
+    }
+    TetRec t = A.tets[k];
+    int v[4] = {t.v[0], t.v[1], t.v[2], t.v[3]};
+    D3 P[4] = {ld3(A.pts, v[0]), ld3(A.pts, v[1]), ld3(A.pts, v[2]), ld3(A.pts, v[3])};
+    if (st) {
+      double vol;
+      tet_lambda(P, p, phi, &vol);
+    } else {
+      // PMMG_barycoord3d_getClosest: nearest vertex, first on ties
+      double best = 0.0;
+      int it = 0;
+#pragma unroll
+      for (int l = 0; l < 4; l++) {
+        double d0 = p.x - P[l].x, d1 = p.y - P[l].y, d2 = p.z - P[l].z;
+        double d = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+        if (l == 0 || d < best) { best = d; it = l; }
+      }
+#pragma unroll
+      for (int l = 0; l < 4; l++) phi[l] = (l == it) ? 1.0 : 0.0;
+    }
+    V.elem[i] = k;
+    V.status[i] = st ? -1 : 0;
+    V.steps[i] = V.steps[i] - 1;
+    unsigned wm = interp_bar<4>(V.sol, V.sd, v, phi, V.out + i * V.sd.S);
+    V.wmask[i] = (uint8_t)(V.wmask[i] | wm);
+  }
+}
+
+// constant-size metric (MMG3D_Set_constantSize restated): all valid points
+__global__ __launch_bounds__(256) void k_const_metric(const int8_t *__restrict__ kind, int64_t nq,
+                                                      double *__restrict__ out, int S, int off,
+                                                      int size, double hsiz,
+                                                      uint8_t *__restrict__ wmask, int imet) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nq;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (kind[i] == KIND_NUL) continue;
+    double *o = out + i * S + off;
+    if (size == 1) {
+      o[0] = hsiz;
+    } else {
+      double v = 1.0 / (hsiz * hsiz);
+      o[0] = v; o[1] = 0.0; o[2] = 0.0; o[3] = v; o[4] = 0.0; o[5] = v;
+    }
+    wmask[i] |= (uint8_t)(1u << imet);
+  }
+}
+
+__global__ void k_run_init(unsigned *stuck_count, unsigned long long *lstats) {
+  if (threadIdx.x == 0) {
+    *stuck_count = 0;
+    lstats[0] = 0; lstats[1] = 0; lstats[2] = 0; lstats[3] = ~0ull;
+  }
+}
+void launch_run_init(unsigned *stuck_count, unsigned long long *lstats, hipStream_t s) {
+  hipLaunchKernelGGL(k_run_init, dim3(1), dim3(64), 0, s, stuck_count, lstats);
+}
+
+void launch_hint_build(const TetRec *tets, const Pt4 *pts, int64_t ne, int stride, int *grid,
+                       GridDesc g, hipStream_t s) {
+  int64_t n = (ne + stride - 1) / stride;
+  int64_t nb = (n + 255) / 256;
+  if (nb > 65536) nb = 65536;
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(k_hint_build, dim3((unsigned)nb), dim3(256), 0, s, tets, pts, ne, stride,
+                     grid, g);
+}
+void launch_locate_vol(const VolArgs &a, hipStream_t s) {
+  int64_t nb = (a.nq + 255) / 256;
+  if (nb < 1) return;
+  hipLaunchKernelGGL(k_locate_vol, dim3((unsigned)nb), dim3(256), 0, s, a);
+}
+void launch_exhaustive(const ExhArgs &e, const VolArgs &v, hipStream_t s) {
+  int64_t nb = (e.ne + 255) / 256;
+  if (nb > 2048) nb = 2048;
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(k_exh_find, dim3((unsigned)nb), dim3(256), 0, s, e);
+  hipLaunchKernelGGL(k_exh_closest, dim3((unsigned)nb), dim3(256), 0, s, e, 0);
+  hipLaunchKernelGGL(k_exh_closest, dim3((unsigned)nb), dim3(256), 0, s, e, 1);
+  hipLaunchKernelGGL(k_exh_finish, dim3(64), dim3(256), 0, s, e, v);
+}
+void launch_const_metric(const int8_t *kind, int64_t nq, double *out, int S, int off, int size,
+                         double hsiz, uint8_t *wmask, int imet, hipStream_t s) {
+  int64_t nb = (nq + 255) / 256;
+  if (nb > 8192) nb = 8192;
+  if (nb < 1) return;
+  hipLaunchKernelGGL(k_const_metric, dim3((unsigned)nb), dim3(256), 0, s, kind, nq, out, S, off,
+                     size, hsiz, wmask, imet);
+}

@@ -1,0 +1,474 @@
+// pmx_stats.hip -- quality and edge-length statistics on gfx950.
+//
+// pmx_tetra_qual  <- PMMG_tetraQual -> MMG3D_tetraQual (reference
+//                    src/quality_pmmg.c:720-733; per-tet kernels restated from
+//                    Mmg MMG5_caltet_iso / MMG5_caltet33_ani, unpinned)
+// pmx_qualhisto   <- PMMG_qualhisto per-group part (src/quality_pmmg.c:156-261)
+//                    with MMG3D_computeInqua's histogram (5 bins)
+// pmx_prilen      <- PMMG_prilen / MMG3D_computePrilen (src/quality_pmmg.c:370-709)
+//
+// Both histograms are one pass over the mesh: per-thread accumulation, a
+// wavefront/LDS tree per workgroup, one partial record per workgroup, and a
+// final single-workgroup reduction in workgroup order (deterministic sums).
+// Unique edges are enumerated without a hash table: tet k owns its local edge
+// ia iff k is the smallest admissible tet index in the edge shell, found by
+// rotating around the edge through the adjacency (early exit on the first
+// smaller index) -- this is the first occurrence in the reference's
+// (k ascending, ia ascending) hash-pop order, so endpoints and orientation of
+// every length match the reference.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <vector>
+#include "pmx_internal.h"
+
+#define ALPHAD 20.7846097          // MMG3D_ALPHAD (12*sqrt(3))
+#define TAG_GEO 2
+#define TAG_REQ 4
+#define TAG_NOM 8
+#define TAG_CRN 32
+
+__constant__ int IARE[6][2] = {{0, 1}, {0, 2}, {0, 3}, {1, 2}, {1, 3}, {2, 3}};
+
+// MMG5_caltet_iso (restated)
+__device__ double caltet_iso(D3 a, D3 b, D3 c, D3 d) {
+  double abx = b.x - a.x, aby = b.y - a.y, abz = b.z - a.z;
+  double acx = c.x - a.x, acy = c.y - a.y, acz = c.z - a.z;
+  double adx = d.x - a.x, ady = d.y - a.y, adz = d.z - a.z;
+  double v1 = acy * adz - acz * ady;
+  double v2 = acz * adx - acx * adz;
+  double v3 = acx * ady - acy * adx;
+  double vol = abx * v1 + aby * v2 + abz * v3;
+  if (vol <= 0.) return 0.0;
+  double bcx = c.x - b.x, bcy = c.y - b.y, bcz = c.z - b.z;
+  double bdx = d.x - b.x, bdy = d.y - b.y, bdz = d.z - b.z;
+  double cdx = d.x - c.x, cdy = d.y - c.y, cdz = d.z - c.z;
+  double rap = abx * abx + aby * aby + abz * abz;
+  rap += acx * acx + acy * acy + acz * acz;
+  rap += adx * adx + ady * ady + adz * adz;
+  rap += bcx * bcx + bcy * bcy + bcz * bcz;
+  rap += bdx * bdx + bdy * bdy + bdz * bdz;
+  rap += cdx * cdx + cdy * cdy + cdz * cdz;
+  if (rap < PMX_EPSD2) return 0.0;
+  rap = rap * sqrt(rap);
+  return vol / rap;
+}
+
+__device__ __forceinline__ double mlen2(const double *m, double x, double y, double z) {
+  return m[0] * x * x + m[3] * y * y + m[5] * z * z + 2.0 * (m[1] * x * y + m[2] * x * z + m[4] * y * z);
+}
+
+// MMG5_caltet33_ani (restated): quality in the mean vertex metric
+__device__ double caltet_ani(D3 a, D3 b, D3 c, D3 d, const double *ma, const double *mb,
+                             const double *mc, const double *md) {
+  double mm[6];
+  for (int i = 0; i < 6; i++) mm[i] = 0.25 * (ma[i] + mb[i] + mc[i] + md[i]);
+  double abx = b.x - a.x, aby = b.y - a.y, abz = b.z - a.z;
+  double acx = c.x - a.x, acy = c.y - a.y, acz = c.z - a.z;
+  double adx = d.x - a.x, ady = d.y - a.y, adz = d.z - a.z;
+  double vol = abx * (acy * adz - acz * ady) + aby * (acz * adx - acx * adz) + abz * (acx * ady - acy * adx);
+  if (vol <= 0.) return 0.0;
+  double det = mm[0] * (mm[3] * mm[5] - mm[4] * mm[4]) - mm[1] * (mm[1] * mm[5] - mm[2] * mm[4]) +
+               mm[2] * (mm[1] * mm[4] - mm[2] * mm[3]);
+  if (det < PMX_EPSD2) return 0.0;
+  det = sqrt(det) * vol;
+  double bcx = c.x - b.x, bcy = c.y - b.y, bcz = c.z - b.z;
+  double bdx = d.x - b.x, bdy = d.y - b.y, bdz = d.z - b.z;
+  double cdx = d.x - c.x, cdy = d.y - c.y, cdz = d.z - c.z;
+  double rap = mlen2(mm, abx, aby, abz);
+  rap += mlen2(mm, acx, acy, acz);
+  rap += mlen2(mm, adx, ady, adz);
+  rap += mlen2(mm, bcx, bcy, bcz);
+  rap += mlen2(mm, bdx, bdy, bdz);
+  rap += mlen2(mm, cdx, cdy, cdz);
+  if (rap < PMX_EPSD2) return 0.0;
+  double num = sqrt(rap) * rap;
+  return det / num;
+}
+
+struct QualPart {
+  double avg, max, min;
+  long long iel, ne, good, med, his[5];
+};
+
+__device__ double tet_quality(const StatArgs &A, int64_t k, const TetRec &t) {
+  D3 a = ld3(A.pts, t.v[0]), b = ld3(A.pts, t.v[1]), c = ld3(A.pts, t.v[2]), d = ld3(A.pts, t.v[3]);
+  if (A.msize == 6) {
+    const double *m = A.sol;
+    return caltet_ani(a, b, c, d, m + (int64_t)t.v[0] * A.S + A.moff, m + (int64_t)t.v[1] * A.S + A.moff,
+                      m + (int64_t)t.v[2] * A.S + A.moff, m + (int64_t)t.v[3] * A.S + A.moff);
+  }
+  return caltet_iso(a, b, c, d);
+}
+
+// quality of every tet (+ optional histogram partials in the same pass)
+__global__ __launch_bounds__(256) void k_qual(StatArgs A, double *qual, QualPart *parts,
+                                              int use_stored) {
+  __shared__ QualPart sh[256];
+  QualPart p;
+  p.avg = 0.0; p.max = 0.0; p.min = 2.0; p.iel = 0x7fffffffffffffffLL; p.ne = 0; p.good = 0; p.med = 0;
+  for (int i = 0; i < 5; i++) p.his[i] = 0;
+  const int64_t per = (A.ne + gridDim.x - 1) / gridDim.x;       // contiguous chunk per block
+  const int64_t k0 = 1 + (int64_t)blockIdx.x * per, k1 = min(A.ne, k0 + per - 1);
+  for (int64_t k = k0 + threadIdx.x; k <= k1; k += blockDim.x) {
+    TetRec t = A.tets[k];
+    if (t.v[0] <= 0) continue;
+    double q = use_stored ? qual[k] : tet_quality(A, k, t);
+    if (!use_stored && qual) qual[k] = q;
+    if (!parts) continue;
+    double rap = ALPHAD * q;
+    p.ne++;
+    if (rap < p.min || (rap == p.min && k < p.iel)) { p.min = rap; p.iel = k; }
+    if (rap > 0.5) p.med++;
+    if (rap > 0.12) p.good++;
+    p.avg += rap;
+    p.max = fmax(p.max, rap);
+    int ir = (int)(5.0 * rap);
+    ir = ir < 4 ? ir : 4;
+    p.his[ir] += 1;
+  }
+  if (!parts) return;
+  sh[threadIdx.x] = p;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      QualPart &x = sh[threadIdx.x];
+      const QualPart &y = sh[threadIdx.x + o];
+      x.avg += y.avg;
+      x.max = fmax(x.max, y.max);
+      if (y.min < x.min || (y.min == x.min && y.iel < x.iel)) { x.min = y.min; x.iel = y.iel; }
+      x.ne += y.ne; x.good += y.good; x.med += y.med;
+      for (int i = 0; i < 5; i++) x.his[i] += y.his[i];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) parts[blockIdx.x] = sh[0];
+}
+
+__global__ __launch_bounds__(256) void k_qual_final(const QualPart *parts, int n, QualPart *res) {
+  __shared__ QualPart sh[256];
+  QualPart p;
+  p.avg = 0.0; p.max = 0.0; p.min = 2.0; p.iel = 0x7fffffffffffffffLL; p.ne = 0; p.good = 0; p.med = 0;
+  for (int i = 0; i < 5; i++) p.his[i] = 0;
+  // contiguous ranges per thread keep the summation order fixed
+  int per = (n + 255) / 256;
+  for (int b = threadIdx.x * per; b < min(n, (int)(threadIdx.x + 1) * per); b++) {
+    const QualPart &y = parts[b];
+    p.avg += y.avg;
+    p.max = fmax(p.max, y.max);
+    if (y.min < p.min || (y.min == p.min && y.iel < p.iel)) { p.min = y.min; p.iel = y.iel; }
+    p.ne += y.ne; p.good += y.good; p.med += y.med;
+    for (int i = 0; i < 5; i++) p.his[i] += y.his[i];
+  }
+  sh[threadIdx.x] = p;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      QualPart &x = sh[threadIdx.x];
+      const QualPart &y = sh[threadIdx.x + o];
+      x.avg += y.avg;
+      x.max = fmax(x.max, y.max);
+      if (y.min < x.min || (y.min == x.min && y.iel < x.iel)) { x.min = y.min; x.iel = y.iel; }
+      x.ne += y.ne; x.good += y.good; x.med += y.med;
+      for (int i = 0; i < 5; i++) x.his[i] += y.his[i];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *res = sh[0];
+}
+
+// ---- edge lengths ---------------------------------------------------------------
+
+struct LenPart {
+  double avlen, lmin, lmax;
+  long long kmin, kmax;          // first-occurrence key 6*k+ia of the extremal edges
+  long long ned, nul, hl[9];
+};
+
+// a tet is skipped when all 4 vertices are non-singular ridge points
+// (reference src/quality_pmmg.c:509-517)
+__device__ __forceinline__ bool tet_admissible(const StatArgs &A, const TetRec &t) {
+  if (!A.ptag) return true;
+  int n = 0;
+  for (int i = 0; i < 4; i++) {
+    unsigned tg = A.ptag[t.v[i]];
+    bool sin = (tg & TAG_CRN) || (tg & TAG_REQ);
+    if (!(sin || (TAG_NOM & tg)) && (tg & TAG_GEO)) continue;
+    n++;
+  }
+  return n > 0;
+}
+
+__device__ __forceinline__ int loc_of(const TetRec &t, int p) {
+  int l = 3;
+  if (t.v[0] == p) l = 0;
+  else if (t.v[1] == p) l = 1;
+  else if (t.v[2] == p) l = 2;
+  return l;
+}
+
+// true iff no admissible tet with index < k contains edge (a,b); the shell is
+// rotated both ways from k through the two faces of k that contain the edge
+__device__ bool owns_edge(const StatArgs &A, int64_t k, const TetRec &t0, int ia) {
+  const int a = t0.v[IARE[ia][0]], b = t0.v[IARE[ia][1]];
+  int others[2], no = 0;
+  for (int l = 0; l < 4; l++)
+    if (l != IARE[ia][0] && l != IARE[ia][1]) others[no++] = l;
+  for (int dir = 0; dir < 2; dir++) {
+    // cross the face opposite `opp`, the third vertex of the face we keep is `keep`
+    int opp = others[dir], keep = t0.v[others[1 - dir]];
+    int cur = t0.nb[opp];
+    int guard = 0;
+    while (cur && cur != (int)k && guard++ < 4096) {
+      TetRec t = A.tets[cur];
+      if (cur < k && tet_admissible(A, t)) return false;
+      // in `cur`, the face we came through contains a, b, and the vertex we
+      // crossed from... the next face contains a, b and the vertex not in
+      // {a, b, keep-side}: leave through the face opposite `keep`
+      int lk = loc_of(t, keep);
+      int nxt = t.nb[lk];
+      // new keep = the vertex of cur not in {a, b, keep}
+      int nk = 0;
+      for (int l = 0; l < 4; l++) {
+        int v = t.v[l];
+        if (v != a && v != b && v != keep) nk = v;
+      }
+      keep = nk;
+      cur = nxt;
+    }
+    if (cur == (int)k) break;      // closed shell: one direction saw every tet
+  }
+  return true;
+}
+
+// MMG5_lenEdg_iso / lenEdg_ani (restated, unpinned)
+__device__ double edge_len(const StatArgs &A, int p1, int p2) {
+  D3 c1 = ld3(A.pts, p1), c2 = ld3(A.pts, p2);
+  double ux = c2.x - c1.x, uy = c2.y - c1.y, uz = c2.z - c1.z;
+  if (A.msize == 6) {
+    const double *m1 = A.sol + (int64_t)p1 * A.S + A.moff, *m2 = A.sol + (int64_t)p2 * A.S + A.moff;
+    double dd1 = mlen2(m1, ux, uy, uz);
+    double dd2 = mlen2(m2, ux, uy, uz);
+    if (dd1 <= 0.0) dd1 = 0.0;
+    if (dd2 <= 0.0) dd2 = 0.0;
+    return (sqrt(dd1) + sqrt(dd2) + 4.0 * sqrt(0.5 * (dd1 + dd2))) / 6.0;
+  }
+  double h1 = A.sol[(int64_t)p1 * A.S + A.moff], h2 = A.sol[(int64_t)p2 * A.S + A.moff];
+  double l = ux * ux + uy * uy + uz * uz;
+  l = sqrt(l);
+  double r = h2 / h1 - 1.0;
+  return (fabs(r) < PMX_EPS) ? (l / h1) : (l / (h2 - h1) * log1p(r));
+}
+
+__device__ __forceinline__ void len_merge(LenPart &x, const LenPart &y) {
+  x.avlen += y.avlen;
+  if (y.lmin < x.lmin || (y.lmin == x.lmin && y.kmin < x.kmin)) { x.lmin = y.lmin; x.kmin = y.kmin; }
+  if (y.lmax > x.lmax || (y.lmax == x.lmax && y.kmax < x.kmax)) { x.lmax = y.lmax; x.kmax = y.kmax; }
+  x.ned += y.ned;
+  x.nul += y.nul;
+  for (int i = 0; i < 9; i++) x.hl[i] += y.hl[i];
+}
+__device__ __forceinline__ void len_init(LenPart &p) {
+  p.avlen = 0.0; p.lmin = 1.e30; p.lmax = 0.0;
+  p.kmin = 0x7fffffffffffffffLL; p.kmax = 0x7fffffffffffffffLL;
+  p.ned = 0; p.nul = 0;
+  for (int i = 0; i < 9; i++) p.hl[i] = 0;
+}
+
+__constant__ double BD[9] = {0.0, 0.3, 0.6, 0.7071, 0.9, 1.3, 1.4142, 2.0, 5.0};
+
+__global__ __launch_bounds__(256) void k_prilen(StatArgs A, LenPart *parts) {
+  __shared__ LenPart sh[256];
+  LenPart p;
+  len_init(p);
+  const int64_t per = (A.ne + gridDim.x - 1) / gridDim.x;
+  const int64_t k0 = 1 + (int64_t)blockIdx.x * per, k1 = min(A.ne, k0 + per - 1);
+  for (int64_t k = k0 + threadIdx.x; k <= k1; k += blockDim.x) {
+    TetRec t = A.tets[k];
+    if (t.v[0] <= 0) continue;
+    if (!tet_admissible(A, t)) continue;
+    for (int ia = 0; ia < 6; ia++) {
+      if (!owns_edge(A, k, t, ia)) continue;
+      int np_ = t.v[IARE[ia][0]], nq_ = t.v[IARE[ia][1]];
+      double len = edge_len(A, np_, nq_);
+      if (!(len != 0.0)) { if (len == 0.0) { p.nul++; continue; } }
+      long long key = 6 * k + ia;
+      p.avlen += len;
+      p.ned++;
+      if (len < p.lmin || (len == p.lmin && key < p.kmin)) { p.lmin = len; p.kmin = key; }
+      if (len > p.lmax || (len == p.lmax && key < p.kmax)) { p.lmax = len; p.kmax = key; }
+      int i;
+      for (i = 0; i < 8; i++)
+        if (BD[i] <= len && len < BD[i + 1]) { p.hl[i]++; break; }
+      if (i == 8) p.hl[8]++;
+    }
+  }
+  sh[threadIdx.x] = p;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) len_merge(sh[threadIdx.x], sh[threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) parts[blockIdx.x] = sh[0];
+}
+
+__global__ __launch_bounds__(256) void k_prilen_final(const LenPart *parts, int n, LenPart *res) {
+  __shared__ LenPart sh[256];
+  LenPart p;
+  len_init(p);
+  int per = (n + 255) / 256;
+  for (int b = threadIdx.x * per; b < min(n, (int)(threadIdx.x + 1) * per); b++) len_merge(p, parts[b]);
+  sh[threadIdx.x] = p;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) len_merge(sh[threadIdx.x], sh[threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *res = sh[0];
+}
+
+// ---- C ABI ----------------------------------------------------------------------
+
+static const int STAT_BLOCKS = 2048;
+
+static bool stat_args(pmx_ctx *ctx, StatArgs &A) {
+  if (!ctx->have_bg) { ctx->err = "statistics: upload a group first"; return false; }
+  A.pts = ctx->d_pts.p;
+  A.tets = ctx->d_tets.p;
+  A.ne = ctx->ne;
+  A.sol = ctx->d_sol.p;
+  A.S = ctx->sd.S;
+  A.msize = ctx->sd.imet >= 0 ? ctx->sd.size[ctx->sd.imet] : 0;
+  A.moff = ctx->sd.imet >= 0 ? ctx->sd.off[ctx->sd.imet] : 0;
+  A.ptag = nullptr;
+  return true;
+}
+
+static bool ensure_red(pmx_ctx *ctx, size_t bytes) {
+  size_t n = (bytes + 7) / 8;
+  if (ctx->d_red.cap >= n && ctx->d_red.p) return true;
+  if (ctx->d_red.p) hipFree(ctx->d_red.p);
+  ctx->d_red.p = nullptr;
+  if (hipMalloc((void **)&ctx->d_red.p, n * 8) != hipSuccess) { ctx->err = "hipMalloc stats"; return false; }
+  ctx->d_red.cap = n;
+  return true;
+}
+
+extern "C" {
+
+int pmx_tetra_qual(pmx_ctx *ctx, double *qual) {
+  if (!ctx) return 0;
+  hipSetDevice(ctx->device);
+  StatArgs A{};
+  if (!stat_args(ctx, A)) return 0;
+  if (ctx->d_qual.cap < (size_t)(ctx->ne + 1)) {
+    if (ctx->d_qual.p) hipFree(ctx->d_qual.p);
+    if (hipMalloc((void **)&ctx->d_qual.p, sizeof(double) * (size_t)(ctx->ne + 1)) != hipSuccess) {
+      ctx->err = "hipMalloc qual";
+      return 0;
+    }
+    ctx->d_qual.cap = (size_t)(ctx->ne + 1);
+  }
+  hipLaunchKernelGGL(k_qual, dim3(STAT_BLOCKS), dim3(256), 0, ctx->stream, A, ctx->d_qual.p,
+                     (QualPart *)nullptr, 0);
+  if (hipGetLastError() != hipSuccess) { ctx->err = "k_qual launch"; return 0; }
+  ctx->have_qual = true;
+  if (qual) {
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) return 0;
+    if (hipMemcpy(qual, ctx->d_qual.p, sizeof(double) * (size_t)(ctx->ne + 1), hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    qual[0] = 0.0;
+  }
+  return 1;
+}
+
+int pmx_qualhisto_async(pmx_ctx *ctx, int use_stored, void *dev_result) {
+  StatArgs A{};
+  if (!stat_args(ctx, A)) return 0;
+  if (use_stored && !ctx->have_qual) { ctx->err = "pmx_qualhisto: no stored quality"; return 0; }
+  if (!ensure_red(ctx, sizeof(QualPart) * (STAT_BLOCKS + 1))) return 0;
+  QualPart *parts = (QualPart *)ctx->d_red.p;
+  hipLaunchKernelGGL(k_qual, dim3(STAT_BLOCKS), dim3(256), 0, ctx->stream, A,
+                     use_stored ? ctx->d_qual.p : (double *)nullptr, parts, use_stored);
+  QualPart *res = dev_result ? (QualPart *)dev_result : parts + STAT_BLOCKS;
+  hipLaunchKernelGGL(k_qual_final, dim3(1), dim3(256), 0, ctx->stream, parts, STAT_BLOCKS, res);
+  return hipGetLastError() == hipSuccess;
+}
+
+int pmx_qualhisto(pmx_ctx *ctx, pmx_qual_stats *st) {
+  if (!ctx || !st) return 0;
+  hipSetDevice(ctx->device);
+  if (!pmx_qualhisto_async(ctx, 0, nullptr)) return 0;
+  QualPart r;
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return 0;
+  if (hipMemcpy(&r, (QualPart *)ctx->d_red.p + STAT_BLOCKS, sizeof r, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  st->ne = r.ne;
+  st->np = ctx->np;
+  st->max = r.max;
+  st->min = r.min;
+  st->avg = r.avg;
+  st->iel = r.ne ? r.iel : 0;
+  st->good = r.good;
+  st->med = r.med;
+  for (int i = 0; i < 5; i++) st->his[i] = r.his[i];
+  return 1;
+}
+
+int pmx_prilen_async(pmx_ctx *ctx, const uint16_t *dtag, void *dev_result) {
+  StatArgs A{};
+  if (!stat_args(ctx, A)) return 0;
+  if (ctx->sd.imet < 0) { ctx->err = "pmx_prilen: no metric"; return 0; }
+  A.ptag = dtag;
+  if (!ensure_red(ctx, sizeof(LenPart) * (STAT_BLOCKS + 1))) return 0;
+  LenPart *parts = (LenPart *)ctx->d_red.p;
+  hipLaunchKernelGGL(k_prilen, dim3(STAT_BLOCKS), dim3(256), 0, ctx->stream, A, parts);
+  LenPart *res = dev_result ? (LenPart *)dev_result : parts + STAT_BLOCKS;
+  hipLaunchKernelGGL(k_prilen_final, dim3(1), dim3(256), 0, ctx->stream, parts, STAT_BLOCKS, res);
+  return hipGetLastError() == hipSuccess;
+}
+
+int pmx_prilen(pmx_ctx *ctx, const uint16_t *point_tag, int64_t tag_stride, int metRidTyp,
+               pmx_len_stats *st) {
+  (void)metRidTyp;   // classic storage only: met->size 1 or 6 on every point
+  if (!ctx || !st) return 0;
+  hipSetDevice(ctx->device);
+  uint16_t *dtag = nullptr;
+  if (point_tag) {
+    std::vector<uint16_t> h((size_t)(ctx->np + 1), 0);
+    for (int64_t i = 1; i <= ctx->np; i++)
+      h[(size_t)i] = *(const uint16_t *)((const char *)point_tag + i * tag_stride);
+    if (hipMalloc((void **)&dtag, h.size() * 2) != hipSuccess) return 0;
+    hipMemcpy(dtag, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+  }
+  int r = pmx_prilen_async(ctx, dtag, nullptr);
+  LenPart res;
+  if (r) {
+    r = hipStreamSynchronize(ctx->stream) == hipSuccess &&
+        hipMemcpy(&res, (LenPart *)ctx->d_red.p + STAT_BLOCKS, sizeof res, hipMemcpyDeviceToHost) == hipSuccess;
+  }
+  if (dtag) hipFree(dtag);
+  if (!r) return 0;
+  st->ned = res.ned;
+  st->nullEdge = res.nul;
+  st->avlen = res.avlen;
+  st->lmin = res.ned ? res.lmin : 1.e30;
+  st->lmax = res.lmax;
+  st->amin = st->bmin = st->amax = st->bmax = 0;
+  // endpoints from the first-occurrence keys
+  if (res.ned) {
+    TetRec t;
+    int64_t k = res.kmin / 6;
+    int ia = (int)(res.kmin % 6);
+    static const int ia0[6] = {0, 0, 0, 1, 1, 2}, ia1[6] = {1, 2, 3, 2, 3, 3};
+    hipMemcpy(&t, ctx->d_tets.p + k, sizeof t, hipMemcpyDeviceToHost);
+    st->amin = t.v[ia0[ia]];
+    st->bmin = t.v[ia1[ia]];
+    k = res.kmax / 6;
+    ia = (int)(res.kmax % 6);
+    hipMemcpy(&t, ctx->d_tets.p + k, sizeof t, hipMemcpyDeviceToHost);
+    st->amax = t.v[ia0[ia]];
+    st->bmax = t.v[ia1[ia]];
+  }
+  for (int i = 0; i < 9; i++) st->hl[i] = res.hl[i];
+  return 1;
+}
+
+}  // extern "C"

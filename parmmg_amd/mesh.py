@@ -1,0 +1,228 @@
+"""Background-mesh container and synthetic inputs (Kuhn cubes, new points, fields).
+
+Arrays follow Mmg's 1-based convention (row 0 unused), exactly what
+``PMMG_create_oldGrp`` leaves in ``old_listgrp`` (reference
+src/grpsplit_pmmg.c:207-418): tets, the tet adjacency ``adja``
+(``adja[4*(k-1)+1+f] = 4*k'+f'``), boundary triangles and their adjacency
+``adjt`` (``adjt[3*(k-1)+1+e] = 3*k'+e'``).
+
+The generator and the Medit reader are test/bench utilities built in
+``libpmx_meshgen.so``; they are not part of the transfer path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import dataclasses
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+MESHGEN_PATH = os.path.join(_HERE, "libpmx_meshgen.so")
+
+TAG_REQ, TAG_BDY, TAG_NUL = 4, 16, 16384
+
+_mg = None
+
+
+def _meshgen() -> C.CDLL:
+    global _mg
+    if _mg is None:
+        if not os.path.exists(MESHGEN_PATH):
+            from . import build
+            build.build_meshgen()
+        lib = C.CDLL(MESHGEN_PATH)
+        i64, vp = C.c_int64, C.c_void_p
+        lib.pmg_kuhn_counts.argtypes = [C.c_int, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)]
+        lib.pmg_kuhn_cube.restype = i64
+        lib.pmg_kuhn_cube.argtypes = [C.c_int, C.c_uint64, C.c_double, vp, vp, vp, vp, vp]
+        lib.pmg_build_adja.restype = i64
+        lib.pmg_build_adja.argtypes = [i64, vp, vp]
+        lib.pmg_build_bdry.restype = i64
+        lib.pmg_build_bdry.argtypes = [i64, vp, vp, vp, i64]
+        lib.pmg_build_adjt.restype = C.c_int
+        lib.pmg_build_adjt.argtypes = [i64, vp, vp]
+        lib.pmg_new_points_count.restype = i64
+        lib.pmg_new_points_count.argtypes = [C.c_int, C.c_int]
+        lib.pmg_new_points.restype = i64
+        lib.pmg_new_points.argtypes = [C.c_int, C.c_uint64, C.c_double, C.c_int, C.c_int, vp, vp]
+        lib.pmg_count_inverted.restype = i64
+        lib.pmg_count_inverted.argtypes = [i64, vp, vp]
+        _mg = lib
+    return _mg
+
+
+def _p(a: np.ndarray) -> C.c_void_p:
+    return C.c_void_p(a.ctypes.data)
+
+
+@dataclasses.dataclass
+class Mesh:
+    xyz: np.ndarray            # (np+1, 3) float64
+    tet: np.ndarray            # (ne+1, 4) int32
+    adja: np.ndarray           # (4*ne+5,) int32
+    tria: np.ndarray           # (nt+1, 3) int32
+    adjt: np.ndarray           # (3*nt+4,) int32
+    hausd: float = 0.01        # Mmg default hausd
+
+    @property
+    def np(self) -> int:
+        return self.xyz.shape[0] - 1
+
+    @property
+    def ne(self) -> int:
+        return self.tet.shape[0] - 1
+
+    @property
+    def nt(self) -> int:
+        return self.tria.shape[0] - 1
+
+    def centroids(self) -> np.ndarray:
+        return self.xyz[self.tet[1:]].mean(axis=1)
+
+
+def kuhn_cube(n: int, seed: int = 20250117, jitter: float = 0.15) -> Mesh:
+    """Jittered Kuhn cube [0,1]^3 with n cells per axis (ne = 6 n^3)."""
+    lib = _meshgen()
+    np_, ne, nt = C.c_int64(), C.c_int64(), C.c_int64()
+    lib.pmg_kuhn_counts(n, C.byref(np_), C.byref(ne), C.byref(nt))
+    xyz = np.zeros((np_.value + 1, 3), np.float64)
+    tet = np.zeros((ne.value + 1, 4), np.int32)
+    adja = np.zeros(4 * ne.value + 5, np.int32)
+    tria = np.zeros((nt.value + 1, 3), np.int32)
+    adjt = np.zeros(3 * nt.value + 4, np.int32)
+    r = lib.pmg_kuhn_cube(n, seed, jitter, _p(xyz), _p(tet), _p(adja), _p(tria), _p(adjt))
+    if r != nt.value:
+        raise RuntimeError("pmg_kuhn_cube failed")
+    return Mesh(xyz, tet, adja, tria, adjt)
+
+
+def from_tets(xyz1: np.ndarray, tet1: np.ndarray, hausd: float = 0.01) -> Mesh:
+    """Build adja, boundary trias and adjt for an arbitrary tet mesh.
+    xyz1 (np+1,3) and tet1 (ne+1,4) are 1-based (row 0 unused)."""
+    lib = _meshgen()
+    xyz = np.ascontiguousarray(xyz1, np.float64)
+    tet = np.ascontiguousarray(tet1, np.int32)
+    ne = tet.shape[0] - 1
+    adja = np.zeros(4 * ne + 5, np.int32)
+    if lib.pmg_build_adja(ne, _p(tet), _p(adja)) != 0:
+        raise ValueError("non-manifold tet mesh")
+    maxnt = 4 * ne
+    tria = np.zeros((maxnt + 1, 3), np.int32)
+    nt = lib.pmg_build_bdry(ne, _p(tet), _p(adja), _p(tria), maxnt)
+    tria = np.ascontiguousarray(tria[: nt + 1])
+    adjt = np.zeros(3 * nt + 4, np.int32)
+    lib.pmg_build_adjt(nt, _p(tria), _p(adjt))
+    return Mesh(xyz, tet, adja, tria, adjt, hausd)
+
+
+def new_points(n: int, seed: int = 12345, jitter: float = 0.3, surface: bool = True,
+               morton: bool = True) -> tuple[np.ndarray, np.ndarray]:
+    """New vertices for an n-cube: jittered cell centres (volume, tag 0) and
+    jittered face-cell centres on the 6 faces (tag MG_BDY), Morton ordered."""
+    lib = _meshgen()
+    cnt = lib.pmg_new_points_count(n, int(surface))
+    xyz = np.zeros((cnt, 3), np.float64)
+    tag = np.zeros(cnt, np.int32)
+    r = lib.pmg_new_points(n, seed, jitter, int(surface), int(morton), _p(xyz), _p(tag))
+    if r != cnt:
+        raise RuntimeError("pmg_new_points failed")
+    return xyz, tag.astype(np.uint16)
+
+
+def count_inverted(m: Mesh) -> int:
+    return int(_meshgen().pmg_count_inverted(m.ne, _p(m.xyz), _p(m.tet)))
+
+
+# ---- analytic fields ----------------------------------
+
+def iso_metric(x: np.ndarray) -> np.ndarray:
+    """h(x) = 0.05 + 0.1 x0, shape (n, 1)."""
+    return (0.05 + 0.1 * x[:, 0])[:, None]
+
+
+def shock_metric(x: np.ndarray) -> np.ndarray:
+    """Anisotropic shock metric across the plane n.x = 0.5, n = (1,1,1)/sqrt(3);
+    stored (m11, m12, m13, m22, m23, m33), shape (n, 6)."""
+    nv = np.full(3, 1.0 / np.sqrt(3.0))
+    d = x @ nv - 0.5
+    hn = np.minimum(0.1, 0.002 + 0.2 * np.abs(d))
+    ht = 0.05
+    a = 1.0 / hn**2
+    b = 1.0 / ht**2
+    nn = np.outer(nv, nv)
+    out = np.empty((x.shape[0], 6))
+    idx = [(0, 0), (0, 1), (0, 2), (1, 1), (1, 2), (2, 2)]
+    for j, (p, q) in enumerate(idx):
+        out[:, j] = a * nn[p, q] + b * ((1.0 if p == q else 0.0) - nn[p, q])
+    return out
+
+
+def level_set(x: np.ndarray) -> np.ndarray:
+    return (np.linalg.norm(x - 0.5, axis=1) - 0.3)[:, None]
+
+
+def velocity(x: np.ndarray) -> np.ndarray:
+    px, py = np.pi * x[:, 0], np.pi * x[:, 1]
+    return np.stack([np.sin(px) * np.cos(py), -np.cos(px) * np.sin(py), np.zeros(x.shape[0])], axis=1)
+
+
+def on_vertices(m: Mesh, f) -> np.ndarray:
+    """Evaluate f on the mesh vertices; row 0 (unused) is zero."""
+    v = f(m.xyz[1:])
+    out = np.zeros((m.np + 1, v.shape[1]))
+    out[1:] = v
+    return out
+
+
+# ---- Medit .mesh reader (fixtures) ----------------------------------------------
+
+def read_medit(path: str, hausd: float = 0.01) -> Mesh:
+    """Read Vertices and Tetrahedra of an ASCII Medit file and rebuild the
+    background structures (adja, boundary trias, adjt)."""
+    with open(path) as f:
+        tok = f.read().split()
+    i = 0
+    xyz = tet = None
+    while i < len(tok):
+        t = tok[i]
+        if t == "Vertices":
+            n = int(tok[i + 1])
+            a = np.array(tok[i + 2: i + 2 + 4 * n], dtype=np.float64).reshape(n, 4)
+            xyz = np.zeros((n + 1, 3))
+            xyz[1:] = a[:, :3]
+            i += 2 + 4 * n
+        elif t == "Tetrahedra":
+            n = int(tok[i + 1])
+            a = np.array(tok[i + 2: i + 2 + 5 * n], dtype=np.int64).reshape(n, 5)
+            tet = np.zeros((n + 1, 4), np.int32)
+            tet[1:] = a[:, :4]
+            i += 2 + 5 * n
+        else:
+            i += 1
+    if xyz is None or tet is None:
+        raise ValueError(f"{path}: no Vertices/Tetrahedra")
+    return from_tets(xyz, tet, hausd)
+
+
+def read_medit_sol(path: str) -> list[np.ndarray]:
+    """Read SolAtVertices of an ASCII .sol file -> list of (np+1, size) arrays
+    (types 1 scalar, 2 vector, 3 tensor)."""
+    with open(path) as f:
+        tok = f.read().split()
+    i = tok.index("SolAtVertices")
+    n = int(tok[i + 1])
+    nsol = int(tok[i + 2])
+    types = [int(t) for t in tok[i + 3: i + 3 + nsol]]
+    sizes = [{1: 1, 2: 3, 3: 6}[t] for t in types]
+    vals = np.array(tok[i + 3 + nsol: i + 3 + nsol + n * sum(sizes)], dtype=np.float64)
+    vals = vals.reshape(n, sum(sizes))
+    out, off = [], 0
+    for s in sizes:
+        a = np.zeros((n + 1, s))
+        a[1:] = vals[:, off: off + s]
+        if s == 6:   # Medit (11,12,22,13,23,33) -> Mmg (11,12,13,22,23,33)
+            a[1:, 2], a[1:, 3] = vals[:, off + 3], vals[:, off + 2]
+        out.append(a)
+        off += s
+    return out

@@ -1,0 +1,235 @@
+"""Host-side mirror of ParMmg's transfer interface, over the C ABI.
+
+Names and argument meaning follow the reference:
+
+* :meth:`Transfer.interp_metrics_and_fields` -- ``PMMG_interpMetricsAndFields``
+  (reference src/interpmesh_pmmg.c:663-741), one call per remesh iteration,
+  groups are independent.
+* :meth:`Transfer.copy_metrics_and_fields_point` --
+  ``PMMG_copyMetricsAndFields_point`` (src/interpmesh_pmmg.c:432-446).
+* :meth:`Transfer.tetra_qual`, :meth:`Transfer.qualhisto`,
+  :meth:`Transfer.prilen` -- ``PMMG_tetraQual`` / ``PMMG_qualhisto`` /
+  ``PMMG_prilen`` (src/quality_pmmg.c).
+
+Errors follow the reference's 1/0 convention at the C ABI and surface here as
+``RuntimeError`` with ``pmx_last_error``.  Everything runs on the GPU; there is
+no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import dataclasses
+
+import numpy as np
+
+from . import _native as N
+from .mesh import Mesh
+
+
+def _dp(a):
+    return a.ctypes.data_as(N.dptr) if a is not None else None
+
+
+def _ip(a):
+    return a.ctypes.data_as(N.iptr) if a is not None else None
+
+
+def mesh_view(m: Mesh) -> N.MeshView:
+    v = N.MeshView()
+    v.np, v.ne, v.nt = m.np, m.ne, m.nt
+    v.point_c = _dp(m.xyz)
+    v.point_stride = 3 * 8
+    v.tetra_v = _ip(m.tet)
+    v.tetra_stride = 4 * 4
+    v.adja = _ip(m.adja)
+    v.tria_v = _ip(m.tria) if m.nt > 0 else None
+    v.tria_stride = 3 * 4
+    v.adjt = _ip(m.adjt) if m.nt > 0 else None
+    v.hausd = m.hausd
+    return v
+
+
+@dataclasses.dataclass
+class Result:
+    sols: list            # per solution: (npts, size) arrays
+    elem: np.ndarray      # located tet (volume) / tria (surface), 1-based
+    status: np.ndarray    # 1 found, -1 found by exhaustive search, 0 closest
+    steps: np.ndarray
+
+
+class Transfer:
+    """One device context (one GPU).  ``device`` = rank % ndev in ParMmg terms."""
+
+    def __init__(self, device: int = 0):
+        self.lib = N.load()
+        self.ctx = self.lib.pmx_create(device)
+        if not self.ctx:
+            raise RuntimeError("pmx_create failed (no HIP device visible)")
+        self._keep = []
+        self.sizes: list[int] = []
+        self.npts = 0
+
+    def close(self):
+        if self.ctx:
+            self.lib.pmx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, r: int, what: str):
+        if not r:
+            raise RuntimeError(f"{what}: {self.lib.pmx_last_error(self.ctx).decode()}")
+
+    def device_info(self) -> str:
+        buf = C.create_string_buffer(256)
+        self._chk(self.lib.pmx_device_info(self.ctx, buf, 256), "pmx_device_info")
+        return buf.value.decode()
+
+    def set_stream(self, stream_ptr: int | None):
+        self._chk(self.lib.pmx_set_stream(self.ctx, C.c_void_p(stream_ptr or 0)), "pmx_set_stream")
+
+    def synchronize(self):
+        self._chk(self.lib.pmx_synchronize(self.ctx), "pmx_synchronize")
+
+    # ---- device-resident interface ------------------------------------------
+    def upload_background(self, m: Mesh, sols: list[np.ndarray], imet: int = 0):
+        """sols: (np+1, size) arrays in Mmg layout; imet: index of the metric or -1."""
+        arr = [np.ascontiguousarray(s, np.float64) for s in sols]
+        views = (N.SolView * max(len(arr), 1))()
+        for i, a in enumerate(arr):
+            views[i].size = a.shape[1] if a.ndim == 2 else 1
+            views[i].m = _dp(a)
+        mv = mesh_view(m)
+        self._chk(self.lib.pmx_upload_background(self.ctx, C.byref(mv), len(arr), views,
+                                                 imet if arr else -1), "pmx_upload_background")
+        self.sizes = [v.size for v in views[: len(arr)]]
+
+    def upload_points(self, xyz: np.ndarray, tags: np.ndarray | None = None):
+        xyz = np.ascontiguousarray(xyz, np.float64)
+        pv = N.PointsView()
+        pv.first, pv.last = 0, xyz.shape[0] - 1
+        pv.c, pv.stride = _dp(xyz), 24
+        if tags is not None:
+            t = np.ascontiguousarray(tags, np.uint16)
+            self._keep = [t]
+            pv.tag, pv.tag_stride = t.ctypes.data_as(N.u16ptr), 2
+        self._chk(self.lib.pmx_upload_points(self.ctx, C.byref(pv)), "pmx_upload_points")
+        self.npts = xyz.shape[0]
+
+    def run(self, hsiz: float = 0.0, timing: bool = False, max_walk: int = 0):
+        o = N.RunOpts()
+        o.hsiz, o.timing, o.max_walk = hsiz, int(timing), max_walk
+        self._chk(self.lib.pmx_run(self.ctx, C.byref(o)), "pmx_run")
+
+    def download(self, init: list[np.ndarray] | None = None) -> Result:
+        n = self.npts
+        outs = []
+        views = (N.SolView * max(len(self.sizes), 1))()
+        for i, sz in enumerate(self.sizes):
+            a = (np.array(init[i], np.float64, copy=True).reshape(n, sz) if init is not None
+                 else np.full((n, sz), np.nan))
+            outs.append(a)
+            views[i].size, views[i].m = sz, _dp(a)
+        elem = np.zeros(n, np.int32)
+        status = np.zeros(n, np.int32)
+        steps = np.zeros(n, np.int32)
+        self._chk(self.lib.pmx_download(self.ctx, views, _ip(elem), _ip(status), _ip(steps)),
+                  "pmx_download")
+        return Result(outs, elem, status, steps)
+
+    def starts(self) -> np.ndarray:
+        s = np.zeros(self.npts, np.int32)
+        self._chk(self.lib.pmx_download_starts(self.ctx, _ip(s)), "pmx_download_starts")
+        return s
+
+    def border(self) -> tuple[np.ndarray, np.ndarray]:
+        e = np.zeros(self.npts, np.int32)
+        v = np.zeros(self.npts, np.int32)
+        self._chk(self.lib.pmx_download_border(self.ctx, _ip(e), _ip(v)), "pmx_download_border")
+        return e, v
+
+    def locate_stats(self) -> dict:
+        st = N.LocateStats()
+        self._chk(self.lib.pmx_locate_stats_get(self.ctx, C.byref(st)), "pmx_locate_stats_get")
+        return {f: getattr(st, f) for f, _ in N.LocateStats._fields_}
+
+    def kernel_ms(self, which: int) -> float:
+        return self.lib.pmx_kernel_ms(self.ctx, which)
+
+    def timing_reset(self):
+        self.lib.pmx_timing_reset(self.ctx)
+
+    def device_buffer(self, which: int) -> int:
+        return self.lib.pmx_device_buffer(self.ctx, which) or 0
+
+    # ---- reference-shaped entry points --------------------------------------
+    def interp_metrics_and_fields(self, groups: list[dict], input_met: int = 1,
+                                  perm_nod_glob: np.ndarray | None = None) -> int:
+        """PMMG_interpMetricsAndFields over ``groups``; each group is a dict with
+        keys ``old_mesh`` (Mesh), ``old_met`` ((np+1,size) or None),
+        ``old_fields`` (list), ``xyz`` (new points, (np+1,3) Mmg layout),
+        ``tags`` (uint16, np+1), ``met`` / ``fields`` (output arrays in Mmg
+        layout, written in place), ``hsiz``."""
+        keep = []
+        G = (N.Group * len(groups))()
+        for g, d in zip(G, groups):
+            xyz = np.ascontiguousarray(d["xyz"], np.float64)
+            tags = np.ascontiguousarray(d["tags"], np.uint16)
+            keep += [xyz, tags]
+            g.points.first, g.points.last = 1, xyz.shape[0] - 1
+            g.points.c, g.points.stride = _dp(xyz), 24
+            g.points.tag, g.points.tag_stride = tags.ctypes.data_as(N.u16ptr), 2
+            g.hsiz = d.get("hsiz", 0.0)
+            om = mesh_view(d["old_mesh"])
+            keep.append(om)
+            g.old_mesh = om
+
+            def sv(a):
+                v = N.SolView()
+                v.size, v.m = a.shape[1], _dp(a)
+                return v
+            if d.get("met") is not None and d.get("old_met") is not None:
+                g.met = C.pointer(sv(d["met"]))
+                g.old_met = C.pointer(sv(d["old_met"]))
+                keep += [g.met, g.old_met]
+            fl = d.get("fields") or []
+            ofl = d.get("old_fields") or []
+            g.nsols = len(fl)
+            if fl:
+                fa = (N.SolView * len(fl))(*[sv(a) for a in fl])
+                ofa = (N.SolView * len(ofl))(*[sv(a) for a in ofl])
+                keep += [fa, ofa]
+                g.fields = C.cast(fa, C.POINTER(N.SolView))
+                g.old_fields = C.cast(ofa, C.POINTER(N.SolView))
+        perm = None
+        if perm_nod_glob is not None:
+            perm = np.ascontiguousarray(perm_nod_glob, np.int32)
+        return self.lib.PMX_interpMetricsAndFields(self.ctx, len(groups), G, _ip(perm), input_met)
+
+    # ---- statistics -----------------------------------------------------------
+    def tetra_qual(self, ne: int) -> np.ndarray:
+        q = np.zeros(ne + 1)
+        self._chk(self.lib.pmx_tetra_qual(self.ctx, _dp(q)), "pmx_tetra_qual")
+        return q
+
+    def qualhisto(self) -> dict:
+        st = N.QualStats()
+        self._chk(self.lib.pmx_qualhisto(self.ctx, C.byref(st)), "pmx_qualhisto")
+        d = {f: getattr(st, f) for f, _ in N.QualStats._fields_}
+        d["his"] = list(st.his)
+        return d
+
+    def prilen(self, tags: np.ndarray | None = None, met_rid_typ: int = 0) -> dict:
+        st = N.LenStats()
+        t = None
+        if tags is not None:
+            t = np.ascontiguousarray(tags, np.uint16)
+        self._chk(self.lib.pmx_prilen(self.ctx, t.ctypes.data_as(N.u16ptr) if t is not None else None,
+                                      2, met_rid_typ, C.byref(st)), "pmx_prilen")
+        d = {f: getattr(st, f) for f, _ in N.LenStats._fields_}
+        d["hl"] = list(st.hl)
+        return d

@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X transfer path (locate + interpolate new vertices).
+
+A step = one PMMG_interpMetricsAndFields pass of one background group on one
+GPU: hint-grid build over the old mesh, adjacency-walk location of every new
+vertex (volume + surface), fused metric/field interpolation, exhaustive
+fallback -- inputs resident in HBM (uploaded before the timed region).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4]
+
+N > 1: launched by torch.distributed.run, one rank per GPU; every rank owns its
+own group (ParMmg groups shard with no data-path collective: weak scaling);
+RCCL all-reduces the quality histogram once after the timed loop.
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# SURVEY.md section 8 configurations (Kuhn cube with n cells per axis)
+CONFIGS = {
+    "C1": dict(n=20, metric="iso", fields=["ls"], desc="unit cube ~48k tets, iso metric + LS"),
+    "C2": dict(n=119, metric="ani", fields=[], desc="10M-tet cube, anisotropic shock metric"),
+    "C3": dict(n=255, metric="iso", fields=["ls", "vel"], desc="100M-tet cube, iso metric + LS + velocity"),
+    "C4": dict(n=255, metric="iso", fields=["ls", "vel"], desc="per-GPU share of 400M tets (2 groups of 50M)"),
+}
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def build_case(cfg: dict, rank: int):
+    from parmmg_amd import mesh as M
+    n = cfg["n"]
+    m = M.kuhn_cube(n, seed=20250117 + rank)
+    x, t = M.new_points(n, seed=12345 + rank)
+    sols = []
+    if cfg["metric"] == "ani":
+        sols.append(M.on_vertices(m, M.shock_metric))
+    else:
+        sols.append(M.on_vertices(m, M.iso_metric))
+    if "ls" in cfg["fields"]:
+        sols.append(M.on_vertices(m, M.level_set))
+    if "vel" in cfg["fields"]:
+        sols.append(M.on_vertices(m, M.velocity))
+    return m, x, t, sols
+
+
+def alg_bytes(N: int, ne: int, np_: int, S: int) -> int:
+    """compulsory bytes of locate+interp for one step."""
+    return N * (24 + 8 * S + 4) + ne * 32 + np_ * (24 + 8 * S)
+
+
+def cpu_baseline(m, x, t, sols, budget_s: float = 20.0) -> dict:
+    """The oracle (CPU restatement of the reference, sequential carry-over
+    walk, one core) on the same workload: the whole step when it fits the
+    budget, else a Morton-contiguous prefix of the new points (the O(ne)
+    precompute is always done in full and charged)."""
+    from oracle import oracle as O
+    t0 = time.perf_counter()
+    o = O.Oracle(m)                       # faceAreas / triaNormals / nodeTrias
+    t_pre = time.perf_counter() - t0
+    n = len(x)
+    S = min(n, 20000)
+    t1 = time.perf_counter()
+    o.interp(x[:S], t[:S], sols, imet=0)
+    dt = time.perf_counter() - t1
+    rate = S / max(dt, 1e-9)
+    if dt * n / S + t_pre <= budget_s:
+        S = n
+        t1 = time.perf_counter()
+        o.interp(x, t, sols, imet=0)
+        dt = time.perf_counter() - t1
+    else:
+        S = int(min(n, max(S, rate * (budget_s - t_pre))))
+        t1 = time.perf_counter()
+        o.interp(x[:S], t[:S], sols, imet=0)
+        dt = time.perf_counter() - t1
+    t_step = t_pre + dt * n / S
+    return {"value": n / t_step, "unit": "vertices/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/pmx_oracle.c (reference algorithm, -O2, 1 thread): "
+                      f"precompute over all {m.ne} tets {t_pre:.2f}s + {S}/{n} new vertices "
+                      f"{dt:.2f}s, extrapolated to the full step"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from parmmg_amd import build
+    build.build_meshgen()
+    build.build_transfer()
+    if rank == 0 and not args.no_cpu:
+        build.build_oracle()
+    from parmmg_amd.transfer import Transfer
+
+    cfg = CONFIGS[args.config]
+    m, x, t, sols = build_case(cfg, rank)
+    S = sum(s.shape[1] for s in sols)
+    tr = Transfer(local)
+    tr.upload_background(m, sols, 0)
+    tr.upload_points(x, t)
+
+    for _ in range(args.warmup):
+        tr.run()
+    tr.synchronize()
+
+    def barrier():
+        if dist is not None:
+            import torch
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    barrier()
+    tr.synchronize()
+    tr.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.run(timing=True)
+    tr.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    k_ms = {name: tr.kernel_ms(i) for i, name in enumerate(["hint", "vol", "bdy", "exhaustive", "total"])}
+    st = tr.locate_stats()
+
+    if dist is not None:
+        import torch
+        tt = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+        # one RCCL all-reduce of the quality histogram (the path's only collective)
+        from parmmg_amd import shard
+        qs = shard.qualhisto_allreduce(tr, dist, local)
+    npts = len(x)
+    total_pts = npts * world * args.steps
+    value = total_pts / el
+    ms = el / args.steps * 1e3
+
+    nvol = int((t == 0).sum())
+    B = alg_bytes(npts, m.ne, m.np, S)
+    b_vol = B * nvol / npts
+    achieved = b_vol / (k_ms["vol"] * 1e-3) / 1e9 if k_ms["vol"] > 0 else None
+
+    out = {
+        "metric": "new vertices located+interpolated/sec",
+        "value": value,
+        "unit": "vertices/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (jittered Kuhn cube, jittered Morton-ordered new vertices, analytic fields)",
+        "config": {"workload": f"{args.config}: {cfg['desc']}", "n_cells": cfg["n"], "ne": m.ne,
+                   "np": m.np, "nt": m.nt, "new_vertices_per_gpu": npts, "S": S,
+                   "groups_per_gpu": 1, "parallelism": f"group-sharded x{world}"},
+        "roofline": {"bound": "hbm", "kernel": "k_locate_vol",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                     "traffic": None,
+                     "alg_bytes_per_launch": b_vol, "avg_launch_ms": k_ms["vol"]},
+        "kernel_ms": k_ms,
+        "step_alg_GBs": B / (ms * 1e-3) / 1e9,
+        "locate": st,
+    }
+    if rank == 0 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(m, x, t, sols)
+    if dist is not None:
+        out["qualhisto_allreduce"] = qs
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

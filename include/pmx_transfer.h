@@ -180,6 +180,16 @@ int pmx_qualhisto(pmx_ctx *ctx, pmx_qual_stats *st);
 int pmx_prilen(pmx_ctx *ctx, const uint16_t *point_tag, int64_t tag_stride,
                int metRidTyp, pmx_len_stats *st);
 
+/* Device-resident variants for the multi-GPU reduction (RCCL all-reduce of the
+ * partials, see parmmg_amd/shard.py): the per-group partial is written, on the
+ * context stream, to dev_result (device memory):
+ *   qualhisto: 13 x 8 B = {double avg,max,min; int64 iel,ne,good,med,his[5]}
+ *   prilen:    16 x 8 B = {double avlen,lmin,lmax; int64 kmin,kmax,ned,
+ *                          nullEdge,hl[9]}  (k = 6*tet+edge of first occurrence)
+ * dev_tag: device uint16 point tags (np+1) or NULL. */
+int pmx_qualhisto_device(pmx_ctx *ctx, int use_stored, void *dev_result);
+int pmx_prilen_device(pmx_ctx *ctx, const uint16_t *dev_tag, void *dev_result);
+
 #ifdef __cplusplus
 }
 #endif

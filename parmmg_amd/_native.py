@@ -101,6 +101,8 @@ SIGNATURES = {
     "pmx_tetra_qual": (C.c_int, [C.c_void_p, dptr]),
     "pmx_qualhisto": (C.c_int, [C.c_void_p, C.POINTER(QualStats)]),
     "pmx_prilen": (C.c_int, [C.c_void_p, u16ptr, i64, C.c_int, C.POINTER(LenStats)]),
+    "pmx_qualhisto_device": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
+    "pmx_prilen_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
 }
 
 _lib = None

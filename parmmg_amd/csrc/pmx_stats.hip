@@ -380,7 +380,7 @@ int pmx_tetra_qual(pmx_ctx *ctx, double *qual) {
   return 1;
 }
 
-int pmx_qualhisto_async(pmx_ctx *ctx, int use_stored, void *dev_result) {
+int pmx_qualhisto_device(pmx_ctx *ctx, int use_stored, void *dev_result) {
   StatArgs A{};
   if (!stat_args(ctx, A)) return 0;
   if (use_stored && !ctx->have_qual) { ctx->err = "pmx_qualhisto: no stored quality"; return 0; }
@@ -396,7 +396,7 @@ int pmx_qualhisto_async(pmx_ctx *ctx, int use_stored, void *dev_result) {
 int pmx_qualhisto(pmx_ctx *ctx, pmx_qual_stats *st) {
   if (!ctx || !st) return 0;
   hipSetDevice(ctx->device);
-  if (!pmx_qualhisto_async(ctx, 0, nullptr)) return 0;
+  if (!pmx_qualhisto_device(ctx, 0, nullptr)) return 0;
   QualPart r;
   if (hipStreamSynchronize(ctx->stream) != hipSuccess) return 0;
   if (hipMemcpy(&r, (QualPart *)ctx->d_red.p + STAT_BLOCKS, sizeof r, hipMemcpyDeviceToHost) != hipSuccess) return 0;
@@ -412,7 +412,7 @@ int pmx_qualhisto(pmx_ctx *ctx, pmx_qual_stats *st) {
   return 1;
 }
 
-int pmx_prilen_async(pmx_ctx *ctx, const uint16_t *dtag, void *dev_result) {
+int pmx_prilen_device(pmx_ctx *ctx, const uint16_t *dtag, void *dev_result) {
   StatArgs A{};
   if (!stat_args(ctx, A)) return 0;
   if (ctx->sd.imet < 0) { ctx->err = "pmx_prilen: no metric"; return 0; }
@@ -438,7 +438,7 @@ int pmx_prilen(pmx_ctx *ctx, const uint16_t *point_tag, int64_t tag_stride, int 
     if (hipMalloc((void **)&dtag, h.size() * 2) != hipSuccess) return 0;
     hipMemcpy(dtag, h.data(), h.size() * 2, hipMemcpyHostToDevice);
   }
-  int r = pmx_prilen_async(ctx, dtag, nullptr);
+  int r = pmx_prilen_device(ctx, dtag, nullptr);
   LenPart res;
   if (r) {
     r = hipStreamSynchronize(ctx->stream) == hipSuccess &&

@@ -223,6 +223,14 @@ class Transfer:
         d["his"] = list(st.his)
         return d
 
+    def qualhisto_device(self, dev_ptr: int, use_stored: bool = False):
+        self._chk(self.lib.pmx_qualhisto_device(self.ctx, int(use_stored), C.c_void_p(dev_ptr)),
+                  "pmx_qualhisto_device")
+
+    def prilen_device(self, dev_ptr: int, dev_tag_ptr: int = 0):
+        self._chk(self.lib.pmx_prilen_device(self.ctx, C.c_void_p(dev_tag_ptr or None),
+                                             C.c_void_p(dev_ptr)), "pmx_prilen_device")
+
     def prilen(self, tags: np.ndarray | None = None, met_rid_typ: int = 0) -> dict:
         st = N.LenStats()
         t = None

@@ -183,7 +183,7 @@ int pmx_prilen(pmx_ctx *ctx, const uint16_t *point_tag, int64_t tag_stride,
 /* Device-resident variants for the multi-GPU reduction (RCCL all-reduce of the
  * partials, see parmmg_amd/shard.py): the per-group partial is written, on the
  * context stream, to dev_result (device memory):
- *   qualhisto: 13 x 8 B = {double avg,max,min; int64 iel,ne,good,med,his[5]}
+ *   qualhisto: 12 x 8 B = {double avg,max,min; int64 iel,ne,good,med,his[5]}
  *   prilen:    16 x 8 B = {double avlen,lmin,lmax; int64 kmin,kmax,ned,
  *                          nullEdge,hl[9]}  (k = 6*tet+edge of first occurrence)
  * dev_tag: device uint16 point tags (np+1) or NULL. */

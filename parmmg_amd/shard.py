@@ -18,7 +18,7 @@ import torch
 
 KEY_MAX = (1 << 63) - 1
 
-# layout of the device partial written by pmx_qualhisto_device (13 x 8 bytes)
+# layout of the device partial written by pmx_qualhisto_device (12 x 8 bytes)
 QUAL_F64 = ("avg", "max", "min")
 QUAL_I64 = ("iel", "ne", "good", "med", "his0", "his1", "his2", "his3", "his4")
 # layout of the device partial written by pmx_prilen_device (16 x 8 bytes)
@@ -50,7 +50,7 @@ def _minloc(val: torch.Tensor, key: torch.Tensor, dist, op_min) -> tuple[float, 
 
 
 def reduce_qual(part: torch.Tensor, rank: int, grp: int, dist) -> dict:
-    """part: float64 tensor of 13 entries laid out as QUAL_F64 + QUAL_I64
+    """part: float64 tensor of 12 entries laid out as QUAL_F64 + QUAL_I64
     (device or CPU).  Returns the global statistics on every rank."""
     f = part[:3].clone()
     i = part.view(torch.int64)[3:].clone()
@@ -95,7 +95,7 @@ def reduce_len(part: torch.Tensor, rank: int, dist) -> dict:
 def qualhisto_allreduce(tr, dist, local: int, grp: int = 0) -> dict:
     """Device partial of the uploaded group -> RCCL all-reduce."""
     dev = torch.device("cuda", local)
-    part = torch.zeros(13, dtype=torch.float64, device=dev)
+    part = torch.zeros(12, dtype=torch.float64, device=dev)
     tr.qualhisto_device(part.data_ptr())
     tr.synchronize()
     import time

@@ -109,37 +109,43 @@ __device__ __forceinline__ int sel4(const int a[4], int i) {
 }
 
 // MMG5_invmat (restated from Mmg @889d408; unpinned)
+// (both branches produce six scalars and mi is written once: keeps it in VGPRs)
 __device__ __forceinline__ bool invmat(const double m[6], double mi[6]) {
   double vmax = fabs(m[1]), t;
   t = fabs(m[2]); if (t > vmax) vmax = t;
   t = fabs(m[4]); if (t > vmax) vmax = t;
-  if (vmax < PMX_EPS) {
-    mi[0] = 1. / m[0];
-    mi[3] = 1. / m[3];
-    mi[5] = 1. / m[5];
-    mi[1] = mi[2] = mi[4] = 0.0;
-    return true;
-  }
-  double vmin = fabs(m[0]);
-  vmax = vmin;
+  double r0, r1, r2, r3, r4, r5;
+  bool ok;
+  if (vmax < PMX_EPS) {                       // diagonal metric
+    r0 = 1. / m[0];
+    r3 = 1. / m[3];
+    r5 = 1. / m[5];
+    r1 = r2 = r4 = 0.0;
+    ok = true;
+  } else {
+    double vmin = fabs(m[0]);
+    vmax = vmin;
 #pragma unroll
-  for (int k = 1; k < 6; k++) {
-    t = fabs(m[k]);
-    if (t < vmin) vmin = t;
-    else if (t > vmax) vmax = t;
+    for (int k = 1; k < 6; k++) {
+      t = fabs(m[k]);
+      if (t < vmin) vmin = t;
+      else if (t > vmax) vmax = t;
+    }
+    double aa = m[3] * m[5] - m[4] * m[4];
+    double bb = m[4] * m[2] - m[1] * m[5];
+    double cc = m[1] * m[4] - m[2] * m[3];
+    double det = m[0] * aa + m[1] * bb + m[2] * cc;
+    ok = !(vmax == 0.0) && !(fabs(det) < PMX_EPSD2);
+    det = 1.0 / det;
+    r0 = aa * det;
+    r1 = bb * det;
+    r2 = cc * det;
+    r3 = (m[0] * m[5] - m[2] * m[2]) * det;
+    r4 = (m[1] * m[2] - m[0] * m[4]) * det;
+    r5 = (m[0] * m[3] - m[1] * m[1]) * det;
   }
-  if (vmax == 0.0) return false;
-  double aa = m[3] * m[5] - m[4] * m[4];
-  double bb = m[4] * m[2] - m[1] * m[5];
-  double cc = m[1] * m[4] - m[2] * m[3];
-  double det = m[0] * aa + m[1] * bb + m[2] * cc;
-  if (fabs(det) < PMX_EPSD2) return false;
-  det = 1.0 / det;
-  mi[0] = aa * det;
-  mi[1] = bb * det;
-  mi[2] = cc * det;
-  mi[3] = (m[0] * m[5] - m[2] * m[2]) * det;
-  mi[4] = (m[1] * m[2] - m[0] * m[4]) * det;
-  mi[5] = (m[0] * m[3] - m[1] * m[1]) * det;
-  return true;
+  if (ok) {
+    mi[0] = r0; mi[1] = r1; mi[2] = r2; mi[3] = r3; mi[4] = r4; mi[5] = r5;
+  }
+  return ok;
 }

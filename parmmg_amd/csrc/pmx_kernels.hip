@@ -90,23 +90,21 @@ __device__ __forceinline__ unsigned interp_bar(const double *__restrict__ sol, c
     if (s == sd.imet && sd.metric_const) continue;
     const int sz = sd.size[s], off = sd.off[s];
     if (sz == 6) {
-      double mi[NV][6];
+      // mint_j = ((phi0*mi0_j + phi1*mi1_j) + phi2*mi2_j) + phi3*mi3_j, the
+      // reference's left-to-right sum, accumulated one vertex at a time so
+      // that only one inverse is live (no scratch)
+      double mint[6], r[6];
       bool ok = true;
 #pragma unroll
       for (int i = 0; i < NV; i++) {
         const double *m = sol + (int64_t)v[i] * sd.S + off;
         double mm[6] = {m[0], m[1], m[2], m[3], m[4], m[5]};
-        if (ok) ok = invmat(mm, mi[i]);
+        double mi[6];
+        ok = ok && invmat(mm, mi);
+#pragma unroll
+        for (int j = 0; j < 6; j++) mint[j] = (i == 0) ? phi[0] * mi[j] : mint[j] + phi[i] * mi[j];
       }
       if (!ok) continue;
-      double mint[6], r[6];
-#pragma unroll
-      for (int j = 0; j < 6; j++) {
-        if (NV == 4)
-          mint[j] = phi[0] * mi[0][j] + phi[1] * mi[1][j] + phi[2] * mi[2][j] + phi[3] * mi[NV - 1][j];
-        else
-          mint[j] = phi[0] * mi[0][j] + phi[1] * mi[1][j] + phi[2] * mi[2][j];
-      }
       if (!invmat(mint, r)) continue;
 #pragma unroll
       for (int j = 0; j < 6; j++) out[off + j] = r[j];

@@ -97,7 +97,8 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pts);
 
 /* ---- the hot path (device resident) ------------------------------------ */
 typedef struct {
-  int    hint_cells_per_tet_log2;  /* hint grid density, default 0 -> auto   */
+  int    hint_stride;              /* hint grid built from every k-th tet,
+                                      0 -> default                           */
   int    max_walk;                 /* walk step cap before exhaustive, 0=auto */
   double hsiz;                     /* >0: constant-size metric shortcut
                                       (src/interpmesh_pmmg.c:497-512)        */

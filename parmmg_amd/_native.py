@@ -49,7 +49,7 @@ class LocateStats(C.Structure):
 
 class RunOpts(C.Structure):
     _fields_ = [
-        ("hint_cells_per_tet_log2", C.c_int), ("max_walk", C.c_int),
+        ("hint_stride", C.c_int), ("max_walk", C.c_int),
         ("hsiz", C.c_double), ("timing", C.c_int),
     ]
 

@@ -40,7 +40,9 @@ struct BdyArgs {
   unsigned *stuck_count;
   int *ovf_list;       // private-list overflow
   unsigned *ovf_count;
-  unsigned long long *lstats;
+  const int *list;       // indices of the boundary points
+  int64_t nlist;
+  uint4 *wstats;         // per-wave walk statistics
 };
 
 // thread-private query state: visited trias + point-flag overrides
@@ -366,30 +368,39 @@ __device__ int tria_hint(const BdyArgs &A, D3 p);
 
 template <int CAP>
 __global__ __launch_bounds__(256) void k_locate_bdy(BdyArgs A) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= A.nq || A.kind[i] != KIND_BDY) return;
-  Pt4 qq = A.q[i];
-  D3 p{qq.x, qq.y, qq.z};
-  int start = tria_hint(A, p);
-  A.start[i] = start;
-  RegState<CAP> s;
-  Bary b;
-  int k, edge, vtx, step;
-  int r = walk_bdy(A, s, p, start, (int)(i + 1), k, b, edge, vtx, step);
-  if (r == 1) {
-    finish_bdy(A, i, k, b, edge, vtx, 1, step);
-    atomicAdd(&A.lstats[4], 1ull);
-    atomicAdd(&A.lstats[5], (unsigned long long)step);
-    atomicMax(&A.lstats[6], (unsigned long long)step);
-    atomicMin(&A.lstats[7], (unsigned long long)step);
-  } else if (r == 2) {
-    unsigned slot = atomicAdd(A.stuck_count, 1u);
-    A.stuck_list[slot] = (int)i;
-    A.steps[i] = -step;
-  } else {
-    unsigned slot = atomicAdd(A.ovf_count, 1u);
-    A.ovf_list[slot] = (int)i;
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned s_cnt = 0, s_sum = 0, s_max = 0, s_min = 0xffffffffu;
+  if (j < A.nlist) {
+    const int64_t i = A.list[j];
+    Pt4 qq = A.q[i];
+    D3 p{qq.x, qq.y, qq.z};
+    int start = tria_hint(A, p);
+    A.start[i] = start;
+    RegState<CAP> s;
+    Bary b;
+    int k, edge, vtx, step;
+    int r = walk_bdy(A, s, p, start, (int)(i + 1), k, b, edge, vtx, step);
+    if (r == 1) {
+      finish_bdy(A, i, k, b, edge, vtx, 1, step);
+      s_cnt = 1; s_sum = (unsigned)step; s_max = (unsigned)step; s_min = (unsigned)step;
+    } else if (r == 2) {
+      unsigned slot = atomicAdd(A.stuck_count, 1u);
+      A.stuck_list[slot] = (int)i;
+      A.steps[i] = -step;
+    } else {
+      unsigned slot = atomicAdd(A.ovf_count, 1u);
+      A.ovf_list[slot] = (int)i;
+    }
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s_cnt += __shfl_xor(s_cnt, o, 64);
+    s_sum += __shfl_xor(s_sum, o, 64);
+    unsigned a = __shfl_xor(s_max, o, 64), b = __shfl_xor(s_min, o, 64);
+    s_max = a > s_max ? a : s_max;
+    s_min = b < s_min ? b : s_min;
+  }
+  if ((threadIdx.x & 63) == 0) A.wstats[j / 64] = make_uint4(s_cnt, s_sum, s_max, s_min);
 }
 
 // overflow pass: same walk with large lists in a global workspace
@@ -615,8 +626,8 @@ bool pmx_ctx::launch_bdy(const VolArgs &a, const pmx_run_opts &o, hipStream_t s)
   B.steps = d_steps.p; B.start = d_start.p; B.edge = d_edge.p; B.vertex = d_vertex.p;
   B.stuck_list = d_blist.p; B.stuck_count = d_counts.p + 1;
   B.ovf_list = d_olist.p; B.ovf_count = d_counts.p + 2;
-  B.lstats = d_lstats.p;
-  int64_t nb = (nq + 255) / 256;
+  B.list = d_bdylist.p; B.nlist = nq_bdy; B.wstats = d_bstat.p;
+  int64_t nb = (nq_bdy + 255) / 256;
   hipLaunchKernelGGL(k_locate_bdy<BDY_CAP>, dim3((unsigned)nb), dim3(256), 0, s, B);
   hipLaunchKernelGGL(k_locate_bdy_ovf, dim3(OVF_THREADS / 64), dim3(64), 0, s, B, d_ows.p, OVF_CAP);
   hipLaunchKernelGGL(k_exh_bdy, dim3(256), dim3(256), 0, s, B);

@@ -15,6 +15,10 @@
 #include "pmx_kernels.h"
 #include "pmx_internal.h"
 
+// hint grid from every 4th tet: 1/4 of the atomics and of the tet bytes of a
+// full build, at ~0.5 extra walk step (r01 measurements)
+#define PMX_DEFAULT_HINT_STRIDE 4
+
 static bool ok(pmx_ctx *c, hipError_t e, const char *what) {
   if (e == hipSuccess) return true;
   c->err = std::string(what) + ": " + hipGetErrorString(e);
@@ -233,6 +237,8 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   const char *pc = (const char *)pv->c;
   const char *tg = (const char *)pv->tag;
   int64_t nv = 0, nb = 0;
+  std::vector<int> vl, bl;           // per-path point lists, input order kept
+  vl.reserve((size_t)n);
   for (int64_t j = 0; j < n; j++) {
     const double *c = (const double *)(pc + (pv->first + j) * pv->stride);
     hq[(size_t)j] = Pt4{c[0], c[1], c[2], 0.0};
@@ -240,8 +246,8 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
     int8_t kd;
     if (tag >= PMX_TAG_NUL) kd = KIND_NUL;
     else if (tag & PMX_TAG_REQ) kd = KIND_SKIP;
-    else if (tag & PMX_TAG_BDY) { kd = KIND_BDY; nb++; }
-    else { kd = KIND_VOL; nv++; }
+    else if (tag & PMX_TAG_BDY) { kd = KIND_BDY; nb++; bl.push_back((int)j); }
+    else { kd = KIND_VOL; nv++; vl.push_back((int)j); }
     hk[(size_t)j] = kd;
   }
   ctx->nq = n;
@@ -262,9 +268,14 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   if (!dgrow(ctx, ctx->d_bestk, nn)) return 0;
   if (!dgrow(ctx, ctx->d_best, nn)) return 0;
   if (!dgrow(ctx, ctx->d_counts, 8)) return 0;
-  if (!dgrow(ctx, ctx->d_lstats, 16)) return 0;
+  if (!dgrow(ctx, ctx->d_vollist, (size_t)std::max<int64_t>(nv, 1))) return 0;
+  if (!dgrow(ctx, ctx->d_bdylist, (size_t)std::max<int64_t>(nb, 1))) return 0;
+  if (!dgrow(ctx, ctx->d_vstat, (size_t)std::max<int64_t>((nv + 63) / 64 + 4, 1))) return 0;
+  if (!dgrow(ctx, ctx->d_bstat, (size_t)std::max<int64_t>((nb + 63) / 64 + 4, 1))) return 0;
   CK(hipMemcpyAsync(ctx->d_q.p, hq.data(), (size_t)n * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_kind.p, hk.data(), (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+  if (nv) CK(hipMemcpyAsync(ctx->d_vollist.p, vl.data(), (size_t)nv * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+  if (nb) CK(hipMemcpyAsync(ctx->d_bdylist.p, bl.data(), (size_t)nb * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
   ctx->have_pts = true;
   ctx->out_S = -1;
@@ -292,7 +303,7 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   hipStream_t st = ctx->stream;
   if (ev) CK(hipEventRecord(ev[0], st));
   CK(hipMemsetAsync(ctx->d_wmask.p, 0, (size_t)std::max<int64_t>(n, 1), st));
-  launch_run_init(ctx->d_counts.p, ctx->d_lstats.p, st);
+  launch_run_init(ctx->d_counts.p, st);
   if (sd.metric_const)
     launch_const_metric(ctx->d_kind.p, n, ctx->d_out.p, S, sd.off[sd.imet], sd.size[sd.imet],
                         opts.hsiz, ctx->d_wmask.p, sd.imet, st);
@@ -302,7 +313,8 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   // reference early exit (src/interpmesh_pmmg.c:509-512): nothing to locate
   if (any_interp) {
     CK(hipMemsetAsync(ctx->d_grid.p, 0, (size_t)ctx->gcells * sizeof(int), st));
-    launch_hint_build(ctx->d_tets.p, ctx->d_pts.p, ctx->ne, 1, ctx->d_grid.p, ctx->grid, st);
+    const int stride = opts.hint_stride > 0 ? opts.hint_stride : PMX_DEFAULT_HINT_STRIDE;
+    launch_hint_build(ctx->d_tets.p, ctx->d_pts.p, ctx->ne, stride, ctx->d_grid.p, ctx->grid, st);
     if (ev) CK(hipEventRecord(ev[1], st));
     VolArgs A{};
     A.pts = ctx->d_pts.p; A.tets = ctx->d_tets.p; A.sol = ctx->d_sol.p; A.sd = sd;
@@ -313,7 +325,7 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     A.start = ctx->d_start.p;
     A.stuck_list = ctx->d_list.p; A.stuck_count = ctx->d_counts.p;
     A.found = ctx->d_found.p; A.bestk = ctx->d_bestk.p; A.best = ctx->d_best.p;
-    A.lstats = ctx->d_lstats.p;
+    A.list = ctx->d_vollist.p; A.nlist = ctx->nq_vol; A.wstats = ctx->d_vstat.p;
     A.max_walk = opts.max_walk > 0 ? opts.max_walk : 512;
     A.xcd_swizzle = 1;
     if (ctx->nq_vol) launch_locate_vol(A, st);
@@ -380,20 +392,32 @@ int pmx_download_border(pmx_ctx *ctx, int *edge, int *vertex) {
 
 int pmx_locate_stats_get(pmx_ctx *ctx, pmx_locate_stats *st) {
   if (!ctx || !ctx->ran || !st) return 0;
-  unsigned long long h[16];
   unsigned cnt[8];
   CK(hipStreamSynchronize(ctx->stream));
-  CK(hipMemcpy(h, ctx->d_lstats.p, sizeof h, hipMemcpyDeviceToHost));
   CK(hipMemcpy(cnt, ctx->d_counts.p, sizeof cnt, hipMemcpyDeviceToHost));
   memset(st, 0, sizeof *st);
   st->nvol = ctx->nq_vol;
   st->nbdy = ctx->nq_bdy;
   st->nexhaust = cnt[0] + cnt[1];
-  unsigned long long located = h[0] + h[4];
-  st->stepmax = (int64_t)std::max(h[2], h[6]);
-  unsigned long long mn = std::min(h[3], h[7]);
+  // reduce the per-wave records of both walks
+  unsigned long long located = 0, sum = 0;
+  unsigned mx = 0, mn = 0xffffffffu;
+  for (int path = 0; path < 2; path++) {
+    int64_t npath = path ? ctx->nq_bdy : ctx->nq_vol;
+    if (!npath) continue;
+    std::vector<uint4> w((size_t)((npath + 63) / 64));
+    CK(hipMemcpy(w.data(), path ? ctx->d_bstat.p : ctx->d_vstat.p, w.size() * sizeof(uint4),
+                 hipMemcpyDeviceToHost));
+    for (const uint4 &r : w) {
+      located += r.x;
+      sum += r.y;
+      mx = std::max(mx, r.z);
+      if (r.x) mn = std::min(mn, r.w);
+    }
+  }
+  st->stepmax = mx;
   st->stepmin = located ? (int64_t)mn : 0;
-  st->stepav = located ? (double)(h[1] + h[5]) / (double)located : 0.0;
+  st->stepav = located ? (double)sum / (double)located : 0.0;
   // points resolved by the exhaustive scans and still not contained anywhere
   std::vector<int> status((size_t)std::max<int64_t>(ctx->nq, 1));
   if (ctx->nq) CK(hipMemcpy(status.data(), ctx->d_status.p, (size_t)ctx->nq * sizeof(int), hipMemcpyDeviceToHost));
@@ -457,7 +481,8 @@ void pmx_ctx::free_all() {
   dfree(d_ntoff); dfree(d_ntlist);
   dfree(d_q); dfree(d_kind); dfree(d_wmask); dfree(d_out); dfree(d_elem); dfree(d_status);
   dfree(d_steps); dfree(d_start); dfree(d_edge); dfree(d_vertex); dfree(d_list); dfree(d_found);
-  dfree(d_bestk); dfree(d_best); dfree(d_counts); dfree(d_lstats);
+  dfree(d_bestk); dfree(d_best); dfree(d_counts); dfree(d_vollist); dfree(d_bdylist);
+  dfree(d_vstat); dfree(d_bstat);
   dfree(d_qual); dfree(d_red); dfree(d_blist); dfree(d_olist); dfree(d_ows);
   if (d_tgrid) hipFree(d_tgrid);
   d_tgrid = nullptr;

@@ -45,7 +45,8 @@ struct pmx_ctx {
   DevBuf<int> d_list, d_found, d_bestk;
   DevBuf<unsigned long long> d_best;
   DevBuf<unsigned> d_counts;            // [0] vol stuck, [1] bdy stuck, [2] bdy overflow
-  DevBuf<unsigned long long> d_lstats;  // [0..3] vol, [4..7] bdy
+  DevBuf<int> d_vollist, d_bdylist;     // compacted point lists per path
+  DevBuf<uint4> d_vstat, d_bstat;       // per-wave walk statistics
   DevBuf<int> d_blist, d_olist, d_ows;
   int *d_tgrid = nullptr;
   size_t d_tgrid_cap = 0;

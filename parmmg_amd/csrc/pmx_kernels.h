@@ -25,7 +25,9 @@ struct VolArgs {
   unsigned *stuck_count;
   int *found, *bestk;
   unsigned long long *best;
-  unsigned long long *lstats;   // [0] located, [1] sum steps, [2] max, [3] min
+  const int *list;              // indices of the volume points (Morton order kept)
+  int64_t nlist;
+  uint4 *wstats;                // per-wave {located, sum steps, max, min}
   int max_walk;
   int xcd_swizzle;
 };
@@ -48,7 +50,7 @@ void launch_locate_vol(const VolArgs &a, hipStream_t s);
 void launch_exhaustive(const ExhArgs &e, const VolArgs &v, hipStream_t s);
 void launch_const_metric(const int8_t *kind, int64_t nq, double *out, int S, int off, int size,
                          double hsiz, uint8_t *wmask, int imet, hipStream_t s);
-void launch_run_init(unsigned *stuck_count, unsigned long long *lstats, hipStream_t s);
+void launch_run_init(unsigned *counts, hipStream_t s);
 
 struct StatArgs {
   const Pt4 *pts;

@@ -131,31 +131,29 @@ __device__ __forceinline__ bool in_ring(const int r[WALK_RING], int k) {
   return h;
 }
 
-__device__ __forceinline__ void wave_stats(unsigned long long *st, unsigned long long cnt,
-                                           unsigned long long sum, unsigned long long mx,
-                                           unsigned long long mn) {
+// Walk statistics: one 4-word record per wavefront (no same-address atomics;
+// reduced on demand by pmx_locate_stats_get).  v0 profile: 4 contended
+// atomics per wave serialised the whole launch.
+__device__ __forceinline__ void wave_stats(uint4 *rec, unsigned cnt, unsigned sum, unsigned mx,
+                                           unsigned mn) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     cnt += __shfl_xor(cnt, o, 64);
     sum += __shfl_xor(sum, o, 64);
-    unsigned long long a = __shfl_xor(mx, o, 64), b = __shfl_xor(mn, o, 64);
+    unsigned a = __shfl_xor(mx, o, 64), b = __shfl_xor(mn, o, 64);
     mx = a > mx ? a : mx;
     mn = b < mn ? b : mn;
   }
-  if ((threadIdx.x & 63) == 0 && cnt) {
-    atomicAdd(&st[0], cnt);
-    atomicAdd(&st[1], sum);
-    atomicMax(&st[2], mx);
-    atomicMin(&st[3], mn);
-  }
+  if ((threadIdx.x & 63) == 0) *rec = make_uint4(cnt, sum, mx, mn);
 }
 
 __global__ __launch_bounds__(256) void k_locate_vol(VolArgs A) {
   int64_t b = A.xcd_swizzle ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
-  int64_t i = b * blockDim.x + threadIdx.x;
-  unsigned long long s_cnt = 0, s_sum = 0, s_max = 0, s_min = ~0ull;
+  int64_t j = b * blockDim.x + threadIdx.x;
+  unsigned s_cnt = 0, s_sum = 0, s_max = 0, s_min = 0xffffffffu;
 
-  if (i < A.nq && A.kind[i] == KIND_VOL) {
+  if (j < A.nlist) {
+    const int64_t i = A.list[j];
     Pt4 qq = A.q[i];
     D3 p{qq.x, qq.y, qq.z};
     int cur = hint_lookup(A.grid, A.g, p);
@@ -211,7 +209,7 @@ __global__ __launch_bounds__(256) void k_locate_vol(VolArgs A) {
       A.steps[i] = -step;
     }
   }
-  wave_stats(A.lstats, s_cnt, s_sum, s_max, s_min);
+  wave_stats(A.wstats + (b * blockDim.x + threadIdx.x) / 64, s_cnt, s_sum, s_max, s_min);
 }
 
 // ---- exhaustive fallback ---------------------------------------------------
@@ -352,14 +350,12 @@ __global__ __launch_bounds__(256) void k_const_metric(const int8_t *__restrict__
   }
 }
 
-__global__ void k_run_init(unsigned *stuck_count, unsigned long long *lstats) {
-  if (threadIdx.x == 0) {
-    *stuck_count = 0;
-    lstats[0] = 0; lstats[1] = 0; lstats[2] = 0; lstats[3] = ~0ull;
-  }
+// counts[0] volume stuck, [1] surface stuck, [2] surface overflow
+__global__ void k_run_init(unsigned *counts) {
+  if (threadIdx.x < 8) counts[threadIdx.x] = 0;
 }
-void launch_run_init(unsigned *stuck_count, unsigned long long *lstats, hipStream_t s) {
-  hipLaunchKernelGGL(k_run_init, dim3(1), dim3(64), 0, s, stuck_count, lstats);
+void launch_run_init(unsigned *counts, hipStream_t s) {
+  hipLaunchKernelGGL(k_run_init, dim3(1), dim3(64), 0, s, counts);
 }
 
 void launch_hint_build(const TetRec *tets, const Pt4 *pts, int64_t ne, int stride, int *grid,
@@ -372,7 +368,7 @@ void launch_hint_build(const TetRec *tets, const Pt4 *pts, int64_t ne, int strid
                      grid, g);
 }
 void launch_locate_vol(const VolArgs &a, hipStream_t s) {
-  int64_t nb = (a.nq + 255) / 256;
+  int64_t nb = (a.nlist + 255) / 256;
   if (nb < 1) return;
   hipLaunchKernelGGL(k_locate_vol, dim3((unsigned)nb), dim3(256), 0, s, a);
 }

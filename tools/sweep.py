@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of run options in ONE process (cdna guide rule 24).
+
+  python tools/sweep.py --config C2 --rounds 5 --opt hint_stride=1,2,4,8
+
+Prints per-variant median/min kernel times (HIP events) and walk statistics.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--opt", default="hint_stride=1,4")
+    args = ap.parse_args()
+    import bench
+    from parmmg_amd import build
+    build.build_meshgen()
+    build.build_transfer()
+    from parmmg_amd.transfer import Transfer
+    cfg = bench.CONFIGS[args.config]
+    m, x, t, sols = bench.build_case(cfg, 0)
+    tr = Transfer(0)
+    tr.upload_background(m, sols, 0)
+    tr.upload_points(x, t)
+    key, vals = args.opt.split("=")
+    vals = [int(v) for v in vals.split(",")]
+    res = {v: {k: [] for k in ("hint", "vol", "bdy", "exhaustive", "total")} for v in vals}
+    stats = {}
+    for _ in range(args.rounds):
+        for v in vals:
+            kw = {key: v}
+            tr.run(**kw)
+            tr.synchronize()
+            tr.timing_reset()
+            for _ in range(args.reps):
+                tr.run(timing=True, **kw)
+            for i, k in enumerate(("hint", "vol", "bdy", "exhaustive", "total")):
+                res[v][k].append(tr.kernel_ms(i))
+            stats[v] = tr.locate_stats()
+    out = {}
+    for v in vals:
+        out[v] = {k: (float(np.median(a)), float(np.min(a))) for k, a in res[v].items()}
+        out[v]["stepav"] = stats[v]["stepav"]
+        out[v]["nexhaust"] = stats[v]["nexhaust"]
+    print(json.dumps({"config": args.config, "opt": key, "ms(median,min)": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -103,6 +103,7 @@ typedef struct {
   double hsiz;                     /* >0: constant-size metric shortcut
                                       (src/interpmesh_pmmg.c:497-512)        */
   int    timing;                   /* record per-kernel HIP events           */
+  int    tune;                     /* kernel variant knobs (0 = defaults)    */
 } pmx_run_opts;
 
 /* Locate every uploaded new point in the background group and interpolate all

@@ -50,7 +50,7 @@ class LocateStats(C.Structure):
 class RunOpts(C.Structure):
     _fields_ = [
         ("hint_stride", C.c_int), ("max_walk", C.c_int),
-        ("hsiz", C.c_double), ("timing", C.c_int),
+        ("hsiz", C.c_double), ("timing", C.c_int), ("tune", C.c_int),
     ]
 
 

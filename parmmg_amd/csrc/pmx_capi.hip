@@ -18,6 +18,7 @@
 // hint grid from every 4th tet: 1/4 of the atomics and of the tet bytes of a
 // full build, at ~0.5 extra walk step (r01 measurements)
 #define PMX_DEFAULT_HINT_STRIDE 4
+#define PMX_DEFAULT_VOL_OCC 1
 
 static bool ok(pmx_ctx *c, hipError_t e, const char *what) {
   if (e == hipSuccess) return true;
@@ -327,6 +328,8 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     A.found = ctx->d_found.p; A.bestk = ctx->d_bestk.p; A.best = ctx->d_best.p;
     A.list = ctx->d_vollist.p; A.nlist = ctx->nq_vol; A.wstats = ctx->d_vstat.p;
     A.max_walk = opts.max_walk > 0 ? opts.max_walk : 512;
+    A.const_bit = sd.metric_const ? (1u << sd.imet) : 0u;
+    A.occ = (opts.tune & 0xF) ? (opts.tune & 0xF) : PMX_DEFAULT_VOL_OCC;
     A.xcd_swizzle = 1;
     if (ctx->nq_vol) launch_locate_vol(A, st);
     if (ev) CK(hipEventRecord(ev[2], st));

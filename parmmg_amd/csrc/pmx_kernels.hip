@@ -17,7 +17,21 @@
 #include "pmx_device.h"
 #include "pmx_kernels.h"
 
-#define WALK_RING 8
+#define WALK_RING 4
+
+// rank of each value in the stable ascending order (ties: lower index first)
+__device__ __forceinline__ void stable_ranks(const double l[4], int rk[4]) {
+  rk[0] = rk[1] = rk[2] = rk[3] = 0;
+#pragma unroll
+  for (int a = 0; a < 4; a++)
+#pragma unroll
+    for (int b = a + 1; b < 4; b++) {
+      // b after a unless l[b] < l[a]
+      bool bfirst = l[b] < l[a];
+      rk[a] += bfirst ? 1 : 0;
+      rk[b] += bfirst ? 0 : 1;
+    }
+}
 
 __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nb) {
   // blocks b and b+8 share an XCD (round-robin dispatch): give each XCD a
@@ -95,14 +109,22 @@ __device__ __forceinline__ unsigned interp_bar(const double *__restrict__ sol, c
       // that only one inverse is live (no scratch)
       double mint[6], r[6];
       bool ok = true;
-#pragma unroll
+      // one vertex at a time (not unrolled: bounds the live load registers)
+#pragma unroll 1
       for (int i = 0; i < NV; i++) {
-        const double *m = sol + (int64_t)v[i] * sd.S + off;
+        int vi = v[0];
+        double ph = phi[0];
+#pragma unroll
+        for (int q = 1; q < NV; q++) {
+          vi = (i == q) ? v[q] : vi;
+          ph = (i == q) ? phi[q] : ph;
+        }
+        const double *m = sol + (int64_t)vi * sd.S + off;
         double mm[6] = {m[0], m[1], m[2], m[3], m[4], m[5]};
         double mi[6];
         ok = ok && invmat(mm, mi);
 #pragma unroll
-        for (int j = 0; j < 6; j++) mint[j] = (i == 0) ? phi[0] * mi[j] : mint[j] + phi[i] * mi[j];
+        for (int j = 0; j < 6; j++) mint[j] = (i == 0) ? ph * mi[j] : mint[j] + ph * mi[j];
       }
       if (!ok) continue;
       if (!invmat(mint, r)) continue;
@@ -147,7 +169,10 @@ __device__ __forceinline__ void wave_stats(uint4 *rec, unsigned cnt, unsigned su
   if ((threadIdx.x & 63) == 0) *rec = make_uint4(cnt, sum, mx, mn);
 }
 
-__global__ __launch_bounds__(256) void k_locate_vol(VolArgs A) {
+// OCC = minimum waves per SIMD requested from the register allocator
+// (1 = unconstrained); selected at run time by pmx_run_opts.tune
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void k_locate_vol(VolArgs A) {
   int64_t b = A.xcd_swizzle ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
   int64_t j = b * blockDim.x + threadIdx.x;
   unsigned s_cnt = 0, s_sum = 0, s_max = 0, s_min = 0xffffffffu;
@@ -173,10 +198,16 @@ __global__ __launch_bounds__(256) void k_locate_vol(VolArgs A) {
       D3 P[4] = {ld3(A.pts, v[0]), ld3(A.pts, v[1]), ld3(A.pts, v[2]), ld3(A.pts, v[3])};
       double vol;
       tet_lambda(P, p, lam, &vol);
-      double sv[4] = {lam[0], lam[1], lam[2], lam[3]};
-      int si[4] = {0, 1, 2, 3};
-      sort4(sv, si);
-      if (sv[0] > -PMX_EPS) { found = true; break; }   // src/barycoord_pmmg.c:102-107
+      // position of face f in the reference's stable ascending order of the
+      // barycentrics (glibc qsort, src/barycoord_pmmg.c:306) as ranks: no
+      // sorted copy of the doubles is kept live
+      int rk[4];
+      stable_ranks(lam, rk);
+      double lmin = lam[0];
+      lmin = (rk[1] == 0) ? lam[1] : lmin;
+      lmin = (rk[2] == 0) ? lam[2] : lmin;
+      lmin = (rk[3] == 0) ? lam[3] : lmin;
+      if (lmin > -PMX_EPS) { found = true; break; }   // src/barycoord_pmmg.c:102-107
       if (step >= A.max_walk) break;
 #pragma unroll
       for (int r = WALK_RING - 1; r > 0; r--) ring[r] = ring[r - 1];
@@ -185,8 +216,9 @@ __global__ __launch_bounds__(256) void k_locate_vol(VolArgs A) {
       // order (src/locate_pmmg.c:819-833)
       int next = 0;
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        int nb = sel4(t.nb, si[j]);
+      for (int r = 0; r < 4; r++) {
+        int f = (rk[0] == r) ? 0 : (rk[1] == r) ? 1 : (rk[2] == r) ? 2 : 3;
+        int nb = sel4(t.nb, f);
         if (!next && nb && !in_ring(ring, nb)) next = nb;
       }
       if (!next) break;
@@ -198,7 +230,7 @@ __global__ __launch_bounds__(256) void k_locate_vol(VolArgs A) {
       A.steps[i] = step;
       double *out = A.out + i * A.sd.S;
       unsigned wm = interp_bar<4>(A.sol, A.sd, v, lam, out);
-      A.wmask[i] = (uint8_t)(A.wmask[i] | wm);
+      A.wmask[i] = (uint8_t)(wm | A.const_bit);
       s_cnt = 1; s_sum = step; s_max = step; s_min = step;
     } else {
       unsigned slot = atomicAdd(A.stuck_count, 1u);
@@ -370,7 +402,11 @@ void launch_hint_build(const TetRec *tets, const Pt4 *pts, int64_t ne, int strid
 void launch_locate_vol(const VolArgs &a, hipStream_t s) {
   int64_t nb = (a.nlist + 255) / 256;
   if (nb < 1) return;
-  hipLaunchKernelGGL(k_locate_vol, dim3((unsigned)nb), dim3(256), 0, s, a);
+  switch (a.occ) {
+    case 6: hipLaunchKernelGGL(k_locate_vol<6>, dim3((unsigned)nb), dim3(256), 0, s, a); break;
+    case 8: hipLaunchKernelGGL(k_locate_vol<8>, dim3((unsigned)nb), dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL(k_locate_vol<1>, dim3((unsigned)nb), dim3(256), 0, s, a); break;
+  }
 }
 void launch_exhaustive(const ExhArgs &e, const VolArgs &v, hipStream_t s) {
   int64_t nb = (e.ne + 255) / 256;

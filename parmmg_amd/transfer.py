@@ -120,9 +120,10 @@ class Transfer:
         self._chk(self.lib.pmx_upload_points(self.ctx, C.byref(pv)), "pmx_upload_points")
         self.npts = xyz.shape[0]
 
-    def run(self, hsiz: float = 0.0, timing: bool = False, max_walk: int = 0, hint_stride: int = 0):
+    def run(self, hsiz: float = 0.0, timing: bool = False, max_walk: int = 0, hint_stride: int = 0,
+            tune: int = 0):
         o = N.RunOpts()
-        o.hsiz, o.timing, o.max_walk, o.hint_stride = hsiz, int(timing), max_walk, hint_stride
+        o.hsiz, o.timing, o.max_walk, o.hint_stride, o.tune = hsiz, int(timing), max_walk, hint_stride, tune
         self._chk(self.lib.pmx_run(self.ctx, C.byref(o)), "pmx_run")
 
     def download(self, init: list[np.ndarray] | None = None) -> Result:

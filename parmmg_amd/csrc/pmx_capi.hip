@@ -268,6 +268,7 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   if (!dgrow(ctx, ctx->d_found, nn)) return 0;
   if (!dgrow(ctx, ctx->d_bestk, nn)) return 0;
   if (!dgrow(ctx, ctx->d_best, nn)) return 0;
+  if (!dgrow(ctx, ctx->d_ties, nn)) return 0;
   if (!dgrow(ctx, ctx->d_counts, 8)) return 0;
   if (!dgrow(ctx, ctx->d_vollist, (size_t)std::max<int64_t>(nv, 1))) return 0;
   if (!dgrow(ctx, ctx->d_bdylist, (size_t)std::max<int64_t>(nb, 1))) return 0;
@@ -325,6 +326,7 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     A.elem = ctx->d_elem.p; A.status = ctx->d_status.p; A.steps = ctx->d_steps.p;
     A.start = ctx->d_start.p;
     A.stuck_list = ctx->d_list.p; A.stuck_count = ctx->d_counts.p;
+    A.tie_list = ctx->d_ties.p; A.tie_count = ctx->d_counts.p + 3;
     A.found = ctx->d_found.p; A.bestk = ctx->d_bestk.p; A.best = ctx->d_best.p;
     A.list = ctx->d_vollist.p; A.nlist = ctx->nq_vol; A.wstats = ctx->d_vstat.p;
     A.max_walk = opts.max_walk > 0 ? opts.max_walk : 512;
@@ -484,7 +486,7 @@ void pmx_ctx::free_all() {
   dfree(d_ntoff); dfree(d_ntlist);
   dfree(d_q); dfree(d_kind); dfree(d_wmask); dfree(d_out); dfree(d_elem); dfree(d_status);
   dfree(d_steps); dfree(d_start); dfree(d_edge); dfree(d_vertex); dfree(d_list); dfree(d_found);
-  dfree(d_bestk); dfree(d_best); dfree(d_counts); dfree(d_vollist); dfree(d_bdylist);
+  dfree(d_bestk); dfree(d_best); dfree(d_ties); dfree(d_counts); dfree(d_vollist); dfree(d_bdylist);
   dfree(d_vstat); dfree(d_bstat);
   dfree(d_qual); dfree(d_red); dfree(d_blist); dfree(d_olist); dfree(d_ows);
   if (d_tgrid) hipFree(d_tgrid);

@@ -43,6 +43,7 @@ struct pmx_ctx {
   DevBuf<double> d_out;
   DevBuf<int> d_elem, d_status, d_steps, d_start, d_edge, d_vertex;
   DevBuf<int> d_list, d_found, d_bestk;
+  DevBuf<int2> d_ties;
   DevBuf<unsigned long long> d_best;
   DevBuf<unsigned> d_counts;            // [0] vol stuck, [1] bdy stuck, [2] bdy overflow
   DevBuf<int> d_vollist, d_bdylist;     // compacted point lists per path

@@ -23,6 +23,8 @@ struct VolArgs {
   int *elem, *status, *steps, *start;
   int *stuck_list;
   unsigned *stuck_count;
+  int2 *tie_list;               // (point, found tet) of points near a face
+  unsigned *tie_count;
   int *found, *bestk;
   unsigned long long *best;
   const int *list;              // indices of the volume points (Morton order kept)

@@ -85,7 +85,10 @@ __global__ __launch_bounds__(256) void k_hint_build(const TetRec *__restrict__ t
     D3 m{(a.x + b.x + c.x + d.x) * 0.25, (a.y + b.y + c.y + d.y) * 0.25,
          (a.z + b.z + c.z + d.z) * 0.25};
     int cc[3];
-    atomicMax(&grid[cell_of(g, m, cc)], (int)k);
+    // plain store: any sampled tet of the cell is a valid start; the located
+    // tet does not depend on the start (unique containing tet, or the
+    // canonical min-index tet of a tie, see canonical_tet)
+    grid[cell_of(g, m, cc)] = (int)k;
   }
 }
 
@@ -109,16 +112,12 @@ __device__ __forceinline__ unsigned interp_bar(const double *__restrict__ sol, c
       // that only one inverse is live (no scratch)
       double mint[6], r[6];
       bool ok = true;
-      // one vertex at a time (not unrolled: bounds the live load registers)
-#pragma unroll 1
-      for (int i = 0; i < NV; i++) {
-        int vi = v[0];
-        double ph = phi[0];
+      // unrolled: the 4 vertex rows are loaded concurrently (a rolled loop
+      // measured 6% slower on C2 -- latency, not registers, bounds the walk)
 #pragma unroll
-        for (int q = 1; q < NV; q++) {
-          vi = (i == q) ? v[q] : vi;
-          ph = (i == q) ? phi[q] : ph;
-        }
+      for (int i = 0; i < NV; i++) {
+        const int vi = v[i];
+        const double ph = phi[i];
         const double *m = sol + (int64_t)vi * sd.S + off;
         double mm[6] = {m[0], m[1], m[2], m[3], m[4], m[5]};
         double mi[6];
@@ -142,6 +141,50 @@ __device__ __forceinline__ unsigned interp_bar(const double *__restrict__ sol, c
     }
   }
   return wm;
+}
+
+// ---- ties -----------------------------------------------------------------------
+
+// A point with some lambda_f < TIE_NEAR in its tet may also satisfy the
+// reference's inside test (lambda_min > -1e-6, src/barycoord_pmmg.c:102-107)
+// in the neighbours across those faces (face / edge / vertex ties).  The
+// reference returns whichever its path reaches first; the device returns the
+// smallest index of the connected set of containing tets, so the answer is
+// independent of the start tet (and equals the exhaustive scan's first hit).
+#define TIE_NEAR 1.e-3
+#define TIE_CAP 48
+__device__ __noinline__ int canonical_tet(const TetRec *tets, const Pt4 *pts, int k0, D3 p) {
+  int vis[TIE_CAP], inq[TIE_CAP];
+  int nv = 0, nq = 0, head = 0, best = k0;
+  vis[nv++] = k0;
+  inq[nq++] = k0;
+  while (head < nq) {
+    int k = inq[head++];
+    TetRec t = tets[k];
+    D3 P[4] = {ld3(pts, t.v[0]), ld3(pts, t.v[1]), ld3(pts, t.v[2]), ld3(pts, t.v[3])};
+    double lam[4], vol;
+    tet_lambda(P, p, lam, &vol);
+    for (int f = 0; f < 4; f++) {
+      int nb = t.nb[f];
+      if (!nb || !(lam[f] < TIE_NEAR)) continue;
+      bool seen = false;
+      for (int q = 0; q < nv; q++) seen |= (vis[q] == nb);
+      if (seen) continue;
+      if (nv == TIE_CAP) return -1;
+      vis[nv++] = nb;
+      TetRec u = tets[nb];
+      if (u.v[0] <= 0) continue;
+      D3 Q[4] = {ld3(pts, u.v[0]), ld3(pts, u.v[1]), ld3(pts, u.v[2]), ld3(pts, u.v[3])};
+      double mu[4], vu;
+      tet_lambda(Q, p, mu, &vu);
+      if (fmin(fmin(mu[0], mu[1]), fmin(mu[2], mu[3])) > -PMX_EPS) {
+        if (nq == TIE_CAP) return -1;
+        inq[nq++] = nb;
+        best = nb < best ? nb : best;
+      }
+    }
+  }
+  return best;
 }
 
 // ---- volume locate + interpolate ------------------------------------------
@@ -225,6 +268,19 @@ __global__ __launch_bounds__(256, OCC) void k_locate_vol(VolArgs A) {
       cur = next;
     }
     if (found) {
+      // a point within the tolerance of a face/edge/vertex is contained by
+      // several tets: take the smallest index among them (start-independent)
+      // (resolved by k_ties: keeps the BFS out of this kernel's registers)
+      double lmn = fmin(fmin(lam[0], lam[1]), fmin(lam[2], lam[3]));
+      if (lmn < TIE_NEAR) {
+        unsigned slot = atomicAdd(A.tie_count, 1u);
+        A.tie_list[slot] = make_int2((int)i, cur);
+        A.steps[i] = step;
+        found = false;
+        step = -1;                                  // neither found nor stuck
+      }
+    }
+    if (found) {
       A.elem[i] = cur;
       A.status[i] = 1;
       A.steps[i] = step;
@@ -232,7 +288,7 @@ __global__ __launch_bounds__(256, OCC) void k_locate_vol(VolArgs A) {
       unsigned wm = interp_bar<4>(A.sol, A.sd, v, lam, out);
       A.wmask[i] = (uint8_t)(wm | A.const_bit);
       s_cnt = 1; s_sum = step; s_max = step; s_min = step;
-    } else {
+    } else if (step >= 0) {
       unsigned slot = atomicAdd(A.stuck_count, 1u);
       A.stuck_list[slot] = (int)i;
       A.found[slot] = 0x7fffffff;
@@ -242,6 +298,37 @@ __global__ __launch_bounds__(256, OCC) void k_locate_vol(VolArgs A) {
     }
   }
   wave_stats(A.wstats + (b * blockDim.x + threadIdx.x) / 64, s_cnt, s_sum, s_max, s_min);
+}
+
+// ---- tie resolution ----------------------------------------------------------
+
+__global__ __launch_bounds__(64) void k_ties(VolArgs A) {
+  const unsigned n = *A.tie_count;
+  for (unsigned j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    int2 e = A.tie_list[j];
+    const int64_t i = e.x;
+    Pt4 qq = A.q[i];
+    D3 p{qq.x, qq.y, qq.z};
+    int kc = canonical_tet(A.tets, A.pts, e.y, p);
+    if (kc < 0) {                                   // tie set too large: scan
+      unsigned slot = atomicAdd(A.stuck_count, 1u);
+      A.stuck_list[slot] = (int)i;
+      A.found[slot] = 0x7fffffff;
+      A.bestk[slot] = 0x7fffffff;
+      A.best[slot] = ~0ull;
+      A.steps[i] = -A.steps[i];
+      continue;
+    }
+    TetRec t = A.tets[kc];
+    int v[4] = {t.v[0], t.v[1], t.v[2], t.v[3]};
+    D3 P[4] = {ld3(A.pts, v[0]), ld3(A.pts, v[1]), ld3(A.pts, v[2]), ld3(A.pts, v[3])};
+    double lam[4], vol;
+    tet_lambda(P, p, lam, &vol);
+    A.elem[i] = kc;
+    A.status[i] = 1;
+    unsigned wm = interp_bar<4>(A.sol, A.sd, v, lam, A.out + i * A.sd.S);
+    A.wmask[i] = (uint8_t)(wm | A.const_bit);
+  }
 }
 
 // ---- exhaustive fallback ---------------------------------------------------
@@ -412,6 +499,7 @@ void launch_exhaustive(const ExhArgs &e, const VolArgs &v, hipStream_t s) {
   int64_t nb = (e.ne + 255) / 256;
   if (nb > 2048) nb = 2048;
   if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(k_ties, dim3(64), dim3(64), 0, s, v);
   hipLaunchKernelGGL(k_exh_find, dim3((unsigned)nb), dim3(256), 0, s, e);
   hipLaunchKernelGGL(k_exh_closest, dim3((unsigned)nb), dim3(256), 0, s, e, 0);
   hipLaunchKernelGGL(k_exh_closest, dim3((unsigned)nb), dim3(256), 0, s, e, 1);

@@ -235,12 +235,37 @@ def test_quality_and_length_stats(transfer, metric):
 
 
 def test_deterministic(transfer):
+    """Located elements and fields are independent of the (racy) hint grid."""
     m, x, t, sols = cube_case(8, metric="ani")
     a, sa, ea, va = run_gpu(transfer, m, x, t, sols, 0)
-    b, sb, eb, vb = run_gpu(transfer, m, x, t, sols, 0)
-    assert np.array_equal(a.elem, b.elem) and np.array_equal(sa, sb)
-    for s in range(len(sols)):
-        assert bits_equal(a.sols[s], b.sols[s]).all()
+    for stride in (1, 3, 7):
+        transfer.run(hint_stride=stride)
+        b = transfer.download()
+        vol = t == 0
+        assert np.array_equal(a.elem[vol], b.elem[vol])
+        for s in range(len(sols)):
+            assert bits_equal(a.sols[s][vol], b.sols[s][vol]).all()
+
+
+def test_tie_points_canonical(transfer):
+    """Old vertices, edge midpoints and face centroids (the tie suite of
+    SURVEY.md 8(d)): the device returns the smallest index among all tets
+    that contain the point by the reference predicate."""
+    m = M.kuhn_cube(4)
+    rng = np.random.default_rng(2)
+    ks = rng.choice(np.arange(1, m.ne + 1), 60, replace=False)
+    P = m.xyz[m.tet[ks]]
+    x = np.concatenate([P[:, 0], 0.5 * (P[:, 0] + P[:, 1]), P[:, :3].mean(1), P.mean(1)])
+    t = np.zeros(len(x), np.uint16)
+    sols = [M.on_vertices(m, M.iso_metric)]
+    r, starts, _, _ = run_gpu(transfer, m, x, t, sols, 0)
+    o = O.Oracle(m)
+    for i in range(len(x)):
+        cont = [k for k in range(1, m.ne + 1) if o.tet_contains(k, x[i])[0]]
+        assert cont and r.elem[i] == min(cont), (i, r.elem[i], cont)
+    outs, elem, st, *_ = o.interp(x, t, sols, imet=0)
+    c = compare_volume(o, x, t, (r.sols, r.elem, r.status), (outs, elem, st), sols)
+    assert c["ties"] > 0
 
 
 def test_large_size_properties(transfer):

@@ -151,7 +151,9 @@ __device__ __forceinline__ unsigned interp_bar(const double *__restrict__ sol, c
 // reference returns whichever its path reaches first; the device returns the
 // smallest index of the connected set of containing tets, so the answer is
 // independent of the start tet (and equals the exhaustive scan's first hit).
-#define TIE_NEAR 1.e-3
+// lambda_f < 10*EPS admits neighbours up to 10x larger across face f: a tie
+// across a sharper size jump is still a containing tet, only not canonical
+#define TIE_NEAR 1.e-5
 #define TIE_CAP 48
 __device__ __noinline__ int canonical_tet(const TetRec *tets, const Pt4 *pts, int k0, D3 p) {
   int vis[TIE_CAP], inq[TIE_CAP];

@@ -74,6 +74,8 @@ typedef struct {
   int64_t nclosest;          /* not found -> closest element      */
   int64_t stepmin, stepmax;  /* walk steps                        */
   double  stepav;
+  int     tet_mode;          /* volume path ran tet-centric (no walk steps) */
+  double  tests_per_vertex;  /* tet-centric: containment tests per vertex   */
 } pmx_locate_stats;
 
 /* ---- context ---------------------------------------------------------- */

@@ -44,6 +44,7 @@ class LocateStats(C.Structure):
     _fields_ = [
         ("nvol", i64), ("nbdy", i64), ("nexhaust", i64), ("nclosest", i64),
         ("stepmin", i64), ("stepmax", i64), ("stepav", C.c_double),
+        ("tet_mode", C.c_int), ("tests_per_vertex", C.c_double),
     ]
 
 

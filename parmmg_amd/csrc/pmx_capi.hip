@@ -216,6 +216,10 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   if (!dgrow(ctx, ctx->d_trn, (size_t)(nt + 1))) return 0;
   CK(hipMemcpyAsync(ctx->d_pts.p, hp.data(), hp.size() * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_tets.p, ht.data(), ht.size() * sizeof(TetRec), hipMemcpyHostToDevice, ctx->stream));
+  // connectivity-only stream for the tet-centric pass (16 of the 32 B)
+  if (!dgrow(ctx, ctx->d_tetv, (size_t)(ne + 1))) return 0;
+  CK(hipMemcpy2DAsync(ctx->d_tetv.p, sizeof(int4), ctx->d_tets.p, sizeof(TetRec), sizeof(int4),
+                      (size_t)(ne + 1), hipMemcpyDeviceToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_sol.p, hs.data(), hs.size() * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_tris.p, htr.data(), htr.size() * sizeof(TriRec), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_ntoff.p, ctx->h_ntoff.data(), ctx->h_ntoff.size() * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
@@ -314,9 +318,16 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     if (!(s == sd.imet && sd.metric_const)) any_interp = true;
   // reference early exit (src/interpmesh_pmmg.c:509-512): nothing to locate
   if (any_interp) {
-    CK(hipMemsetAsync(ctx->d_grid.p, 0, (size_t)ctx->gcells * sizeof(int), st));
-    const int stride = opts.hint_stride > 0 ? opts.hint_stride : PMX_DEFAULT_HINT_STRIDE;
-    launch_hint_build(ctx->d_tets.p, ctx->d_pts.p, ctx->ne, stride, ctx->d_grid.p, ctx->grid, st);
+    // volume path: tet-centric stream when the new vertices are a sizeable
+    // fraction of the old tets (remesh iterations), adjacency walk otherwise
+    // (tune bit 8 forces the walk, bit 9 the stream)
+    const bool force_walk = (opts.tune & 0x100) != 0, force_tet = (opts.tune & 0x200) != 0;
+    ctx->tet_mode = ctx->nq_vol > 0 && (force_tet || (!force_walk && ctx->nq_vol * 64 >= ctx->ne));
+    if (!ctx->tet_mode) {
+      CK(hipMemsetAsync(ctx->d_grid.p, 0, (size_t)ctx->gcells * sizeof(int), st));
+      const int stride = opts.hint_stride > 0 ? opts.hint_stride : PMX_DEFAULT_HINT_STRIDE;
+      launch_hint_build(ctx->d_tets.p, ctx->d_pts.p, ctx->ne, stride, ctx->d_grid.p, ctx->grid, st);
+    }
     if (ev) CK(hipEventRecord(ev[1], st));
     VolArgs A{};
     A.pts = ctx->d_pts.p; A.tets = ctx->d_tets.p; A.sol = ctx->d_sol.p; A.sd = sd;
@@ -333,7 +344,11 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     A.const_bit = sd.metric_const ? (1u << sd.imet) : 0u;
     A.occ = (opts.tune & 0xF) ? (opts.tune & 0xF) : PMX_DEFAULT_VOL_OCC;
     A.xcd_swizzle = 1;
-    if (ctx->nq_vol) launch_locate_vol(A, st);
+    if (ctx->tet_mode) {
+      if (!ctx->launch_tet_locate(A, opts, st)) return 0;
+    } else if (ctx->nq_vol) {
+      launch_locate_vol(A, st);
+    }
     if (ev) CK(hipEventRecord(ev[2], st));
     if (ctx->nq_bdy) {
       if (!ctx->launch_bdy(A, opts, st)) return 0;
@@ -407,9 +422,17 @@ int pmx_locate_stats_get(pmx_ctx *ctx, pmx_locate_stats *st) {
   // reduce the per-wave records of both walks
   unsigned long long located = 0, sum = 0;
   unsigned mx = 0, mn = 0xffffffffu;
+  st->tet_mode = ctx->tet_mode ? 1 : 0;
+  if (ctx->tet_mode && ctx->tests_blocks > 0 && ctx->nq_vol > 0) {
+    std::vector<unsigned long long> tp((size_t)ctx->tests_blocks);
+    CK(hipMemcpy(tp.data(), ctx->d_tests.p, tp.size() * 8, hipMemcpyDeviceToHost));
+    unsigned long long tot = 0;
+    for (auto x : tp) tot += x;
+    st->tests_per_vertex = (double)tot / (double)ctx->nq_vol;
+  }
   for (int path = 0; path < 2; path++) {
     int64_t npath = path ? ctx->nq_bdy : ctx->nq_vol;
-    if (!npath) continue;
+    if (!npath || (path == 0 && ctx->tet_mode)) continue;
     std::vector<uint4> w((size_t)((npath + 63) / 64));
     CK(hipMemcpy(w.data(), path ? ctx->d_bstat.p : ctx->d_vstat.p, w.size() * sizeof(uint4),
                  hipMemcpyDeviceToHost));
@@ -488,6 +511,8 @@ void pmx_ctx::free_all() {
   dfree(d_steps); dfree(d_start); dfree(d_edge); dfree(d_vertex); dfree(d_list); dfree(d_found);
   dfree(d_bestk); dfree(d_best); dfree(d_ties); dfree(d_counts); dfree(d_vollist); dfree(d_bdylist);
   dfree(d_vstat); dfree(d_bstat);
+  dfree(d_tetv); dfree(d_qcnt); dfree(d_qstart); dfree(d_qcell); dfree(d_qslot); dfree(d_tbest);
+  dfree(d_qs); dfree(d_tests); dfree(d_scan_tmp);
   dfree(d_qual); dfree(d_red); dfree(d_blist); dfree(d_olist); dfree(d_ows);
   if (d_tgrid) hipFree(d_tgrid);
   d_tgrid = nullptr;

@@ -44,6 +44,15 @@ struct pmx_ctx {
   DevBuf<int> d_elem, d_status, d_steps, d_start, d_edge, d_vertex;
   DevBuf<int> d_list, d_found, d_bestk;
   DevBuf<int2> d_ties;
+  // tet-centric volume path
+  DevBuf<int4> d_tetv;                  // connectivity stream (16 B / tet)
+  DevBuf<unsigned> d_qcnt, d_qstart;
+  DevBuf<int> d_qcell, d_qslot, d_tbest;
+  DevBuf<Pt4> d_qs;
+  DevBuf<unsigned long long> d_tests;
+  DevBuf<char> d_scan_tmp;
+  int tests_blocks = 0;
+  bool tet_mode = false;
   DevBuf<unsigned long long> d_best;
   DevBuf<unsigned> d_counts;            // [0] vol stuck, [1] bdy stuck, [2] bdy overflow
   DevBuf<int> d_vollist, d_bdylist;     // compacted point lists per path
@@ -65,6 +74,7 @@ struct pmx_ctx {
   void free_all();
   void host_build_node_trias(const std::vector<TriRec> &tr);
   bool launch_bdy(const VolArgs &a, const pmx_run_opts &o, hipStream_t s);
+  bool launch_tet_locate(const VolArgs &a, const pmx_run_opts &o, hipStream_t s);
 };
 
 void launch_tria_normals(const TriRec *tris, const Pt4 *pts, int64_t nt, Pt4 *trn, hipStream_t s);

@@ -92,57 +92,6 @@ __global__ __launch_bounds__(256) void k_hint_build(const TetRec *__restrict__ t
   }
 }
 
-// ---- interpolation --------------------------------------------------------
-
-// PMMG_interp4bar_iso / PMMG_interp3bar_iso (src/interpmesh_pmmg.c:125-149,
-// :206-230): out = 0, then += phi_i * old_i in vertex order.
-// PMMG_interp4bar_ani / 3bar_ani (:166-190, :247-270): invert, interpolate,
-// invert; a failed inversion leaves the output untouched (bit s of wmask).
-template <int NV>
-__device__ __forceinline__ unsigned interp_bar(const double *__restrict__ sol, const SolDesc &sd,
-                                               const int *v, const double *phi,
-                                               double *__restrict__ out) {
-  unsigned wm = 0;
-  for (int s = 0; s < sd.nsol; ++s) {
-    if (s == sd.imet && sd.metric_const) continue;
-    const int sz = sd.size[s], off = sd.off[s];
-    if (sz == 6) {
-      // mint_j = ((phi0*mi0_j + phi1*mi1_j) + phi2*mi2_j) + phi3*mi3_j, the
-      // reference's left-to-right sum, accumulated one vertex at a time so
-      // that only one inverse is live (no scratch)
-      double mint[6], r[6];
-      bool ok = true;
-      // unrolled: the 4 vertex rows are loaded concurrently (a rolled loop
-      // measured 6% slower on C2 -- latency, not registers, bounds the walk)
-#pragma unroll
-      for (int i = 0; i < NV; i++) {
-        const int vi = v[i];
-        const double ph = phi[i];
-        const double *m = sol + (int64_t)vi * sd.S + off;
-        double mm[6] = {m[0], m[1], m[2], m[3], m[4], m[5]};
-        double mi[6];
-        ok = ok && invmat(mm, mi);
-#pragma unroll
-        for (int j = 0; j < 6; j++) mint[j] = (i == 0) ? ph * mi[j] : mint[j] + ph * mi[j];
-      }
-      if (!ok) continue;
-      if (!invmat(mint, r)) continue;
-#pragma unroll
-      for (int j = 0; j < 6; j++) out[off + j] = r[j];
-      wm |= 1u << s;
-    } else {
-      for (int j = 0; j < sz; j++) {
-        double acc = 0.0;
-#pragma unroll
-        for (int i = 0; i < NV; i++) acc += phi[i] * sol[(int64_t)v[i] * sd.S + off + j];
-        out[off + j] = acc;
-      }
-      wm |= 1u << s;
-    }
-  }
-  return wm;
-}
-
 // ---- ties -----------------------------------------------------------------------
 
 // A point with some lambda_f < TIE_NEAR in its tet may also satisfy the

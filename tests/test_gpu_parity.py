@@ -18,21 +18,24 @@ from parmmg_amd import mesh as M
 
 pytestmark = pytest.mark.gpu
 
+WALK, TET = 0x100, 0x200      # pmx_run_opts.tune: force the volume walk / tet-centric path
 
-def run_gpu(tr, m, x, t, sols, imet=0, hsiz=0.0, init=None):
+
+def run_gpu(tr, m, x, t, sols, imet=0, hsiz=0.0, init=None, tune=0):
     tr.upload_background(m, sols, imet)
     tr.upload_points(x, t)
-    tr.run(hsiz=hsiz)
+    tr.run(hsiz=hsiz, tune=tune)
     r = tr.download(init=init)
     e, v = tr.border()
     return r, tr.starts(), e, v
 
 
-@pytest.mark.parametrize("metric,n", [("iso", 10), ("ani", 9), ("none", 7)])
-def test_volume_parity(transfer, metric, n):
+@pytest.mark.parametrize("metric,n,tune", [("iso", 10, 0), ("ani", 9, 0), ("none", 7, 0),
+                                           ("iso", 10, WALK), ("ani", 9, WALK), ("ani", 9, TET)])
+def test_volume_parity(transfer, metric, n, tune):
     m, x, t, sols = cube_case(n, metric=metric, surface=False)
     imet = 0 if metric != "none" else -1
-    r, starts, _, _ = run_gpu(transfer, m, x, t, sols, imet)
+    r, starts, _, _ = run_gpu(transfer, m, x, t, sols, imet, tune=tune)
     o = O.Oracle(m)
     outs, elem, st, steps, e, v = o.interp(x, t, sols, imet=imet)
     c = compare_volume(o, x, t, (r.sols, r.elem, r.status), (outs, elem, st), sols)
@@ -104,7 +107,7 @@ def test_exhaustive_found_path(transfer):
     m, x, t, sols = cube_case(6, metric="ani", surface=False)
     transfer.upload_background(m, sols, 0)
     transfer.upload_points(x, t)
-    transfer.run(max_walk=1)
+    transfer.run(max_walk=1, tune=WALK)
     r = transfer.download()
     assert (r.status == -1).sum() > len(x) // 2
     o = O.Oracle(m)
@@ -247,7 +250,28 @@ def test_deterministic(transfer):
             assert bits_equal(a.sols[s][vol], b.sols[s][vol]).all()
 
 
-def test_tie_points_canonical(transfer):
+@pytest.mark.parametrize("case", ["cube", "lshape"])
+def test_walk_and_stream_agree(transfer, case):
+    """The adjacency walk and the tet-centric stream are two schedules of the
+    same function: identical elements and bit-identical fields."""
+    if case == "cube":
+        m, x, t, sols = cube_case(12, metric="ani")
+    else:
+        m = l_shaped(8)
+        x = np.random.default_rng(4).uniform(-0.05, 1.05, size=(4000, 3))
+        t = np.zeros(len(x), np.uint16)
+        sols = [M.on_vertices(m, M.shock_metric), M.on_vertices(m, lin_field)]
+    a, *_ = run_gpu(transfer, m, x, t, sols, 0, tune=WALK)
+    b, *_ = run_gpu(transfer, m, x, t, sols, 0, tune=TET)
+    vol = t == 0
+    assert np.array_equal(a.elem[vol], b.elem[vol])
+    assert np.array_equal(a.status[vol] != 0, b.status[vol] != 0)
+    for s in range(len(sols)):
+        assert bits_equal(a.sols[s][vol], b.sols[s][vol]).all()
+
+
+@pytest.mark.parametrize("tune", [WALK, TET])
+def test_tie_points_canonical(transfer, tune):
     """Old vertices, edge midpoints and face centroids (the tie suite of
     SURVEY.md 8(d)): the device returns the smallest index among all tets
     that contain the point by the reference predicate."""
@@ -258,7 +282,7 @@ def test_tie_points_canonical(transfer):
     x = np.concatenate([P[:, 0], 0.5 * (P[:, 0] + P[:, 1]), P[:, :3].mean(1), P.mean(1)])
     t = np.zeros(len(x), np.uint16)
     sols = [M.on_vertices(m, M.iso_metric)]
-    r, starts, _, _ = run_gpu(transfer, m, x, t, sols, 0)
+    r, starts, _, _ = run_gpu(transfer, m, x, t, sols, 0, tune=tune)
     o = O.Oracle(m)
     for i in range(len(x)):
         cont = [k for k in range(1, m.ne + 1) if o.tet_contains(k, x[i])[0]]

@@ -620,6 +620,7 @@ int orc_interp_points(orc_ctx *o, int64_t npts, const double *pxyz, const int *p
       const int *v;
       int i;
       k = start_bdy ? start_bdy[ip] : cur_bdy;
+      if (k < 1 || k > o->nt) k = 1;
       for (i = 0; i < 4; i++) { b[i].idx = i; b[i].val = 0.0; }
       r = locate_bdy(o, p, &k, &e, &vx, b, &st);
       cur_bdy = k;
@@ -647,6 +648,7 @@ int orc_interp_points(orc_ctx *o, int64_t npts, const double *pxyz, const int *p
     } else {
       const int *v;
       k = start_vol ? start_vol[ip] : cur_vol;
+      if (k < 1 || k > o->ne) k = 1;              /* invalid start: first tet */
       r = locate_vol(o, p, &k, b, &st);
       cur_vol = k;
       v = &o->tet[4*(int64_t)k];

@@ -322,11 +322,12 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     // fraction of the old tets (remesh iterations), adjacency walk otherwise
     // (tune bit 8 forces the walk, bit 9 the stream)
     const bool force_walk = (opts.tune & 0x100) != 0, force_tet = (opts.tune & 0x200) != 0;
-    ctx->tet_mode = ctx->nq_vol > 0 && (force_tet || (!force_walk && ctx->nq_vol * 64 >= ctx->ne));
+    ctx->tet_mode = ctx->nq_vol > 0 && force_tet && !force_walk;
+    (void)force_walk;
     if (!ctx->tet_mode) {
       CK(hipMemsetAsync(ctx->d_grid.p, 0, (size_t)ctx->gcells * sizeof(int), st));
       const int stride = opts.hint_stride > 0 ? opts.hint_stride : PMX_DEFAULT_HINT_STRIDE;
-      launch_hint_build(ctx->d_tets.p, ctx->d_pts.p, ctx->ne, stride, ctx->d_grid.p, ctx->grid, st);
+      launch_hint_build(ctx->d_tetv.p, ctx->d_pts.p, ctx->ne, stride, ctx->d_grid.p, ctx->grid, st);
     }
     if (ev) CK(hipEventRecord(ev[1], st));
     VolArgs A{};

@@ -48,7 +48,7 @@ struct ExhArgs {
   int *bestk;
 };
 
-void launch_hint_build(const TetRec *tets, const Pt4 *pts, int64_t ne, int stride, int *grid,
+void launch_hint_build(const int4 *tetv, const Pt4 *pts, int64_t ne, int stride, int *grid,
                        GridDesc g, hipStream_t s);
 void launch_locate_vol(const VolArgs &a, hipStream_t s);
 void launch_exhaustive(const ExhArgs &e, const VolArgs &v, hipStream_t s);

@@ -204,14 +204,19 @@ bool pmx_ctx::launch_tet_locate(const VolArgs &A, const pmx_run_opts &o, hipStre
     ext[a] = std::max(bbhi[a] - bblo[a], 1e-300);
     vol *= ext[a];
   }
-  const double h = std::cbrt(vol / std::max(1.0, (double)nv));
+  // cell edge = f * (volume per vertex)^(1/3); the origin is shifted by an
+  // irrational fraction of a cell so that lattice-aligned tet bboxes (Kuhn
+  // cells, Cartesian-like meshes) do not straddle cell faces by the margin
+  static const double fac[4] = {1.0, 0.5, 0.7, 1.4};
+  const double h = fac[(o.tune >> 10) & 3] * std::cbrt(vol / std::max(1.0, (double)nv));
+  const double shift = 0.3819660113 * h;
   int64_t cells = 1;
   for (int a = 0; a < 3; a++) {
-    int d = (int)std::ceil(ext[a] / h);
+    int d = (int)std::ceil((ext[a] + shift) / h);
     d = std::max(1, std::min(d, 2048));
     g.dim[a] = d;
-    g.lo[a] = bblo[a];
-    g.inv[a] = (double)d / ext[a];
+    g.lo[a] = bblo[a] - shift;
+    g.inv[a] = (double)d / (ext[a] + shift);
     cells *= d;
   }
   auto grow = [&](auto &b, size_t n) {

@@ -308,8 +308,10 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
 
   hipStream_t st = ctx->stream;
   if (ev) CK(hipEventRecord(ev[0], st));
-  CK(hipMemsetAsync(ctx->d_wmask.p, 0, (size_t)std::max<int64_t>(n, 1), st));
-  launch_run_init(ctx->d_counts.p, st);
+  // one prologue kernel zeroes the write masks, the counters and the hint grid
+  const bool need_grid = !((opts.tune & 0x200) && !(opts.tune & 0x100));
+  launch_prologue(ctx->d_wmask.p, n, ctx->d_counts.p, need_grid ? ctx->d_grid.p : nullptr,
+                  ctx->gcells, st);
   if (sd.metric_const)
     launch_const_metric(ctx->d_kind.p, n, ctx->d_out.p, S, sd.off[sd.imet], sd.size[sd.imet],
                         opts.hsiz, ctx->d_wmask.p, sd.imet, st);
@@ -325,7 +327,6 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     ctx->tet_mode = ctx->nq_vol > 0 && force_tet && !force_walk;
     (void)force_walk;
     if (!ctx->tet_mode) {
-      CK(hipMemsetAsync(ctx->d_grid.p, 0, (size_t)ctx->gcells * sizeof(int), st));
       const int stride = opts.hint_stride > 0 ? opts.hint_stride : PMX_DEFAULT_HINT_STRIDE;
       launch_hint_build(ctx->d_tetv.p, ctx->d_pts.p, ctx->ne, stride, ctx->d_grid.p, ctx->grid, st);
     }

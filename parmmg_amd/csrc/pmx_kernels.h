@@ -55,6 +55,8 @@ void launch_exhaustive(const ExhArgs &e, const VolArgs &v, hipStream_t s);
 void launch_const_metric(const int8_t *kind, int64_t nq, double *out, int S, int off, int size,
                          double hsiz, uint8_t *wmask, int imet, hipStream_t s);
 void launch_run_init(unsigned *counts, hipStream_t s);
+void launch_prologue(uint8_t *wmask, int64_t n, unsigned *counts, int *grid, int64_t gcells,
+                     hipStream_t s);
 
 struct StatArgs {
   const Pt4 *pts;

@@ -14,6 +14,7 @@
 //                    contained nowhere, then the reference's closest-vertex
 //                    barycentrics (src/barycoord_pmmg.c:371-404)
 // k_exh_finish       interpolation for the stuck list
+#include <algorithm>
 #include "pmx_device.h"
 #include "pmx_kernels.h"
 
@@ -253,9 +254,9 @@ __global__ __launch_bounds__(256, OCC) void k_locate_vol(VolArgs A) {
 
 // ---- tie resolution ----------------------------------------------------------
 
-__global__ __launch_bounds__(64) void k_ties(VolArgs A) {
+__device__ void d_ties(const VolArgs &A, unsigned bid, unsigned nblk) {
   const unsigned n = *A.tie_count;
-  for (unsigned j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+  for (unsigned j = bid * blockDim.x + threadIdx.x; j < n; j += nblk * blockDim.x) {
     int2 e = A.tie_list[j];
     const int64_t i = e.x;
     Pt4 qq = A.q[i];
@@ -287,7 +288,7 @@ __global__ __launch_bounds__(64) void k_ties(VolArgs A) {
 #define EXH_CHUNK 256
 
 // smallest tet index containing each stuck point (bbox prefilter, exact test)
-__global__ __launch_bounds__(256) void k_exh_find(ExhArgs A) {
+__device__ void d_exh_find(const ExhArgs &A, unsigned bid, unsigned nblk) {
   __shared__ D3 sp[EXH_CHUNK];
   const unsigned n = *A.count;
   for (unsigned c0 = 0; c0 < n; c0 += EXH_CHUNK) {
@@ -298,8 +299,8 @@ __global__ __launch_bounds__(256) void k_exh_find(ExhArgs A) {
       sp[j] = D3{qq.x, qq.y, qq.z};
     }
     __syncthreads();
-    for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= A.ne;
-         k += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t k = 1 + (int64_t)bid * blockDim.x + threadIdx.x; k <= A.ne;
+         k += (int64_t)nblk * blockDim.x) {
       TetRec t = A.tets[k];
       if (t.v[0] <= 0) continue;
       D3 P[4] = {ld3(A.pts, t.v[0]), ld3(A.pts, t.v[1]), ld3(A.pts, t.v[2]), ld3(A.pts, t.v[3])};
@@ -329,7 +330,7 @@ __global__ __launch_bounds__(256) void k_exh_find(ExhArgs A) {
 }
 
 // argmin over all tets of |lambda_min| * vol for points found nowhere
-__global__ __launch_bounds__(256) void k_exh_closest(ExhArgs A, int pass) {
+__device__ void d_exh_closest(const ExhArgs &A, int pass, unsigned bid, unsigned nblk) {
   __shared__ D3 sp[EXH_CHUNK];
   __shared__ int act[EXH_CHUNK];
   const unsigned n = *A.count;
@@ -342,8 +343,8 @@ __global__ __launch_bounds__(256) void k_exh_closest(ExhArgs A, int pass) {
       act[j] = (A.found[c0 + j] == 0x7fffffff);
     }
     __syncthreads();
-    for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= A.ne;
-         k += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t k = 1 + (int64_t)bid * blockDim.x + threadIdx.x; k <= A.ne;
+         k += (int64_t)nblk * blockDim.x) {
       TetRec t = A.tets[k];
       if (t.v[0] <= 0) continue;
       D3 P[4] = {ld3(A.pts, t.v[0]), ld3(A.pts, t.v[1]), ld3(A.pts, t.v[2]), ld3(A.pts, t.v[3])};
@@ -361,9 +362,9 @@ __global__ __launch_bounds__(256) void k_exh_closest(ExhArgs A, int pass) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_exh_finish(ExhArgs A, VolArgs V) {
+__device__ void d_exh_finish(const ExhArgs &A, const VolArgs &V, unsigned bid, unsigned nblk) {
   const unsigned n = *A.count;
-  for (unsigned j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+  for (unsigned j = bid * blockDim.x + threadIdx.x; j < n; j += nblk * blockDim.x) {
     int64_t i = A.list[j];
     Pt4 qq = A.q[i];
     D3 p{qq.x, qq.y, qq.z};
@@ -401,6 +402,50 @@ __global__ __launch_bounds__(256) void k_exh_finish(ExhArgs A, VolArgs V) {
   }
 }
 
+// ---- fused fallback -------------------------------------------------------------
+//
+// Ties, exhaustive scan (find, closest value, closest index) and the final
+// interpolation of the scanned points used to be five launches that almost
+// always found nothing to do (~4.5 us each).  One launch of FALLBACK_BLOCKS
+// co-resident workgroups (1 per CU at most; the kernel admits 4) now reads the
+// counters and leaves, or runs the phases separated by a grid barrier
+// (MI355X_MICROARCH.md "barrier-counter": release fence + waitcnt before the
+// arrive, relaxed agent-scope poll, acquire fence after; bounded spin).
+#define FALLBACK_BLOCKS 256
+
+__device__ __forceinline__ unsigned ld_agent(const unsigned *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ void grid_barrier(unsigned *bar, unsigned target) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    atomicAdd(bar, 1u);
+    for (long it = 0; ld_agent(bar) < target && it < (1L << 26); it++) __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_fallback(ExhArgs E, VolArgs V) {
+  const unsigned nb = gridDim.x, b = blockIdx.x;
+  unsigned *bar = V.stuck_count + 4;           // counts[4], zeroed by k_run_init
+  if (ld_agent(V.tie_count) == 0 && ld_agent(V.stuck_count) == 0) return;
+  d_ties(V, b, nb);
+  grid_barrier(bar, nb);
+  if (ld_agent(V.stuck_count) == 0) return;
+  d_exh_find(E, b, nb);
+  grid_barrier(bar, 2 * nb);
+  d_exh_closest(E, 0, b, nb);
+  grid_barrier(bar, 3 * nb);
+  d_exh_closest(E, 1, b, nb);
+  grid_barrier(bar, 4 * nb);
+  d_exh_finish(E, V, b, nb);
+}
+
 // constant-size metric (MMG3D_Set_constantSize restated): all valid points
 __global__ __launch_bounds__(256) void k_const_metric(const int8_t *__restrict__ kind, int64_t nq,
                                                       double *__restrict__ out, int S, int off,
@@ -428,6 +473,26 @@ void launch_run_init(unsigned *counts, hipStream_t s) {
   hipLaunchKernelGGL(k_run_init, dim3(1), dim3(64), 0, s, counts);
 }
 
+__global__ __launch_bounds__(256) void k_prologue(uint8_t *wmask, int64_t n, unsigned *counts,
+                                                  int *grid, int64_t gcells) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
+  if (t < 8) counts[t] = 0;
+  const int64_t n16 = n / 16;
+  for (int64_t i = t; i < n16; i += st) reinterpret_cast<uint4 *>(wmask)[i] = make_uint4(0, 0, 0, 0);
+  for (int64_t i = n16 * 16 + t; i < n; i += st) wmask[i] = 0;
+  if (grid) {
+    const int64_t g4 = gcells / 4;
+    for (int64_t i = t; i < g4; i += st) reinterpret_cast<int4 *>(grid)[i] = make_int4(0, 0, 0, 0);
+    for (int64_t i = g4 * 4 + t; i < gcells; i += st) grid[i] = 0;
+  }
+}
+void launch_prologue(uint8_t *wmask, int64_t n, unsigned *counts, int *grid, int64_t gcells,
+                     hipStream_t s) {
+  int64_t work = std::max<int64_t>(n / 16, grid ? gcells / 4 : 0);
+  int64_t nb = std::min<int64_t>(std::max<int64_t>((work + 255) / 256, 1), 4096);
+  hipLaunchKernelGGL(k_prologue, dim3((unsigned)nb), dim3(256), 0, s, wmask, n, counts, grid, gcells);
+}
+
 void launch_hint_build(const int4 *tetv, const Pt4 *pts, int64_t ne, int stride, int *grid,
                        GridDesc g, hipStream_t s) {
   int64_t n = (ne + stride - 1) / stride;
@@ -450,11 +515,8 @@ void launch_exhaustive(const ExhArgs &e, const VolArgs &v, hipStream_t s) {
   int64_t nb = (e.ne + 255) / 256;
   if (nb > 2048) nb = 2048;
   if (nb < 1) nb = 1;
-  hipLaunchKernelGGL(k_ties, dim3(64), dim3(64), 0, s, v);
-  hipLaunchKernelGGL(k_exh_find, dim3((unsigned)nb), dim3(256), 0, s, e);
-  hipLaunchKernelGGL(k_exh_closest, dim3((unsigned)nb), dim3(256), 0, s, e, 0);
-  hipLaunchKernelGGL(k_exh_closest, dim3((unsigned)nb), dim3(256), 0, s, e, 1);
-  hipLaunchKernelGGL(k_exh_finish, dim3(64), dim3(256), 0, s, e, v);
+  (void)nb;
+  hipLaunchKernelGGL(k_fallback, dim3(FALLBACK_BLOCKS), dim3(256), 0, s, e, v);
 }
 void launch_const_metric(const int8_t *kind, int64_t nq, double *out, int S, int off, int size,
                          double hsiz, uint8_t *wmask, int imet, hipStream_t s) {

@@ -568,7 +568,9 @@ void launch_tria_normals(const TriRec *tris, const Pt4 *pts, int64_t nt, Pt4 *tr
   hipLaunchKernelGGL(k_tria_normals, dim3((unsigned)nb), dim3(256), 0, s, tris, pts, nt, trn);
 }
 
-#define BDY_CAP 32
+// surface walks are short (1.5 steps on C2): 8 private slots, the rare longer
+// walk is redone by k_locate_bdy_ovf with a global workspace
+#define BDY_CAP 8
 #define OVF_CAP 2048
 #define OVF_THREADS (64 * 64)
 

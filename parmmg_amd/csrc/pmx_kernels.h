@@ -31,8 +31,8 @@ struct VolArgs {
   int64_t nlist;
   uint4 *wstats;                // per-wave {located, sum steps, max, min}
   int max_walk;
-  unsigned const_bit;
-  int occ;                      // k_locate_vol register/occupancy variant           // wmask bit of a constant-size metric (0 if none)
+  unsigned const_bit;           // wmask bit of a constant-size metric (0 if none)
+  int occ;                      // k_locate_vol register/occupancy variant
   int xcd_swizzle;
 };
 

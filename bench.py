@@ -58,6 +58,24 @@ def alg_bytes(N: int, ne: int, np_: int, S: int) -> int:
     return N * (24 + 8 * S + 4) + ne * 32 + np_ * (24 + 8 * S)
 
 
+def profiled_traffic(config: str, kernel: str = "k_locate_vol"):
+    """HBM bytes per launch of the dominant kernel from the newest committed
+    rocprofv3 PMC summary of this config (tools/profile.sh ->
+    tools/prof_summary.py -> profiles/rNN_<config>_<tag>.json): 2*FETCH_SIZE +
+    WRITE_SIZE per MI355X_MICROARCH.md section HBM.  None if not profiled."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config.lower()}_*.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        for k, e in d.get("kernels", {}).items():
+            if k.split("<")[0] == kernel and e.get("traffic"):
+                return e["traffic"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def cpu_baseline(m, x, t, sols, budget_s: float = 20.0) -> dict:
     """The oracle (CPU restatement of the reference, sequential carry-over
     walk, one core) on the same workload: the whole step when it fits the
@@ -162,6 +180,7 @@ def main():
     B = alg_bytes(npts, m.ne, m.np, S)
     b_vol = B * nvol / npts
     achieved = b_vol / (k_ms["vol"] * 1e-3) / 1e9 if k_ms["vol"] > 0 else None
+    traffic, traffic_src = profiled_traffic(args.config)
 
     out = {
         "metric": "new vertices located+interpolated/sec",
@@ -182,7 +201,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "k_locate_vol",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                     "traffic": None,
+                     "traffic": traffic, "traffic_source": traffic_src,
                      "alg_bytes_per_launch": b_vol, "avg_launch_ms": k_ms["vol"]},
         "kernel_ms": k_ms,
         "step_alg_GBs": B / (ms * 1e-3) / 1e9,

@@ -19,6 +19,7 @@
 // full build, at ~0.5 extra walk step (r01 measurements)
 #define PMX_DEFAULT_HINT_STRIDE 4
 #define PMX_DEFAULT_VOL_OCC 1
+#define PMX_EV_PER_RUN 7
 
 static bool ok(pmx_ctx *c, hipError_t e, const char *what) {
   if (e == hipSuccess) return true;
@@ -59,6 +60,12 @@ pmx_ctx *pmx_create(int device) {
     return nullptr;
   }
   ctx->stream = ctx->own;
+  if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess) {
+    pmx_destroy(ctx);
+    return nullptr;
+  }
   return ctx;
 }
 
@@ -68,6 +75,10 @@ void pmx_destroy(pmx_ctx *ctx) {
   hipStreamSynchronize(ctx->stream);
   ctx->free_all();
   for (auto &e : ctx->events) hipEventDestroy(e);
+  if (ctx->side) hipStreamSynchronize(ctx->side);
+  if (ctx->ev_fork) hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_join) hipEventDestroy(ctx->ev_join);
+  if (ctx->side) hipStreamDestroy(ctx->side);
   if (ctx->own) hipStreamDestroy(ctx->own);
   delete ctx;
 }
@@ -220,6 +231,16 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   if (!dgrow(ctx, ctx->d_tetv, (size_t)(ne + 1))) return 0;
   CK(hipMemcpy2DAsync(ctx->d_tetv.p, sizeof(int4), ctx->d_tets.p, sizeof(TetRec), sizeof(int4),
                       (size_t)(ne + 1), hipMemcpyDeviceToDevice, ctx->stream));
+  // packed hint sample (the connectivity of every PMX_DEFAULT_HINT_STRIDE-th
+  // tet, contiguous): the per-step hint build streams ne/4 * 16 B instead of
+  // touching every line of the connectivity stream
+  {
+    const int64_t ns = (ne + PMX_DEFAULT_HINT_STRIDE - 1) / PMX_DEFAULT_HINT_STRIDE;
+    if (!dgrow(ctx, ctx->d_tets_s, (size_t)std::max<int64_t>(ns, 1))) return 0;
+    CK(hipMemcpy2DAsync(ctx->d_tets_s.p, sizeof(int4), ctx->d_tets.p + 1,
+                        sizeof(TetRec) * PMX_DEFAULT_HINT_STRIDE, sizeof(int4), (size_t)ns,
+                        hipMemcpyDeviceToDevice, ctx->stream));
+  }
   CK(hipMemcpyAsync(ctx->d_sol.p, hs.data(), hs.size() * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_tris.p, htr.data(), htr.size() * sizeof(TriRec), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_ntoff.p, ctx->h_ntoff.data(), ctx->h_ntoff.size() * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
@@ -290,6 +311,24 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
 
 // ---- the step ---------------------------------------------------------------
 
+static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &opts, VolArgs &A) {
+  A.pts = ctx->d_pts.p; A.tets = ctx->d_tets.p; A.sol = ctx->d_sol.p; A.sd = sd;
+  A.q = ctx->d_q.p; A.kind = ctx->d_kind.p; A.nq = ctx->nq; A.ne = ctx->ne;
+  A.grid = ctx->d_grid.p; A.g = ctx->grid;
+  A.out = ctx->d_out.p; A.wmask = ctx->d_wmask.p;
+  A.elem = ctx->d_elem.p; A.status = ctx->d_status.p; A.steps = ctx->d_steps.p;
+  A.start = ctx->d_start.p;
+  A.stuck_list = ctx->d_list.p; A.stuck_count = ctx->d_counts.p;
+  A.tie_list = ctx->d_ties.p; A.tie_count = ctx->d_counts.p + 3;
+  A.found = ctx->d_found.p; A.bestk = ctx->d_bestk.p; A.best = ctx->d_best.p;
+  A.list = ctx->d_vollist.p; A.nlist = ctx->nq_vol; A.wstats = ctx->d_vstat.p;
+  A.max_walk = opts.max_walk > 0 ? opts.max_walk : 512;
+  A.const_bit = sd.metric_const ? (1u << sd.imet) : 0u;
+  A.occ = (opts.tune & 0xF) ? (opts.tune & 0xF) : PMX_DEFAULT_VOL_OCC;
+  A.xcd_swizzle = 1;
+  A.inline_ties = (opts.tune & 0x4000) ? 0 : 1;   // tune bit 14: all ties to k_fallback
+}
+
 int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   if (!ctx) return 0;
   if (!ctx->have_bg || !ctx->have_pts) { ctx->err = "pmx_run: upload background and points first"; return 0; }
@@ -326,36 +365,59 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     const bool force_walk = (opts.tune & 0x100) != 0, force_tet = (opts.tune & 0x200) != 0;
     ctx->tet_mode = ctx->nq_vol > 0 && force_tet && !force_walk;
     (void)force_walk;
+    // surface path placement (tune bits 11/12): default = forked after the
+    // volume hint build (overlaps the walk, which is latency-bound and leaves
+    // issue slots; forking before the bandwidth-bound hint build slowed it by
+    // 40%: r01 sweep), 0x800 = serial on the main stream, 0x1000 = forked
+    // right after the prologue
+    const int bdy_mode = (opts.tune & 0x800) ? 1 : (opts.tune & 0x1000) ? 0 : 2;
+    VolArgs A{};
+    fill_vol_args(ctx, sd, opts, A);
+    if (ctx->nq_bdy && bdy_mode == 0) {
+      // fork: the surface locate (its own hint grid, walk, fallbacks) shares
+      // nothing with the volume path but the zeroed counters and masks
+      CK(hipEventRecord(ctx->ev_fork, st));
+      CK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+      if (ev) CK(hipEventRecord(ev[3], ctx->side));
+      if (!ctx->launch_bdy(A, opts, ctx->side)) return 0;
+      if (ev) CK(hipEventRecord(ev[5], ctx->side));
+      CK(hipEventRecord(ctx->ev_join, ctx->side));
+    }
     if (!ctx->tet_mode) {
       const int stride = opts.hint_stride > 0 ? opts.hint_stride : PMX_DEFAULT_HINT_STRIDE;
-      launch_hint_build(ctx->d_tetv.p, ctx->d_pts.p, ctx->ne, stride, ctx->d_grid.p, ctx->grid, st);
+      // tune bit 13: strided reads of the connectivity stream (r01 A/B)
+      const bool packed = stride == PMX_DEFAULT_HINT_STRIDE && !(opts.tune & 0x2000);
+      launch_hint_build(ctx->d_tetv.p, packed ? ctx->d_tets_s.p : nullptr, ctx->d_pts.p, ctx->ne,
+                        stride, ctx->d_grid.p, ctx->grid, st);
     }
     if (ev) CK(hipEventRecord(ev[1], st));
-    VolArgs A{};
-    A.pts = ctx->d_pts.p; A.tets = ctx->d_tets.p; A.sol = ctx->d_sol.p; A.sd = sd;
-    A.q = ctx->d_q.p; A.kind = ctx->d_kind.p; A.nq = n; A.ne = ctx->ne;
-    A.grid = ctx->d_grid.p; A.g = ctx->grid;
-    A.out = ctx->d_out.p; A.wmask = ctx->d_wmask.p;
-    A.elem = ctx->d_elem.p; A.status = ctx->d_status.p; A.steps = ctx->d_steps.p;
-    A.start = ctx->d_start.p;
-    A.stuck_list = ctx->d_list.p; A.stuck_count = ctx->d_counts.p;
-    A.tie_list = ctx->d_ties.p; A.tie_count = ctx->d_counts.p + 3;
-    A.found = ctx->d_found.p; A.bestk = ctx->d_bestk.p; A.best = ctx->d_best.p;
-    A.list = ctx->d_vollist.p; A.nlist = ctx->nq_vol; A.wstats = ctx->d_vstat.p;
-    A.max_walk = opts.max_walk > 0 ? opts.max_walk : 512;
-    A.const_bit = sd.metric_const ? (1u << sd.imet) : 0u;
-    A.occ = (opts.tune & 0xF) ? (opts.tune & 0xF) : PMX_DEFAULT_VOL_OCC;
-    A.xcd_swizzle = 1;
+    if (ctx->nq_bdy && bdy_mode == 2) {
+      CK(hipEventRecord(ctx->ev_fork, st));
+      CK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+      if (ev) CK(hipEventRecord(ev[3], ctx->side));
+      if (!ctx->launch_bdy(A, opts, ctx->side)) return 0;
+      if (ev) CK(hipEventRecord(ev[5], ctx->side));
+      CK(hipEventRecord(ctx->ev_join, ctx->side));
+    }
     if (ctx->tet_mode) {
       if (!ctx->launch_tet_locate(A, opts, st)) return 0;
     } else if (ctx->nq_vol) {
-      launch_locate_vol(A, st);
+      // tune bit 10: the r01 kernel k_locate_vol (A/B reference)
+      if (opts.tune & 0x400) launch_locate_vol(A, st);
+      else launch_walk(A, st);
     }
     if (ev) CK(hipEventRecord(ev[2], st));
-    if (ctx->nq_bdy) {
+    if (ctx->nq_bdy && bdy_mode != 1) {
+      CK(hipStreamWaitEvent(st, ctx->ev_join, 0));     // surface path done
+    } else if (ctx->nq_bdy) {
+      if (ev) CK(hipEventRecord(ev[3], st));
       if (!ctx->launch_bdy(A, opts, st)) return 0;
+      if (ev) CK(hipEventRecord(ev[5], st));
+    } else if (ev) {
+      CK(hipEventRecord(ev[3], st));
+      CK(hipEventRecord(ev[5], st));
     }
-    if (ev) CK(hipEventRecord(ev[3], st));
+    if (ev) CK(hipEventRecord(ev[6], st));
     ExhArgs E{};
     E.pts = ctx->d_pts.p; E.tets = ctx->d_tets.p; E.ne = ctx->ne; E.q = ctx->d_q.p;
     E.list = ctx->d_list.p; E.count = ctx->d_counts.p; E.found = ctx->d_found.p;
@@ -363,7 +425,7 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     if (ctx->nq_vol) launch_exhaustive(E, A, st);
     if (ev) CK(hipEventRecord(ev[4], st));
   } else if (ev) {
-    for (int k = 1; k < 5; k++) CK(hipEventRecord(ev[k], st));
+    for (int k = 1; k < PMX_EV_PER_RUN; k++) CK(hipEventRecord(ev[k], st));
   }
   CK(hipGetLastError());
   ctx->ran = true;
@@ -481,10 +543,12 @@ double pmx_kernel_ms(pmx_ctx *ctx, int which) {
   hipStreamSynchronize(ctx->stream);
   double tot = 0.0;
   for (int r = 0; r < ctx->ev_used; r++) {
-    hipEvent_t *e = &ctx->events[(size_t)r * 5];
+    hipEvent_t *e = &ctx->events[(size_t)r * PMX_EV_PER_RUN];
     float ms = 0.f;
-    if (which == 4) hipEventElapsedTime(&ms, e[0], e[4]);
-    else hipEventElapsedTime(&ms, e[which], e[which + 1]);
+    // events: 0 start, 1 hint built, 2 volume walk done, 3/5 surface path
+    // start/end (side stream), 6 joined, 4 end
+    static const int from[5] = {0, 1, 3, 6, 0}, to[5] = {1, 2, 5, 4, 4};
+    hipEventElapsedTime(&ms, e[from[which]], e[to[which]]);
     tot += ms;
   }
   return tot / ctx->ev_used;
@@ -495,13 +559,13 @@ double pmx_kernel_ms(pmx_ctx *ctx, int which) {
 // ---- pmx_ctx members ----------------------------------------------------------
 
 hipEvent_t *pmx_ctx::next_event_slot() {
-  size_t need = (size_t)(ev_used + 1) * 5;
+  size_t need = (size_t)(ev_used + 1) * PMX_EV_PER_RUN;
   while (events.size() < need) {
     hipEvent_t e;
     hipEventCreate(&e);
     events.push_back(e);
   }
-  hipEvent_t *r = &events[(size_t)ev_used * 5];
+  hipEvent_t *r = &events[(size_t)ev_used * PMX_EV_PER_RUN];
   ev_used++;
   return r;
 }

@@ -14,6 +14,10 @@ template <class T> struct DevBuf {
 struct pmx_ctx {
   int device = 0;
   hipStream_t own = nullptr, stream = nullptr;
+  // the surface path runs on `side`, forked after the prologue and joined
+  // before the fallback: it overlaps the volume hint build and walk
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::string err;
 
   // background group
@@ -46,6 +50,7 @@ struct pmx_ctx {
   DevBuf<int2> d_ties;
   // tet-centric volume path
   DevBuf<int4> d_tetv;                  // connectivity stream (16 B / tet)
+  DevBuf<int4> d_tets_s;                // packed sample: tets 1, 1+S, 1+2S.. (S = hint stride)
   DevBuf<unsigned> d_qcnt, d_qstart;
   DevBuf<int> d_qcell, d_qslot, d_tbest;
   DevBuf<Pt4> d_qs;

@@ -34,6 +34,7 @@ struct VolArgs {
   unsigned const_bit;           // wmask bit of a constant-size metric (0 if none)
   int occ;                      // k_locate_vol register/occupancy variant
   int xcd_swizzle;
+  int inline_ties;               // k_walk: resolve face ties in place
 };
 
 struct ExhArgs {
@@ -48,9 +49,10 @@ struct ExhArgs {
   int *bestk;
 };
 
-void launch_hint_build(const int4 *tetv, const Pt4 *pts, int64_t ne, int stride, int *grid,
-                       GridDesc g, hipStream_t s);
+void launch_hint_build(const int4 *tetv, const int4 *packed, const Pt4 *pts, int64_t ne,
+                       int stride, int *grid, GridDesc g, hipStream_t s);
 void launch_locate_vol(const VolArgs &a, hipStream_t s);
+void launch_walk(const VolArgs &a, hipStream_t s);
 void launch_exhaustive(const ExhArgs &e, const VolArgs &v, hipStream_t s);
 void launch_const_metric(const int8_t *kind, int64_t nq, double *out, int S, int off, int size,
                          double hsiz, uint8_t *wmask, int imet, hipStream_t s);

@@ -72,7 +72,7 @@ __device__ int hint_lookup(const int *grid, const GridDesc &g, D3 p) {
   return 1;
 }
 
-__global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ tetv,
+__global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ src, int64_t sstride,
                                                     const Pt4 *__restrict__ pts, int64_t ne,
                                                     int stride, int *__restrict__ grid,
                                                     GridDesc g) {
@@ -80,7 +80,9 @@ __global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ tet
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n;
        t += (int64_t)gridDim.x * blockDim.x) {
     int64_t k = 1 + t * stride;
-    int4 v = tetv[k];                 // 16-B connectivity stream, not the 32-B record
+    // sampled tet k: from the packed sample stream (sstride 1, coalesced) or
+    // from every stride-th record of the 16-B connectivity stream
+    int4 v = src[t * sstride];
     if (v.x <= 0) continue;
     D3 a = ld3(pts, v.x), b = ld3(pts, v.y), c = ld3(pts, v.z), d = ld3(pts, v.w);
     D3 m{(a.x + b.x + c.x + d.x) * 0.25, (a.y + b.y + c.y + d.y) * 0.25,
@@ -493,14 +495,16 @@ void launch_prologue(uint8_t *wmask, int64_t n, unsigned *counts, int *grid, int
   hipLaunchKernelGGL(k_prologue, dim3((unsigned)nb), dim3(256), 0, s, wmask, n, counts, grid, gcells);
 }
 
-void launch_hint_build(const int4 *tetv, const Pt4 *pts, int64_t ne, int stride, int *grid,
-                       GridDesc g, hipStream_t s) {
+void launch_hint_build(const int4 *tetv, const int4 *packed, const Pt4 *pts, int64_t ne,
+                       int stride, int *grid, GridDesc g, hipStream_t s) {
   int64_t n = (ne + stride - 1) / stride;
   int64_t nb = (n + 255) / 256;
   if (nb > 65536) nb = 65536;
   if (nb < 1) nb = 1;
-  hipLaunchKernelGGL(k_hint_build, dim3((unsigned)nb), dim3(256), 0, s, tetv, pts, ne, stride,
-                     grid, g);
+  const int4 *src = packed ? packed : tetv + 1;
+  const int64_t sstride = packed ? 1 : stride;
+  hipLaunchKernelGGL(k_hint_build, dim3((unsigned)nb), dim3(256), 0, s, src, sstride, pts, ne,
+                     stride, grid, g);
 }
 void launch_locate_vol(const VolArgs &a, hipStream_t s) {
   int64_t nb = (a.nlist + 255) / 256;

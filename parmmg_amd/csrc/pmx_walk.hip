@@ -1,0 +1,367 @@
+// pmx_walk.hip -- the production volume kernel: k_walk (locate + interpolate).
+//
+// Same contract as k_locate_vol (pmx_kernels.hip): one thread per new volume
+// vertex, adjacency walk from the hint grid (PMMG_locatePointVol, reference
+// src/locate_pmmg.c:786-883), fused PMMG_interp4bar_{iso,ani}
+// (src/interpmesh_pmmg.c:206-270), stuck lanes and near-face ties compacted
+// into lists for k_fallback.  The located tet, its barycentrics and the fields
+// are bit-identical to k_locate_vol's; what changes is the cost of a step:
+//
+//  * direction without divisions: a walk step only needs the ORDER of the
+//    barycentrics and the sign test lambda_min > -1e-6.  lambda_f = -num_f/vol
+//    (src/barycoord_pmmg.c:238-257) is ranked through -num_f * (1/vol) (one
+//    division instead of four, <= 2 ulp from the quotient); when that
+//    estimate comes within 1e-13 of the threshold the four exact quotients
+//    are formed and decide, so "found" and the barycentrics used for the
+//    interpolation are exactly the reference's.  The path may differ from a
+//    walk ranked on exact quotients only where two barycentrics are within
+//    2 ulp of each other; the answer does not depend on the path (unique
+//    containing tet, or the canonical min-index tet of a tie -- k_ties).
+//  * vertex reuse: the next tet shares a face (3 vertices) with the current
+//    one; only its opposite vertex is gathered (1 instead of 4 32-B gathers
+//    per step after the first), the shared coordinates are permuted in VGPRs.
+//  * layout specialisation: the interpolation is compiled for the solution
+//    layout (one anisotropic metric; S isotropic/vector components; generic)
+//    so the register allocation is not the maximum over every layout.
+#include "pmx_device.h"
+#include "pmx_kernels.h"
+
+#define WALK_RING 4
+#define TIE_NEAR 1.e-5
+#define APPROX_GUARD 1.e-13
+
+__device__ __forceinline__ int64_t walk_xcd_remap(int64_t b, int64_t nb) {
+  // blocks b and b+8 share an XCD (round-robin dispatch): each XCD gets a
+  // contiguous range of the Morton-ordered queries so its L2 sees neighbours
+  int64_t xcd = b & 7, r = b >> 3, q = nb >> 3, rem = nb & 7;
+  return (xcd < rem) ? xcd * (q + 1) + r : rem * (q + 1) + (xcd - rem) * q + r;
+}
+
+__device__ __forceinline__ int wclamp(double t, int n) {
+  if (!(t > 0.0)) return 0;                 // also catches NaN
+  if (t >= (double)(n - 1)) return n - 1;
+  return (int)t;
+}
+
+// empty hint cell: nearest non-empty cell in growing shells (rare; kept out of
+// line so that its loops do not inflate the walk's register allocation)
+__device__ __noinline__ int hint_search(const int *grid, int gx, int gy, int gz, int cx, int cy,
+                                        int cz) {
+  for (int r = 1; r <= 3; r++) {
+    for (int dz = -r; dz <= r; dz++)
+      for (int dy = -r; dy <= r; dy++)
+        for (int dx = -r; dx <= r; dx++) {
+          if (max(abs(dx), max(abs(dy), abs(dz))) != r) continue;
+          int x = cx + dx, y = cy + dy, z = cz + dz;
+          if (x < 0 || y < 0 || z < 0 || x >= gx || y >= gy || z >= gz) continue;
+          int kk = grid[(int64_t)x + (int64_t)gx * ((int64_t)y + (int64_t)gy * z)];
+          if (kk) return kk;
+        }
+  }
+  return 1;
+}
+
+__device__ __forceinline__ int walk_hint(const int *grid, const GridDesc &g, D3 p) {
+  int cx = wclamp((p.x - g.lo[0]) * g.inv[0], g.dim[0]);
+  int cy = wclamp((p.y - g.lo[1]) * g.inv[1], g.dim[1]);
+  int cz = wclamp((p.z - g.lo[2]) * g.inv[2], g.dim[2]);
+  int k = grid[(int64_t)cx + (int64_t)g.dim[0] * ((int64_t)cy + (int64_t)g.dim[1] * cz)];
+  return k ? k : hint_search(grid, g.dim[0], g.dim[1], g.dim[2], cx, cy, cz);
+}
+
+// numerators of the barycentrics: lambda_f = -num_f / vol, with exactly the
+// operations of tet_lambda (pmx_device.h) before its division
+__device__ __forceinline__ void face_nums(const D3 P[4], D3 p, double num[4], double *volp) {
+  double vol = orvol(P[0], P[1], P[2], P[3]);
+  D3 n0 = nonunit_normal(P[1], P[2], P[3]);
+  D3 n1 = nonunit_normal(P[0], P[3], P[2]);
+  D3 n2 = nonunit_normal(P[0], P[1], P[3]);
+  D3 n3 = nonunit_normal(P[0], P[2], P[1]);
+  num[0] = (p.x - P[1].x) * n0.x + (p.y - P[1].y) * n0.y + (p.z - P[1].z) * n0.z;
+  num[1] = (p.x - P[0].x) * n1.x + (p.y - P[0].y) * n1.y + (p.z - P[0].z) * n1.z;
+  num[2] = (p.x - P[0].x) * n2.x + (p.y - P[0].y) * n2.y + (p.z - P[0].z) * n2.z;
+  num[3] = (p.x - P[0].x) * n3.x + (p.y - P[0].y) * n3.y + (p.z - P[0].z) * n3.z;
+  *volp = vol;
+}
+
+__device__ __forceinline__ void wranks(const double l[4], int rk[4]) {
+  rk[0] = rk[1] = rk[2] = rk[3] = 0;
+#pragma unroll
+  for (int a = 0; a < 4; a++)
+#pragma unroll
+    for (int b = a + 1; b < 4; b++) {
+      bool bfirst = l[b] < l[a];          // stable: b after a unless strictly smaller
+      rk[a] += bfirst ? 1 : 0;
+      rk[b] += bfirst ? 0 : 1;
+    }
+}
+
+__device__ __forceinline__ void wave_stats_w(uint4 *rec, unsigned cnt, unsigned sum, unsigned mx,
+                                             unsigned mn) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += __shfl_xor(cnt, o, 64);
+    sum += __shfl_xor(sum, o, 64);
+    unsigned a = __shfl_xor(mx, o, 64), b = __shfl_xor(mn, o, 64);
+    mx = a > mx ? a : mx;
+    mn = b < mn ? b : mn;
+  }
+  if ((threadIdx.x & 63) == 0) *rec = make_uint4(cnt, sum, mx, mn);
+}
+
+// a[i] for a 4-array held in registers: masked OR (a select chain is turned
+// back into an indexed private-array load, i.e. scratch, by the compiler)
+__device__ __forceinline__ int pick4(const int a[4], int i) {
+  return (a[0] & -(int)(i == 0)) | (a[1] & -(int)(i == 1)) | (a[2] & -(int)(i == 2)) |
+         (a[3] & -(int)(i == 3));
+}
+
+__device__ __forceinline__ D3 dsel(bool c, D3 a, D3 b) {
+  return D3{c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z};
+}
+
+// ---- layout-specialised interpolation --------------------------------------
+//
+// LAYOUT_ANI: one solution, the 6-component metric (C2): interp4bar_ani.
+// LAYOUT_ISO: every solution of size 1 or 3 and no constant metric: a row of
+//             S doubles per vertex, out_j = ((0 + phi0 a0j) + phi1 a1j) ...
+//             (interp4bar_iso, src/interpmesh_pmmg.c:206-230, order kept).
+// LAYOUT_GEN: interp_bar<4> of pmx_device.h.
+enum { LAYOUT_GEN = 0, LAYOUT_ANI = 1, LAYOUT_ISO = 2 };
+
+template <int LAYOUT, int S>
+__device__ __forceinline__ unsigned interp_layout(const double *__restrict__ sol, const SolDesc &sd,
+                                                  const int *v, const double *phi,
+                                                  double *__restrict__ out) {
+  if constexpr (LAYOUT == LAYOUT_ANI) {
+    double mint[6], r[6];
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const double2 *m = reinterpret_cast<const double2 *>(sol + (int64_t)v[i] * 6);
+      double2 a = m[0], b = m[1], c = m[2];
+      double mm[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+      double mi[6];
+      ok = ok && invmat(mm, mi);
+#pragma unroll
+      for (int j = 0; j < 6; j++) mint[j] = (i == 0) ? phi[i] * mi[j] : mint[j] + phi[i] * mi[j];
+    }
+    if (!ok || !invmat(mint, r)) return 0u;
+    double2 *o = reinterpret_cast<double2 *>(out);
+    o[0] = make_double2(r[0], r[1]);
+    o[1] = make_double2(r[2], r[3]);
+    o[2] = make_double2(r[4], r[5]);
+    return 1u;
+  } else if constexpr (LAYOUT == LAYOUT_ISO) {
+    double acc[S];
+#pragma unroll
+    for (int j = 0; j < S; j++) acc[j] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const double *row = sol + (int64_t)v[i] * S;
+#pragma unroll
+      for (int j = 0; j < S; j++) acc[j] += phi[i] * row[j];
+    }
+#pragma unroll
+    for (int j = 0; j < S; j++) out[j] = acc[j];
+    return (1u << sd.nsol) - 1u;
+  } else {
+    return interp_bar<4>(sol, sd, v, phi, out);
+  }
+}
+
+// Near-face cases of the canonical tie rule resolved in place (canonical_tet,
+// pmx_kernels.hip, is the general BFS over the containing set; this is the
+// same rule for the two shapes that make up almost every tie):
+//  * no near face has an interior neighbour: the set is {cur};
+//  * exactly one near face f with neighbour n: the set is {cur} if n does not
+//    contain p, {cur, n} if it does and n has no further near face with an
+//    interior neighbour other than cur -> min(cur, n).
+// Returns true when the general BFS is needed (edge / vertex ties, chains).
+// On return false, cur/t/lam hold the canonical tet and its barycentrics.
+__device__ __forceinline__ bool face_tie(const VolArgs &A, D3 p, int &cur, TetRec &t, double lam[4]) {
+  int nnear = 0, f1 = 0;
+#pragma unroll
+  for (int f = 0; f < 4; f++) {
+    const bool nf = t.nb[f] != 0 && lam[f] < TIE_NEAR;
+    nnear += nf ? 1 : 0;
+    f1 = nf ? f : f1;
+  }
+  if (nnear == 0) return false;
+  if (nnear > 1) return true;
+  const int n = pick4(t.nb, f1);
+  const TetRec u = A.tets[n];
+  if (u.v[0] <= 0) return false;
+  const D3 Q[4] = {ld3(A.pts, u.v[0]), ld3(A.pts, u.v[1]), ld3(A.pts, u.v[2]), ld3(A.pts, u.v[3])};
+  double mu[4], vu;
+  tet_lambda(Q, p, mu, &vu);
+  if (!(fmin(fmin(mu[0], mu[1]), fmin(mu[2], mu[3])) > -PMX_EPS)) return false;
+  bool more = false;
+#pragma unroll
+  for (int g = 0; g < 4; g++) more |= (u.nb[g] != 0 && u.nb[g] != cur && mu[g] < TIE_NEAR);
+  if (more) return true;
+  if (n < cur) {
+    cur = n;
+    t = u;
+#pragma unroll
+    for (int f = 0; f < 4; f++) lam[f] = mu[f];
+  }
+  return false;
+}
+
+template <int LAYOUT, int S, bool TIES>
+__global__ __launch_bounds__(256) void k_walk(VolArgs A) {
+  const int64_t b = walk_xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t j = b * blockDim.x + threadIdx.x;
+  unsigned s_cnt = 0, s_sum = 0, s_max = 0, s_min = 0xffffffffu;
+
+  if (j < A.nlist) {
+    const int64_t i = A.list[j];
+    const Pt4 qq = A.q[i];
+    const D3 p{qq.x, qq.y, qq.z};
+    int cur = walk_hint(A.grid, A.g, p);
+    A.start[i] = cur;
+    int ring[WALK_RING];
+#pragma unroll
+    for (int r = 0; r < WALK_RING; r++) ring[r] = 0;
+    int step = 0;
+    bool found = false;
+    TetRec t = A.tets[cur];
+    D3 P[4];
+    double lam[4];
+    if (t.v[0] <= 0) step = 1;                        // !MG_EOK start: let the scan decide
+    else {
+      P[0] = ld3(A.pts, t.v[0]); P[1] = ld3(A.pts, t.v[1]);
+      P[2] = ld3(A.pts, t.v[2]); P[3] = ld3(A.pts, t.v[3]);
+      for (;;) {
+        step++;
+        double num[4], vol;
+        face_nums(P, p, num, &vol);
+        const double rv = 1.0 / vol;
+#pragma unroll
+        for (int f = 0; f < 4; f++) lam[f] = -(num[f] * rv);
+        double lmin = fmin(fmin(lam[0], lam[1]), fmin(lam[2], lam[3]));
+        if (lmin > -PMX_EPS - APPROX_GUARD) {
+          // near or inside: the reference's quotients decide
+#pragma unroll
+          for (int f = 0; f < 4; f++) lam[f] = -num[f] / vol;
+          lmin = fmin(fmin(lam[0], lam[1]), fmin(lam[2], lam[3]));
+          if (lmin > -PMX_EPS) { found = true; break; }     // src/barycoord_pmmg.c:102-107
+        }
+        if (step >= A.max_walk) break;
+        int rk[4];
+        wranks(lam, rk);
+#pragma unroll
+        for (int r = WALK_RING - 1; r > 0; r--) ring[r] = ring[r - 1];
+        ring[0] = cur;
+        // first interior, not recently visited neighbour in ascending-lambda
+        // order (src/locate_pmmg.c:819-833)
+        int next = 0;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          int f = (rk[0] == r) ? 0 : (rk[1] == r) ? 1 : (rk[2] == r) ? 2 : 3;
+          int nb = pick4(t.nb, f);
+          bool seen = false;
+#pragma unroll
+          for (int q = 0; q < WALK_RING; q++) seen |= (ring[q] == nb);
+          if (!next && nb && !seen) next = nb;
+        }
+        if (!next) break;
+        const TetRec u = A.tets[next];
+        cur = next;
+        if (u.v[0] <= 0) { t = u; break; }                  // !MG_EOK: let the scan decide
+        // shared face: permute the known coordinates, gather the new vertex
+        bool m[4][4];
+        int nnew = 0, lnew = 0;
+#pragma unroll
+        for (int l = 0; l < 4; l++) {
+#pragma unroll
+          for (int k = 0; k < 4; k++) m[l][k] = (u.v[l] == t.v[k]);
+          bool any = m[l][0] | m[l][1] | m[l][2] | m[l][3];
+          nnew += any ? 0 : 1;
+          lnew = any ? lnew : l;
+        }
+        if (nnew == 1) {
+          const D3 pn = ld3(A.pts, pick4(u.v, lnew));
+          D3 Q[4];
+#pragma unroll
+          for (int l = 0; l < 4; l++)
+            Q[l] = dsel(m[l][0], P[0], dsel(m[l][1], P[1], dsel(m[l][2], P[2], dsel(m[l][3], P[3], pn))));
+#pragma unroll
+          for (int l = 0; l < 4; l++) P[l] = Q[l];
+        } else {                                               // inconsistent adjacency
+          P[0] = ld3(A.pts, u.v[0]); P[1] = ld3(A.pts, u.v[1]);
+          P[2] = ld3(A.pts, u.v[2]); P[3] = ld3(A.pts, u.v[3]);
+        }
+        t = u;
+      }
+    }
+    if (found) {
+      double lmn = fmin(fmin(lam[0], lam[1]), fmin(lam[2], lam[3]));
+      if (lmn < TIE_NEAR && (!TIES || face_tie(A, p, cur, t, lam))) {
+        // within the tolerance of several tets: canonical tet by k_ties
+        unsigned slot = atomicAdd(A.tie_count, 1u);
+        A.tie_list[slot] = make_int2((int)i, cur);
+        A.steps[i] = step;
+        found = false;
+        step = -1;
+      }
+    }
+    if (found) {
+      A.elem[i] = cur;
+      A.status[i] = 1;
+      A.steps[i] = step;
+      const int v[4] = {t.v[0], t.v[1], t.v[2], t.v[3]};
+      unsigned wm = interp_layout<LAYOUT, S>(A.sol, A.sd, v, lam, A.out + i * A.sd.S);
+      A.wmask[i] = (uint8_t)(wm | A.const_bit);
+      s_cnt = 1; s_sum = step; s_max = step; s_min = step;
+    } else if (step >= 0) {
+      unsigned slot = atomicAdd(A.stuck_count, 1u);
+      A.stuck_list[slot] = (int)i;
+      A.found[slot] = 0x7fffffff;
+      A.bestk[slot] = 0x7fffffff;
+      A.best[slot] = ~0ull;
+      A.steps[i] = -step;
+    }
+  }
+  wave_stats_w(A.wstats + (b * blockDim.x + threadIdx.x) / 64, s_cnt, s_sum, s_max, s_min);
+}
+
+// layout of the solutions for the walk kernel
+static int walk_layout(const SolDesc &sd, int *S) {
+  *S = sd.S;
+  if (sd.nsol == 1 && sd.size[0] == 6 && sd.imet == 0 && !sd.metric_const) return LAYOUT_ANI;
+  bool iso = !sd.metric_const && sd.S >= 1 && sd.S <= 8;
+  for (int s = 0; s < sd.nsol; s++) iso = iso && sd.size[s] != 6;
+  return iso ? LAYOUT_ISO : LAYOUT_GEN;
+}
+
+template <int LAYOUT, int S>
+static void launch_walk_t(const VolArgs &a, int ties, int64_t nb, hipStream_t s) {
+  if (ties)
+    hipLaunchKernelGGL((k_walk<LAYOUT, S, true>), dim3((unsigned)nb), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_walk<LAYOUT, S, false>), dim3((unsigned)nb), dim3(256), 0, s, a);
+}
+
+void launch_walk(const VolArgs &a, hipStream_t s) {
+  const int64_t nb = (a.nlist + 255) / 256;
+  if (nb < 1) return;
+  int S = 0;
+  const int lay = walk_layout(a.sd, &S);
+  const int ties = a.inline_ties;
+  if (lay == LAYOUT_ANI) return launch_walk_t<LAYOUT_ANI, 6>(a, ties, nb, s);
+  if (lay == LAYOUT_ISO) {
+    switch (S) {
+      case 1: return launch_walk_t<LAYOUT_ISO, 1>(a, ties, nb, s);
+      case 2: return launch_walk_t<LAYOUT_ISO, 2>(a, ties, nb, s);
+      case 3: return launch_walk_t<LAYOUT_ISO, 3>(a, ties, nb, s);
+      case 4: return launch_walk_t<LAYOUT_ISO, 4>(a, ties, nb, s);
+      case 5: return launch_walk_t<LAYOUT_ISO, 5>(a, ties, nb, s);
+      case 6: return launch_walk_t<LAYOUT_ISO, 6>(a, ties, nb, s);
+      case 7: return launch_walk_t<LAYOUT_ISO, 7>(a, ties, nb, s);
+      default: return launch_walk_t<LAYOUT_ISO, 8>(a, ties, nb, s);
+    }
+  }
+  launch_walk_t<LAYOUT_GEN, 0>(a, ties, nb, s);
+}

@@ -19,6 +19,9 @@ from parmmg_amd import mesh as M
 pytestmark = pytest.mark.gpu
 
 WALK, TET = 0x100, 0x200      # pmx_run_opts.tune: force the volume walk / tet-centric path
+R01 = 0x400                   # the r01 walk kernel k_locate_vol instead of k_walk
+SERIAL_BDY = 0x800            # surface path on the main stream (no fork)
+NOTIES = 0x4000               # k_walk: every near-face point to the k_ties BFS
 
 
 def run_gpu(tr, m, x, t, sols, imet=0, hsiz=0.0, init=None, tune=0):
@@ -31,7 +34,9 @@ def run_gpu(tr, m, x, t, sols, imet=0, hsiz=0.0, init=None, tune=0):
 
 
 @pytest.mark.parametrize("metric,n,tune", [("iso", 10, 0), ("ani", 9, 0), ("none", 7, 0),
-                                           ("iso", 10, WALK), ("ani", 9, WALK), ("ani", 9, TET)])
+                                           ("iso", 10, WALK), ("ani", 9, WALK), ("ani", 9, TET),
+                                           ("ani", 9, R01), ("iso", 10, R01 | SERIAL_BDY),
+                                           ("iso", 10, NOTIES)])
 def test_volume_parity(transfer, metric, n, tune):
     m, x, t, sols = cube_case(n, metric=metric, surface=False)
     imet = 0 if metric != "none" else -1
@@ -270,7 +275,7 @@ def test_walk_and_stream_agree(transfer, case):
         assert bits_equal(a.sols[s][vol], b.sols[s][vol]).all()
 
 
-@pytest.mark.parametrize("tune", [WALK, TET])
+@pytest.mark.parametrize("tune", [WALK, WALK | NOTIES, WALK | R01, TET])
 def test_tie_points_canonical(transfer, tune):
     """Old vertices, edge midpoints and face centroids (the tie suite of
     SURVEY.md 8(d)): the device returns the smallest index among all tets

@@ -126,6 +126,9 @@ int pmx_locate_stats_get(pmx_ctx *ctx, pmx_locate_stats *st);
 /* Device pointers of the resident result buffers (for collectives / chaining):
  * which = 0 packed solutions [npts][S], 1 elem, 2 status. */
 void *pmx_device_buffer(pmx_ctx *ctx, int which);
+/* Inspection: copy the volume hint grid of the last run to host (cap cells);
+ * returns the number of cells (0 on error). */
+int64_t pmx_debug_hint_grid(pmx_ctx *ctx, int *host, int64_t cap);
 
 /* Kernel timing of the last pmx_run with opts.timing != 0, in ms:
  * which = 0 hint build, 1 volume locate+interp, 2 surface locate+interp,

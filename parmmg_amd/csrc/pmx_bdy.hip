@@ -600,7 +600,9 @@ bool pmx_ctx::launch_bdy(const VolArgs &a, const pmx_run_opts &o, hipStream_t s)
   area = 2.0 * (ext[0] * ext[1] + ext[1] * ext[2] + ext[0] * ext[2]);
   double h = std::sqrt(area / std::max(1.0, (double)nt / 2.0));
   for (int ax = 0; ax < 3; ax++) {
-    int d = (int)std::ceil(ext[ax] / h);
+    // 1e-9 slack: libm cbrt/sqrt are not correctly rounded and a cell count
+    // of exactly n must not become n+1 (misaligned with a lattice-like mesh)
+    int d = (int)std::ceil(ext[ax] / h * (1.0 - 1e-9));
     d = std::max(1, std::min(d, 1024));
     tg.dim[ax] = d;
     tg.lo[ax] = bblo[ax];

@@ -206,7 +206,10 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   GridDesc g;
   int64_t cells = 1;
   for (int a = 0; a < 3; a++) {
-    int d = (int)std::ceil(ext[a] / h);
+    // 1e-9 slack: libm cbrt is not correctly rounded, and 255.00000000000003
+    // cells must stay 255 (r01: C3 got 256 per axis, misaligned with the
+    // mesh: 10% empty cells, 0.73 instead of 0.44 cells start distance)
+    int d = (int)std::ceil(ext[a] / h * (1.0 - 1e-9));
     d = std::max(1, std::min(d, 4096));
     g.dim[a] = d;
     g.lo[a] = lo[a];
@@ -229,17 +232,14 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   CK(hipMemcpyAsync(ctx->d_tets.p, ht.data(), ht.size() * sizeof(TetRec), hipMemcpyHostToDevice, ctx->stream));
   // connectivity-only stream for the tet-centric pass (16 of the 32 B)
   if (!dgrow(ctx, ctx->d_tetv, (size_t)(ne + 1))) return 0;
-  CK(hipMemcpy2DAsync(ctx->d_tetv.p, sizeof(int4), ctx->d_tets.p, sizeof(TetRec), sizeof(int4),
-                      (size_t)(ne + 1), hipMemcpyDeviceToDevice, ctx->stream));
+  launch_tet_conn(ctx->d_tets.p, 1, ne + 1, ctx->d_tetv.p, ctx->stream);
   // packed hint sample (the connectivity of every PMX_DEFAULT_HINT_STRIDE-th
   // tet, contiguous): the per-step hint build streams ne/4 * 16 B instead of
   // touching every line of the connectivity stream
   {
     const int64_t ns = (ne + PMX_DEFAULT_HINT_STRIDE - 1) / PMX_DEFAULT_HINT_STRIDE;
     if (!dgrow(ctx, ctx->d_tets_s, (size_t)std::max<int64_t>(ns, 1))) return 0;
-    CK(hipMemcpy2DAsync(ctx->d_tets_s.p, sizeof(int4), ctx->d_tets.p + 1,
-                        sizeof(TetRec) * PMX_DEFAULT_HINT_STRIDE, sizeof(int4), (size_t)ns,
-                        hipMemcpyDeviceToDevice, ctx->stream));
+    launch_tet_conn(ctx->d_tets.p + 1, PMX_DEFAULT_HINT_STRIDE, ns, ctx->d_tets_s.p, ctx->stream);
   }
   CK(hipMemcpyAsync(ctx->d_sol.p, hs.data(), hs.size() * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_tris.p, htr.data(), htr.size() * sizeof(TriRec), hipMemcpyHostToDevice, ctx->stream));
@@ -388,7 +388,7 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
       // tune bit 13: strided reads of the connectivity stream (r01 A/B)
       const bool packed = stride == PMX_DEFAULT_HINT_STRIDE && !(opts.tune & 0x2000);
       launch_hint_build(ctx->d_tetv.p, packed ? ctx->d_tets_s.p : nullptr, ctx->d_pts.p, ctx->ne,
-                        stride, ctx->d_grid.p, ctx->grid, st);
+                        stride, ctx->d_grid.p, ctx->grid, (opts.tune & 0x8000) ? 1 : 0, st);
     }
     if (ev) CK(hipEventRecord(ev[1], st));
     if (ctx->nq_bdy && bdy_mode == 2) {
@@ -530,6 +530,15 @@ void *pmx_device_buffer(pmx_ctx *ctx, int which) {
     case 2: return ctx->d_status.p;
     default: return nullptr;
   }
+}
+
+int64_t pmx_debug_hint_grid(pmx_ctx *ctx, int *host, int64_t cap) {
+  if (!ctx || !ctx->ran || !host) return 0;
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return 0;
+  const int64_t n = std::min<int64_t>(cap, ctx->gcells);
+  if (hipMemcpy(host, ctx->d_grid.p, sizeof(int) * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess)
+    return 0;
+  return ctx->gcells;
 }
 
 int pmx_timing_reset(pmx_ctx *ctx) {

@@ -50,9 +50,10 @@ struct ExhArgs {
 };
 
 void launch_hint_build(const int4 *tetv, const int4 *packed, const Pt4 *pts, int64_t ne,
-                       int stride, int *grid, GridDesc g, hipStream_t s);
+                       int stride, int *grid, GridDesc g, int mid, hipStream_t s);
 void launch_locate_vol(const VolArgs &a, hipStream_t s);
 void launch_walk(const VolArgs &a, hipStream_t s);
+void launch_tet_conn(const TetRec *src, int64_t stride, int64_t n, int4 *dst, hipStream_t s);
 void launch_exhaustive(const ExhArgs &e, const VolArgs &v, hipStream_t s);
 void launch_const_metric(const int8_t *kind, int64_t nq, double *out, int S, int off, int size,
                          double hsiz, uint8_t *wmask, int imet, hipStream_t s);

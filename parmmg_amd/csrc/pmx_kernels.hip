@@ -72,27 +72,51 @@ __device__ int hint_lookup(const int *grid, const GridDesc &g, D3 p) {
   return 1;
 }
 
+template <bool MID>
 __global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ src, int64_t sstride,
                                                     const Pt4 *__restrict__ pts, int64_t ne,
                                                     int stride, int *__restrict__ grid,
                                                     GridDesc g) {
-  int64_t n = (ne + stride - 1) / stride;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    int64_t k = 1 + t * stride;
-    // sampled tet k: from the packed sample stream (sstride 1, coalesced) or
-    // from every stride-th record of the 16-B connectivity stream
-    int4 v = src[t * sstride];
-    if (v.x <= 0) continue;
-    D3 a = ld3(pts, v.x), b = ld3(pts, v.y), c = ld3(pts, v.z), d = ld3(pts, v.w);
-    D3 m{(a.x + b.x + c.x + d.x) * 0.25, (a.y + b.y + c.y + d.y) * 0.25,
-         (a.z + b.z + c.z + d.z) * 0.25};
-    int cc[3];
-    // plain store: any sampled tet of the cell is a valid start; the located
-    // tet does not depend on the start (unique containing tet, or the
-    // canonical min-index tet of a tie, see canonical_tet)
-    grid[cell_of(g, m, cc)] = (int)k;
+  // one sample per thread; XCD-aware block order: each XCD's L2 serves a
+  // contiguous range of samples, i.e. neighbouring tets sharing vertices
+  const int64_t n = (ne + stride - 1) / stride;
+  const int64_t t = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int64_t k = 1 + t * stride;
+  // sampled tet k: from the packed sample stream (sstride 1, coalesced) or
+  // from every stride-th record of the 16-B connectivity stream
+  const int4 v = src[t * sstride];
+  if (v.x <= 0) return;
+  D3 m;
+  if (MID) {
+    // midpoint of edge v0-v1: a point of the tet's closure, 2 gathers
+    const D3 a = ld3(pts, v.x), b = ld3(pts, v.y);
+    m = D3{(a.x + b.x) * 0.5, (a.y + b.y) * 0.5, (a.z + b.z) * 0.5};
+  } else {
+    const D3 a = ld3(pts, v.x), b = ld3(pts, v.y), c = ld3(pts, v.z), d = ld3(pts, v.w);
+    m = D3{(a.x + b.x + c.x + d.x) * 0.25, (a.y + b.y + c.y + d.y) * 0.25,
+           (a.z + b.z + c.z + d.z) * 0.25};
   }
+  int cc[3];
+  // plain store: any sampled tet of the cell is a valid start; the located
+  // tet does not depend on the start (unique containing tet, or the
+  // canonical min-index tet of a tie, see canonical_tet)
+  grid[cell_of(g, m, cc)] = (int)k;
+}
+
+// connectivity stream out of the tet records: dst[i] = src[i * stride].v
+// (a kernel rather than a pitched 2-D copy: no row-count limits at 1e8 tets)
+__global__ __launch_bounds__(256) void k_tet_conn(const TetRec *__restrict__ src, int64_t stride,
+                                                  int64_t n, int4 *__restrict__ dst) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int4 *r = reinterpret_cast<const int4 *>(src + i * stride);
+    dst[i] = r[0];
+  }
+}
+void launch_tet_conn(const TetRec *src, int64_t stride, int64_t n, int4 *dst, hipStream_t s) {
+  int64_t nb = std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), 16384);
+  hipLaunchKernelGGL(k_tet_conn, dim3((unsigned)nb), dim3(256), 0, s, src, stride, n, dst);
 }
 
 // ---- ties -----------------------------------------------------------------------
@@ -496,15 +520,17 @@ void launch_prologue(uint8_t *wmask, int64_t n, unsigned *counts, int *grid, int
 }
 
 void launch_hint_build(const int4 *tetv, const int4 *packed, const Pt4 *pts, int64_t ne,
-                       int stride, int *grid, GridDesc g, hipStream_t s) {
-  int64_t n = (ne + stride - 1) / stride;
-  int64_t nb = (n + 255) / 256;
-  if (nb > 65536) nb = 65536;
-  if (nb < 1) nb = 1;
+                       int stride, int *grid, GridDesc g, int mid, hipStream_t s) {
+  const int64_t n = (ne + stride - 1) / stride;
+  const int64_t nb = std::max<int64_t>((n + 255) / 256, 1);
   const int4 *src = packed ? packed : tetv + 1;
   const int64_t sstride = packed ? 1 : stride;
-  hipLaunchKernelGGL(k_hint_build, dim3((unsigned)nb), dim3(256), 0, s, src, sstride, pts, ne,
-                     stride, grid, g);
+  if (mid)
+    hipLaunchKernelGGL(k_hint_build<true>, dim3((unsigned)nb), dim3(256), 0, s, src, sstride, pts,
+                       ne, stride, grid, g);
+  else
+    hipLaunchKernelGGL(k_hint_build<false>, dim3((unsigned)nb), dim3(256), 0, s, src, sstride, pts,
+                       ne, stride, grid, g);
 }
 void launch_locate_vol(const VolArgs &a, hipStream_t s) {
   int64_t nb = (a.nlist + 255) / 256;

@@ -212,7 +212,7 @@ bool pmx_ctx::launch_tet_locate(const VolArgs &A, const pmx_run_opts &o, hipStre
   const double shift = 0.3819660113 * h;
   int64_t cells = 1;
   for (int a = 0; a < 3; a++) {
-    int d = (int)std::ceil((ext[a] + shift) / h);
+    int d = (int)std::ceil((ext[a] + shift) / h * (1.0 - 1e-9));
     d = std::max(1, std::min(d, 2048));
     g.dim[a] = d;
     g.lo[a] = bblo[a] - shift;

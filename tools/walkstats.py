@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Walk diagnostics on a bench config (GPU): histogram of walk steps, distance
+from the hint start, ties / stuck counts.
+
+  python tools/walkstats.py --config C2 [--tune T] [--hint-stride S]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--tune", type=int, default=0)
+    ap.add_argument("--hint-stride", type=int, default=0)
+    args = ap.parse_args()
+    import bench
+    from parmmg_amd import build
+    build.build_meshgen()
+    build.build_transfer()
+    from parmmg_amd.transfer import Transfer
+    cfg = bench.CONFIGS[args.config]
+    m, x, t, sols = bench.build_case(cfg, 0)
+    tr = Transfer(0)
+    tr.upload_background(m, sols, 0)
+    tr.upload_points(x, t)
+    tr.run(tune=args.tune, hint_stride=args.hint_stride)
+    r = tr.download()
+    st = tr.starts()
+    vol = t == 0
+    steps = r.steps[vol]
+    h = np.bincount(np.clip(np.abs(steps), 0, 20))
+    c = m.centroids()
+    d = np.linalg.norm(c[st[vol] - 1] - x[vol], axis=1) * cfg["n"]
+    ng = cfg["n"] ** 3
+    grid = np.zeros(ng, np.int32)
+    tr.lib.pmx_debug_hint_grid(tr.ctx, grid.ctypes.data, ng)
+    # the cell of each sampled tet's centroid, recomputed on the host
+    ks = np.arange(1, m.ne + 1, 4)
+    cen = m.xyz[m.tet[ks]].mean(axis=1)
+    cell = np.clip((cen * cfg["n"]).astype(np.int64), 0, cfg["n"] - 1)
+    ci = cell[:, 0] + cfg["n"] * (cell[:, 1] + cfg["n"] * cell[:, 2])
+    ok = np.zeros(ng, bool)
+    gi = grid.astype(np.int64)
+    nz = gi > 0
+    # a cell's hint must be one of the samples whose centroid is in that cell
+    samp_cell = np.full(m.ne + 1, -1, np.int64)
+    samp_cell[ks] = ci
+    ok[nz] = samp_cell[gi[nz]] == np.nonzero(nz)[0]
+    out_grid = {"cells": ng, "empty": int((~nz).sum()), "wrong_cell": int((nz & ~ok).sum())}
+    del cen, cell, ci, samp_cell
+    out = {"grid": out_grid, "config": args.config, "n": cfg["n"], "nvol": int(vol.sum()),
+           "steps_hist": {int(i): int(v) for i, v in enumerate(h) if v},
+           "steps_mean": float(np.abs(steps).mean()),
+           "start_dist_cells": {"mean": float(d.mean()), "p50": float(np.median(d)),
+                                "p99": float(np.percentile(d, 99)), "max": float(d.max())},
+           "status": {int(k): int(v) for k, v in zip(*np.unique(r.status[vol], return_counts=True))},
+           "stats": tr.locate_stats()}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

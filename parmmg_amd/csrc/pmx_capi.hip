@@ -294,7 +294,7 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   if (!dgrow(ctx, ctx->d_bestk, nn)) return 0;
   if (!dgrow(ctx, ctx->d_best, nn)) return 0;
   if (!dgrow(ctx, ctx->d_ties, nn)) return 0;
-  if (!dgrow(ctx, ctx->d_counts, 8)) return 0;
+  if (!dgrow(ctx, ctx->d_counts, 32)) return 0;   // [0..7] counters, [16..31] 8 x u64 chunk counters
   if (!dgrow(ctx, ctx->d_vollist, (size_t)std::max<int64_t>(nv, 1))) return 0;
   if (!dgrow(ctx, ctx->d_bdylist, (size_t)std::max<int64_t>(nb, 1))) return 0;
   if (!dgrow(ctx, ctx->d_vstat, (size_t)std::max<int64_t>((nv + 63) / 64 + 4, 1))) return 0;
@@ -302,6 +302,12 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   CK(hipMemcpyAsync(ctx->d_q.p, hq.data(), (size_t)n * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_kind.p, hk.data(), (size_t)n, hipMemcpyHostToDevice, ctx->stream));
   if (nv) CK(hipMemcpyAsync(ctx->d_vollist.p, vl.data(), (size_t)nv * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+  // the volume points' coordinates once more, contiguous in list order: the
+  // persistent walk streams them per 64-point chunk (no list -> q indirection)
+  std::vector<Pt4> hqv((size_t)std::max<int64_t>(nv, 1));
+  for (int64_t j = 0; j < nv; j++) hqv[(size_t)j] = hq[(size_t)vl[(size_t)j]];
+  if (!dgrow(ctx, ctx->d_qv, hqv.size())) return 0;
+  if (nv) CK(hipMemcpyAsync(ctx->d_qv.p, hqv.data(), (size_t)nv * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
   if (nb) CK(hipMemcpyAsync(ctx->d_bdylist.p, bl.data(), (size_t)nb * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
   ctx->have_pts = true;
@@ -327,6 +333,9 @@ static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &o
   A.occ = (opts.tune & 0xF) ? (opts.tune & 0xF) : PMX_DEFAULT_VOL_OCC;
   A.xcd_swizzle = 1;
   A.inline_ties = (opts.tune & 0x4000) ? 0 : 1;   // tune bit 14: all ties to k_fallback
+  A.qv = ctx->d_qv.p;
+  A.wctr = reinterpret_cast<unsigned long long *>(ctx->d_counts.p + 16);
+  A.region = ((ctx->nq_vol + 7) / 8 + 63) / 64 * 64;
 }
 
 int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
@@ -403,7 +412,9 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
       if (!ctx->launch_tet_locate(A, opts, st)) return 0;
     } else if (ctx->nq_vol) {
       // tune bit 10: the r01 kernel k_locate_vol (A/B reference)
+      // tune bit 16: the persistent-lane k_walkp (r01: 2.7x slower at 2 waves/SIMD)
       if (opts.tune & 0x400) launch_locate_vol(A, st);
+      else if (opts.tune & 0x10000) launch_walkp(A, st);
       else launch_walk(A, st);
     }
     if (ev) CK(hipEventRecord(ev[2], st));

@@ -35,6 +35,9 @@ struct VolArgs {
   int occ;                      // k_locate_vol register/occupancy variant
   int xcd_swizzle;
   int inline_ties;               // k_walk: resolve face ties in place
+  const Pt4 *qv;                // coordinates of the volume points in list order
+  unsigned long long *wctr;     // k_walkp: per-XCD-region chunk counters [8]
+  int64_t region;               // k_walkp: points per region (multiple of 64)
 };
 
 struct ExhArgs {
@@ -53,6 +56,7 @@ void launch_hint_build(const int4 *tetv, const int4 *packed, const Pt4 *pts, int
                        int stride, int *grid, GridDesc g, int mid, hipStream_t s);
 void launch_locate_vol(const VolArgs &a, hipStream_t s);
 void launch_walk(const VolArgs &a, hipStream_t s);
+void launch_walkp(const VolArgs &a, hipStream_t s);
 void launch_tet_conn(const TetRec *src, int64_t stride, int64_t n, int4 *dst, hipStream_t s);
 void launch_exhaustive(const ExhArgs &e, const VolArgs &v, hipStream_t s);
 void launch_const_metric(const int8_t *kind, int64_t nq, double *out, int S, int off, int size,

@@ -502,7 +502,7 @@ void launch_run_init(unsigned *counts, hipStream_t s) {
 __global__ __launch_bounds__(256) void k_prologue(uint8_t *wmask, int64_t n, unsigned *counts,
                                                   int *grid, int64_t gcells) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
-  if (t < 8) counts[t] = 0;
+  if (t < 32) counts[t] = 0;
   const int64_t n16 = n / 16;
   for (int64_t i = t; i < n16; i += st) reinterpret_cast<uint4 *>(wmask)[i] = make_uint4(0, 0, 0, 0);
   for (int64_t i = n16 * 16 + t; i < n; i += st) wmask[i] = 0;

@@ -23,6 +23,7 @@
 //  * layout specialisation: the interpolation is compiled for the solution
 //    layout (one anisotropic metric; S isotropic/vector components; generic)
 //    so the register allocation is not the maximum over every layout.
+#include <algorithm>
 #include "pmx_device.h"
 #include "pmx_kernels.h"
 
@@ -209,8 +210,8 @@ __device__ __forceinline__ bool face_tie(const VolArgs &A, D3 p, int &cur, TetRe
   return false;
 }
 
-template <int LAYOUT, int S, bool TIES>
-__global__ __launch_bounds__(256) void k_walk(VolArgs A) {
+template <int LAYOUT, int S, bool TIES, int OCC>
+__global__ __launch_bounds__(256, OCC) void k_walk(VolArgs A) {
   const int64_t b = walk_xcd_remap(blockIdx.x, gridDim.x);
   const int64_t j = b * blockDim.x + threadIdx.x;
   unsigned s_cnt = 0, s_sum = 0, s_max = 0, s_min = 0xffffffffu;
@@ -336,12 +337,18 @@ static int walk_layout(const SolDesc &sd, int *S) {
   return iso ? LAYOUT_ISO : LAYOUT_GEN;
 }
 
+// OCC: minimum waves per SIMD asked of the register allocator (1 = free)
+template <int LAYOUT, int S, int OCC>
+static void launch_walk_o(const VolArgs &a, int ties, int64_t nb, hipStream_t s) {
+  if (ties)
+    hipLaunchKernelGGL((k_walk<LAYOUT, S, true, OCC>), dim3((unsigned)nb), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_walk<LAYOUT, S, false, OCC>), dim3((unsigned)nb), dim3(256), 0, s, a);
+}
 template <int LAYOUT, int S>
 static void launch_walk_t(const VolArgs &a, int ties, int64_t nb, hipStream_t s) {
-  if (ties)
-    hipLaunchKernelGGL((k_walk<LAYOUT, S, true>), dim3((unsigned)nb), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((k_walk<LAYOUT, S, false>), dim3((unsigned)nb), dim3(256), 0, s, a);
+  if (a.occ == 5) launch_walk_o<LAYOUT, S, 5>(a, ties, nb, s);
+  else launch_walk_o<LAYOUT, S, 1>(a, ties, nb, s);
 }
 
 void launch_walk(const VolArgs &a, hipStream_t s) {
@@ -364,4 +371,292 @@ void launch_walk(const VolArgs &a, hipStream_t s) {
     }
   }
   launch_walk_t<LAYOUT_GEN, 0>(a, ties, nb, s);
+}
+
+// ---- persistent-lane walk (k_walkp) ----------------------------------------
+//
+// k_walk runs each wavefront for the LONGEST walk among its 64 lanes: on C2
+// the walk-step histogram is 17/33/33/17 % for 1/2/3/4 steps, so every wave
+// iterates 4 times for 2.45 useful steps per lane (61 % lane utilisation).
+// k_walkp keeps the lanes busy instead:
+//  * a persistent grid (occupancy-sized) of waves pulls chunks of 64
+//    Morton-consecutive points from per-XCD counters (one atomic per chunk;
+//    an XCD's L2 sees a contiguous region, idle XCDs steal from the others);
+//  * a lane whose point is located takes the next point of the chunk
+//    (ballot rank + shuffles) and starts walking in the same iteration;
+//  * located points are queued in LDS (point, tet vertices, barycentrics) and
+//    interpolated 64 at a time with every lane active.
+// Walk steps, tie handling, stuck points and the interpolation are those of
+// k_walk: the outputs are identical.
+#define WQ_CAP 128
+
+struct WalkQ {
+  int i[WQ_CAP];
+  int v[4][WQ_CAP];
+  double lam[4][WQ_CAP];
+};
+
+__device__ __forceinline__ unsigned long long lanes_below() {
+  const int lane = threadIdx.x & 63;
+  return lane ? (~0ull >> (64 - lane)) : 0ull;
+}
+
+__device__ __forceinline__ int wuni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int LAYOUT, int S>
+__device__ __forceinline__ void interp_queued(const VolArgs &A, const WalkQ &Q, int slot) {
+  const int i = Q.i[slot];
+  const int v[4] = {Q.v[0][slot], Q.v[1][slot], Q.v[2][slot], Q.v[3][slot]};
+  const double phi[4] = {Q.lam[0][slot], Q.lam[1][slot], Q.lam[2][slot], Q.lam[3][slot]};
+  const unsigned wm = interp_layout<LAYOUT, S>(A.sol, A.sd, v, phi, A.out + (int64_t)i * A.sd.S);
+  A.wmask[i] = (uint8_t)(wm | A.const_bit);
+}
+
+template <int LAYOUT, int S, bool TIES>
+__global__ __launch_bounds__(256) void k_walkp(VolArgs A) {
+  __shared__ WalkQ Qs[4];
+  const int lane = threadIdx.x & 63;
+  WalkQ &Q = Qs[threadIdx.x >> 6];
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  unsigned s_cnt = 0, s_sum = 0, s_max = 0, s_min = 0xffffffffu;
+
+  // chunk stream (wave-uniform state)
+  int reg = blockIdx.x & 7, tries = 0, b_cnt = 0, b_used = 0, qn = 0;
+  // this lane's element of the current chunk
+  int b_i = -1, b_h = 0;
+  double b_x = 0.0, b_y = 0.0, b_z = 0.0;
+
+  // this lane's walk
+  int i = -1, cur = 0, step = 0;
+  bool fresh = false;
+  D3 p{0.0, 0.0, 0.0};
+  TetRec t;
+#pragma unroll
+  for (int l = 0; l < 4; l++) { t.v[l] = 0; t.nb[l] = 0; }
+  D3 P[4];
+#pragma unroll
+  for (int l = 0; l < 4; l++) P[l] = D3{0.0, 0.0, 0.0};
+  int ring[WALK_RING];
+#pragma unroll
+  for (int r = 0; r < WALK_RING; r++) ring[r] = 0;
+  double lam[4] = {0.0, 0.0, 0.0, 0.0};
+
+  for (;;) {
+    // ---- refill idle lanes from the chunk stream
+    for (;;) {
+      const unsigned long long idle = __ballot(i < 0);
+      if (!idle) break;
+      if (b_used >= b_cnt) {
+        if (tries >= 8) break;
+        unsigned long long c = 0;
+        if (lane == 0) c = atomicAdd(A.wctr + reg, 64ull);
+        c = ((unsigned long long)(unsigned)__shfl((int)(c >> 32), 0) << 32) |
+            (unsigned)__shfl((int)(c & 0xffffffffu), 0);
+        const int64_t lo = (int64_t)reg * A.region + (int64_t)c;
+        const int64_t hi = min((int64_t)(reg + 1) * A.region, A.nlist);
+        if (lo >= hi) {
+          reg = (reg + 1) & 7;
+          tries++;
+          continue;
+        }
+        b_cnt = wuni((int)min((int64_t)64, hi - lo));
+        b_used = 0;
+        if (lane < b_cnt) {
+          const int64_t jj = lo + lane;
+          b_i = A.list[jj];
+          const Pt4 qq = A.qv[jj];
+          b_x = qq.x; b_y = qq.y; b_z = qq.z;
+          b_h = walk_hint(A.grid, A.g, D3{b_x, b_y, b_z});
+        }
+      }
+      const int rank = __popcll(idle & lanes_below());
+      const int avail = b_cnt - b_used;
+      const int src = (b_used + rank) & 63;
+      const int si = __shfl(b_i, src), sh = __shfl(b_h, src);
+      const double sx = __shfl(b_x, src), sy = __shfl(b_y, src), sz = __shfl(b_z, src);
+      if (i < 0 && rank < avail) {
+        i = si;
+        p = D3{sx, sy, sz};
+        cur = sh;
+        fresh = true;
+        step = 0;
+#pragma unroll
+        for (int r = 0; r < WALK_RING; r++) ring[r] = 0;
+        A.start[i] = cur;
+      }
+      b_used = wuni(b_used + min(__popcll(idle), avail));
+    }
+    if (!__ballot(i >= 0)) break;
+
+    // ---- one walk step for every lane holding a point
+    bool done = false, found = false;
+    if (i >= 0) {
+      const TetRec u = A.tets[cur];
+      step++;
+      if (u.v[0] <= 0) {
+        done = true;                                   // !MG_EOK: let the scan decide
+      } else {
+        if (fresh) {
+          P[0] = ld3(A.pts, u.v[0]); P[1] = ld3(A.pts, u.v[1]);
+          P[2] = ld3(A.pts, u.v[2]); P[3] = ld3(A.pts, u.v[3]);
+        } else {
+          // shared face: permute the known coordinates, gather the new vertex
+          bool m[4][4];
+          int nnew = 0, lnew = 0;
+#pragma unroll
+          for (int l = 0; l < 4; l++) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) m[l][k] = (u.v[l] == t.v[k]);
+            const bool any = m[l][0] | m[l][1] | m[l][2] | m[l][3];
+            nnew += any ? 0 : 1;
+            lnew = any ? lnew : l;
+          }
+          if (nnew == 1) {
+            const D3 pn = ld3(A.pts, pick4(u.v, lnew));
+            D3 W[4];
+#pragma unroll
+            for (int l = 0; l < 4; l++)
+              W[l] = dsel(m[l][0], P[0], dsel(m[l][1], P[1], dsel(m[l][2], P[2], dsel(m[l][3], P[3], pn))));
+#pragma unroll
+            for (int l = 0; l < 4; l++) P[l] = W[l];
+          } else {                                     // inconsistent adjacency
+            P[0] = ld3(A.pts, u.v[0]); P[1] = ld3(A.pts, u.v[1]);
+            P[2] = ld3(A.pts, u.v[2]); P[3] = ld3(A.pts, u.v[3]);
+          }
+        }
+        t = u;
+        fresh = false;
+        double num[4], vol;
+        face_nums(P, p, num, &vol);
+        const double rv = 1.0 / vol;
+#pragma unroll
+        for (int f = 0; f < 4; f++) lam[f] = -(num[f] * rv);
+        double lmin = fmin(fmin(lam[0], lam[1]), fmin(lam[2], lam[3]));
+        if (lmin > -PMX_EPS - APPROX_GUARD) {
+#pragma unroll
+          for (int f = 0; f < 4; f++) lam[f] = -num[f] / vol;
+          lmin = fmin(fmin(lam[0], lam[1]), fmin(lam[2], lam[3]));
+          found = lmin > -PMX_EPS;                     // src/barycoord_pmmg.c:102-107
+        }
+        if (found || step >= A.max_walk) {
+          done = true;
+        } else {
+          int rk[4];
+          wranks(lam, rk);
+#pragma unroll
+          for (int r = WALK_RING - 1; r > 0; r--) ring[r] = ring[r - 1];
+          ring[0] = cur;
+          int next = 0;
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int f = (rk[0] == r) ? 0 : (rk[1] == r) ? 1 : (rk[2] == r) ? 2 : 3;
+            const int nb = pick4(t.nb, f);
+            bool seen = false;
+#pragma unroll
+            for (int q = 0; q < WALK_RING; q++) seen |= (ring[q] == nb);
+            if (!next && nb && !seen) next = nb;
+          }
+          if (next) cur = next;
+          else done = true;
+        }
+      }
+    }
+    // ---- finish: located -> LDS queue, near-face ties -> k_ties, else stuck
+    bool push = false;
+    if (done) {
+      bool tie = false;
+      if (found) {
+        const double lmn = fmin(fmin(lam[0], lam[1]), fmin(lam[2], lam[3]));
+        tie = lmn < TIE_NEAR && (!TIES || face_tie(A, p, cur, t, lam));
+      }
+      if (found && !tie) {
+        A.elem[i] = cur;
+        A.status[i] = 1;
+        A.steps[i] = step;
+        push = true;
+        s_cnt++; s_sum += step;
+        s_max = max(s_max, (unsigned)step);
+        s_min = min(s_min, (unsigned)step);
+      } else if (found) {
+        const unsigned slot = atomicAdd(A.tie_count, 1u);
+        A.tie_list[slot] = make_int2(i, cur);
+        A.steps[i] = step;
+      } else {
+        const unsigned slot = atomicAdd(A.stuck_count, 1u);
+        A.stuck_list[slot] = i;
+        A.found[slot] = 0x7fffffff;
+        A.bestk[slot] = 0x7fffffff;
+        A.best[slot] = ~0ull;
+        A.steps[i] = -step;
+      }
+    }
+    const unsigned long long pm = __ballot(push);
+    if (push) {
+      const int slot = qn + __popcll(pm & lanes_below());
+      Q.i[slot] = i;
+#pragma unroll
+      for (int l = 0; l < 4; l++) { Q.v[l][slot] = t.v[l]; Q.lam[l][slot] = lam[l]; }
+    }
+    qn = wuni(qn + __popcll(pm));
+    if (done) i = -1;
+    if (qn >= 64) {
+      wave_sync();
+      interp_queued<LAYOUT, S>(A, Q, qn - 64 + lane);
+      qn -= 64;
+      wave_sync();
+    }
+  }
+  if (qn > 0) {
+    wave_sync();
+    if (lane < qn) interp_queued<LAYOUT, S>(A, Q, lane);
+  }
+  // per-wave statistics; records of waves this grid does not have are zeroed
+  wave_stats_w(A.wstats + wave, s_cnt, s_sum, s_max, s_min);
+  const int64_t nrec = (A.nlist + 63) / 64;
+  for (int64_t r = wave + nwaves; r < nrec; r += nwaves)
+    if (lane == 0) A.wstats[r] = make_uint4(0, 0, 0, 0xffffffffu);
+}
+
+template <int LAYOUT, int S>
+static void launch_walkp_t(const VolArgs &a, int ties, hipStream_t s) {
+  const void *fn = ties ? (const void *)k_walkp<LAYOUT, S, true> : (const void *)k_walkp<LAYOUT, S, false>;
+  int dev = 0, cus = 0, per_cu = 0;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0);
+  const int64_t chunks = (a.nlist + 63) / 64;
+  int64_t nb = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
+  nb = std::max<int64_t>(1, std::min<int64_t>(nb, (chunks + 3) / 4));
+  if (ties)
+    hipLaunchKernelGGL((k_walkp<LAYOUT, S, true>), dim3((unsigned)nb), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_walkp<LAYOUT, S, false>), dim3((unsigned)nb), dim3(256), 0, s, a);
+}
+
+void launch_walkp(const VolArgs &a, hipStream_t s) {
+  if (a.nlist < 1) return;
+  int S = 0;
+  const int lay = walk_layout(a.sd, &S);
+  const int ties = a.inline_ties;
+  if (lay == LAYOUT_ANI) return launch_walkp_t<LAYOUT_ANI, 6>(a, ties, s);
+  if (lay == LAYOUT_ISO) {
+    switch (S) {
+      case 1: return launch_walkp_t<LAYOUT_ISO, 1>(a, ties, s);
+      case 2: return launch_walkp_t<LAYOUT_ISO, 2>(a, ties, s);
+      case 3: return launch_walkp_t<LAYOUT_ISO, 3>(a, ties, s);
+      case 4: return launch_walkp_t<LAYOUT_ISO, 4>(a, ties, s);
+      case 5: return launch_walkp_t<LAYOUT_ISO, 5>(a, ties, s);
+      case 6: return launch_walkp_t<LAYOUT_ISO, 6>(a, ties, s);
+      case 7: return launch_walkp_t<LAYOUT_ISO, 7>(a, ties, s);
+      default: return launch_walkp_t<LAYOUT_ISO, 8>(a, ties, s);
+    }
+  }
+  launch_walkp_t<LAYOUT_GEN, 0>(a, ties, s);
 }

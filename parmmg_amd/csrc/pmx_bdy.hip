@@ -72,6 +72,53 @@ template <class St> __device__ __forceinline__ int st_cap(const St &s);
 template <int C> __device__ __forceinline__ int st_cap(const RegState<C> &) { return C; }
 template <> __device__ __forceinline__ int st_cap(const GlobState &s) { return s.capv; }
 
+// RegState: every access at a compile-time index (unrolled, predicated), so
+// the lists live in VGPRs; a runtime index would put them in scratch and make
+// each visited / flag lookup a dependent memory round trip (r01: the surface
+// walk was latency-bound on exactly that)
+template <int C> __device__ __forceinline__ bool visited(RegState<C> &s, int t) {
+  bool h = false;
+#pragma unroll
+  for (int i = 0; i < C; i++) h |= (i < s.nv) & (s.vis[i] == t);
+  return h;
+}
+template <int C> __device__ __forceinline__ void mark_visited(RegState<C> &s, int t) {
+  if (visited(s, t)) return;
+  if (s.nv >= C) { s.over = true; return; }
+#pragma unroll
+  for (int i = 0; i < C; i++)
+    if (i == s.nv) s.vis[i] = t;
+  s.nv++;
+}
+template <int C> __device__ __forceinline__ int get_flag(RegState<C> &s, const BdyArgs &A, int p) {
+  bool hit = false;
+  int f = 0;
+#pragma unroll
+  for (int i = 0; i < C; i++) {
+    const bool m = (i < s.no) & (s.ovp[i] == p);
+    f = m ? s.ovf[i] : f;
+    hit |= m;
+  }
+  return hit ? f : A.ntoff[p + 1] - A.ntoff[p];
+}
+template <int C> __device__ __forceinline__ void set_flag(RegState<C> &s, int p, int f) {
+  bool upd = false;
+#pragma unroll
+  for (int i = 0; i < C; i++) {
+    const bool m = (i < s.no) & (s.ovp[i] == p);
+    s.ovf[i] = m ? f : s.ovf[i];
+    upd |= m;
+  }
+  if (upd) return;
+  if (s.no >= C) { s.over = true; return; }
+#pragma unroll
+  for (int i = 0; i < C; i++) {
+    s.ovp[i] = (i == s.no) ? p : s.ovp[i];
+    s.ovf[i] = (i == s.no) ? f : s.ovf[i];
+  }
+  s.no++;
+}
+
 template <class St> __device__ bool visited(St &s, int t) {
   for (int i = 0; i < s.nv; i++)
     if (s.V(i) == t) return true;
@@ -281,10 +328,14 @@ __device__ void interp_tria(const BdyArgs &A, int k, const Bary &b, int edge, in
     } else if (sz == 6) {                             // PMMG_interp3bar_ani
       double mi[3][6], mint[6], r[6];
       bool okk = true;
-      for (int i = 0; i < 3 && okk; i++) {
+      // unrolled (static indices keep mi in VGPRs); && stops at the first
+      // failed inversion like the reference loop
+#pragma unroll
+      for (int i = 0; i < 3; i++) {
         double m[6];
+#pragma unroll
         for (int j = 0; j < 6; j++) m[j] = A.sol[(int64_t)v[i] * sd.S + off + j];
-        okk = invmat(m, mi[i]);
+        okk = okk && invmat(m, mi[i]);
       }
       if (!okk) continue;
       for (int j = 0; j < 6; j++) mint[j] = phi[0] * mi[0][j] + phi[1] * mi[1][j] + phi[2] * mi[2][j];
@@ -574,6 +625,35 @@ void launch_tria_normals(const TriRec *tris, const Pt4 *pts, int64_t nt, Pt4 *tr
 #define OVF_CAP 2048
 #define OVF_THREADS (64 * 64)
 
+// the coarser tria hint grid over the background bbox (about 2 trias per
+// cell in each direction of the surface)
+bool pmx_ctx::size_tria_grid() {
+  double ext[3];
+  int64_t cells = 1;
+  for (int ax = 0; ax < 3; ax++) ext[ax] = std::max(bbhi[ax] - bblo[ax], 1e-300);
+  const double area = 2.0 * (ext[0] * ext[1] + ext[1] * ext[2] + ext[0] * ext[2]);
+  const double h = std::sqrt(area / std::max(1.0, (double)nt / 2.0));
+  for (int ax = 0; ax < 3; ax++) {
+    // 1e-9 slack: libm cbrt/sqrt are not correctly rounded and a cell count
+    // of exactly n must not become n+1 (misaligned with a lattice-like mesh)
+    int d = (int)std::ceil(ext[ax] / h * (1.0 - 1e-9));
+    d = std::max(1, std::min(d, 1024));
+    tgd.dim[ax] = d;
+    tgd.lo[ax] = bblo[ax];
+    tgd.inv[ax] = (double)d / ext[ax];
+    cells *= d;
+  }
+  tcells = nt > 0 ? cells : 0;
+  if (tcells && d_tgrid_cap < (size_t)cells) {
+    if (d_tgrid) hipFree(d_tgrid);
+    d_tgrid = nullptr;
+    d_tgrid_cap = 0;
+    if (hipMalloc((void **)&d_tgrid, sizeof(int) * (size_t)cells) != hipSuccess) { err = "hipMalloc tgrid"; return false; }
+    d_tgrid_cap = (size_t)cells;
+  }
+  return true;
+}
+
 bool pmx_ctx::launch_bdy(const VolArgs &a, const pmx_run_opts &o, hipStream_t s) {
   if (nt < 1) { err = "surface points present but the background has no boundary trias"; return false; }
   // tria hint grid: a coarser grid over the same bbox (about 2 trias / cell
@@ -590,32 +670,9 @@ bool pmx_ctx::launch_bdy(const VolArgs &a, const pmx_run_opts &o, hipStream_t s)
     if (hipMalloc((void **)&d_ows.p, sizeof(int) * (size_t)OVF_THREADS * 3 * OVF_CAP) != hipSuccess) { err = "hipMalloc ows"; return false; }
     d_ows.cap = (size_t)OVF_THREADS * 3 * OVF_CAP;
   }
-  // tria grid: reuse d_found as storage is not possible (stuck slots); use a
-  // dedicated coarse grid stored past the tet grid cells
-  GridDesc tg;
-  double ext[3];
-  int64_t cells = 1;
-  double area = 0.0;
-  for (int ax = 0; ax < 3; ax++) ext[ax] = std::max(bbhi[ax] - bblo[ax], 1e-300);
-  area = 2.0 * (ext[0] * ext[1] + ext[1] * ext[2] + ext[0] * ext[2]);
-  double h = std::sqrt(area / std::max(1.0, (double)nt / 2.0));
-  for (int ax = 0; ax < 3; ax++) {
-    // 1e-9 slack: libm cbrt/sqrt are not correctly rounded and a cell count
-    // of exactly n must not become n+1 (misaligned with a lattice-like mesh)
-    int d = (int)std::ceil(ext[ax] / h * (1.0 - 1e-9));
-    d = std::max(1, std::min(d, 1024));
-    tg.dim[ax] = d;
-    tg.lo[ax] = bblo[ax];
-    tg.inv[ax] = (double)d / ext[ax];
-    cells *= d;
-  }
-  if (d_tgrid_cap < (size_t)cells) {
-    if (d_tgrid) hipFree(d_tgrid);
-    d_tgrid = nullptr;
-    if (hipMalloc((void **)&d_tgrid, sizeof(int) * (size_t)cells) != hipSuccess) { err = "hipMalloc tgrid"; return false; }
-    d_tgrid_cap = (size_t)cells;
-  }
-  hipMemsetAsync(d_tgrid, 0, sizeof(int) * (size_t)cells, s);
+  // tria hint grid: sized and allocated with the background
+  // (pmx_ctx::size_tria_grid), zeroed by the step's prologue kernel
+  const GridDesc tg = tgd;
   {
     int64_t nb = (nt + 255) / 256;
     if (nb > 4096) nb = 4096;

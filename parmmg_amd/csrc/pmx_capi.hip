@@ -219,12 +219,14 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   ctx->grid = g;
   ctx->gcells = cells;
   for (int a = 0; a < 3; a++) { ctx->bblo[a] = lo[a]; ctx->bbhi[a] = hi[a]; }
+  if (!ctx->size_tria_grid()) return 0;
 
   if (!dgrow(ctx, ctx->d_pts, (size_t)(np + 1))) return 0;
   if (!dgrow(ctx, ctx->d_tets, (size_t)(ne + 1))) return 0;
   if (!dgrow(ctx, ctx->d_sol, hs.size())) return 0;
   if (!dgrow(ctx, ctx->d_tris, (size_t)(nt + 1))) return 0;
   if (!dgrow(ctx, ctx->d_grid, (size_t)cells)) return 0;
+  if (!dgrow(ctx, ctx->d_grid64, (size_t)cells)) return 0;
   if (!dgrow(ctx, ctx->d_ntoff, ctx->h_ntoff.size())) return 0;
   if (!dgrow(ctx, ctx->d_ntlist, std::max<size_t>(ctx->h_ntlist.size(), 1))) return 0;
   if (!dgrow(ctx, ctx->d_trn, (size_t)(nt + 1))) return 0;
@@ -297,7 +299,8 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   if (!dgrow(ctx, ctx->d_counts, 32)) return 0;   // [0..7] counters, [16..31] 8 x u64 chunk counters
   if (!dgrow(ctx, ctx->d_vollist, (size_t)std::max<int64_t>(nv, 1))) return 0;
   if (!dgrow(ctx, ctx->d_bdylist, (size_t)std::max<int64_t>(nb, 1))) return 0;
-  if (!dgrow(ctx, ctx->d_vstat, (size_t)std::max<int64_t>((nv + 63) / 64 + 4, 1))) return 0;
+  // one record per wave of the largest k_walk block (1024 threads)
+  if (!dgrow(ctx, ctx->d_vstat, (size_t)std::max<int64_t>((nv + 1023) / 1024 * 16 + 4, 1))) return 0;
   if (!dgrow(ctx, ctx->d_bstat, (size_t)std::max<int64_t>((nb + 63) / 64 + 4, 1))) return 0;
   CK(hipMemcpyAsync(ctx->d_q.p, hq.data(), (size_t)n * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_kind.p, hk.data(), (size_t)n, hipMemcpyHostToDevice, ctx->stream));
@@ -336,6 +339,10 @@ static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &o
   A.qv = ctx->d_qv.p;
   A.wctr = reinterpret_cast<unsigned long long *>(ctx->d_counts.p + 16);
   A.region = ((ctx->nq_vol + 7) / 8 + 63) / 64 * 64;
+  // tune bits 17/18: 512 / 1024 threads per k_walk block
+  A.block = (opts.tune & 0x40000) ? 1024 : (opts.tune & 0x20000) ? 512 : 256;
+  // tune bit 20: central hint (per cell, the sample closest to the centre)
+  A.grid64 = (opts.tune & 0x100000) ? ctx->d_grid64.p : nullptr;
 }
 
 int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
@@ -359,7 +366,7 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   // one prologue kernel zeroes the write masks, the counters and the hint grid
   const bool need_grid = !((opts.tune & 0x200) && !(opts.tune & 0x100));
   launch_prologue(ctx->d_wmask.p, n, ctx->d_counts.p, need_grid ? ctx->d_grid.p : nullptr,
-                  ctx->gcells, st);
+                  ctx->gcells, ctx->nq_bdy ? ctx->d_tgrid : nullptr, ctx->tcells, st);
   if (sd.metric_const)
     launch_const_metric(ctx->d_kind.p, n, ctx->d_out.p, S, sd.off[sd.imet], sd.size[sd.imet],
                         opts.hsiz, ctx->d_wmask.p, sd.imet, st);
@@ -379,10 +386,12 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     // issue slots; forking before the bandwidth-bound hint build slowed it by
     // 40%: r01 sweep), 0x800 = serial on the main stream, 0x1000 = forked
     // right after the prologue
-    const int bdy_mode = (opts.tune & 0x800) ? 1 : (opts.tune & 0x1000) ? 0 : 2;
+    // 0x80000 = forked after the prologue and joined before the volume walk
+    // (overlaps the hint build only)
+    const int bdy_mode = (opts.tune & 0x800) ? 1 : (opts.tune & 0x1000) ? 0 : (opts.tune & 0x80000) ? 3 : 2;
     VolArgs A{};
     fill_vol_args(ctx, sd, opts, A);
-    if (ctx->nq_bdy && bdy_mode == 0) {
+    if (ctx->nq_bdy && (bdy_mode == 0 || bdy_mode == 3)) {
       // fork: the surface locate (its own hint grid, walk, fallbacks) shares
       // nothing with the volume path but the zeroed counters and masks
       CK(hipEventRecord(ctx->ev_fork, st));
@@ -396,9 +405,12 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
       const int stride = opts.hint_stride > 0 ? opts.hint_stride : PMX_DEFAULT_HINT_STRIDE;
       // tune bit 13: strided reads of the connectivity stream (r01 A/B)
       const bool packed = stride == PMX_DEFAULT_HINT_STRIDE && !(opts.tune & 0x2000);
+      if (A.grid64) launch_fill64(ctx->d_grid64.p, ctx->gcells, st);
       launch_hint_build(ctx->d_tetv.p, packed ? ctx->d_tets_s.p : nullptr, ctx->d_pts.p, ctx->ne,
-                        stride, ctx->d_grid.p, ctx->grid, (opts.tune & 0x8000) ? 1 : 0, st);
+                        stride, ctx->d_grid.p, ctx->grid, (opts.tune & 0x8000) ? 1 : 0, st,
+                        const_cast<unsigned long long *>(A.grid64));
     }
+    if (ctx->nq_bdy && bdy_mode == 3) CK(hipStreamWaitEvent(st, ctx->ev_join, 0));
     if (ev) CK(hipEventRecord(ev[1], st));
     if (ctx->nq_bdy && bdy_mode == 2) {
       CK(hipEventRecord(ctx->ev_fork, st));
@@ -418,13 +430,13 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
       else launch_walk(A, st);
     }
     if (ev) CK(hipEventRecord(ev[2], st));
-    if (ctx->nq_bdy && bdy_mode != 1) {
+    if (ctx->nq_bdy && (bdy_mode == 0 || bdy_mode == 2)) {
       CK(hipStreamWaitEvent(st, ctx->ev_join, 0));     // surface path done
-    } else if (ctx->nq_bdy) {
+    } else if (ctx->nq_bdy && bdy_mode == 1) {
       if (ev) CK(hipEventRecord(ev[3], st));
       if (!ctx->launch_bdy(A, opts, st)) return 0;
       if (ev) CK(hipEventRecord(ev[5], st));
-    } else if (ev) {
+    } else if (ev && !ctx->nq_bdy) {
       CK(hipEventRecord(ev[3], st));
       CK(hipEventRecord(ev[5], st));
     }
@@ -591,7 +603,7 @@ hipEvent_t *pmx_ctx::next_event_slot() {
 }
 
 void pmx_ctx::free_all() {
-  dfree(d_pts); dfree(d_tets); dfree(d_sol); dfree(d_tris); dfree(d_trn); dfree(d_grid);
+  dfree(d_pts); dfree(d_tets); dfree(d_sol); dfree(d_tris); dfree(d_trn); dfree(d_grid); dfree(d_grid64);
   dfree(d_ntoff); dfree(d_ntlist);
   dfree(d_q); dfree(d_kind); dfree(d_wmask); dfree(d_out); dfree(d_elem); dfree(d_status);
   dfree(d_steps); dfree(d_start); dfree(d_edge); dfree(d_vertex); dfree(d_list); dfree(d_found);

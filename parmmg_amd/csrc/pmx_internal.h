@@ -34,6 +34,7 @@ struct pmx_ctx {
   DevBuf<TriRec> d_tris;
   DevBuf<Pt4> d_trn;
   DevBuf<int> d_grid;
+  DevBuf<unsigned long long> d_grid64;    // central-hint grid: (dist2 f32 bits << 32 | tet) minima
   DevBuf<int> d_ntoff, d_ntlist;
   std::vector<int> h_ntoff, h_ntlist;
 
@@ -66,6 +67,8 @@ struct pmx_ctx {
   DevBuf<int> d_blist, d_olist, d_ows;
   int *d_tgrid = nullptr;
   size_t d_tgrid_cap = 0;
+  GridDesc tgd{};
+  int64_t tcells = 0;
 
   // statistics
   DevBuf<double> d_qual;
@@ -80,6 +83,7 @@ struct pmx_ctx {
   void free_all();
   void host_build_node_trias(const std::vector<TriRec> &tr);
   bool launch_bdy(const VolArgs &a, const pmx_run_opts &o, hipStream_t s);
+  bool size_tria_grid();
   bool launch_tet_locate(const VolArgs &a, const pmx_run_opts &o, hipStream_t s);
 };
 

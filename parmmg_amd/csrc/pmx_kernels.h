@@ -38,6 +38,8 @@ struct VolArgs {
   const Pt4 *qv;                // coordinates of the volume points in list order
   unsigned long long *wctr;     // k_walkp: per-XCD-region chunk counters [8]
   int64_t region;               // k_walkp: points per region (multiple of 64)
+  int block;                    // k_walk threads per block (256 / 512 / 1024)
+  const unsigned long long *grid64;  // central hint grid (null: plain int grid)
 };
 
 struct ExhArgs {
@@ -53,7 +55,9 @@ struct ExhArgs {
 };
 
 void launch_hint_build(const int4 *tetv, const int4 *packed, const Pt4 *pts, int64_t ne,
-                       int stride, int *grid, GridDesc g, int mid, hipStream_t s);
+                       int stride, int *grid, GridDesc g, int mid, hipStream_t s,
+                       unsigned long long *grid64 = nullptr);
+void launch_fill64(unsigned long long *p, int64_t n, hipStream_t s);
 void launch_locate_vol(const VolArgs &a, hipStream_t s);
 void launch_walk(const VolArgs &a, hipStream_t s);
 void launch_walkp(const VolArgs &a, hipStream_t s);
@@ -63,7 +67,7 @@ void launch_const_metric(const int8_t *kind, int64_t nq, double *out, int S, int
                          double hsiz, uint8_t *wmask, int imet, hipStream_t s);
 void launch_run_init(unsigned *counts, hipStream_t s);
 void launch_prologue(uint8_t *wmask, int64_t n, unsigned *counts, int *grid, int64_t gcells,
-                     hipStream_t s);
+                     int *tgrid, int64_t tcells, hipStream_t s);
 
 struct StatArgs {
   const Pt4 *pts;

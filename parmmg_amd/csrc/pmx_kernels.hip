@@ -72,11 +72,12 @@ __device__ int hint_lookup(const int *grid, const GridDesc &g, D3 p) {
   return 1;
 }
 
-template <bool MID>
+template <bool MID, bool CENTRAL>
 __global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ src, int64_t sstride,
                                                     const Pt4 *__restrict__ pts, int64_t ne,
                                                     int stride, int *__restrict__ grid,
-                                                    GridDesc g) {
+                                                    GridDesc g,
+                                                    unsigned long long *__restrict__ grid64) {
   // one sample per thread; XCD-aware block order: each XCD's L2 serves a
   // contiguous range of samples, i.e. neighbouring tets sharing vertices
   const int64_t n = (ne + stride - 1) / stride;
@@ -98,10 +99,33 @@ __global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ src
            (a.z + b.z + c.z + d.z) * 0.25};
   }
   int cc[3];
-  // plain store: any sampled tet of the cell is a valid start; the located
-  // tet does not depend on the start (unique containing tet, or the
-  // canonical min-index tet of a tie, see canonical_tet)
-  grid[cell_of(g, m, cc)] = (int)k;
+  const int64_t cell = cell_of(g, m, cc);
+  if (CENTRAL) {
+    // the sample whose centroid is closest to the cell centre (ties: lowest
+    // tet index): deterministic, and a shorter walk from anywhere in the cell
+    const double dx = m.x - (g.lo[0] + (cc[0] + 0.5) / g.inv[0]);
+    const double dy = m.y - (g.lo[1] + (cc[1] + 0.5) / g.inv[1]);
+    const double dz = m.z - (g.lo[2] + (cc[2] + 0.5) / g.inv[2]);
+    const float d2 = (float)(dx * dx + dy * dy + dz * dz);
+    const unsigned long long key =
+        ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned long long)(unsigned)k;
+    atomicMin(grid64 + cell, key);
+  } else {
+    // plain store: any sampled tet of the cell is a valid start; the located
+    // tet does not depend on the start (unique containing tet, or the
+    // canonical min-index tet of a tie, see canonical_tet)
+    grid[cell] = (int)k;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_fill64(unsigned long long *p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = ~0ull;
+}
+void launch_fill64(unsigned long long *p, int64_t n, hipStream_t s) {
+  const int64_t nb = std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), 4096);
+  hipLaunchKernelGGL(k_fill64, dim3((unsigned)nb), dim3(256), 0, s, p, n);
 }
 
 // connectivity stream out of the tet records: dst[i] = src[i * stride].v
@@ -500,37 +524,48 @@ void launch_run_init(unsigned *counts, hipStream_t s) {
 }
 
 __global__ __launch_bounds__(256) void k_prologue(uint8_t *wmask, int64_t n, unsigned *counts,
-                                                  int *grid, int64_t gcells) {
+                                                  int *grid, int64_t gcells, int *tgrid,
+                                                  int64_t tcells) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
   if (t < 32) counts[t] = 0;
   const int64_t n16 = n / 16;
   for (int64_t i = t; i < n16; i += st) reinterpret_cast<uint4 *>(wmask)[i] = make_uint4(0, 0, 0, 0);
   for (int64_t i = n16 * 16 + t; i < n; i += st) wmask[i] = 0;
-  if (grid) {
-    const int64_t g4 = gcells / 4;
-    for (int64_t i = t; i < g4; i += st) reinterpret_cast<int4 *>(grid)[i] = make_int4(0, 0, 0, 0);
-    for (int64_t i = g4 * 4 + t; i < gcells; i += st) grid[i] = 0;
+  int *gs[2] = {grid, tgrid};
+  const int64_t cs[2] = {gcells, tcells};
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    int *g = gs[k];
+    if (!g) continue;
+    const int64_t g4 = cs[k] / 4;
+    for (int64_t i = t; i < g4; i += st) reinterpret_cast<int4 *>(g)[i] = make_int4(0, 0, 0, 0);
+    for (int64_t i = g4 * 4 + t; i < cs[k]; i += st) g[i] = 0;
   }
 }
 void launch_prologue(uint8_t *wmask, int64_t n, unsigned *counts, int *grid, int64_t gcells,
-                     hipStream_t s) {
-  int64_t work = std::max<int64_t>(n / 16, grid ? gcells / 4 : 0);
+                     int *tgrid, int64_t tcells, hipStream_t s) {
+  int64_t work = std::max<int64_t>(n / 16, std::max<int64_t>(grid ? gcells / 4 : 0, tgrid ? tcells / 4 : 0));
   int64_t nb = std::min<int64_t>(std::max<int64_t>((work + 255) / 256, 1), 4096);
-  hipLaunchKernelGGL(k_prologue, dim3((unsigned)nb), dim3(256), 0, s, wmask, n, counts, grid, gcells);
+  hipLaunchKernelGGL(k_prologue, dim3((unsigned)nb), dim3(256), 0, s, wmask, n, counts, grid, gcells,
+                     tgrid, tcells);
 }
 
 void launch_hint_build(const int4 *tetv, const int4 *packed, const Pt4 *pts, int64_t ne,
-                       int stride, int *grid, GridDesc g, int mid, hipStream_t s) {
+                       int stride, int *grid, GridDesc g, int mid, hipStream_t s,
+                       unsigned long long *grid64) {
   const int64_t n = (ne + stride - 1) / stride;
   const int64_t nb = std::max<int64_t>((n + 255) / 256, 1);
   const int4 *src = packed ? packed : tetv + 1;
   const int64_t sstride = packed ? 1 : stride;
-  if (mid)
-    hipLaunchKernelGGL(k_hint_build<true>, dim3((unsigned)nb), dim3(256), 0, s, src, sstride, pts,
-                       ne, stride, grid, g);
+  if (grid64)
+    hipLaunchKernelGGL((k_hint_build<false, true>), dim3((unsigned)nb), dim3(256), 0, s, src, sstride,
+                       pts, ne, stride, grid, g, grid64);
+  else if (mid)
+    hipLaunchKernelGGL((k_hint_build<true, false>), dim3((unsigned)nb), dim3(256), 0, s, src, sstride,
+                       pts, ne, stride, grid, g, grid64);
   else
-    hipLaunchKernelGGL(k_hint_build<false>, dim3((unsigned)nb), dim3(256), 0, s, src, sstride, pts,
-                       ne, stride, grid, g);
+    hipLaunchKernelGGL((k_hint_build<false, false>), dim3((unsigned)nb), dim3(256), 0, s, src, sstride,
+                       pts, ne, stride, grid, g, grid64);
 }
 void launch_locate_vol(const VolArgs &a, hipStream_t s) {
   int64_t nb = (a.nlist + 255) / 256;

@@ -62,11 +62,35 @@ __device__ __noinline__ int hint_search(const int *grid, int gx, int gy, int gz,
   return 1;
 }
 
-__device__ __forceinline__ int walk_hint(const int *grid, const GridDesc &g, D3 p) {
+// central-hint grid: empty cells hold ~0 (no sample)
+__device__ __noinline__ int hint_search64(const unsigned long long *grid, int gx, int gy, int gz,
+                                          int cx, int cy, int cz) {
+  for (int r = 1; r <= 3; r++) {
+    for (int dz = -r; dz <= r; dz++)
+      for (int dy = -r; dy <= r; dy++)
+        for (int dx = -r; dx <= r; dx++) {
+          if (max(abs(dx), max(abs(dy), abs(dz))) != r) continue;
+          int x = cx + dx, y = cy + dy, z = cz + dz;
+          if (x < 0 || y < 0 || z < 0 || x >= gx || y >= gy || z >= gz) continue;
+          unsigned long long kk = grid[(int64_t)x + (int64_t)gx * ((int64_t)y + (int64_t)gy * z)];
+          if (kk != ~0ull) return (int)(unsigned)(kk & 0xffffffffu);
+        }
+  }
+  return 1;
+}
+
+__device__ __forceinline__ int walk_hint(const int *grid, const GridDesc &g, D3 p,
+                                         const unsigned long long *grid64 = nullptr) {
   int cx = wclamp((p.x - g.lo[0]) * g.inv[0], g.dim[0]);
   int cy = wclamp((p.y - g.lo[1]) * g.inv[1], g.dim[1]);
   int cz = wclamp((p.z - g.lo[2]) * g.inv[2], g.dim[2]);
-  int k = grid[(int64_t)cx + (int64_t)g.dim[0] * ((int64_t)cy + (int64_t)g.dim[1] * cz)];
+  const int64_t c = (int64_t)cx + (int64_t)g.dim[0] * ((int64_t)cy + (int64_t)g.dim[1] * cz);
+  if (grid64) {
+    const unsigned long long kk = grid64[c];
+    return kk != ~0ull ? (int)(unsigned)(kk & 0xffffffffu)
+                       : hint_search64(grid64, g.dim[0], g.dim[1], g.dim[2], cx, cy, cz);
+  }
+  int k = grid[c];
   return k ? k : hint_search(grid, g.dim[0], g.dim[1], g.dim[2], cx, cy, cz);
 }
 
@@ -210,8 +234,8 @@ __device__ __forceinline__ bool face_tie(const VolArgs &A, D3 p, int &cur, TetRe
   return false;
 }
 
-template <int LAYOUT, int S, bool TIES, int OCC>
-__global__ __launch_bounds__(256, OCC) void k_walk(VolArgs A) {
+template <int LAYOUT, int S, bool TIES, int OCC, int BS>
+__global__ __launch_bounds__(BS, OCC) void k_walk(VolArgs A) {
   const int64_t b = walk_xcd_remap(blockIdx.x, gridDim.x);
   const int64_t j = b * blockDim.x + threadIdx.x;
   unsigned s_cnt = 0, s_sum = 0, s_max = 0, s_min = 0xffffffffu;
@@ -220,7 +244,7 @@ __global__ __launch_bounds__(256, OCC) void k_walk(VolArgs A) {
     const int64_t i = A.list[j];
     const Pt4 qq = A.q[i];
     const D3 p{qq.x, qq.y, qq.z};
-    int cur = walk_hint(A.grid, A.g, p);
+    int cur = walk_hint(A.grid, A.g, p, A.grid64);
     A.start[i] = cur;
     int ring[WALK_RING];
 #pragma unroll
@@ -337,18 +361,24 @@ static int walk_layout(const SolDesc &sd, int *S) {
   return iso ? LAYOUT_ISO : LAYOUT_GEN;
 }
 
-// OCC: minimum waves per SIMD asked of the register allocator (1 = free)
-template <int LAYOUT, int S, int OCC>
-static void launch_walk_o(const VolArgs &a, int ties, int64_t nb, hipStream_t s) {
+// OCC: minimum waves per SIMD asked of the register allocator (1 = free);
+// BS: threads per block (the waves of one block share a CU and its L1: a
+// larger block keeps more Morton-adjacent points on one CU)
+template <int LAYOUT, int S, int OCC, int BS>
+static void launch_walk_o(const VolArgs &a, int ties, hipStream_t s) {
+  const int64_t nb = (a.nlist + BS - 1) / BS;
   if (ties)
-    hipLaunchKernelGGL((k_walk<LAYOUT, S, true, OCC>), dim3((unsigned)nb), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_walk<LAYOUT, S, true, OCC, BS>), dim3((unsigned)nb), dim3(BS), 0, s, a);
   else
-    hipLaunchKernelGGL((k_walk<LAYOUT, S, false, OCC>), dim3((unsigned)nb), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_walk<LAYOUT, S, false, OCC, BS>), dim3((unsigned)nb), dim3(BS), 0, s, a);
 }
 template <int LAYOUT, int S>
 static void launch_walk_t(const VolArgs &a, int ties, int64_t nb, hipStream_t s) {
-  if (a.occ == 5) launch_walk_o<LAYOUT, S, 5>(a, ties, nb, s);
-  else launch_walk_o<LAYOUT, S, 1>(a, ties, nb, s);
+  (void)nb;
+  if (a.block == 1024) launch_walk_o<LAYOUT, S, 1, 1024>(a, ties, s);
+  else if (a.block == 512) launch_walk_o<LAYOUT, S, 1, 512>(a, ties, s);
+  else if (a.occ == 5) launch_walk_o<LAYOUT, S, 5, 256>(a, ties, s);
+  else launch_walk_o<LAYOUT, S, 1, 256>(a, ties, s);
 }
 
 void launch_walk(const VolArgs &a, hipStream_t s) {
@@ -473,7 +503,7 @@ __global__ __launch_bounds__(256) void k_walkp(VolArgs A) {
           b_i = A.list[jj];
           const Pt4 qq = A.qv[jj];
           b_x = qq.x; b_y = qq.y; b_z = qq.z;
-          b_h = walk_hint(A.grid, A.g, D3{b_x, b_y, b_z});
+          b_h = walk_hint(A.grid, A.g, D3{b_x, b_y, b_z}, A.grid64);
         }
       }
       const int rank = __popcll(idle & lanes_below());

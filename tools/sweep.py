@@ -22,13 +22,16 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--opt", default="hint_stride=1,4")
+    ap.add_argument("--n", type=int, default=0, help="override the config's cells per axis")
     args = ap.parse_args()
     import bench
     from parmmg_amd import build
     build.build_meshgen()
     build.build_transfer()
     from parmmg_amd.transfer import Transfer
-    cfg = bench.CONFIGS[args.config]
+    cfg = dict(bench.CONFIGS[args.config])
+    if args.n:
+        cfg["n"] = args.n
     m, x, t, sols = bench.build_case(cfg, 0)
     tr = Transfer(0)
     tr.upload_background(m, sols, 0)
@@ -53,7 +56,8 @@ def main():
         out[v] = {k: (float(np.median(a)), float(np.min(a))) for k, a in res[v].items()}
         out[v]["stepav"] = stats[v]["stepav"]
         out[v]["nexhaust"] = stats[v]["nexhaust"]
-    print(json.dumps({"config": args.config, "opt": key, "ms(median,min)": out}, indent=1))
+    print(json.dumps({"config": args.config, "n": cfg["n"], "npts": int(len(x)), "opt": key,
+                      "ms(median,min)": out}, indent=1))
 
 
 if __name__ == "__main__":

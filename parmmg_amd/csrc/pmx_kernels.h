@@ -72,6 +72,7 @@ void launch_prologue(uint8_t *wmask, int64_t n, unsigned *counts, int *grid, int
 struct StatArgs {
   const Pt4 *pts;
   const TetRec *tets;
+  const int4 *tetv;             // connectivity stream (v only)
   int64_t ne;
   const double *sol;
   int S, msize, moff;

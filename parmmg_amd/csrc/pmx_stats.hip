@@ -110,7 +110,10 @@ __global__ __launch_bounds__(256) void k_qual(StatArgs A, double *qual, QualPart
   const int64_t per = (A.ne + gridDim.x - 1) / gridDim.x;       // contiguous chunk per block
   const int64_t k0 = 1 + (int64_t)blockIdx.x * per, k1 = min(A.ne, k0 + per - 1);
   for (int64_t k = k0 + threadIdx.x; k <= k1; k += blockDim.x) {
-    TetRec t = A.tets[k];
+    // 16-B connectivity stream: the neighbours are not needed here
+    const int4 cv = A.tetv[k];
+    TetRec t;
+    t.v[0] = cv.x; t.v[1] = cv.y; t.v[2] = cv.z; t.v[3] = cv.w;
     if (t.v[0] <= 0) continue;
     double q = use_stored ? qual[k] : tet_quality(A, k, t);
     if (!use_stored && qual) qual[k] = q;
@@ -124,7 +127,9 @@ __global__ __launch_bounds__(256) void k_qual(StatArgs A, double *qual, QualPart
     p.max = fmax(p.max, rap);
     int ir = (int)(5.0 * rap);
     ir = ir < 4 ? ir : 4;
-    p.his[ir] += 1;
+    // predicated, static indices: the histogram stays in VGPRs (no scratch)
+#pragma unroll
+    for (int i = 0; i < 5; i++) p.his[i] += (i == ir) ? 1 : 0;
   }
   if (!parts) return;
   sh[threadIdx.x] = p;
@@ -198,6 +203,15 @@ __device__ __forceinline__ bool tet_admissible(const StatArgs &A, const TetRec &
   return n > 0;
 }
 
+__device__ __forceinline__ int pick_v(const TetRec &t, int l) {
+  return (t.v[0] & -(int)(l == 0)) | (t.v[1] & -(int)(l == 1)) | (t.v[2] & -(int)(l == 2)) |
+         (t.v[3] & -(int)(l == 3));
+}
+__device__ __forceinline__ int pick_nb(const TetRec &t, int l) {
+  return (t.nb[0] & -(int)(l == 0)) | (t.nb[1] & -(int)(l == 1)) | (t.nb[2] & -(int)(l == 2)) |
+         (t.nb[3] & -(int)(l == 3));
+}
+
 __device__ __forceinline__ int loc_of(const TetRec &t, int p) {
   int l = 3;
   if (t.v[0] == p) l = 0;
@@ -209,23 +223,32 @@ __device__ __forceinline__ int loc_of(const TetRec &t, int p) {
 // true iff no admissible tet with index < k contains edge (a,b); the shell is
 // rotated both ways from k through the two faces of k that contain the edge
 __device__ bool owns_edge(const StatArgs &A, int64_t k, const TetRec &t0, int ia) {
-  const int a = t0.v[IARE[ia][0]], b = t0.v[IARE[ia][1]];
-  int others[2], no = 0;
-  for (int l = 0; l < 4; l++)
-    if (l != IARE[ia][0] && l != IARE[ia][1]) others[no++] = l;
+  // local edge ia = (i0, i1); the two other local vertices (o0 < o1)
+  const int i0 = IARE[ia][0], i1 = IARE[ia][1];
+  const int a = pick_v(t0, i0), b = pick_v(t0, i1);
+  const int o0 = (i0 != 0 && i1 != 0) ? 0 : (i0 != 1 && i1 != 1) ? 1 : 2;
+  const int o1 = 6 - i0 - i1 - o0;
+  // without point tags every tet is admissible: a face neighbour of smaller
+  // index disowns the edge before any load (the common exit)
+  if (!A.ptag) {
+    const int n0 = pick_nb(t0, o0), n1 = pick_nb(t0, o1);
+    if ((n0 && n0 < k) || (n1 && n1 < k)) return false;
+  }
   for (int dir = 0; dir < 2; dir++) {
     // cross the face opposite `opp`, the third vertex of the face we keep is `keep`
-    int opp = others[dir], keep = t0.v[others[1 - dir]];
-    int cur = t0.nb[opp];
+    const int opp = dir ? o1 : o0;
+    int keep = pick_v(t0, dir ? o0 : o1);
+    int cur = pick_nb(t0, opp);
     int guard = 0;
     while (cur && cur != (int)k && guard++ < 4096) {
+      if (cur < k && !A.ptag) return false;         // decided before the load
       TetRec t = A.tets[cur];
       if (cur < k && tet_admissible(A, t)) return false;
       // in `cur`, the face we came through contains a, b, and the vertex we
       // crossed from... the next face contains a, b and the vertex not in
       // {a, b, keep-side}: leave through the face opposite `keep`
       int lk = loc_of(t, keep);
-      int nxt = t.nb[lk];
+      int nxt = pick_nb(t, lk);
       // new keep = the vertex of cur not in {a, b, keep}
       int nk = 0;
       for (int l = 0; l < 4; l++) {
@@ -288,7 +311,7 @@ __global__ __launch_bounds__(256) void k_prilen(StatArgs A, LenPart *parts) {
     if (!tet_admissible(A, t)) continue;
     for (int ia = 0; ia < 6; ia++) {
       if (!owns_edge(A, k, t, ia)) continue;
-      int np_ = t.v[IARE[ia][0]], nq_ = t.v[IARE[ia][1]];
+      int np_ = pick_v(t, IARE[ia][0]), nq_ = pick_v(t, IARE[ia][1]);
       double len = edge_len(A, np_, nq_);
       if (!(len != 0.0)) { if (len == 0.0) { p.nul++; continue; } }
       long long key = 6 * k + ia;
@@ -296,10 +319,13 @@ __global__ __launch_bounds__(256) void k_prilen(StatArgs A, LenPart *parts) {
       p.ned++;
       if (len < p.lmin || (len == p.lmin && key < p.kmin)) { p.lmin = len; p.kmin = key; }
       if (len > p.lmax || (len == p.lmax && key < p.kmax)) { p.lmax = len; p.kmax = key; }
-      int i;
-      for (i = 0; i < 8; i++)
-        if (BD[i] <= len && len < BD[i + 1]) { p.hl[i]++; break; }
-      if (i == 8) p.hl[8]++;
+      // first bin i < 8 with BD[i] <= len < BD[i+1], else 8 (predicated,
+      // static indices: hl stays in VGPRs)
+      int bin = 8;
+#pragma unroll
+      for (int i = 7; i >= 0; i--) bin = (BD[i] <= len && len < BD[i + 1]) ? i : bin;
+#pragma unroll
+      for (int i = 0; i < 9; i++) p.hl[i] += (i == bin) ? 1 : 0;
     }
   }
   sh[threadIdx.x] = p;
@@ -328,12 +354,18 @@ __global__ __launch_bounds__(256) void k_prilen_final(const LenPart *parts, int 
 
 // ---- C ABI ----------------------------------------------------------------------
 
-static const int STAT_BLOCKS = 2048;
+// partial records per pass: a function of ne only (the fixed-order final
+// reduction then gives the same sums on every run); enough workgroups to fill
+// 256 CUs several times over, each a contiguous range of >= 2048 tets
+static int stat_blocks(int64_t ne) {
+  return (int)std::max<int64_t>(256, std::min<int64_t>(16384, ne / 2048));
+}
 
 static bool stat_args(pmx_ctx *ctx, StatArgs &A) {
   if (!ctx->have_bg) { ctx->err = "statistics: upload a group first"; return false; }
   A.pts = ctx->d_pts.p;
   A.tets = ctx->d_tets.p;
+  A.tetv = ctx->d_tetv.p;
   A.ne = ctx->ne;
   A.sol = ctx->d_sol.p;
   A.S = ctx->sd.S;
@@ -368,7 +400,7 @@ int pmx_tetra_qual(pmx_ctx *ctx, double *qual) {
     }
     ctx->d_qual.cap = (size_t)(ctx->ne + 1);
   }
-  hipLaunchKernelGGL(k_qual, dim3(STAT_BLOCKS), dim3(256), 0, ctx->stream, A, ctx->d_qual.p,
+  hipLaunchKernelGGL(k_qual, dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A, ctx->d_qual.p,
                      (QualPart *)nullptr, 0);
   if (hipGetLastError() != hipSuccess) { ctx->err = "k_qual launch"; return 0; }
   ctx->have_qual = true;
@@ -384,12 +416,12 @@ int pmx_qualhisto_device(pmx_ctx *ctx, int use_stored, void *dev_result) {
   StatArgs A{};
   if (!stat_args(ctx, A)) return 0;
   if (use_stored && !ctx->have_qual) { ctx->err = "pmx_qualhisto: no stored quality"; return 0; }
-  if (!ensure_red(ctx, sizeof(QualPart) * (STAT_BLOCKS + 1))) return 0;
+  if (!ensure_red(ctx, sizeof(QualPart) * (stat_blocks(ctx->ne) + 1))) return 0;
   QualPart *parts = (QualPart *)ctx->d_red.p;
-  hipLaunchKernelGGL(k_qual, dim3(STAT_BLOCKS), dim3(256), 0, ctx->stream, A,
+  hipLaunchKernelGGL(k_qual, dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
                      use_stored ? ctx->d_qual.p : (double *)nullptr, parts, use_stored);
-  QualPart *res = dev_result ? (QualPart *)dev_result : parts + STAT_BLOCKS;
-  hipLaunchKernelGGL(k_qual_final, dim3(1), dim3(256), 0, ctx->stream, parts, STAT_BLOCKS, res);
+  QualPart *res = dev_result ? (QualPart *)dev_result : parts + stat_blocks(ctx->ne);
+  hipLaunchKernelGGL(k_qual_final, dim3(1), dim3(256), 0, ctx->stream, parts, stat_blocks(ctx->ne), res);
   return hipGetLastError() == hipSuccess;
 }
 
@@ -399,7 +431,7 @@ int pmx_qualhisto(pmx_ctx *ctx, pmx_qual_stats *st) {
   if (!pmx_qualhisto_device(ctx, 0, nullptr)) return 0;
   QualPart r;
   if (hipStreamSynchronize(ctx->stream) != hipSuccess) return 0;
-  if (hipMemcpy(&r, (QualPart *)ctx->d_red.p + STAT_BLOCKS, sizeof r, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  if (hipMemcpy(&r, (QualPart *)ctx->d_red.p + stat_blocks(ctx->ne), sizeof r, hipMemcpyDeviceToHost) != hipSuccess) return 0;
   st->ne = r.ne;
   st->np = ctx->np;
   st->max = r.max;
@@ -417,11 +449,11 @@ int pmx_prilen_device(pmx_ctx *ctx, const uint16_t *dtag, void *dev_result) {
   if (!stat_args(ctx, A)) return 0;
   if (ctx->sd.imet < 0) { ctx->err = "pmx_prilen: no metric"; return 0; }
   A.ptag = dtag;
-  if (!ensure_red(ctx, sizeof(LenPart) * (STAT_BLOCKS + 1))) return 0;
+  if (!ensure_red(ctx, sizeof(LenPart) * (stat_blocks(ctx->ne) + 1))) return 0;
   LenPart *parts = (LenPart *)ctx->d_red.p;
-  hipLaunchKernelGGL(k_prilen, dim3(STAT_BLOCKS), dim3(256), 0, ctx->stream, A, parts);
-  LenPart *res = dev_result ? (LenPart *)dev_result : parts + STAT_BLOCKS;
-  hipLaunchKernelGGL(k_prilen_final, dim3(1), dim3(256), 0, ctx->stream, parts, STAT_BLOCKS, res);
+  hipLaunchKernelGGL(k_prilen, dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A, parts);
+  LenPart *res = dev_result ? (LenPart *)dev_result : parts + stat_blocks(ctx->ne);
+  hipLaunchKernelGGL(k_prilen_final, dim3(1), dim3(256), 0, ctx->stream, parts, stat_blocks(ctx->ne), res);
   return hipGetLastError() == hipSuccess;
 }
 
@@ -442,7 +474,7 @@ int pmx_prilen(pmx_ctx *ctx, const uint16_t *point_tag, int64_t tag_stride, int 
   LenPart res;
   if (r) {
     r = hipStreamSynchronize(ctx->stream) == hipSuccess &&
-        hipMemcpy(&res, (LenPart *)ctx->d_red.p + STAT_BLOCKS, sizeof res, hipMemcpyDeviceToHost) == hipSuccess;
+        hipMemcpy(&res, (LenPart *)ctx->d_red.p + stat_blocks(ctx->ne), sizeof res, hipMemcpyDeviceToHost) == hipSuccess;
   }
   if (dtag) hipFree(dtag);
   if (!r) return 0;

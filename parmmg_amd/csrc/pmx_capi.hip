@@ -611,7 +611,7 @@ void pmx_ctx::free_all() {
   dfree(d_vstat); dfree(d_bstat);
   dfree(d_tetv); dfree(d_qcnt); dfree(d_qstart); dfree(d_qcell); dfree(d_qslot); dfree(d_tbest);
   dfree(d_qs); dfree(d_tests); dfree(d_scan_tmp);
-  dfree(d_qual); dfree(d_red); dfree(d_blist); dfree(d_olist); dfree(d_ows);
+  dfree(d_qual); dfree(d_red); dfree(d_emask); dfree(d_elist); dfree(d_bcount); dfree(d_blist); dfree(d_olist); dfree(d_ows);
   if (d_tgrid) hipFree(d_tgrid);
   d_tgrid = nullptr;
   d_tgrid_cap = 0;

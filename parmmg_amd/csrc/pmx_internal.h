@@ -73,6 +73,9 @@ struct pmx_ctx {
   // statistics
   DevBuf<double> d_qual;
   DevBuf<unsigned long long> d_red;
+  DevBuf<uint8_t> d_emask;              // prilen: per-tet mask of edges whose shell is rotated
+  DevBuf<uint32_t> d_elist;             // prilen: compacted (tet*8 + edge) list
+  DevBuf<unsigned> d_bcount;            // prilen: per-block counts -> offsets, [nb] total
   bool have_qual = false;
 
   // timing

@@ -9,7 +9,7 @@
 //
 // Both histograms are one pass over the mesh: per-thread accumulation, a
 // wavefront/LDS tree per workgroup, one partial record per workgroup, and a
-// final single-workgroup reduction in workgroup order (deterministic sums).
+// two-level final reduction in workgroup order (deterministic sums).
 // Unique edges are enumerated without a hash table: tet k owns its local edge
 // ia iff k is the smallest admissible tet index in the edge shell, found by
 // rotating around the edge through the adjacency (early exit on the first
@@ -90,9 +90,10 @@ struct QualPart {
   long long iel, ne, good, med, his[5];
 };
 
+template <bool ANI>
 __device__ double tet_quality(const StatArgs &A, int64_t k, const TetRec &t) {
   D3 a = ld3(A.pts, t.v[0]), b = ld3(A.pts, t.v[1]), c = ld3(A.pts, t.v[2]), d = ld3(A.pts, t.v[3]);
-  if (A.msize == 6) {
+  if (ANI) {
     const double *m = A.sol;
     return caltet_ani(a, b, c, d, m + (int64_t)t.v[0] * A.S + A.moff, m + (int64_t)t.v[1] * A.S + A.moff,
                       m + (int64_t)t.v[2] * A.S + A.moff, m + (int64_t)t.v[3] * A.S + A.moff);
@@ -101,12 +102,17 @@ __device__ double tet_quality(const StatArgs &A, int64_t k, const TetRec &t) {
 }
 
 // quality of every tet (+ optional histogram partials in the same pass)
+// ANI: the metric is a 6-component tensor (compiled apart: the iso variant
+// does not carry the tensor path's registers)
+template <bool ANI>
 __global__ __launch_bounds__(256) void k_qual(StatArgs A, double *qual, QualPart *parts,
                                               int use_stored) {
   __shared__ QualPart sh[256];
-  QualPart p;
-  p.avg = 0.0; p.max = 0.0; p.min = 2.0; p.iel = 0x7fffffffffffffffLL; p.ne = 0; p.good = 0; p.med = 0;
-  for (int i = 0; i < 5; i++) p.his[i] = 0;
+  // thread-local accumulators with 32-bit counts (a thread sees < 2^32 tets):
+  // half the registers of QualPart's 64-bit fields
+  double avg = 0.0, qmax = 0.0, qmin = 2.0;
+  long long iel = 0x7fffffffffffffffLL;
+  unsigned cne = 0, cgood = 0, cmed = 0, chis[5] = {0, 0, 0, 0, 0};
   const int64_t per = (A.ne + gridDim.x - 1) / gridDim.x;       // contiguous chunk per block
   const int64_t k0 = 1 + (int64_t)blockIdx.x * per, k1 = min(A.ne, k0 + per - 1);
   for (int64_t k = k0 + threadIdx.x; k <= k1; k += blockDim.x) {
@@ -115,23 +121,28 @@ __global__ __launch_bounds__(256) void k_qual(StatArgs A, double *qual, QualPart
     TetRec t;
     t.v[0] = cv.x; t.v[1] = cv.y; t.v[2] = cv.z; t.v[3] = cv.w;
     if (t.v[0] <= 0) continue;
-    double q = use_stored ? qual[k] : tet_quality(A, k, t);
+    double q = use_stored ? qual[k] : tet_quality<ANI>(A, k, t);
     if (!use_stored && qual) qual[k] = q;
     if (!parts) continue;
     double rap = ALPHAD * q;
-    p.ne++;
-    if (rap < p.min || (rap == p.min && k < p.iel)) { p.min = rap; p.iel = k; }
-    if (rap > 0.5) p.med++;
-    if (rap > 0.12) p.good++;
-    p.avg += rap;
-    p.max = fmax(p.max, rap);
+    cne++;
+    if (rap < qmin || (rap == qmin && k < iel)) { qmin = rap; iel = k; }
+    if (rap > 0.5) cmed++;
+    if (rap > 0.12) cgood++;
+    avg += rap;
+    qmax = fmax(qmax, rap);
     int ir = (int)(5.0 * rap);
     ir = ir < 4 ? ir : 4;
     // predicated, static indices: the histogram stays in VGPRs (no scratch)
 #pragma unroll
-    for (int i = 0; i < 5; i++) p.his[i] += (i == ir) ? 1 : 0;
+    for (int i = 0; i < 5; i++) chis[i] += (i == ir) ? 1u : 0u;
   }
   if (!parts) return;
+  QualPart p;
+  p.avg = avg; p.max = qmax; p.min = qmin; p.iel = iel;
+  p.ne = cne; p.good = cgood; p.med = cmed;
+#pragma unroll
+  for (int i = 0; i < 5; i++) p.his[i] = chis[i];
   sh[threadIdx.x] = p;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
@@ -154,9 +165,12 @@ __global__ __launch_bounds__(256) void k_qual_final(const QualPart *parts, int n
   QualPart p;
   p.avg = 0.0; p.max = 0.0; p.min = 2.0; p.iel = 0x7fffffffffffffffLL; p.ne = 0; p.good = 0; p.med = 0;
   for (int i = 0; i < 5; i++) p.his[i] = 0;
-  // contiguous ranges per thread keep the summation order fixed
-  int per = (n + 255) / 256;
-  for (int b = threadIdx.x * per; b < min(n, (int)(threadIdx.x + 1) * per); b++) {
+  // this block's contiguous range, contiguous sub-ranges per thread: the
+  // summation order is fixed (launched twice: FINAL_GRID blocks, then one)
+  const int pb = (n + gridDim.x - 1) / gridDim.x;
+  const int lo = blockIdx.x * pb, hi = min(n, lo + pb);
+  int per = (hi - lo + 255) / 256;
+  for (int b = lo + threadIdx.x * per; b < min(hi, lo + (int)(threadIdx.x + 1) * per); b++) {
     const QualPart &y = parts[b];
     p.avg += y.avg;
     p.max = fmax(p.max, y.max);
@@ -178,7 +192,7 @@ __global__ __launch_bounds__(256) void k_qual_final(const QualPart *parts, int n
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) *res = sh[0];
+  if (threadIdx.x == 0) res[blockIdx.x] = sh[0];
 }
 
 // ---- edge lengths ---------------------------------------------------------------
@@ -220,49 +234,6 @@ __device__ __forceinline__ int loc_of(const TetRec &t, int p) {
   return l;
 }
 
-// true iff no admissible tet with index < k contains edge (a,b); the shell is
-// rotated both ways from k through the two faces of k that contain the edge
-__device__ bool owns_edge(const StatArgs &A, int64_t k, const TetRec &t0, int ia) {
-  // local edge ia = (i0, i1); the two other local vertices (o0 < o1)
-  const int i0 = IARE[ia][0], i1 = IARE[ia][1];
-  const int a = pick_v(t0, i0), b = pick_v(t0, i1);
-  const int o0 = (i0 != 0 && i1 != 0) ? 0 : (i0 != 1 && i1 != 1) ? 1 : 2;
-  const int o1 = 6 - i0 - i1 - o0;
-  // without point tags every tet is admissible: a face neighbour of smaller
-  // index disowns the edge before any load (the common exit)
-  if (!A.ptag) {
-    const int n0 = pick_nb(t0, o0), n1 = pick_nb(t0, o1);
-    if ((n0 && n0 < k) || (n1 && n1 < k)) return false;
-  }
-  for (int dir = 0; dir < 2; dir++) {
-    // cross the face opposite `opp`, the third vertex of the face we keep is `keep`
-    const int opp = dir ? o1 : o0;
-    int keep = pick_v(t0, dir ? o0 : o1);
-    int cur = pick_nb(t0, opp);
-    int guard = 0;
-    while (cur && cur != (int)k && guard++ < 4096) {
-      if (cur < k && !A.ptag) return false;         // decided before the load
-      TetRec t = A.tets[cur];
-      if (cur < k && tet_admissible(A, t)) return false;
-      // in `cur`, the face we came through contains a, b, and the vertex we
-      // crossed from... the next face contains a, b and the vertex not in
-      // {a, b, keep-side}: leave through the face opposite `keep`
-      int lk = loc_of(t, keep);
-      int nxt = pick_nb(t, lk);
-      // new keep = the vertex of cur not in {a, b, keep}
-      int nk = 0;
-      for (int l = 0; l < 4; l++) {
-        int v = t.v[l];
-        if (v != a && v != b && v != keep) nk = v;
-      }
-      keep = nk;
-      cur = nxt;
-    }
-    if (cur == (int)k) break;      // closed shell: one direction saw every tet
-  }
-  return true;
-}
-
 // MMG5_lenEdg_iso / lenEdg_ani (restated, unpinned)
 __device__ double edge_len(const StatArgs &A, int p1, int p2) {
   D3 c1 = ld3(A.pts, p1), c2 = ld3(A.pts, p2);
@@ -299,57 +270,237 @@ __device__ __forceinline__ void len_init(LenPart &p) {
 
 __constant__ double BD[9] = {0.0, 0.3, 0.6, 0.7071, 0.9, 1.3, 1.4142, 2.0, 5.0};
 
-__global__ __launch_bounds__(256) void k_prilen(StatArgs A, LenPart *parts) {
+// ---- prilen: unique edges by shell ownership, compacted ------------------------
+//
+// Tet k owns its local edge ia iff no admissible tet of smaller index shares
+// it (the first occurrence in the reference's (k, ia) hash-pop order).  A
+// per-thread loop over tets rotating each shell in turn left ~1 lane in 6
+// with a shell to rotate on a lattice-ordered mesh (r01: 40 ms at 125M tets),
+// so the shells to rotate are compacted first:
+//  1. k_len_mark: per tet, edges decided without a load -- disowned by a
+//     smaller face neighbour (no point tags), or owned because both faces
+//     around the edge are boundary faces (shell = {k}, measured right away) --
+//     and a 6-bit mask of the edges whose shell must be rotated;
+//  2. k_len_scan + k_len_compact: those (tet, edge) pairs, in (k, ia) order,
+//     into a list (deterministic positions: block counts + exclusive scan);
+//  3. k_len_rotate: one list entry per thread, every lane rotating a shell.
+// Sums are reduced in a fixed order (phase-1 partials, then phase-3 partials,
+// two-level final reduction): the result does not depend on the schedule.
+
+__device__ __forceinline__ void edge_others(int ia, int &o0, int &o1) {
+  const int i0 = IARE[ia][0], i1 = IARE[ia][1];
+  o0 = (i0 != 0 && i1 != 0) ? 0 : (i0 != 1 && i1 != 1) ? 1 : 2;
+  o1 = 6 - i0 - i1 - o0;
+}
+
+struct LenAcc {
+  double avlen = 0.0, lmin = 1.e30, lmax = 0.0;
+  long long kmin = 0x7fffffffffffffffLL, kmax = 0x7fffffffffffffffLL;
+  unsigned ned = 0, nul = 0, hl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  __device__ void add(const StatArgs &A, const TetRec &t, int64_t k, int ia) {
+    const int np_ = pick_v(t, IARE[ia][0]), nq_ = pick_v(t, IARE[ia][1]);
+    const double len = edge_len(A, np_, nq_);
+    if (!(len != 0.0)) { if (len == 0.0) { nul++; return; } }
+    const long long key = 6 * k + ia;
+    avlen += len;
+    ned++;
+    if (len < lmin || (len == lmin && key < kmin)) { lmin = len; kmin = key; }
+    if (len > lmax || (len == lmax && key < kmax)) { lmax = len; kmax = key; }
+    int bin = 8;
+#pragma unroll
+    for (int i = 7; i >= 0; i--) bin = (BD[i] <= len && len < BD[i + 1]) ? i : bin;
+#pragma unroll
+    for (int i = 0; i < 9; i++) hl[i] += (i == bin) ? 1u : 0u;
+  }
+  __device__ void store(LenPart *sh, LenPart *out) const {
+    LenPart p;
+    p.avlen = avlen; p.lmin = lmin; p.lmax = lmax; p.kmin = kmin; p.kmax = kmax;
+    p.ned = ned; p.nul = nul;
+#pragma unroll
+    for (int i = 0; i < 9; i++) p.hl[i] = hl[i];
+    sh[threadIdx.x] = p;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) len_merge(sh[threadIdx.x], sh[threadIdx.x + o]);
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = sh[0];
+  }
+};
+
+__device__ __forceinline__ unsigned block_sum(unsigned v, unsigned *sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+__global__ __launch_bounds__(256) void k_len_mark(StatArgs A, LenPart *parts, uint8_t *emask,
+                                                  unsigned *bcount) {
   __shared__ LenPart sh[256];
-  LenPart p;
-  len_init(p);
+  __shared__ unsigned shc[4];
+  LenAcc acc;
+  unsigned cnt = 0;
   const int64_t per = (A.ne + gridDim.x - 1) / gridDim.x;
   const int64_t k0 = 1 + (int64_t)blockIdx.x * per, k1 = min(A.ne, k0 + per - 1);
   for (int64_t k = k0 + threadIdx.x; k <= k1; k += blockDim.x) {
-    TetRec t = A.tets[k];
-    if (t.v[0] <= 0) continue;
-    if (!tet_admissible(A, t)) continue;
-    for (int ia = 0; ia < 6; ia++) {
-      if (!owns_edge(A, k, t, ia)) continue;
-      int np_ = pick_v(t, IARE[ia][0]), nq_ = pick_v(t, IARE[ia][1]);
-      double len = edge_len(A, np_, nq_);
-      if (!(len != 0.0)) { if (len == 0.0) { p.nul++; continue; } }
-      long long key = 6 * k + ia;
-      p.avlen += len;
-      p.ned++;
-      if (len < p.lmin || (len == p.lmin && key < p.kmin)) { p.lmin = len; p.kmin = key; }
-      if (len > p.lmax || (len == p.lmax && key < p.kmax)) { p.lmax = len; p.kmax = key; }
-      // first bin i < 8 with BD[i] <= len < BD[i+1], else 8 (predicated,
-      // static indices: hl stays in VGPRs)
-      int bin = 8;
-#pragma unroll
-      for (int i = 7; i >= 0; i--) bin = (BD[i] <= len && len < BD[i + 1]) ? i : bin;
-#pragma unroll
-      for (int i = 0; i < 9; i++) p.hl[i] += (i == bin) ? 1 : 0;
+    const TetRec t = A.tets[k];
+    unsigned m = 0;
+    if (t.v[0] > 0 && tet_admissible(A, t)) {
+      for (int ia = 0; ia < 6; ia++) {
+        int o0, o1;
+        edge_others(ia, o0, o1);
+        const int n0 = pick_nb(t, o0), n1 = pick_nb(t, o1);
+        if (!A.ptag && ((n0 && n0 < k) || (n1 && n1 < k))) continue;   // disowned
+        if (!n0 && !n1) { acc.add(A, t, k, ia); continue; }             // shell = {k}
+        m |= 1u << ia;
+      }
     }
+    emask[k] = (uint8_t)m;
+    cnt += __popc(m);
   }
-  sh[threadIdx.x] = p;
+  const unsigned tot = block_sum(cnt, shc);
+  if (threadIdx.x == 0) bcount[blockIdx.x] = tot;
+  acc.store(sh, parts + blockIdx.x);
+}
+
+// exclusive scan of the per-block counts (one workgroup; n <= 16384)
+__global__ __launch_bounds__(256) void k_len_scan(unsigned *bcount, int n, unsigned *total) {
+  __shared__ unsigned sh[256];
+  const int per = (n + 255) / 256;
+  const int b0 = threadIdx.x * per, b1 = min(n, b0 + per);
+  unsigned s = 0;
+  for (int b = b0; b < b1; b++) s += bcount[b];
+  sh[threadIdx.x] = s;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) len_merge(sh[threadIdx.x], sh[threadIdx.x + o]);
+  if (threadIdx.x == 0) {
+    unsigned run = 0;
+    for (int i = 0; i < 256; i++) { unsigned v = sh[i]; sh[i] = run; run += v; }
+    *total = run;
+  }
+  __syncthreads();
+  unsigned run = sh[threadIdx.x];
+  for (int b = b0; b < b1; b++) { unsigned v = bcount[b]; bcount[b] = run; run += v; }
+}
+
+__global__ __launch_bounds__(256) void k_len_compact(const uint8_t *emask, int64_t ne,
+                                                     const unsigned *boff, uint32_t *list) {
+  __shared__ unsigned sh[256];
+  const int64_t per = (ne + gridDim.x - 1) / gridDim.x;
+  const int64_t k0 = 1 + (int64_t)blockIdx.x * per, k1 = min(ne, k0 + per - 1);
+  unsigned base = boff[blockIdx.x];
+  for (int64_t kb = k0; kb <= k1; kb += blockDim.x) {
+    const int64_t k = kb + threadIdx.x;
+    const unsigned m = (k <= k1) ? emask[k] : 0u;
+    const unsigned c = __popc(m);
+    // block-wide exclusive scan of c (Hillis-Steele in LDS)
+    sh[threadIdx.x] = c;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+      const unsigned v = (int)threadIdx.x >= o ? sh[threadIdx.x - o] : 0u;
+      __syncthreads();
+      sh[threadIdx.x] += v;
+      __syncthreads();
+    }
+    unsigned pos = base + sh[threadIdx.x] - c;
+    const unsigned stot = sh[255];
+    for (int ia = 0; ia < 6; ia++)
+      if ((m >> ia) & 1u) list[pos++] = (uint32_t)(k * 8 + ia);
+    base += stot;
     __syncthreads();
   }
-  if (threadIdx.x == 0) parts[blockIdx.x] = sh[0];
+}
+
+// True iff no admissible tet with index < k contains edge ia of tet k.  The
+// shell is rotated from k through the two faces of k that contain the edge,
+// both directions advanced together (two independent loads in flight): a
+// smaller index is met after min(d0, d1) steps, and a closed shell is covered
+// when the two cursors meet, in half the dependent steps.
+__device__ bool owns_edge_bidir(const StatArgs &A, int64_t k, const TetRec &t0, int ia) {
+  const int i0 = IARE[ia][0], i1 = IARE[ia][1];
+  const int a = pick_v(t0, i0), b = pick_v(t0, i1);
+  int o0, o1;
+  edge_others(ia, o0, o1);
+  int c0 = pick_nb(t0, o0), c1 = pick_nb(t0, o1);
+  int keep0 = pick_v(t0, o1), keep1 = pick_v(t0, o0);
+  for (int guard = 0; guard < 4096; guard++) {
+    if (c0 == (int)k) c0 = 0;                    // a direction that wrapped around
+    if (c1 == (int)k) c1 = 0;
+    if (!c0 && !c1) return true;                 // both ends reached: every tet seen
+    if (!A.ptag && ((c0 && c0 < k) || (c1 && c1 < k))) return false;
+    if (c0 && c0 == c1) {                        // the cursors meet on one tet
+      const TetRec t = A.tets[c0];
+      return !(c0 < k && tet_admissible(A, t));
+    }
+    TetRec t0r, t1r;
+    if (c0) t0r = A.tets[c0];
+    if (c1) t1r = A.tets[c1];
+    int n0 = 0, n1 = 0;
+    if (c0) {
+      if (c0 < k && tet_admissible(A, t0r)) return false;
+      n0 = pick_nb(t0r, loc_of(t0r, keep0));
+      int nk = 0;
+#pragma unroll
+      for (int l = 0; l < 4; l++) {
+        const int v = t0r.v[l];
+        nk = (v != a && v != b && v != keep0) ? v : nk;
+      }
+      keep0 = nk;
+    }
+    if (c1) {
+      if (c1 < k && tet_admissible(A, t1r)) return false;
+      n1 = pick_nb(t1r, loc_of(t1r, keep1));
+      int nk = 0;
+#pragma unroll
+      for (int l = 0; l < 4; l++) {
+        const int v = t1r.v[l];
+        nk = (v != a && v != b && v != keep1) ? v : nk;
+      }
+      keep1 = nk;
+    }
+    // closed shell: the next tet of one direction is the one the other just saw
+    if (c0 && c1 && (n0 == c1 || n1 == c0)) return true;
+    c0 = c0 ? n0 : 0;
+    c1 = c1 ? n1 : 0;
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(256) void k_len_rotate(StatArgs A, const uint32_t *list,
+                                                    const unsigned *total, LenPart *parts) {
+  __shared__ LenPart sh[256];
+  LenAcc acc;
+  const int64_t n = *total;
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t e0 = (int64_t)blockIdx.x * per, e1 = min(n, e0 + per);
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+    const uint32_t it = list[e];
+    const int64_t k = it >> 3;
+    const int ia = (int)(it & 7u);
+    const TetRec t = A.tets[k];
+    if (owns_edge_bidir(A, k, t, ia)) acc.add(A, t, k, ia);
+  }
+  acc.store(sh, parts + blockIdx.x);
 }
 
 __global__ __launch_bounds__(256) void k_prilen_final(const LenPart *parts, int n, LenPart *res) {
   __shared__ LenPart sh[256];
   LenPart p;
   len_init(p);
-  int per = (n + 255) / 256;
-  for (int b = threadIdx.x * per; b < min(n, (int)(threadIdx.x + 1) * per); b++) len_merge(p, parts[b]);
+  const int pb = (n + gridDim.x - 1) / gridDim.x;
+  const int lo = blockIdx.x * pb, hi = min(n, lo + pb);
+  int per = (hi - lo + 255) / 256;
+  for (int b = lo + threadIdx.x * per; b < min(hi, lo + (int)(threadIdx.x + 1) * per); b++)
+    len_merge(p, parts[b]);
   sh[threadIdx.x] = p;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) len_merge(sh[threadIdx.x], sh[threadIdx.x + o]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) *res = sh[0];
+  if (threadIdx.x == 0) res[blockIdx.x] = sh[0];
 }
 
 // ---- C ABI ----------------------------------------------------------------------
@@ -357,6 +508,7 @@ __global__ __launch_bounds__(256) void k_prilen_final(const LenPart *parts, int 
 // partial records per pass: a function of ne only (the fixed-order final
 // reduction then gives the same sums on every run); enough workgroups to fill
 // 256 CUs several times over, each a contiguous range of >= 2048 tets
+#define FINAL_GRID 64
 static int stat_blocks(int64_t ne) {
   return (int)std::max<int64_t>(256, std::min<int64_t>(16384, ne / 2048));
 }
@@ -374,6 +526,19 @@ static bool stat_args(pmx_ctx *ctx, StatArgs &A) {
   A.ptag = nullptr;
   return true;
 }
+
+template <class T> static bool dgrow_t(pmx_ctx *ctx, DevBuf<T> &b, size_t n) {
+  if (b.p && b.cap >= n) return true;
+  if (b.p) hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  if (hipMalloc((void **)&b.p, n * sizeof(T)) != hipSuccess) { ctx->err = "hipMalloc prilen"; return false; }
+  b.cap = n;
+  return true;
+}
+static bool dgrow_u8(pmx_ctx *ctx, DevBuf<uint8_t> &b, size_t n) { return dgrow_t(ctx, b, n); }
+static bool dgrow_u32(pmx_ctx *ctx, DevBuf<uint32_t> &b, size_t n) { return dgrow_t(ctx, b, n); }
+static bool dgrow_u32(pmx_ctx *ctx, DevBuf<unsigned> &b, size_t n, int) { return dgrow_t(ctx, b, n); }
 
 static bool ensure_red(pmx_ctx *ctx, size_t bytes) {
   size_t n = (bytes + 7) / 8;
@@ -400,8 +565,12 @@ int pmx_tetra_qual(pmx_ctx *ctx, double *qual) {
     }
     ctx->d_qual.cap = (size_t)(ctx->ne + 1);
   }
-  hipLaunchKernelGGL(k_qual, dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A, ctx->d_qual.p,
-                     (QualPart *)nullptr, 0);
+  if (A.msize == 6)
+    hipLaunchKernelGGL(k_qual<true>, dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
+                       ctx->d_qual.p, (QualPart *)nullptr, 0);
+  else
+    hipLaunchKernelGGL(k_qual<false>, dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
+                       ctx->d_qual.p, (QualPart *)nullptr, 0);
   if (hipGetLastError() != hipSuccess) { ctx->err = "k_qual launch"; return 0; }
   ctx->have_qual = true;
   if (qual) {
@@ -416,12 +585,19 @@ int pmx_qualhisto_device(pmx_ctx *ctx, int use_stored, void *dev_result) {
   StatArgs A{};
   if (!stat_args(ctx, A)) return 0;
   if (use_stored && !ctx->have_qual) { ctx->err = "pmx_qualhisto: no stored quality"; return 0; }
-  if (!ensure_red(ctx, sizeof(QualPart) * (stat_blocks(ctx->ne) + 1))) return 0;
+  if (!ensure_red(ctx, sizeof(QualPart) * (stat_blocks(ctx->ne) + FINAL_GRID + 1))) return 0;
   QualPart *parts = (QualPart *)ctx->d_red.p;
-  hipLaunchKernelGGL(k_qual, dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
-                     use_stored ? ctx->d_qual.p : (double *)nullptr, parts, use_stored);
-  QualPart *res = dev_result ? (QualPart *)dev_result : parts + stat_blocks(ctx->ne);
-  hipLaunchKernelGGL(k_qual_final, dim3(1), dim3(256), 0, ctx->stream, parts, stat_blocks(ctx->ne), res);
+  if (A.msize == 6)
+    hipLaunchKernelGGL(k_qual<true>, dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
+                       use_stored ? ctx->d_qual.p : (double *)nullptr, parts, use_stored);
+  else
+    hipLaunchKernelGGL(k_qual<false>, dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
+                       use_stored ? ctx->d_qual.p : (double *)nullptr, parts, use_stored);
+  QualPart *mid = parts + stat_blocks(ctx->ne);
+  QualPart *res = dev_result ? (QualPart *)dev_result : mid + FINAL_GRID;
+  hipLaunchKernelGGL(k_qual_final, dim3(FINAL_GRID), dim3(256), 0, ctx->stream, parts,
+                     stat_blocks(ctx->ne), mid);
+  hipLaunchKernelGGL(k_qual_final, dim3(1), dim3(256), 0, ctx->stream, mid, FINAL_GRID, res);
   return hipGetLastError() == hipSuccess;
 }
 
@@ -431,7 +607,7 @@ int pmx_qualhisto(pmx_ctx *ctx, pmx_qual_stats *st) {
   if (!pmx_qualhisto_device(ctx, 0, nullptr)) return 0;
   QualPart r;
   if (hipStreamSynchronize(ctx->stream) != hipSuccess) return 0;
-  if (hipMemcpy(&r, (QualPart *)ctx->d_red.p + stat_blocks(ctx->ne), sizeof r, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  if (hipMemcpy(&r, (QualPart *)ctx->d_red.p + stat_blocks(ctx->ne) + FINAL_GRID, sizeof r, hipMemcpyDeviceToHost) != hipSuccess) return 0;
   st->ne = r.ne;
   st->np = ctx->np;
   st->max = r.max;
@@ -444,16 +620,33 @@ int pmx_qualhisto(pmx_ctx *ctx, pmx_qual_stats *st) {
   return 1;
 }
 
+// result slot of the prilen reduction in d_red (after both partial arrays)
+static int64_t len_res_slot(pmx_ctx *ctx) { return 2 * (int64_t)stat_blocks(ctx->ne) + FINAL_GRID; }
+
 int pmx_prilen_device(pmx_ctx *ctx, const uint16_t *dtag, void *dev_result) {
   StatArgs A{};
   if (!stat_args(ctx, A)) return 0;
   if (ctx->sd.imet < 0) { ctx->err = "pmx_prilen: no metric"; return 0; }
+  if (ctx->ne >= (1LL << 29)) { ctx->err = "pmx_prilen: ne >= 2^29 per group"; return 0; }
   A.ptag = dtag;
-  if (!ensure_red(ctx, sizeof(LenPart) * (stat_blocks(ctx->ne) + 1))) return 0;
+  const int nb = stat_blocks(ctx->ne);
+  if (!ensure_red(ctx, sizeof(LenPart) * (2 * (size_t)nb + FINAL_GRID + 1))) return 0;
   LenPart *parts = (LenPart *)ctx->d_red.p;
-  hipLaunchKernelGGL(k_prilen, dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A, parts);
-  LenPart *res = dev_result ? (LenPart *)dev_result : parts + stat_blocks(ctx->ne);
-  hipLaunchKernelGGL(k_prilen_final, dim3(1), dim3(256), 0, ctx->stream, parts, stat_blocks(ctx->ne), res);
+  LenPart *res = dev_result ? (LenPart *)dev_result : parts + len_res_slot(ctx);
+  if (!dgrow_u8(ctx, ctx->d_emask, (size_t)(ctx->ne + 1)) ||
+      !dgrow_u32(ctx, ctx->d_elist, (size_t)(6 * ctx->ne + 1)) ||
+      !dgrow_u32(ctx, ctx->d_bcount, (size_t)nb + 1))
+    return 0;
+  unsigned *bc = ctx->d_bcount.p, *total = ctx->d_bcount.p + nb;
+  hipLaunchKernelGGL(k_len_mark, dim3(nb), dim3(256), 0, ctx->stream, A, parts, ctx->d_emask.p, bc);
+  hipLaunchKernelGGL(k_len_scan, dim3(1), dim3(256), 0, ctx->stream, bc, nb, total);
+  hipLaunchKernelGGL(k_len_compact, dim3(nb), dim3(256), 0, ctx->stream, ctx->d_emask.p, ctx->ne, bc,
+                     ctx->d_elist.p);
+  hipLaunchKernelGGL(k_len_rotate, dim3(nb), dim3(256), 0, ctx->stream, A, ctx->d_elist.p, total,
+                     parts + nb);
+  LenPart *mid = parts + 2 * nb;
+  hipLaunchKernelGGL(k_prilen_final, dim3(FINAL_GRID), dim3(256), 0, ctx->stream, parts, 2 * nb, mid);
+  hipLaunchKernelGGL(k_prilen_final, dim3(1), dim3(256), 0, ctx->stream, mid, FINAL_GRID, res);
   return hipGetLastError() == hipSuccess;
 }
 
@@ -474,7 +667,7 @@ int pmx_prilen(pmx_ctx *ctx, const uint16_t *point_tag, int64_t tag_stride, int 
   LenPart res;
   if (r) {
     r = hipStreamSynchronize(ctx->stream) == hipSuccess &&
-        hipMemcpy(&res, (LenPart *)ctx->d_red.p + stat_blocks(ctx->ne), sizeof res, hipMemcpyDeviceToHost) == hipSuccess;
+        hipMemcpy(&res, (LenPart *)ctx->d_red.p + len_res_slot(ctx), sizeof res, hipMemcpyDeviceToHost) == hipSuccess;
   }
   if (dtag) hipFree(dtag);
   if (!r) return 0;

@@ -47,6 +47,26 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+class _locked:
+    """Inter-process lock around a build step: the ranks of a multi-GPU job
+    all call the build; one compiles, the others wait and find it fresh."""
+
+    def __init__(self, name: str):
+        self.path = os.path.join(PKG, f".{name}.lock")
+
+    def __enter__(self):
+        import fcntl
+        self.f = open(self.path, "w")
+        fcntl.flock(self.f, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        import fcntl
+        fcntl.flock(self.f, fcntl.LOCK_UN)
+        self.f.close()
+        return False
+
+
 def _run(cmd: list[str]) -> None:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -59,18 +79,23 @@ def build_transfer(force: bool = False) -> str:
     deps = srcs + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     deps.append(os.path.join(INC, "pmx_transfer.h"))
     if force or _stale(TRANSFER_SO, deps):
-        tmp = TRANSFER_SO + ".tmp"
-        _run([_hipcc(), *HIPCC_FLAGS, "-I", INC, "-I", CSRC, *srcs, "-o", tmp])
-        os.replace(tmp, TRANSFER_SO)
+        with _locked("transfer"):
+            if force or _stale(TRANSFER_SO, deps):
+                tmp = TRANSFER_SO + f".{os.getpid()}.tmp"
+                _run([_hipcc(), *HIPCC_FLAGS, "-I", INC, "-I", CSRC, *srcs, "-o", tmp])
+                os.replace(tmp, TRANSFER_SO)
     return TRANSFER_SO
 
 
 def build_meshgen(force: bool = False) -> str:
     src = os.path.join(CSRC, "meshgen.c")
     if force or _stale(MESHGEN_SO, [src]):
-        tmp = MESHGEN_SO + ".tmp"
-        _run(["gcc", "-O2", "-std=c99", "-fPIC", "-shared", "-fopenmp", src, "-o", tmp, "-lm"])
-        os.replace(tmp, MESHGEN_SO)
+        with _locked("meshgen"):
+            if force or _stale(MESHGEN_SO, [src]):
+                tmp = MESHGEN_SO + f".{os.getpid()}.tmp"
+                _run(["gcc", "-O2", "-std=c99", "-fPIC", "-shared", "-fopenmp", src, "-o", tmp,
+                      "-lm"])
+                os.replace(tmp, MESHGEN_SO)
     return MESHGEN_SO
 
 
@@ -78,12 +103,14 @@ def build_oracle(force: bool = False) -> str:
     srcs = [os.path.join(ORACLE, f) for f in sorted(os.listdir(ORACLE)) if f.endswith(".c")]
     deps = srcs + [os.path.join(ORACLE, "pmx_oracle.h")]
     if force or _stale(ORACLE_SO, deps):
-        tmp = ORACLE_SO + ".tmp"
-        # x86-64 baseline (SSE2, no FMA), no contraction: the reference's
-        # Release arithmetic (CMakeLists.txt:100-116) without -ffast-math
-        _run(["gcc", "-O2", "-std=c99", "-fPIC", "-shared", "-ffp-contract=off",
-              "-fno-fast-math", *srcs, "-o", tmp, "-lm"])
-        os.replace(tmp, ORACLE_SO)
+        with _locked("oracle"):
+            if force or _stale(ORACLE_SO, deps):
+                tmp = ORACLE_SO + f".{os.getpid()}.tmp"
+                # x86-64 baseline (SSE2, no FMA), no contraction: the reference's
+                # Release arithmetic (CMakeLists.txt:100-116) without -ffast-math
+                _run(["gcc", "-O2", "-std=c99", "-fPIC", "-shared", "-ffp-contract=off",
+                      "-fno-fast-math", *srcs, "-o", tmp, "-lm"])
+                os.replace(tmp, ORACLE_SO)
     return ORACLE_SO
 
 

@@ -154,19 +154,15 @@ __device__ __forceinline__ double qarea(D3 a, D3 b, D3 c, D3 n) {
 struct Bary { double val[4]; int idx[4]; };
 
 // PMMG_barycoord2d_compute + sort + isInside (src/barycoord_pmmg.c:191-223,
-// :274-284) on the geometry of tria g with the normal of tria kn
-__device__ bool tria_eval(const BdyArgs &A, int g, int kn, D3 p, Bary &b) {
-  TriRec t = A.tris[g];
-  Pt4 nn = A.trn[kn];
-  D3 n{nn.x, nn.y, nn.z};
-  D3 c = ld3(A.pts, t.v[0]);
+// :274-284) on the geometry P (area) of a tria with the unit normal n;
+// returns the signed normal distance h in b.val[3]
+__device__ __forceinline__ bool tria_eval_pre(const D3 P[3], D3 n, double area, D3 p, Bary &b) {
+  const D3 c = P[0];
   double h = 0.0;
   h += (p.x - c.x) * n.x;
   h += (p.y - c.y) * n.y;
   h += (p.z - c.z) * n.z;
   D3 q{p.x - h * n.x, p.y - h * n.y, p.z - h * n.z};
-  double area = A.trn[g].w;
-  D3 P[3] = {ld3(A.pts, t.v[0]), ld3(A.pts, t.v[1]), ld3(A.pts, t.v[2])};
   b.val[0] = qarea(q, P[1], P[2], n) / area;
   b.val[1] = qarea(q, P[2], P[0], n) / area;
   b.val[2] = qarea(q, P[0], P[1], n) / area;
@@ -174,6 +170,13 @@ __device__ bool tria_eval(const BdyArgs &A, int g, int kn, D3 p, Bary &b) {
   b.val[3] = h; b.idx[3] = 3;
   sort3(b.val, b.idx);
   return b.val[0] > -PMX_EPS;
+}
+
+__device__ bool tria_eval(const BdyArgs &A, int g, int kn, D3 p, Bary &b) {
+  const TriRec t = A.tris[g];
+  const Pt4 nn = A.trn[kn];
+  const D3 P[3] = {ld3(A.pts, t.v[0]), ld3(A.pts, t.v[1]), ld3(A.pts, t.v[2])};
+  return tria_eval_pre(P, D3{nn.x, nn.y, nn.z}, A.trn[g].w, p, b);
 }
 
 __device__ __forceinline__ double norm3(double a, double b, double c) {
@@ -184,40 +187,39 @@ __device__ __forceinline__ double norm3(double a, double b, double c) {
   return sqrt(r);
 }
 
-// centroid distance of tria g (closest tracking, src/locate_pmmg.c:398-416)
-__device__ __forceinline__ double centroid_dist(const BdyArgs &A, int g, D3 p) {
-  TriRec t = A.tris[g];
+// centroid distance of a tria (closest tracking, src/locate_pmmg.c:398-416)
+__device__ __forceinline__ double centroid_dist_pre(const D3 P[3], D3 p) {
   double d0 = p.x, d1 = p.y, d2 = p.z;
+#pragma unroll
   for (int j = 0; j < 3; j++) {
-    D3 c = ld3(A.pts, t.v[j]);
-    d0 -= c.x / 3.0;
-    d1 -= c.y / 3.0;
-    d2 -= c.z / 3.0;
+    d0 -= P[j].x / 3.0;
+    d1 -= P[j].y / 3.0;
+    d2 -= P[j].z / 3.0;
   }
   return norm3(d0, d1, d2);
 }
-
-// PMMG_locateChkDistTria (src/locate_pmmg.c:347-366)
-__device__ __forceinline__ bool chk_dist(const BdyArgs &A, int g, int kn, D3 p) {
-  TriRec t = A.tris[g];
-  Pt4 nn = A.trn[kn];
-  D3 c = ld3(A.pts, t.v[0]);
-  double h = 0.0;
-  h += (p.x - c.x) * nn.x;
-  h += (p.y - c.y) * nn.y;
-  h += (p.z - c.z) * nn.z;
-  return !(fabs(h) > A.hausd);
+__device__ __forceinline__ double centroid_dist(const BdyArgs &A, int g, D3 p) {
+  const TriRec t = A.tris[g];
+  const D3 P[3] = {ld3(A.pts, t.v[0]), ld3(A.pts, t.v[1]), ld3(A.pts, t.v[2])};
+  return centroid_dist_pre(P, p);
 }
 
-// PMMG_locatePointInTria (src/locate_pmmg.c:385-423), geometry g, normal kn
+// PMMG_locatePointInTria (src/locate_pmmg.c:385-423), geometry g, normal kn:
+// the tria, its normal and its 3 vertices are gathered once; the evaluation,
+// the centroid distance and PMMG_locateChkDistTria (:347-366, the same h as
+// the evaluation: vertex 0 of g against the normal of kn) share them
 template <class St>
-__device__ bool in_tria(const BdyArgs &A, St &s, int g, int kn, D3 p, Bary &b, double &cdist,
+__device__ __forceinline__ bool in_tria(const BdyArgs &A, St &s, int g, int kn, D3 p, Bary &b, double &cdist,
                         int &ctria) {
   mark_visited(s, g);
-  bool found = tria_eval(A, g, kn, p, b);
-  double nrm = centroid_dist(A, g, p);
+  const TriRec t = A.tris[g];
+  const Pt4 nn = A.trn[kn];
+  const double area = A.trn[g].w;
+  const D3 P[3] = {ld3(A.pts, t.v[0]), ld3(A.pts, t.v[1]), ld3(A.pts, t.v[2])};
+  const bool found = tria_eval_pre(P, D3{nn.x, nn.y, nn.z}, area, p, b);
+  const double nrm = centroid_dist_pre(P, p);
   if (nrm < cdist) { cdist = nrm; ctria = kn; }
-  if (!chk_dist(A, g, kn, p)) return false;
+  if (fabs(b.val[3]) > A.hausd) return false;
   return found;
 }
 

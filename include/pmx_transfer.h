@@ -130,6 +130,31 @@ void *pmx_device_buffer(pmx_ctx *ctx, int which);
  * returns the number of cells (0 on error). */
 int64_t pmx_debug_hint_grid(pmx_ctx *ctx, int *host, int64_t cap);
 
+/* ---- background topology on the device (the old-group
+ * snapshot of src/grpsplit_pmmg.c:207-418) ------------------------------- */
+
+/* Tet face adjacency, Mmg layout: adja[4*(k-1)+1+f] = 4*k'+f' (0 = boundary),
+ * 4*ne+5 ints.  Replaces MMG3D_hashTetra's adjacency (called by ParMmg at
+ * src/libparmmg1.c:272, src/distributemesh_pmmg.c:1185, src/metis_pmmg.c:756).
+ * Tets with v[0] <= 0 are skipped.  Returns 1, or 0 on error / non-manifold
+ * faces (pmx_last_error).  pmx_upload_background builds it the same way when
+ * its mesh view has adja == NULL. */
+int pmx_build_adja(pmx_ctx *ctx, int64_t ne, int64_t np, const int *tetra_v,
+                   int64_t tetra_stride, int *adja);
+
+/* Boundary trias (faces with adja 0) in (tet, face) order, vertices in
+ * MMG5_idir order: tria[3*k+j], k = 1..nt (row 0 unused, maxnt rows at most);
+ * and, if adjt != NULL, their edge adjacency adjt[3*(k-1)+1+e] = 3*k'+e'
+ * (edge e = vertices (e+1)%3, (e+2)%3; 0 unless exactly 2 trias share it).
+ * Replaces MMG5_chkBdryTria + MMG3D_hashTria on the snapshot
+ * (src/grpsplit_pmmg.c:403-414).  Returns nt, or -1 on error. */
+int64_t pmx_build_bdry(pmx_ctx *ctx, int64_t ne, int64_t np, const int *tetra_v,
+                       int64_t tetra_stride, const int *adja, int *tria, int64_t maxnt,
+                       int *adjt);
+
+/* Device time (ms) of the last pmx_build_adja / pmx_build_bdry. */
+double pmx_topo_ms(pmx_ctx *ctx);
+
 /* Kernel timing of the last pmx_run with opts.timing != 0, in ms:
  * which = 0 hint build, 1 volume locate+interp, 2 surface locate+interp,
  * 3 exhaustive fallback, 4 total. */

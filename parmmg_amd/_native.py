@@ -96,6 +96,11 @@ SIGNATURES = {
     "pmx_locate_stats_get": (C.c_int, [C.c_void_p, C.POINTER(LocateStats)]),
     "pmx_device_buffer": (C.c_void_p, [C.c_void_p, C.c_int]),
     "pmx_debug_hint_grid": (C.c_int64, [C.c_void_p, C.c_void_p, C.c_int64]),
+    "pmx_build_adja": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64,
+                                 C.c_void_p]),
+    "pmx_build_bdry": (C.c_int64, [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64,
+                                   C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]),
+    "pmx_topo_ms": (C.c_double, [C.c_void_p]),
     "pmx_kernel_ms": (C.c_double, [C.c_void_p, C.c_int]),
     "pmx_timing_reset": (C.c_int, [C.c_void_p]),
     "PMX_interpMetricsAndFields": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(Group), iptr, C.c_int]),

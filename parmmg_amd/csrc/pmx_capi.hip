@@ -116,9 +116,17 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     ctx->err = "pmx_upload_background: mesh sizes out of range";
     return 0;
   }
-  if (!m->point_c || !m->tetra_v || !m->adja) {
-    ctx->err = "pmx_upload_background: point_c, tetra_v and adja are required";
+  if (!m->point_c || !m->tetra_v) {
+    ctx->err = "pmx_upload_background: point_c and tetra_v are required";
     return 0;
+  }
+  // no adjacency given (MMG3D_hashTetra not run on the host): face matching on
+  // the device (pmx_topo.hip)
+  std::vector<int> built_adja;
+  const int *adja_in = m->adja;
+  if (!adja_in) {
+    if (!pmx_ctx_build_adja_host(ctx, m, built_adja)) return 0;
+    adja_in = built_adja.data();
   }
   if (nsol < 0 || nsol > PMX_MAX_SOLS || imet >= nsol) {
     ctx->err = "pmx_upload_background: bad solution list";
@@ -149,7 +157,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     TetRec &r = ht[(size_t)k];
     for (int l = 0; l < 4; l++) {
       r.v[l] = v[l];
-      r.nb[l] = m->adja[4 * (k - 1) + 1 + l] / 4;
+      r.nb[l] = adja_in[4 * (k - 1) + 1 + l] / 4;
     }
   }
   // solutions -> interleaved [np+1][S]

@@ -79,6 +79,7 @@ struct pmx_ctx {
   bool have_qual = false;
 
   // timing
+  double topo_ms = 0.0;                 // device time of the last topology build
   std::vector<hipEvent_t> events;
   int ev_used = 0;
 
@@ -90,5 +91,6 @@ struct pmx_ctx {
   bool launch_tet_locate(const VolArgs &a, const pmx_run_opts &o, hipStream_t s);
 };
 
+bool pmx_ctx_build_adja_host(pmx_ctx *ctx, const pmx_mesh_view *m, std::vector<int> &adja);
 void launch_tria_normals(const TriRec *tris, const Pt4 *pts, int64_t nt, Pt4 *trn, hipStream_t s);
 extern "C" int pmx_timing_reset(pmx_ctx *ctx);

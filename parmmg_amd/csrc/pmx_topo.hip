@@ -1,0 +1,368 @@
+// pmx_topo.hip -- background-mesh topology on gfx950.
+//
+// pmx_build_adja  <- MMG3D_hashTetra's face adjacency (Mmg; called by ParMmg
+//                    at src/libparmmg1.c:272, src/distributemesh_pmmg.c:1185,
+//                    src/metis_pmmg.c:756, ...): adja[4*(k-1)+1+f] = 4*k'+f'
+// pmx_build_bdry  <- MMG5_chkBdryTria + MMG3D_hashTria on the old-group
+//                    snapshot (src/grpsplit_pmmg.c:400-414): boundary trias
+//                    of the faces without a neighbour, in (tet, face) order,
+//                    vertices in MMG5_idir order, and their edge adjacency
+//                    adjt[3*(k-1)+1+e] = 3*k'+e'
+//
+// Hash-free face matching: every face (edge) record goes to the bucket of its
+// smallest vertex (count, exclusive scan, scatter); a face's partner is the
+// record of the same bucket with the same two other vertices.  Buckets hold
+// ~4 ne / np ~ 24 faces, the threads of one bucket are adjacent and read its
+// records together.  The result does not depend on the order inside a bucket:
+// an interior face of a valid mesh has exactly one partner (a face with more
+// than one is non-manifold: reported, left 0, like the CPU builders of
+// parmmg_amd/csrc/meshgen.c that the tests compare against).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <algorithm>
+#include <string>
+#include <vector>
+#include "pmx_internal.h"
+
+// MMG5_idir: local vertices of face f (opposite vertex f), outward order
+__constant__ int TOPO_IDIR[4][3] = {{1, 2, 3}, {0, 3, 2}, {0, 1, 3}, {0, 2, 1}};
+
+__device__ __forceinline__ void sort3i(int &a, int &b, int &c) {
+  int t;
+  if (a > b) { t = a; a = b; b = t; }
+  if (b > c) { t = b; b = c; c = t; }
+  if (a > b) { t = a; a = b; b = t; }
+}
+
+// ---- tet faces -------------------------------------------------------------------
+
+__global__ __launch_bounds__(256) void k_face_count(const int4 *__restrict__ tv, int64_t ne,
+                                                    unsigned *__restrict__ cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // face index 4(k-1)+f
+  if (i >= 4 * ne) return;
+  const int64_t k = i / 4 + 1;
+  const int f = (int)(i & 3);
+  const int4 t = tv[k];
+  if (t.x <= 0) return;                          // !MG_EOK: no faces
+  const int v[4] = {t.x, t.y, t.z, t.w};
+  int a = v[TOPO_IDIR[f][0]], b = v[TOPO_IDIR[f][1]], c = v[TOPO_IDIR[f][2]];
+  sort3i(a, b, c);
+  atomicAdd(cnt + a, 1u);
+}
+
+__global__ __launch_bounds__(256) void k_face_scatter(const int4 *__restrict__ tv, int64_t ne,
+                                                      unsigned *__restrict__ cursor,
+                                                      int4 *__restrict__ rec) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 4 * ne) return;
+  const int64_t k = i / 4 + 1;
+  const int f = (int)(i & 3);
+  const int4 t = tv[k];
+  if (t.x <= 0) return;                          // !MG_EOK: no faces
+  const int v[4] = {t.x, t.y, t.z, t.w};
+  int a = v[TOPO_IDIR[f][0]], b = v[TOPO_IDIR[f][1]], c = v[TOPO_IDIR[f][2]];
+  sort3i(a, b, c);
+  const unsigned s = atomicAdd(cursor + a, 1u);
+  rec[s] = make_int4(a, b, c, (int)(4 * k + f));
+}
+
+// one thread per record: its partner in the bucket of its smallest vertex
+__global__ __launch_bounds__(256) void k_face_match(const int4 *__restrict__ rec, int64_t nb,
+                                                    const unsigned *__restrict__ off,
+                                                    int *__restrict__ adja,
+                                                    unsigned *__restrict__ nbad) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= (int64_t)off[nb]) return;                // records of valid tets only
+  const int4 me = rec[s];
+  const unsigned lo = off[me.x], hi = off[me.x + 1];
+  int partner = 0, n = 0;
+  for (unsigned r = lo; r < hi; r++) {
+    const int4 o = rec[r];
+    if (r != (unsigned)s && o.y == me.y && o.z == me.z) { partner = o.w; n++; }
+  }
+  adja[me.w - 3] = (n == 1) ? partner : 0;       // 4*(k-1)+1+f = owner - 3
+  if (n > 1) atomicAdd(nbad, 1u);
+}
+
+// ---- boundary trias and their edge adjacency -------------------------------------
+
+__global__ __launch_bounds__(256) void k_bdry_count(const int4 *__restrict__ tv,
+                                                    const int *__restrict__ adja, int64_t ne,
+                                                    unsigned *__restrict__ cnt) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (k > ne) return;
+  unsigned c = 0;
+  if (tv[k].x > 0) {                              // !MG_EOK tets have no faces
+#pragma unroll
+    for (int f = 0; f < 4; f++) c += adja[4 * (k - 1) + 1 + f] == 0 ? 1u : 0u;
+  }
+  cnt[k - 1] = c;
+}
+
+__global__ __launch_bounds__(256) void k_bdry_write(const int4 *__restrict__ tv,
+                                                    const int *__restrict__ adja, int64_t ne,
+                                                    const unsigned *__restrict__ pos,
+                                                    int *__restrict__ tria) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (k > ne) return;
+  const int4 t = tv[k];
+  if (t.x <= 0) return;
+  const int v[4] = {t.x, t.y, t.z, t.w};
+  int64_t p = pos[k - 1] + 1;                    // 1-based tria index, (k, f) order
+  for (int f = 0; f < 4; f++) {
+    if (adja[4 * (k - 1) + 1 + f]) continue;
+    tria[3 * p + 0] = v[TOPO_IDIR[f][0]];
+    tria[3 * p + 1] = v[TOPO_IDIR[f][1]];
+    tria[3 * p + 2] = v[TOPO_IDIR[f][2]];
+    p++;
+  }
+}
+
+// edge e of tria k joins its vertices (e+1)%3 and (e+2)%3
+__global__ __launch_bounds__(256) void k_edge_count(const int *__restrict__ tria, int64_t nt,
+                                                    unsigned *__restrict__ cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // 3(k-1)+e
+  if (i >= 3 * nt) return;
+  const int64_t k = i / 3 + 1;
+  const int e = (int)(i % 3);
+  const int a = tria[3 * k + (e + 1) % 3], b = tria[3 * k + (e + 2) % 3];
+  atomicAdd(cnt + min(a, b), 1u);
+}
+
+__global__ __launch_bounds__(256) void k_edge_scatter(const int *__restrict__ tria, int64_t nt,
+                                                      unsigned *__restrict__ cursor,
+                                                      int2 *__restrict__ rec) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 3 * nt) return;
+  const int64_t k = i / 3 + 1;
+  const int e = (int)(i % 3);
+  const int a = tria[3 * k + (e + 1) % 3], b = tria[3 * k + (e + 2) % 3];
+  const unsigned s = atomicAdd(cursor + min(a, b), 1u);
+  rec[s] = make_int2(max(a, b), (int)(3 * k + e));
+}
+
+__global__ __launch_bounds__(256) void k_edge_match(const int2 *__restrict__ rec, int64_t nrec,
+                                                    const unsigned *__restrict__ off,
+                                                    const int *__restrict__ bucket_of,
+                                                    int *__restrict__ adjt) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nrec) return;
+  const int2 me = rec[s];
+  const int a = bucket_of[s];
+  const unsigned lo = off[a], hi = off[a + 1];
+  int partner = 0, n = 0;
+  for (unsigned r = lo; r < hi; r++) {
+    const int2 o = rec[r];
+    if (r != (unsigned)s && o.x == me.x) { partner = o.y; n++; }
+  }
+  adjt[me.y - 2] = (n == 1) ? partner : 0;       // 3*(k-1)+1+e = owner - 2
+}
+
+// bucket index of every record (the records of bucket a fill [off[a], off[a+1]))
+__global__ __launch_bounds__(256) void k_bucket_of(const unsigned *__restrict__ off, int64_t nb,
+                                                   int *__restrict__ bucket_of) {
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= nb) return;
+  for (unsigned r = off[a]; r < off[a + 1]; r++) bucket_of[r] = (int)a;
+}
+
+// ---- host side ---------------------------------------------------------------------
+
+namespace {
+
+struct Scratch {
+  std::vector<void *> p;
+  ~Scratch() {
+    for (void *q : p) hipFree(q);
+  }
+  template <class T> T *get(size_t n) {
+    void *q = nullptr;
+    if (hipMalloc(&q, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) return nullptr;
+    p.push_back(q);
+    return (T *)q;
+  }
+};
+
+unsigned nblk(int64_t n) { return (unsigned)std::max<int64_t>((n + 255) / 256, 1); }
+
+// exclusive scan of n counts into off[0..n] (off[n] = total)
+bool scan_counts(const unsigned *cnt, unsigned *off, int64_t n, hipStream_t s, Scratch &sc) {
+  size_t bytes = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, cnt, off, (int)(n + 1), s);
+  void *tmp = sc.get<char>(bytes);
+  if (!tmp) return false;
+  return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, cnt, off, (int)(n + 1), s) == hipSuccess;
+}
+
+// strided host connectivity -> device int4 stream (1-based, slot 0 zero)
+int4 *upload_tets(pmx_ctx *ctx, int64_t ne, int64_t np, const int *tetra_v, int64_t stride,
+                  Scratch &sc) {
+  std::vector<int4> h((size_t)(ne + 1));
+  h[0] = make_int4(0, 0, 0, 0);
+  const char *tc = (const char *)tetra_v;
+  for (int64_t k = 1; k <= ne; k++) {
+    const int *v = (const int *)(tc + k * stride);
+    if (v[0] <= 0) { h[(size_t)k] = make_int4(0, 0, 0, 0); continue; }   // !MG_EOK
+    for (int l = 0; l < 4; l++)
+      if (v[l] < 1 || v[l] > np) {
+        ctx->err = "topology: tet vertex index out of range";
+        return nullptr;
+      }
+    h[(size_t)k] = make_int4(v[0], v[1], v[2], v[3]);
+  }
+  int4 *d = sc.get<int4>(h.size());
+  if (!d) return nullptr;
+  if (hipMemcpyAsync(d, h.data(), h.size() * sizeof(int4), hipMemcpyHostToDevice, ctx->stream) !=
+      hipSuccess)
+    return nullptr;
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return nullptr;
+  return d;
+}
+
+bool topo_fail(pmx_ctx *ctx, const char *what) {
+  ctx->err = what;
+  return false;
+}
+
+// device adjacency from the device connectivity stream
+bool build_adja_dev(pmx_ctx *ctx, const int4 *tv, int64_t ne, int64_t np, int *dadja, Scratch &sc,
+                    unsigned *nbad_out) {
+  hipStream_t s = ctx->stream;
+  unsigned *cnt = sc.get<unsigned>((size_t)(np + 2));
+  unsigned *off = sc.get<unsigned>((size_t)(np + 2));
+  int4 *rec = sc.get<int4>((size_t)(4 * ne));
+  unsigned *nbad = sc.get<unsigned>(1);
+  if (!cnt || !off || !rec || !nbad) return topo_fail(ctx, "pmx_build_adja: hipMalloc");
+  hipMemsetAsync(cnt, 0, sizeof(unsigned) * (size_t)(np + 2), s);
+  hipMemsetAsync(nbad, 0, sizeof(unsigned), s);
+  hipMemsetAsync(dadja, 0, sizeof(int) * (size_t)(4 * ne + 5), s);
+  hipLaunchKernelGGL(k_face_count, dim3(nblk(4 * ne)), dim3(256), 0, s, tv, ne, cnt);
+  if (!scan_counts(cnt, off, np + 1, s, sc)) return topo_fail(ctx, "pmx_build_adja: scan");
+  hipMemcpyAsync(cnt, off, sizeof(unsigned) * (size_t)(np + 2), hipMemcpyDeviceToDevice, s);
+  hipLaunchKernelGGL(k_face_scatter, dim3(nblk(4 * ne)), dim3(256), 0, s, tv, ne, cnt, rec);
+  hipLaunchKernelGGL(k_face_match, dim3(nblk(4 * ne)), dim3(256), 0, s, rec, np + 1, off, dadja,
+                     nbad);
+  if (hipMemcpyAsync(nbad_out, nbad, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return topo_fail(ctx, "pmx_build_adja: launch");
+  return true;
+}
+
+}  // namespace
+
+// internal: adjacency of the tets of an upload without one (pmx_upload_background)
+bool pmx_ctx_build_adja_host(pmx_ctx *ctx, const pmx_mesh_view *m, std::vector<int> &adja) {
+  Scratch sc;
+  int4 *tv = upload_tets(ctx, m->ne, m->np, m->tetra_v, m->tetra_stride, sc);
+  if (!tv) return topo_fail(ctx, "pmx_upload_background: adjacency upload");
+  int *dadja = sc.get<int>((size_t)(4 * m->ne + 5));
+  unsigned nbad = 0;
+  if (!dadja || !build_adja_dev(ctx, tv, m->ne, m->np, dadja, sc, &nbad)) return false;
+  adja.resize((size_t)(4 * m->ne + 5));
+  if (hipMemcpy(adja.data(), dadja, adja.size() * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+    return topo_fail(ctx, "pmx_upload_background: adjacency download");
+  if (nbad) return topo_fail(ctx, "pmx_upload_background: non-manifold tet faces");
+  return true;
+}
+
+extern "C" {
+
+int pmx_build_adja(pmx_ctx *ctx, int64_t ne, int64_t np, const int *tetra_v, int64_t tetra_stride,
+                   int *adja) {
+  if (!ctx || !tetra_v || !adja || ne < 1 || np < 1 || 4 * ne >= (1LL << 31)) {
+    if (ctx) ctx->err = "pmx_build_adja: bad arguments";
+    return 0;
+  }
+  hipSetDevice(ctx->device);
+  Scratch sc;
+  int4 *tv = upload_tets(ctx, ne, np, tetra_v, tetra_stride, sc);
+  if (!tv) return 0;                             // pmx_last_error says why
+  int *dadja = sc.get<int>((size_t)(4 * ne + 5));
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  hipEventRecord(e0, ctx->stream);
+  unsigned nbad = 0;
+  const bool ok = dadja && build_adja_dev(ctx, tv, ne, np, dadja, sc, &nbad);
+  hipEventRecord(e1, ctx->stream);
+  hipEventSynchronize(e1);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, e0, e1);
+  ctx->topo_ms = ms;
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  if (!ok) return 0;
+  if (hipMemcpy(adja, dadja, sizeof(int) * (size_t)(4 * ne + 5), hipMemcpyDeviceToHost) != hipSuccess)
+    return topo_fail(ctx, "pmx_build_adja: download"), 0;
+  if (nbad) return topo_fail(ctx, "pmx_build_adja: non-manifold tet faces (left 0)"), 0;
+  return 1;
+}
+
+int64_t pmx_build_bdry(pmx_ctx *ctx, int64_t ne, int64_t np, const int *tetra_v,
+                       int64_t tetra_stride, const int *adja, int *tria, int64_t maxnt, int *adjt) {
+  if (!ctx || !tetra_v || !adja || !tria || ne < 1 || np < 1) {
+    if (ctx) ctx->err = "pmx_build_bdry: bad arguments";
+    return -1;
+  }
+  hipSetDevice(ctx->device);
+  hipStream_t s = ctx->stream;
+  Scratch sc;
+  int4 *tv = upload_tets(ctx, ne, np, tetra_v, tetra_stride, sc);
+  int *dadja = sc.get<int>((size_t)(4 * ne + 5));
+  unsigned *tcnt = sc.get<unsigned>((size_t)(ne + 1));
+  unsigned *tpos = sc.get<unsigned>((size_t)(ne + 1));
+  if (!tv || !dadja || !tcnt || !tpos) return topo_fail(ctx, "pmx_build_bdry: hipMalloc"), -1;
+  hipMemcpyAsync(dadja, adja, sizeof(int) * (size_t)(4 * ne + 5), hipMemcpyHostToDevice, s);
+  hipMemsetAsync(tcnt, 0, sizeof(unsigned) * (size_t)(ne + 1), s);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  hipEventRecord(e0, s);
+  hipLaunchKernelGGL(k_bdry_count, dim3(nblk(ne)), dim3(256), 0, s, tv, dadja, ne, tcnt);
+  if (!scan_counts(tcnt, tpos, ne, s, sc)) return topo_fail(ctx, "pmx_build_bdry: scan"), -1;
+  unsigned nt_u = 0;
+  hipMemcpyAsync(&nt_u, tpos + ne, sizeof(unsigned), hipMemcpyDeviceToHost, s);
+  hipStreamSynchronize(s);
+  const int64_t nt = nt_u;
+  if (nt > maxnt) return topo_fail(ctx, "pmx_build_bdry: more boundary faces than maxnt"), -1;
+  int *dtria = sc.get<int>((size_t)(3 * (nt + 1)));
+  if (!dtria) return topo_fail(ctx, "pmx_build_bdry: hipMalloc"), -1;
+  hipMemsetAsync(dtria, 0, sizeof(int) * 3, s);
+  hipLaunchKernelGGL(k_bdry_write, dim3(nblk(ne)), dim3(256), 0, s, tv, dadja, ne, tpos, dtria);
+  int *dadjt = nullptr;
+  if (adjt && nt > 0) {
+    unsigned *cnt = sc.get<unsigned>((size_t)(np + 2));
+    unsigned *off = sc.get<unsigned>((size_t)(np + 2));
+    int2 *rec = sc.get<int2>((size_t)(3 * nt));
+    int *bof = sc.get<int>((size_t)(3 * nt));
+    dadjt = sc.get<int>((size_t)(3 * nt + 4));
+    if (!cnt || !off || !rec || !bof || !dadjt) return topo_fail(ctx, "pmx_build_bdry: hipMalloc"), -1;
+    hipMemsetAsync(cnt, 0, sizeof(unsigned) * (size_t)(np + 2), s);
+    hipMemsetAsync(dadjt, 0, sizeof(int) * (size_t)(3 * nt + 4), s);
+    hipLaunchKernelGGL(k_edge_count, dim3(nblk(3 * nt)), dim3(256), 0, s, dtria, nt, cnt);
+    if (!scan_counts(cnt, off, np + 1, s, sc)) return topo_fail(ctx, "pmx_build_bdry: scan"), -1;
+    hipMemcpyAsync(cnt, off, sizeof(unsigned) * (size_t)(np + 2), hipMemcpyDeviceToDevice, s);
+    hipLaunchKernelGGL(k_edge_scatter, dim3(nblk(3 * nt)), dim3(256), 0, s, dtria, nt, cnt, rec);
+    hipLaunchKernelGGL(k_bucket_of, dim3(nblk(np + 1)), dim3(256), 0, s, off, np + 1, bof);
+    hipLaunchKernelGGL(k_edge_match, dim3(nblk(3 * nt)), dim3(256), 0, s, rec, 3 * nt, off, bof,
+                       dadjt);
+  }
+  hipEventRecord(e1, s);
+  hipEventSynchronize(e1);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, e0, e1);
+  ctx->topo_ms = ms;
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  if (hipGetLastError() != hipSuccess) return topo_fail(ctx, "pmx_build_bdry: launch"), -1;
+  if (hipMemcpy(tria, dtria, sizeof(int) * (size_t)(3 * (nt + 1)), hipMemcpyDeviceToHost) != hipSuccess)
+    return topo_fail(ctx, "pmx_build_bdry: download"), -1;
+  if (dadjt &&
+      hipMemcpy(adjt, dadjt, sizeof(int) * (size_t)(3 * nt + 4), hipMemcpyDeviceToHost) != hipSuccess)
+    return topo_fail(ctx, "pmx_build_bdry: download"), -1;
+  return nt;
+}
+
+double pmx_topo_ms(pmx_ctx *ctx) { return ctx ? ctx->topo_ms : -1.0; }
+
+}  // extern "C"

@@ -167,6 +167,33 @@ class Transfer:
     def device_buffer(self, which: int) -> int:
         return self.lib.pmx_device_buffer(self.ctx, which) or 0
 
+    # ---- background topology (MMG3D_hashTetra, MMG5_chkBdryTria + hashTria) --
+    def build_adja(self, tet: np.ndarray, np_: int) -> np.ndarray:
+        """Tet face adjacency on the device, Mmg layout (4*ne+5 ints)."""
+        t = np.ascontiguousarray(tet, np.int32)
+        ne = t.shape[0] - 1
+        adja = np.zeros(4 * ne + 5, np.int32)
+        self._chk(self.lib.pmx_build_adja(self.ctx, ne, np_, t.ctypes.data, 16, adja.ctypes.data),
+                  "pmx_build_adja")
+        return adja
+
+    def build_bdry(self, tet: np.ndarray, np_: int, adja: np.ndarray):
+        """Boundary trias ((nt+1, 3), row 0 unused) and their adjacency."""
+        t = np.ascontiguousarray(tet, np.int32)
+        a = np.ascontiguousarray(adja, np.int32)
+        ne = t.shape[0] - 1
+        maxnt = 4 * ne
+        tria = np.zeros((maxnt + 1, 3), np.int32)
+        adjt = np.zeros(3 * maxnt + 4, np.int32)
+        nt = self.lib.pmx_build_bdry(self.ctx, ne, np_, t.ctypes.data, 16, a.ctypes.data,
+                                     tria.ctypes.data, maxnt, adjt.ctypes.data)
+        if nt < 0:
+            raise RuntimeError(f"pmx_build_bdry: {self.lib.pmx_last_error(self.ctx).decode()}")
+        return np.ascontiguousarray(tria[: nt + 1]), np.ascontiguousarray(adjt[: 3 * nt + 4])
+
+    def topo_ms(self) -> float:
+        return self.lib.pmx_topo_ms(self.ctx)
+
     # ---- reference-shaped entry points --------------------------------------
     def interp_metrics_and_fields(self, groups: list[dict], input_met: int = 1,
                                   perm_nod_glob: np.ndarray | None = None) -> int:

@@ -184,11 +184,26 @@ __device__ __forceinline__ unsigned interp_layout(const double *__restrict__ sol
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       const double *row = sol + (int64_t)v[i] * S;
+      if constexpr ((S & 1) == 0) {
+        // even stride: rows are 16-B aligned (upload pads odd S), 16-B loads
 #pragma unroll
-      for (int j = 0; j < S; j++) acc[j] += phi[i] * row[j];
+        for (int j = 0; j < S; j += 2) {
+          const double2 d = *reinterpret_cast<const double2 *>(row + j);
+          acc[j] += phi[i] * d.x;
+          acc[j + 1] += phi[i] * d.y;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < S; j++) acc[j] += phi[i] * row[j];
+      }
     }
+    if constexpr ((S & 1) == 0) {
 #pragma unroll
-    for (int j = 0; j < S; j++) out[j] = acc[j];
+      for (int j = 0; j < S; j += 2) *reinterpret_cast<double2 *>(out + j) = make_double2(acc[j], acc[j + 1]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < S; j++) out[j] = acc[j];
+    }
     return (1u << sd.nsol) - 1u;
   } else {
     return interp_bar<4>(sol, sd, v, phi, out);

@@ -58,7 +58,7 @@ def alg_bytes(N: int, ne: int, np_: int, S: int) -> int:
     return N * (24 + 8 * S + 4) + ne * 32 + np_ * (24 + 8 * S)
 
 
-def profiled_traffic(config: str, kernel: str = "k_walk"):
+def profiled_traffic(config: str, kernel: str = "k_walks"):
     """HBM bytes per launch of the dominant kernel from the newest committed
     rocprofv3 PMC summary of this config (tools/profile.sh ->
     tools/prof_summary.py -> profiles/rNN_<config>_<tag>.json): 2*FETCH_SIZE +
@@ -198,7 +198,7 @@ def main():
         "config": {"workload": f"{args.config}: {cfg['desc']}", "n_cells": cfg["n"], "ne": m.ne,
                    "np": m.np, "nt": m.nt, "new_vertices_per_gpu": npts, "S": S,
                    "groups_per_gpu": 1, "parallelism": f"group-sharded x{world}"},
-        "roofline": {"bound": "hbm", "kernel": "k_walk",
+        "roofline": {"bound": "hbm", "kernel": "k_walks",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                      "traffic": traffic, "traffic_source": traffic_src,

@@ -265,6 +265,9 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   if (!ctx->h_ntlist.empty())
     CK(hipMemcpyAsync(ctx->d_ntlist.p, ctx->h_ntlist.data(), ctx->h_ntlist.size() * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
   if (nt > 0) launch_tria_normals(ctx->d_tris.p, ctx->d_pts.p, nt, ctx->d_trn.p, ctx->stream);
+  // dense coordinates for the walk: the uploaded vertices in a second layout
+  if (!dgrow(ctx, ctx->d_xyz, (size_t)(np + 1) * 3)) return 0;
+  launch_build_xyz(ctx->d_pts.p, np + 1, ctx->d_xyz.p, ctx->stream);
   CK(hipGetLastError());
   CK(hipStreamSynchronize(ctx->stream));   // host staging vectors die here
   ctx->have_bg = true;
@@ -359,6 +362,15 @@ static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &o
   A.block = (opts.tune & 0x40000) ? 1024 : (opts.tune & 0x20000) ? 512 : 256;
   // tune bit 20: central hint (per cell, the sample closest to the centre)
   A.grid64 = (opts.tune & 0x100000) ? ctx->d_grid64.p : nullptr;
+  // tune bits 21-23: k_walk sensitivity experiments (results unchanged):
+  // 1 = every step's f64 face arithmetic done twice, 2 = an extra 32-B tet
+  // record gather per step, 3 = an extra 32-B vertex gather per step
+  A.exp = (opts.tune >> 21) & 7;
+  // tune bit 24: the reference-order walk k_walk instead of the slot walk;
+  // tune bit 25: the slot walk on the 32-B Pt4 records instead of the dense
+  // 24-B coordinates
+  A.ref_walk = (opts.tune & 0x1000000) ? 1 : 0;
+  A.xyz = (opts.tune & 0x2000000) ? nullptr : ctx->d_xyz.p;
 }
 
 int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
@@ -424,7 +436,8 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
       if (A.grid64) launch_fill64(ctx->d_grid64.p, ctx->gcells, st);
       launch_hint_build(ctx->d_tetv.p, packed ? ctx->d_tets_s.p : nullptr, ctx->d_pts.p, ctx->ne,
                         stride, ctx->d_grid.p, ctx->grid, (opts.tune & 0x8000) ? 1 : 0, st,
-                        const_cast<unsigned long long *>(A.grid64));
+                        const_cast<unsigned long long *>(A.grid64),
+                        (opts.tune & 0x4000000) ? nullptr : ctx->d_xyz.p);   // bit 26: Pt4 reads
     }
     if (ctx->nq_bdy && bdy_mode == 3) CK(hipStreamWaitEvent(st, ctx->ev_join, 0));
     if (ev) CK(hipEventRecord(ev[1], st));
@@ -619,7 +632,7 @@ hipEvent_t *pmx_ctx::next_event_slot() {
 }
 
 void pmx_ctx::free_all() {
-  dfree(d_pts); dfree(d_tets); dfree(d_sol); dfree(d_tris); dfree(d_trn); dfree(d_grid); dfree(d_grid64);
+  dfree(d_pts); dfree(d_tets); dfree(d_sol); dfree(d_xyz); dfree(d_tris); dfree(d_trn); dfree(d_grid); dfree(d_grid64);
   dfree(d_ntoff); dfree(d_ntlist);
   dfree(d_q); dfree(d_kind); dfree(d_wmask); dfree(d_out); dfree(d_elem); dfree(d_status);
   dfree(d_steps); dfree(d_start); dfree(d_edge); dfree(d_vertex); dfree(d_list); dfree(d_found);

@@ -31,6 +31,7 @@ struct pmx_ctx {
   DevBuf<Pt4> d_pts;
   DevBuf<TetRec> d_tets;
   DevBuf<double> d_sol;
+  DevBuf<double> d_xyz;                 // dense coordinates, 3 doubles per vertex
   DevBuf<TriRec> d_tris;
   DevBuf<Pt4> d_trn;
   DevBuf<int> d_grid;

@@ -40,6 +40,9 @@ struct VolArgs {
   int64_t region;               // k_walkp: points per region (multiple of 64)
   int block;                    // k_walk threads per block (256 / 512 / 1024)
   const unsigned long long *grid64;  // central hint grid (null: plain int grid)
+  int exp;                      // k_walk sensitivity experiment (0 = production)
+  const double *xyz;            // dense 24-B coordinates (k_build_xyz), null: use pts
+  int ref_walk;                 // 1: k_walk (reference-order walk) instead of k_walks
 };
 
 struct ExhArgs {
@@ -56,11 +59,12 @@ struct ExhArgs {
 
 void launch_hint_build(const int4 *tetv, const int4 *packed, const Pt4 *pts, int64_t ne,
                        int stride, int *grid, GridDesc g, int mid, hipStream_t s,
-                       unsigned long long *grid64 = nullptr);
+                       unsigned long long *grid64 = nullptr, const double *xyz = nullptr);
 void launch_fill64(unsigned long long *p, int64_t n, hipStream_t s);
 void launch_locate_vol(const VolArgs &a, hipStream_t s);
 void launch_walk(const VolArgs &a, hipStream_t s);
 void launch_walkp(const VolArgs &a, hipStream_t s);
+void launch_build_xyz(const Pt4 *pts, int64_t n, double *out, hipStream_t s);
 void launch_tet_conn(const TetRec *src, int64_t stride, int64_t n, int4 *dst, hipStream_t s);
 void launch_exhaustive(const ExhArgs &e, const VolArgs &v, hipStream_t s);
 void launch_const_metric(const int8_t *kind, int64_t nq, double *out, int S, int off, int size,

@@ -72,12 +72,13 @@ __device__ int hint_lookup(const int *grid, const GridDesc &g, D3 p) {
   return 1;
 }
 
-template <bool MID, bool CENTRAL>
+template <bool MID, bool CENTRAL, bool DX = false>
 __global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ src, int64_t sstride,
                                                     const Pt4 *__restrict__ pts, int64_t ne,
                                                     int stride, int *__restrict__ grid,
                                                     GridDesc g,
-                                                    unsigned long long *__restrict__ grid64) {
+                                                    unsigned long long *__restrict__ grid64,
+                                                    const double *__restrict__ xyz = nullptr) {
   // one sample per thread; XCD-aware block order: each XCD's L2 serves a
   // contiguous range of samples, i.e. neighbouring tets sharing vertices
   const int64_t n = (ne + stride - 1) / stride;
@@ -94,7 +95,12 @@ __global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ src
     const D3 a = ld3(pts, v.x), b = ld3(pts, v.y);
     m = D3{(a.x + b.x) * 0.5, (a.y + b.y) * 0.5, (a.z + b.z) * 0.5};
   } else {
-    const D3 a = ld3(pts, v.x), b = ld3(pts, v.y), c = ld3(pts, v.z), d = ld3(pts, v.w);
+    // DX: from the dense 24-B coordinates (VolArgs::xyz)
+    auto ldp = [&](int i) -> D3 {
+      if constexpr (DX) return D3{xyz[3 * (int64_t)i], xyz[3 * (int64_t)i + 1], xyz[3 * (int64_t)i + 2]};
+      else return ld3(pts, i);
+    };
+    const D3 a = ldp(v.x), b = ldp(v.y), c = ldp(v.z), d = ldp(v.w);
     m = D3{(a.x + b.x + c.x + d.x) * 0.25, (a.y + b.y + c.y + d.y) * 0.25,
            (a.z + b.z + c.z + d.z) * 0.25};
   }
@@ -552,20 +558,23 @@ void launch_prologue(uint8_t *wmask, int64_t n, unsigned *counts, int *grid, int
 
 void launch_hint_build(const int4 *tetv, const int4 *packed, const Pt4 *pts, int64_t ne,
                        int stride, int *grid, GridDesc g, int mid, hipStream_t s,
-                       unsigned long long *grid64) {
+                       unsigned long long *grid64, const double *xyz) {
   const int64_t n = (ne + stride - 1) / stride;
   const int64_t nb = std::max<int64_t>((n + 255) / 256, 1);
   const int4 *src = packed ? packed : tetv + 1;
   const int64_t sstride = packed ? 1 : stride;
   if (grid64)
     hipLaunchKernelGGL((k_hint_build<false, true>), dim3((unsigned)nb), dim3(256), 0, s, src, sstride,
-                       pts, ne, stride, grid, g, grid64);
+                       pts, ne, stride, grid, g, grid64, nullptr);
   else if (mid)
     hipLaunchKernelGGL((k_hint_build<true, false>), dim3((unsigned)nb), dim3(256), 0, s, src, sstride,
-                       pts, ne, stride, grid, g, grid64);
+                       pts, ne, stride, grid, g, grid64, nullptr);
+  else if (xyz)
+    hipLaunchKernelGGL((k_hint_build<false, false, true>), dim3((unsigned)nb), dim3(256), 0, s, src,
+                       sstride, pts, ne, stride, grid, g, grid64, xyz);
   else
     hipLaunchKernelGGL((k_hint_build<false, false>), dim3((unsigned)nb), dim3(256), 0, s, src, sstride,
-                       pts, ne, stride, grid, g, grid64);
+                       pts, ne, stride, grid, g, grid64, nullptr);
 }
 void launch_locate_vol(const VolArgs &a, hipStream_t s) {
   int64_t nb = (a.nlist + 255) / 256;

@@ -154,6 +154,35 @@ __device__ __forceinline__ D3 dsel(bool c, D3 a, D3 b) {
 // LAYOUT_GEN: interp_bar<4> of pmx_device.h.
 enum { LAYOUT_GEN = 0, LAYOUT_ANI = 1, LAYOUT_ISO = 2 };
 
+// dense coordinates for the slot walk (VolArgs::xyz): x, y, z of every old
+// vertex, 24 B apart.  Built once per background upload, a second layout of
+// the uploaded vertices (the walk's vertex gathers then touch 5.3 vertices per
+// 128-B line instead of 4; measured r01: k_walks 2.6 % faster on C3).
+__global__ __launch_bounds__(256) void k_build_xyz(const Pt4 *__restrict__ pts, int64_t n,
+                                                   double *__restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const Pt4 p = pts[i];
+    out[3 * i] = p.x;
+    out[3 * i + 1] = p.y;
+    out[3 * i + 2] = p.z;
+  }
+}
+void launch_build_xyz(const Pt4 *pts, int64_t n, double *out, hipStream_t s) {
+  const int64_t nb = std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), 65536);
+  hipLaunchKernelGGL(k_build_xyz, dim3((unsigned)nb), dim3(256), 0, s, pts, n, out);
+}
+
+// layout of the solutions for the walk kernel
+static int walk_layout(const SolDesc &sd, int *S) {
+  *S = sd.S;
+  if (sd.nsol == 1 && sd.size[0] == 6 && sd.imet == 0 && !sd.metric_const) return LAYOUT_ANI;
+  bool iso = !sd.metric_const && sd.S >= 1 && sd.S <= 8;
+  for (int s = 0; s < sd.nsol; s++) iso = iso && sd.size[s] != 6;
+  return iso ? LAYOUT_ISO : LAYOUT_GEN;
+}
+
+
 template <int LAYOUT, int S>
 __device__ __forceinline__ unsigned interp_layout(const double *__restrict__ sol, const SolDesc &sd,
                                                   const int *v, const double *phi,
@@ -249,7 +278,7 @@ __device__ __forceinline__ bool face_tie(const VolArgs &A, D3 p, int &cur, TetRe
   return false;
 }
 
-template <int LAYOUT, int S, bool TIES, int OCC, int BS>
+template <int LAYOUT, int S, bool TIES, int OCC, int BS, int EXP = 0>
 __global__ __launch_bounds__(BS, OCC) void k_walk(VolArgs A) {
   const int64_t b = walk_xcd_remap(blockIdx.x, gridDim.x);
   const int64_t j = b * blockDim.x + threadIdx.x;
@@ -277,6 +306,26 @@ __global__ __launch_bounds__(BS, OCC) void k_walk(VolArgs A) {
         step++;
         double num[4], vol;
         face_nums(P, p, num, &vol);
+        if constexpr (EXP == 1) {            // sensitivity: the face arithmetic twice
+          D3 Pc[4];
+#pragma unroll
+          for (int l = 0; l < 4; l++) {
+            Pc[l] = P[l];
+            asm volatile("" : "+v"(Pc[l].x), "+v"(Pc[l].y), "+v"(Pc[l].z));
+          }
+          double n2[4], v2;
+          face_nums(Pc, p, n2, &v2);
+          asm volatile("" ::"v"(n2[0]), "v"(n2[1]), "v"(n2[2]), "v"(n2[3]), "v"(v2));
+        }
+        if constexpr (EXP == 2) {            // sensitivity: one more tet record gather
+          const TetRec e = A.tets[cur + 1];
+          asm volatile("" ::"v"(e.v[0]), "v"(e.v[1]), "v"(e.v[2]), "v"(e.v[3]), "v"(e.nb[0]),
+                       "v"(e.nb[1]), "v"(e.nb[2]), "v"(e.nb[3]));
+        }
+        if constexpr (EXP == 3) {            // sensitivity: one more vertex gather
+          const Pt4 e = A.pts[t.v[0] + 1];
+          asm volatile("" ::"v"(e.x), "v"(e.y), "v"(e.z));
+        }
         const double rv = 1.0 / vol;
 #pragma unroll
         for (int f = 0; f < 4; f++) lam[f] = -(num[f] * rv);
@@ -367,14 +416,222 @@ __global__ __launch_bounds__(BS, OCC) void k_walk(VolArgs A) {
   wave_stats_w(A.wstats + (b * blockDim.x + threadIdx.x) / 64, s_cnt, s_sum, s_max, s_min);
 }
 
-// layout of the solutions for the walk kernel
-static int walk_layout(const SolDesc &sd, int *S) {
-  *S = sd.S;
-  if (sd.nsol == 1 && sd.size[0] == 6 && sd.imet == 0 && !sd.metric_const) return LAYOUT_ANI;
-  bool iso = !sd.metric_const && sd.S >= 1 && sd.S <= 8;
-  for (int s = 0; s < sd.nsol; s++) iso = iso && sd.size[s] != 6;
-  return iso ? LAYOUT_ISO : LAYOUT_GEN;
+// ---- slot walk (k_walks) -------------------------------------------------------
+//
+// The walk DIRECTION needs neither the reference's operation order nor the
+// tet's own vertex order -- only "found" and the interpolation weights must be
+// the reference's quotients.  k_walks therefore walks on slot-ordered state:
+//  * slot k holds a vertex id I[k], its coordinates C[k] and the neighbour
+//    NB[k] across the face opposite it; a step through the face opposite slot
+//    s replaces slot s by the neighbour's fourth vertex (one select per slot,
+//    instead of permuting all four coordinates into the new tet's order);
+//  * the barycentric numerators are signed sub-volumes about p: with
+//    d_k = C_k - p, w0 = d1.(d2 x d3), w1 = -d0.(d2 x d3), w2 = d3.(d0 x d1),
+//    w3 = -d2.(d0 x d1) and vol = sum w (2 cross + 4 dot products, no
+//    division); every step reflects the slot order's orientation, so the
+//    sign flips;
+//  * the lane leaves the loop when min w > -(EPS + SLOT_GUARD) vol (the
+//    reference's threshold with a margin far above this estimate's error);
+//    then, once per lane, the coordinates are put in tet order and the
+//    reference's quotients (tet_lambda's operations) decide.  A candidate
+//    they reject (|lambda_min + EPS| < guard) continues with the reference-
+//    order walk of k_walk.
+// The located tet does not depend on the path (unique containing tet, or the
+// canonical tet of a tie), so k_walks returns k_walk's results bit for bit.
+#define SLOT_GUARD 1.e-10
+
+__device__ __forceinline__ D3 dcross(D3 a, D3 b) {
+  return D3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
+__device__ __forceinline__ double ddot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+
+// one reference-order step decision (k_walk's): the first interior, not
+// recently visited neighbour in ascending-lambda order; 0 if none
+__device__ __forceinline__ int exact_next(const TetRec &t, const double lam[4], int ring[WALK_RING],
+                                          int cur) {
+  int rk[4];
+  wranks(lam, rk);
+#pragma unroll
+  for (int r = WALK_RING - 1; r > 0; r--) ring[r] = ring[r - 1];
+  ring[0] = cur;
+  int next = 0;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    int f = (rk[0] == r) ? 0 : (rk[1] == r) ? 1 : (rk[2] == r) ? 2 : 3;
+    int nb = pick4(t.nb, f);
+    bool seen = false;
+#pragma unroll
+    for (int q = 0; q < WALK_RING; q++) seen |= (ring[q] == nb);
+    if (!next && nb && !seen) next = nb;
+  }
+  return next;
+}
+
+template <int LAYOUT, int S, bool TIES, bool DENSE>
+__global__ __launch_bounds__(256) void k_walks(VolArgs A) {
+  const int64_t b = walk_xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t j = b * blockDim.x + threadIdx.x;
+  unsigned s_cnt = 0, s_sum = 0, s_max = 0, s_min = 0xffffffffu;
+  // DENSE: the walk's coordinates from the 24-B xyz stream (5.3 vertices per
+  // 128-B line instead of 4 for the 32-B Pt4 records)
+  auto ldc = [&](int v) -> D3 {
+    if constexpr (DENSE) {
+      const double *r = A.xyz + (int64_t)v * 3;
+      return D3{r[0], r[1], r[2]};
+    } else {
+      return ld3(A.pts, v);
+    }
+  };
+
+  if (j < A.nlist) {
+    // list order == Morton order of the volume points: both reads coalesced
+    // and independent (no list -> point dependent gather)
+    const int64_t i = A.list[j];
+    const Pt4 qq = A.qv[j];
+    const D3 p{qq.x, qq.y, qq.z};
+    int cur = walk_hint(A.grid, A.g, p, A.grid64);
+    A.start[i] = cur;
+    int ring[WALK_RING];
+#pragma unroll
+    for (int r = 0; r < WALK_RING; r++) ring[r] = 0;
+    int step = 0;
+    bool found = false;
+    TetRec t = A.tets[cur];
+    double lam[4];
+    if (t.v[0] <= 0) step = 1;                        // !MG_EOK start: let the scan decide
+    else {
+      D3 C[4] = {ldc(t.v[0]), ldc(t.v[1]), ldc(t.v[2]), ldc(t.v[3])};
+      int I[4] = {t.v[0], t.v[1], t.v[2], t.v[3]};
+      int NB[4] = {t.nb[0], t.nb[1], t.nb[2], t.nb[3]};
+      bool neg = false, cand = false;
+      for (;;) {
+        step++;
+        D3 d[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) d[k] = D3{C[k].x - p.x, C[k].y - p.y, C[k].z - p.z};
+        const D3 c23 = dcross(d[2], d[3]), c01 = dcross(d[0], d[1]);
+        double w[4] = {ddot(d[1], c23), -ddot(d[0], c23), ddot(d[3], c01), -ddot(d[2], c01)};
+        if (neg) {
+#pragma unroll
+          for (int k = 0; k < 4; k++) w[k] = -w[k];
+        }
+        const double vol = (w[0] + w[1]) + (w[2] + w[3]);
+        const double wmin = fmin(fmin(w[0], w[1]), fmin(w[2], w[3]));
+        // near or inside (or a degenerate / inverted tet): the reference decides
+        if (!(vol > 0.0) || wmin > -(PMX_EPS + SLOT_GUARD) * vol) { cand = true; break; }
+        if (step >= A.max_walk) break;
+#pragma unroll
+        for (int r = WALK_RING - 1; r > 0; r--) ring[r] = ring[r - 1];
+        ring[0] = cur;
+        // the admissible slot (interior, not recently visited neighbour) with
+        // the smallest barycentric
+        int sb = -1;
+        double wb = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int nb = NB[k];
+          bool seen = false;
+#pragma unroll
+          for (int q = 0; q < WALK_RING; q++) seen |= (ring[q] == nb);
+          const bool take = nb && !seen && (sb < 0 || w[k] < wb);
+          sb = take ? k : sb;
+          wb = take ? w[k] : wb;
+        }
+        if (sb < 0) break;
+        const int next = pick4(NB, sb);
+        const TetRec u = A.tets[next];
+        cur = next;
+        t = u;
+        if (u.v[0] <= 0) break;                            // !MG_EOK: let the scan decide
+        // the neighbour's fourth vertex replaces slot sb
+        int nnew = 0, lnew = 0;
+#pragma unroll
+        for (int l = 0; l < 4; l++) {
+          const bool any = (u.v[l] == I[0]) | (u.v[l] == I[1]) | (u.v[l] == I[2]) | (u.v[l] == I[3]);
+          nnew += any ? 0 : 1;
+          lnew = any ? lnew : l;
+        }
+        if (nnew != 1) {                                   // inconsistent adjacency: reload
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            C[k] = ldc(u.v[k]);
+            I[k] = u.v[k];
+            NB[k] = u.nb[k];
+          }
+          neg = false;
+          continue;
+        }
+        const int vn = pick4(u.v, lnew);
+        const D3 pn = ldc(vn);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          C[k] = dsel(k == sb, pn, C[k]);
+          I[k] = (k == sb) ? vn : I[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          NB[k] = (u.nb[0] & -(int)(u.v[0] == I[k])) | (u.nb[1] & -(int)(u.v[1] == I[k])) |
+                  (u.nb[2] & -(int)(u.v[2] == I[k])) | (u.nb[3] & -(int)(u.v[3] == I[k]));
+        neg = !neg;
+      }
+      if (cand) {
+        // coordinates in tet order, then the reference's quotients; a
+        // rejected candidate continues in the reference's order (rare)
+        D3 P[4];
+#pragma unroll
+        for (int l = 0; l < 4; l++)
+          P[l] = dsel(t.v[l] == I[0], C[0],
+                      dsel(t.v[l] == I[1], C[1], dsel(t.v[l] == I[2], C[2], C[3])));
+        for (;;) {
+          double num[4], vol;
+          face_nums(P, p, num, &vol);
+#pragma unroll
+          for (int f = 0; f < 4; f++) lam[f] = -num[f] / vol;
+          const double lmin = fmin(fmin(lam[0], lam[1]), fmin(lam[2], lam[3]));
+          if (lmin > -PMX_EPS) { found = true; break; }    // src/barycoord_pmmg.c:102-107
+          if (step >= A.max_walk) break;
+          const int next = exact_next(t, lam, ring, cur);
+          if (!next) break;
+          t = A.tets[next];
+          cur = next;
+          if (t.v[0] <= 0) break;
+          step++;
+#pragma unroll
+          for (int l = 0; l < 4; l++) P[l] = ldc(t.v[l]);
+        }
+      }
+    }
+    if (found) {
+      double lmn = fmin(fmin(lam[0], lam[1]), fmin(lam[2], lam[3]));
+      if (lmn < TIE_NEAR && (!TIES || face_tie(A, p, cur, t, lam))) {
+        unsigned slot = atomicAdd(A.tie_count, 1u);
+        A.tie_list[slot] = make_int2((int)i, cur);
+        A.steps[i] = step;
+        found = false;
+        step = -1;
+      }
+    }
+    if (found) {
+      A.elem[i] = cur;
+      A.status[i] = 1;
+      A.steps[i] = step;
+      const int v[4] = {t.v[0], t.v[1], t.v[2], t.v[3]};
+      unsigned wm = interp_layout<LAYOUT, S>(A.sol, A.sd, v, lam, A.out + i * A.sd.S);
+      A.wmask[i] = (uint8_t)(wm | A.const_bit);
+      s_cnt = 1; s_sum = step; s_max = step; s_min = step;
+    } else if (step >= 0) {
+      unsigned slot = atomicAdd(A.stuck_count, 1u);
+      A.stuck_list[slot] = (int)i;
+      A.found[slot] = 0x7fffffff;
+      A.bestk[slot] = 0x7fffffff;
+      A.best[slot] = ~0ull;
+      A.steps[i] = -step;
+    }
+  }
+  wave_stats_w(A.wstats + (b * blockDim.x + threadIdx.x) / 64, s_cnt, s_sum, s_max, s_min);
+}
+
+
 
 // OCC: minimum waves per SIMD asked of the register allocator (1 = free);
 // BS: threads per block (the waves of one block share a CU and its L1: a
@@ -382,7 +639,22 @@ static int walk_layout(const SolDesc &sd, int *S) {
 template <int LAYOUT, int S, int OCC, int BS>
 static void launch_walk_o(const VolArgs &a, int ties, hipStream_t s) {
   const int64_t nb = (a.nlist + BS - 1) / BS;
-  if (ties)
+  constexpr bool X = OCC == 1 && BS == 256;   // default shape
+  if (X && ties && a.exp >= 1 && a.exp <= 3) {
+    // sensitivity experiments on k_walk
+    if (a.exp == 1) hipLaunchKernelGGL((k_walk<LAYOUT, S, true, OCC, BS, X ? 1 : 0>), dim3((unsigned)nb), dim3(BS), 0, s, a);
+    else if (a.exp == 2) hipLaunchKernelGGL((k_walk<LAYOUT, S, true, OCC, BS, X ? 2 : 0>), dim3((unsigned)nb), dim3(BS), 0, s, a);
+    else hipLaunchKernelGGL((k_walk<LAYOUT, S, true, OCC, BS, X ? 3 : 0>), dim3((unsigned)nb), dim3(BS), 0, s, a);
+  } else if (X && !a.ref_walk) {
+    // production: the slot walk, dense coordinates unless disabled
+    if (a.xyz) {
+      if (ties) hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true>), dim3((unsigned)nb), dim3(BS), 0, s, a);
+      else hipLaunchKernelGGL((k_walks<LAYOUT, S, false, true>), dim3((unsigned)nb), dim3(BS), 0, s, a);
+    } else {
+      if (ties) hipLaunchKernelGGL((k_walks<LAYOUT, S, true, false>), dim3((unsigned)nb), dim3(BS), 0, s, a);
+      else hipLaunchKernelGGL((k_walks<LAYOUT, S, false, false>), dim3((unsigned)nb), dim3(BS), 0, s, a);
+    }
+  } else if (ties)
     hipLaunchKernelGGL((k_walk<LAYOUT, S, true, OCC, BS>), dim3((unsigned)nb), dim3(BS), 0, s, a);
   else
     hipLaunchKernelGGL((k_walk<LAYOUT, S, false, OCC, BS>), dim3((unsigned)nb), dim3(BS), 0, s, a);

@@ -22,6 +22,8 @@ WALK, TET = 0x100, 0x200      # pmx_run_opts.tune: force the volume walk / tet-c
 R01 = 0x400                   # the r01 walk kernel k_locate_vol instead of k_walk
 SERIAL_BDY = 0x800            # surface path on the main stream (no fork)
 NOTIES = 0x4000               # k_walk: every near-face point to the k_ties BFS
+REFWALK = 0x1000000           # the reference-order walk k_walk instead of the slot walk k_walks
+PT4WALK = 0x2000000           # k_walks on the 32-B Pt4 records instead of the dense coordinates
 
 
 def run_gpu(tr, m, x, t, sols, imet=0, hsiz=0.0, init=None, tune=0):
@@ -36,7 +38,8 @@ def run_gpu(tr, m, x, t, sols, imet=0, hsiz=0.0, init=None, tune=0):
 @pytest.mark.parametrize("metric,n,tune", [("iso", 10, 0), ("ani", 9, 0), ("none", 7, 0),
                                            ("iso", 10, WALK), ("ani", 9, WALK), ("ani", 9, TET),
                                            ("ani", 9, R01), ("iso", 10, R01 | SERIAL_BDY),
-                                           ("iso", 10, NOTIES)])
+                                           ("iso", 10, NOTIES), ("ani", 9, REFWALK),
+                                           ("iso", 10, REFWALK | NOTIES), ("ani", 9, PT4WALK)])
 def test_volume_parity(transfer, metric, n, tune):
     m, x, t, sols = cube_case(n, metric=metric, surface=False)
     imet = 0 if metric != "none" else -1
@@ -275,7 +278,26 @@ def test_walk_and_stream_agree(transfer, case):
         assert bits_equal(a.sols[s][vol], b.sols[s][vol]).all()
 
 
-@pytest.mark.parametrize("tune", [WALK, WALK | NOTIES, WALK | R01, TET])
+@pytest.mark.parametrize("metric", ["iso", "ani"])
+def test_slot_and_reference_walks_agree(transfer, metric):
+    """The slot walk (k_walks, dense or Pt4 coordinates) and the
+    reference-order walk (k_walk) are different paths to the same located tet:
+    identical elements, statuses and bit-identical fields, ties included."""
+    m, x, t, sols = cube_case(16, metric=metric, surface=False, fields=metric == "iso")
+    P = m.xyz[m.tet[1::97]]
+    x = np.concatenate([x, P[:, 0], 0.5 * (P[:, 0] + P[:, 1]), P[:, :3].mean(1)])
+    t = np.zeros(len(x), np.uint16)
+    a, *_ = run_gpu(transfer, m, x, t, sols, 0, tune=WALK)
+    for tune in (WALK | REFWALK, WALK | PT4WALK):
+        b, *_ = run_gpu(transfer, m, x, t, sols, 0, tune=tune)
+        assert np.array_equal(a.elem, b.elem)
+        assert np.array_equal(a.status, b.status)
+        for s in range(len(sols)):
+            assert bits_equal(a.sols[s], b.sols[s]).all()
+
+
+@pytest.mark.parametrize("tune", [WALK, WALK | NOTIES, WALK | R01, TET, WALK | REFWALK,
+                                  WALK | PT4WALK, WALK | NOTIES | REFWALK])
 def test_tie_points_canonical(transfer, tune):
     """Old vertices, edge midpoints and face centroids (the tie suite of
     SURVEY.md 8(d)): the device returns the smallest index among all tets

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--opt", default="hint_stride=1,4")
     ap.add_argument("--n", type=int, default=0, help="override the config's cells per axis")
+    ap.add_argument("--check", action="store_true",
+                    help="compare every variant's results bit for bit with the first one's")
     args = ap.parse_args()
     import bench
     from parmmg_amd import build
@@ -40,6 +42,20 @@ def main():
     vals = [int(v) for v in vals.split(",")]
     res = {v: {k: [] for k in ("hint", "vol", "bdy", "exhaustive", "total")} for v in vals}
     stats = {}
+    mism = {}
+    if args.check:
+        ref = None
+        for v in vals:
+            tr.run(**{key: v})
+            r = tr.download()
+            if ref is None:
+                ref = r
+                continue
+            bad = int(np.count_nonzero(r.elem != ref.elem))
+            bad += int(np.count_nonzero(r.status != ref.status))
+            for a, b in zip(r.sols, ref.sols):
+                bad += int(np.count_nonzero(a.view(np.uint64) != b.view(np.uint64)))
+            mism[v] = bad
     for _ in range(args.rounds):
         for v in vals:
             kw = {key: v}
@@ -56,6 +72,8 @@ def main():
         out[v] = {k: (float(np.median(a)), float(np.min(a))) for k, a in res[v].items()}
         out[v]["stepav"] = stats[v]["stepav"]
         out[v]["nexhaust"] = stats[v]["nexhaust"]
+        if v in mism:
+            out[v]["mismatches"] = mism[v]
     print(json.dumps({"config": args.config, "n": cfg["n"], "npts": int(len(x)), "opt": key,
                       "ms(median,min)": out}, indent=1))
 

@@ -117,7 +117,10 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *opts);
  * left untouched).  elem/status/steps may be NULL. */
 int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem,
                  int *status, int *steps);
-/* Per-point start element used by the device walk (debug/parity). */
+/* Per-point start element used by the device walk (debug/parity).  Volume
+ * points' starts are recorded only by a pmx_run with tune bit 0x8000000
+ * (PMX_TUNE_RECORD_STARTS); surface points' always. */
+#define PMX_TUNE_RECORD_STARTS 0x8000000
 int pmx_download_starts(pmx_ctx *ctx, int *start);
 /* Per-point reference-style extras for boundary points: edge/vertex (-1 unset). */
 int pmx_download_border(pmx_ctx *ctx, int *edge, int *vertex);

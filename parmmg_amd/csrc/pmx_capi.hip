@@ -324,12 +324,17 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   CK(hipMemcpyAsync(ctx->d_q.p, hq.data(), (size_t)n * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_kind.p, hk.data(), (size_t)n, hipMemcpyHostToDevice, ctx->stream));
   if (nv) CK(hipMemcpyAsync(ctx->d_vollist.p, vl.data(), (size_t)nv * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
-  // the volume points' coordinates once more, contiguous in list order: the
-  // persistent walk streams them per 64-point chunk (no list -> q indirection)
-  std::vector<Pt4> hqv((size_t)std::max<int64_t>(nv, 1));
-  for (int64_t j = 0; j < nv; j++) hqv[(size_t)j] = hq[(size_t)vl[(size_t)j]];
+  // the volume points' coordinates once more, dense (24 B) and contiguous in
+  // list order: the walks read them coalesced, without a list -> q gather
+  std::vector<double> hqv((size_t)std::max<int64_t>(nv, 1) * 3);
+  for (int64_t j = 0; j < nv; j++) {
+    const Pt4 &c = hq[(size_t)vl[(size_t)j]];
+    hqv[3 * (size_t)j] = c.x;
+    hqv[3 * (size_t)j + 1] = c.y;
+    hqv[3 * (size_t)j + 2] = c.z;
+  }
   if (!dgrow(ctx, ctx->d_qv, hqv.size())) return 0;
-  if (nv) CK(hipMemcpyAsync(ctx->d_qv.p, hqv.data(), (size_t)nv * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
+  if (nv) CK(hipMemcpyAsync(ctx->d_qv.p, hqv.data(), (size_t)nv * 3 * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
   if (nb) CK(hipMemcpyAsync(ctx->d_bdylist.p, bl.data(), (size_t)nb * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
   ctx->have_pts = true;
@@ -370,6 +375,9 @@ static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &o
   // tune bit 25: the slot walk on the 32-B Pt4 records instead of the dense
   // 24-B coordinates
   A.ref_walk = (opts.tune & 0x1000000) ? 1 : 0;
+  // tune bit 27: record the volume walks' start tets (pmx_download_starts;
+  // diagnostics and tests -- not an output of the reference)
+  A.rec_start = (opts.tune & 0x8000000) ? 1 : 0;
   A.xyz = (opts.tune & 0x2000000) ? nullptr : ctx->d_xyz.p;
 }
 

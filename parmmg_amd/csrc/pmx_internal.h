@@ -63,7 +63,7 @@ struct pmx_ctx {
   DevBuf<unsigned long long> d_best;
   DevBuf<unsigned> d_counts;            // [0] vol stuck, [1] bdy stuck, [2] bdy overflow
   DevBuf<int> d_vollist, d_bdylist;     // compacted point lists per path
-  DevBuf<Pt4> d_qv;                     // volume point coordinates in d_vollist order
+  DevBuf<double> d_qv;                  // volume points, dense xyz in list order
   DevBuf<uint4> d_vstat, d_bstat;       // per-wave walk statistics
   DevBuf<int> d_blist, d_olist, d_ows;
   int *d_tgrid = nullptr;

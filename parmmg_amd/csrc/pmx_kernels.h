@@ -35,7 +35,7 @@ struct VolArgs {
   int occ;                      // k_locate_vol register/occupancy variant
   int xcd_swizzle;
   int inline_ties;               // k_walk: resolve face ties in place
-  const Pt4 *qv;                // coordinates of the volume points in list order
+  const double *qv;             // coordinates of the volume points in list order (xyz, 24 B)
   unsigned long long *wctr;     // k_walkp: per-XCD-region chunk counters [8]
   int64_t region;               // k_walkp: points per region (multiple of 64)
   int block;                    // k_walk threads per block (256 / 512 / 1024)
@@ -43,6 +43,7 @@ struct VolArgs {
   int exp;                      // k_walk sensitivity experiment (0 = production)
   const double *xyz;            // dense 24-B coordinates (k_build_xyz), null: use pts
   int ref_walk;                 // 1: k_walk (reference-order walk) instead of k_walks
+  int rec_start;                // k_walks: write the start tet of every point (diagnostics)
 };
 
 struct ExhArgs {

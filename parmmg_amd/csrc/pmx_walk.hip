@@ -487,10 +487,9 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
     // list order == Morton order of the volume points: both reads coalesced
     // and independent (no list -> point dependent gather)
     const int64_t i = A.list[j];
-    const Pt4 qq = A.qv[j];
-    const D3 p{qq.x, qq.y, qq.z};
+    const D3 p{A.qv[3 * j], A.qv[3 * j + 1], A.qv[3 * j + 2]};
     int cur = walk_hint(A.grid, A.g, p, A.grid64);
-    A.start[i] = cur;
+    if (A.rec_start) A.start[i] = cur;
     int ring[WALK_RING];
 #pragma unroll
     for (int r = 0; r < WALK_RING; r++) ring[r] = 0;
@@ -788,7 +787,7 @@ __global__ __launch_bounds__(256) void k_walkp(VolArgs A) {
         if (lane < b_cnt) {
           const int64_t jj = lo + lane;
           b_i = A.list[jj];
-          const Pt4 qq = A.qv[jj];
+          const Pt4 qq{A.qv[3 * jj], A.qv[3 * jj + 1], A.qv[3 * jj + 2], 0.0};
           b_x = qq.x; b_y = qq.y; b_z = qq.z;
           b_h = walk_hint(A.grid, A.g, D3{b_x, b_y, b_z}, A.grid64);
         }

@@ -121,7 +121,11 @@ class Transfer:
         self.npts = xyz.shape[0]
 
     def run(self, hsiz: float = 0.0, timing: bool = False, max_walk: int = 0, hint_stride: int = 0,
-            tune: int = 0):
+            tune: int = 0, record_starts: bool = False):
+        """One step.  record_starts: keep every volume point's walk start tet
+        for starts() (diagnostics; the production step does not write it)."""
+        if record_starts:
+            tune |= 0x8000000
         o = N.RunOpts()
         o.hsiz, o.timing, o.max_walk, o.hint_stride, o.tune = hsiz, int(timing), max_walk, hint_stride, tune
         self._chk(self.lib.pmx_run(self.ctx, C.byref(o)), "pmx_run")

@@ -29,7 +29,7 @@ PT4WALK = 0x2000000           # k_walks on the 32-B Pt4 records instead of the d
 def run_gpu(tr, m, x, t, sols, imet=0, hsiz=0.0, init=None, tune=0):
     tr.upload_background(m, sols, imet)
     tr.upload_points(x, t)
-    tr.run(hsiz=hsiz, tune=tune)
+    tr.run(hsiz=hsiz, tune=tune, record_starts=True)
     r = tr.download(init=init)
     e, v = tr.border()
     return r, tr.starts(), e, v

@@ -31,7 +31,7 @@ def main():
     tr = Transfer(0)
     tr.upload_background(m, sols, 0)
     tr.upload_points(x, t)
-    tr.run(tune=args.tune, hint_stride=args.hint_stride)
+    tr.run(tune=args.tune, hint_stride=args.hint_stride, record_starts=True)
     r = tr.download()
     st = tr.starts()
     vol = t == 0

@@ -31,7 +31,10 @@ CONFIGS = {
     "C1": dict(n=20, metric="iso", fields=["ls"], desc="unit cube ~48k tets, iso metric + LS"),
     "C2": dict(n=119, metric="ani", fields=[], desc="10M-tet cube, anisotropic shock metric"),
     "C3": dict(n=255, metric="iso", fields=["ls", "vel"], desc="100M-tet cube, iso metric + LS + velocity"),
-    "C4": dict(n=255, metric="iso", fields=["ls", "vel"], desc="per-GPU share of 400M tets (2 groups of 50M)"),
+    # 400M tets = 16 ParMmg groups of ~25M (the group size cap,
+    # src/parmmg.h:209) over 8 GPUs: 2 groups of 25M tets per GPU
+    "C4": dict(n=161, groups=2, metric="iso", fields=["ls", "vel"],
+               desc="per-GPU share of 400M tets over 8 GPUs (2 groups of 25M)"),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -135,15 +138,32 @@ def main():
     from parmmg_amd.transfer import Transfer
 
     cfg = CONFIGS[args.config]
-    m, x, t, sols = build_case(cfg, rank)
+    ngrp = cfg.get("groups", 1)
+    # every group of this rank in its own context (own stream): the groups'
+    # steps are enqueued back to back and may overlap on the device
+    cases, trs = [], []
+    for g in range(ngrp):
+        m, x, t, sols = build_case(cfg, rank * ngrp + g)
+        tr = Transfer(local)
+        tr.upload_background(m, sols, 0)
+        tr.upload_points(x, t)
+        cases.append((m, x, t, sols))
+        trs.append(tr)
+    m, x, t, sols = cases[0]
+    tr = trs[0]
     S = sum(s.shape[1] for s in sols)
-    tr = Transfer(local)
-    tr.upload_background(m, sols, 0)
-    tr.upload_points(x, t)
+
+    def step(timing=False):
+        for g in trs:
+            g.run(timing=timing)
+
+    def sync():
+        for g in trs:
+            g.synchronize()
 
     for _ in range(args.warmup):
-        tr.run()
-    tr.synchronize()
+        step()
+    sync()
 
     def barrier():
         if dist is not None:
@@ -152,12 +172,13 @@ def main():
             torch.cuda.synchronize()
 
     barrier()
-    tr.synchronize()
-    tr.timing_reset()
+    sync()
+    for g in trs:
+        g.timing_reset()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        tr.run(timing=True)
-    tr.synchronize()
+        step(timing=True)
+    sync()
     barrier()
     el = time.perf_counter() - t0
     k_ms = {name: tr.kernel_ms(i) for i, name in enumerate(["hint", "vol", "bdy", "exhaustive", "total"])}
@@ -172,7 +193,7 @@ def main():
         from parmmg_amd import shard
         qs = shard.qualhisto_allreduce(tr, dist, local)
     npts = len(x)
-    total_pts = npts * world * args.steps
+    total_pts = sum(len(c[1]) for c in cases) * world * args.steps
     value = total_pts / el
     ms = el / args.steps * 1e3
 
@@ -196,8 +217,9 @@ def main():
         "dtype": "f64",
         "data": "synthetic (jittered Kuhn cube, jittered Morton-ordered new vertices, analytic fields)",
         "config": {"workload": f"{args.config}: {cfg['desc']}", "n_cells": cfg["n"], "ne": m.ne,
-                   "np": m.np, "nt": m.nt, "new_vertices_per_gpu": npts, "S": S,
-                   "groups_per_gpu": 1, "parallelism": f"group-sharded x{world}"},
+                   "np": m.np, "nt": m.nt,
+                   "new_vertices_per_gpu": sum(len(c[1]) for c in cases), "S": S,
+                   "groups_per_gpu": ngrp, "parallelism": f"group-sharded x{world}"},
         "roofline": {"bound": "hbm", "kernel": "k_walks",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None,

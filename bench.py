@@ -199,6 +199,8 @@ def main():
 
     nvol = int((t == 0).sum())
     B = alg_bytes(npts, m.ne, m.np, S)
+    # all groups of this rank (C4: 2 concurrent groups, one stream each)
+    B_all = sum(alg_bytes(len(c[1]), c[0].ne, c[0].np, S) for c in cases)
     b_vol = B * nvol / npts
     achieved = b_vol / (k_ms["vol"] * 1e-3) / 1e9 if k_ms["vol"] > 0 else None
     traffic, traffic_src = profiled_traffic(args.config)
@@ -224,9 +226,12 @@ def main():
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                      "traffic": traffic, "traffic_source": traffic_src,
-                     "alg_bytes_per_launch": b_vol, "avg_launch_ms": k_ms["vol"]},
+                     "alg_bytes_per_launch": b_vol, "avg_launch_ms": k_ms["vol"],
+                     # >1: that many groups' walks run at once on separate
+                     # streams, each launch's duration includes the others'
+                     "concurrent_launches": ngrp},
         "kernel_ms": k_ms,
-        "step_alg_GBs": B / (ms * 1e-3) / 1e9,
+        "step_alg_GBs": B_all / (ms * 1e-3) / 1e9,
         "locate": st,
     }
     if rank == 0 and not args.no_cpu:

@@ -267,7 +267,10 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   if (nt > 0) launch_tria_normals(ctx->d_tris.p, ctx->d_pts.p, nt, ctx->d_trn.p, ctx->stream);
   // dense coordinates for the walk: the uploaded vertices in a second layout
   if (!dgrow(ctx, ctx->d_xyz, (size_t)(np + 1) * 3)) return 0;
-  launch_build_xyz(ctx->d_pts.p, np + 1, ctx->d_xyz.p, ctx->stream);
+  if (!dgrow(ctx, ctx->d_xyzf, (size_t)(np + 1) * 3)) return 0;
+  launch_build_xyz(ctx->d_pts.p, np + 1, ctx->d_xyz.p, ctx->d_xyzf.p, ctx->stream);
+  if (!dgrow(ctx, ctx->d_xyzq, (size_t)(np + 1))) return 0;
+  launch_quant_xyz(ctx->d_pts.p, np + 1, ctx->grid, ctx->d_xyzq.p, ctx->stream);
   CK(hipGetLastError());
   CK(hipStreamSynchronize(ctx->stream));   // host staging vectors die here
   ctx->have_bg = true;
@@ -445,7 +448,12 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
       launch_hint_build(ctx->d_tetv.p, packed ? ctx->d_tets_s.p : nullptr, ctx->d_pts.p, ctx->ne,
                         stride, ctx->d_grid.p, ctx->grid, (opts.tune & 0x8000) ? 1 : 0, st,
                         const_cast<unsigned long long *>(A.grid64),
-                        (opts.tune & 0x4000000) ? nullptr : ctx->d_xyz.p);   // bit 26: Pt4 reads
+                        (opts.tune & 0x4000000) ? nullptr : ctx->d_xyz.p,    // bit 26: Pt4 reads
+                        // centroids: default fixed-point grid coordinates (r01
+                        // C3 hint: double 0.295, float 0.217, fixed 0.197 ms);
+                        // bit 28: double, bit 29: single precision
+                        (opts.tune & 0x30000000) == 0x20000000 ? ctx->d_xyzf.p : nullptr,
+                        (opts.tune & 0x30000000) ? nullptr : ctx->d_xyzq.p);
     }
     if (ctx->nq_bdy && bdy_mode == 3) CK(hipStreamWaitEvent(st, ctx->ev_join, 0));
     if (ev) CK(hipEventRecord(ev[1], st));
@@ -640,7 +648,7 @@ hipEvent_t *pmx_ctx::next_event_slot() {
 }
 
 void pmx_ctx::free_all() {
-  dfree(d_pts); dfree(d_tets); dfree(d_sol); dfree(d_xyz); dfree(d_tris); dfree(d_trn); dfree(d_grid); dfree(d_grid64);
+  dfree(d_pts); dfree(d_tets); dfree(d_sol); dfree(d_xyz); dfree(d_xyzf); dfree(d_xyzq); dfree(d_tris); dfree(d_trn); dfree(d_grid); dfree(d_grid64);
   dfree(d_ntoff); dfree(d_ntlist);
   dfree(d_q); dfree(d_kind); dfree(d_wmask); dfree(d_out); dfree(d_elem); dfree(d_status);
   dfree(d_steps); dfree(d_start); dfree(d_edge); dfree(d_vertex); dfree(d_list); dfree(d_found);

@@ -32,6 +32,8 @@ struct pmx_ctx {
   DevBuf<TetRec> d_tets;
   DevBuf<double> d_sol;
   DevBuf<double> d_xyz;                 // dense coordinates, 3 doubles per vertex
+  DevBuf<float> d_xyzf;                 // the same in single precision (hint centroids)
+  DevBuf<unsigned long long> d_xyzq;    // fixed-point grid coordinates (hint centroids)
   DevBuf<TriRec> d_tris;
   DevBuf<Pt4> d_trn;
   DevBuf<int> d_grid;

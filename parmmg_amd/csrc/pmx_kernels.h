@@ -60,12 +60,16 @@ struct ExhArgs {
 
 void launch_hint_build(const int4 *tetv, const int4 *packed, const Pt4 *pts, int64_t ne,
                        int stride, int *grid, GridDesc g, int mid, hipStream_t s,
-                       unsigned long long *grid64 = nullptr, const double *xyz = nullptr);
+                       unsigned long long *grid64 = nullptr, const double *xyz = nullptr,
+                       const float *xyzf = nullptr, const unsigned long long *xyzq = nullptr);
+// fraction bits of the fixed-point grid coordinates (dim <= 4096: 12 + 9 = 21 bits)
+#define HINT_QF 9
+void launch_quant_xyz(const Pt4 *pts, int64_t n, GridDesc g, unsigned long long *q, hipStream_t s);
 void launch_fill64(unsigned long long *p, int64_t n, hipStream_t s);
 void launch_locate_vol(const VolArgs &a, hipStream_t s);
 void launch_walk(const VolArgs &a, hipStream_t s);
 void launch_walkp(const VolArgs &a, hipStream_t s);
-void launch_build_xyz(const Pt4 *pts, int64_t n, double *out, hipStream_t s);
+void launch_build_xyz(const Pt4 *pts, int64_t n, double *out, float *outf, hipStream_t s);
 void launch_tet_conn(const TetRec *src, int64_t stride, int64_t n, int4 *dst, hipStream_t s);
 void launch_exhaustive(const ExhArgs &e, const VolArgs &v, hipStream_t s);
 void launch_const_metric(const int8_t *kind, int64_t nq, double *out, int S, int off, int size,

@@ -72,13 +72,15 @@ __device__ int hint_lookup(const int *grid, const GridDesc &g, D3 p) {
   return 1;
 }
 
-template <bool MID, bool CENTRAL, bool DX = false>
+template <bool MID, bool CENTRAL, bool DX = false, bool FX = false, bool QX = false>
 __global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ src, int64_t sstride,
                                                     const Pt4 *__restrict__ pts, int64_t ne,
                                                     int stride, int *__restrict__ grid,
                                                     GridDesc g,
                                                     unsigned long long *__restrict__ grid64,
-                                                    const double *__restrict__ xyz = nullptr) {
+                                                    const double *__restrict__ xyz = nullptr,
+                                                    const float *__restrict__ xyzf = nullptr,
+                                                    const unsigned long long *__restrict__ xyzq = nullptr) {
   // one sample per thread; XCD-aware block order: each XCD's L2 serves a
   // contiguous range of samples, i.e. neighbouring tets sharing vertices
   const int64_t n = (ne + stride - 1) / stride;
@@ -90,7 +92,34 @@ __global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ src
   const int4 v = src[t * sstride];
   if (v.x <= 0) return;
   D3 m;
-  if (MID) {
+  if constexpr (QX) {
+    // QX: the vertices' grid coordinates in 21-bit fixed point (HINT_QF
+    // fraction bits, packed x | y << 21 | z << 42 at upload): one 8-B gather
+    // per vertex, the centroid's cell by integer sums and a shift
+    const unsigned long long a = xyzq[v.x], b = xyzq[v.y], c = xyzq[v.z], d = xyzq[v.w];
+    const unsigned long long M = (1ull << 21) - 1;
+    int cq[3];
+#pragma unroll
+    for (int ax = 0; ax < 3; ax++) {
+      const int sh = 21 * ax;
+      const unsigned s4 = (unsigned)((a >> sh) & M) + (unsigned)((b >> sh) & M) +
+                          (unsigned)((c >> sh) & M) + (unsigned)((d >> sh) & M);
+      cq[ax] = min((int)(s4 >> (HINT_QF + 2)), g.dim[ax] - 1);
+    }
+    grid[(int64_t)cq[0] + (int64_t)g.dim[0] * ((int64_t)cq[1] + (int64_t)g.dim[1] * cq[2])] = (int)k;
+    return;
+  } else if constexpr (FX) {
+    // FX: centroid from the 12-B single-precision copy of the coordinates (one
+    // 12-B gather per vertex instead of 24 B in two loads).  The cell only
+    // picks a start tet, and the located tet does not depend on the start.
+    auto ldf = [&](int i) -> float3 {
+      const float *r = xyzf + 3 * (int64_t)i;
+      return make_float3(r[0], r[1], r[2]);
+    };
+    const float3 a = ldf(v.x), b = ldf(v.y), c = ldf(v.z), d = ldf(v.w);
+    m = D3{(double)((a.x + b.x + c.x + d.x) * 0.25f), (double)((a.y + b.y + c.y + d.y) * 0.25f),
+           (double)((a.z + b.z + c.z + d.z) * 0.25f)};
+  } else if (MID) {
     // midpoint of edge v0-v1: a point of the tet's closure, 2 gathers
     const D3 a = ld3(pts, v.x), b = ld3(pts, v.y);
     m = D3{(a.x + b.x) * 0.5, (a.y + b.y) * 0.5, (a.z + b.z) * 0.5};
@@ -122,6 +151,30 @@ __global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ src
     // canonical min-index tet of a tie, see canonical_tet)
     grid[cell] = (int)k;
   }
+}
+
+// grid coordinates of the vertices in fixed point for k_hint_build<QX>:
+// q = (x - lo) * inv * 2^HINT_QF, clamped to [0, dim * 2^HINT_QF - 1]
+__global__ __launch_bounds__(256) void k_quant_xyz(const Pt4 *__restrict__ pts, int64_t n, GridDesc g,
+                                                   unsigned long long *__restrict__ q) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const Pt4 p = pts[i];
+    const double c[3] = {p.x, p.y, p.z};
+    unsigned long long r = 0;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      const double t = (c[a] - g.lo[a]) * g.inv[a] * (double)(1 << HINT_QF);
+      const long long hi = ((long long)g.dim[a] << HINT_QF) - 1;
+      const long long u = !(t > 0.0) ? 0 : (t >= (double)hi ? hi : (long long)t);
+      r |= (unsigned long long)u << (21 * a);
+    }
+    q[i] = r;
+  }
+}
+void launch_quant_xyz(const Pt4 *pts, int64_t n, GridDesc g, unsigned long long *q, hipStream_t s) {
+  const int64_t nb = std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), 65536);
+  hipLaunchKernelGGL(k_quant_xyz, dim3((unsigned)nb), dim3(256), 0, s, pts, n, g, q);
 }
 
 __global__ __launch_bounds__(256) void k_fill64(unsigned long long *p, int64_t n) {
@@ -558,7 +611,8 @@ void launch_prologue(uint8_t *wmask, int64_t n, unsigned *counts, int *grid, int
 
 void launch_hint_build(const int4 *tetv, const int4 *packed, const Pt4 *pts, int64_t ne,
                        int stride, int *grid, GridDesc g, int mid, hipStream_t s,
-                       unsigned long long *grid64, const double *xyz) {
+                       unsigned long long *grid64, const double *xyz, const float *xyzf,
+                       const unsigned long long *xyzq) {
   const int64_t n = (ne + stride - 1) / stride;
   const int64_t nb = std::max<int64_t>((n + 255) / 256, 1);
   const int4 *src = packed ? packed : tetv + 1;
@@ -566,6 +620,12 @@ void launch_hint_build(const int4 *tetv, const int4 *packed, const Pt4 *pts, int
   if (grid64)
     hipLaunchKernelGGL((k_hint_build<false, true>), dim3((unsigned)nb), dim3(256), 0, s, src, sstride,
                        pts, ne, stride, grid, g, grid64, nullptr);
+  else if (xyzq)
+    hipLaunchKernelGGL((k_hint_build<false, false, false, false, true>), dim3((unsigned)nb), dim3(256), 0,
+                       s, src, sstride, pts, ne, stride, grid, g, grid64, nullptr, nullptr, xyzq);
+  else if (xyzf)
+    hipLaunchKernelGGL((k_hint_build<false, false, false, true>), dim3((unsigned)nb), dim3(256), 0, s,
+                       src, sstride, pts, ne, stride, grid, g, grid64, nullptr, xyzf);
   else if (mid)
     hipLaunchKernelGGL((k_hint_build<true, false>), dim3((unsigned)nb), dim3(256), 0, s, src, sstride,
                        pts, ne, stride, grid, g, grid64, nullptr);

@@ -159,18 +159,45 @@ enum { LAYOUT_GEN = 0, LAYOUT_ANI = 1, LAYOUT_ISO = 2 };
 // the uploaded vertices (the walk's vertex gathers then touch 5.3 vertices per
 // 128-B line instead of 4; measured r01: k_walks 2.6 % faster on C3).
 __global__ __launch_bounds__(256) void k_build_xyz(const Pt4 *__restrict__ pts, int64_t n,
-                                                   double *__restrict__ out) {
+                                                   double *__restrict__ out,
+                                                   float *__restrict__ outf) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const Pt4 p = pts[i];
     out[3 * i] = p.x;
     out[3 * i + 1] = p.y;
     out[3 * i + 2] = p.z;
+    // single-precision copy for the hint build's centroids (k_hint_build FX)
+    outf[3 * i] = (float)p.x;
+    outf[3 * i + 1] = (float)p.y;
+    outf[3 * i + 2] = (float)p.z;
   }
 }
-void launch_build_xyz(const Pt4 *pts, int64_t n, double *out, hipStream_t s) {
+void launch_build_xyz(const Pt4 *pts, int64_t n, double *out, float *outf, hipStream_t s) {
   const int64_t nb = std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), 65536);
-  hipLaunchKernelGGL(k_build_xyz, dim3((unsigned)nb), dim3(256), 0, s, pts, n, out);
+  hipLaunchKernelGGL(k_build_xyz, dim3((unsigned)nb), dim3(256), 0, s, pts, n, out, outf);
+}
+
+// tet record load; NT: non-temporal (streaming) hint, the record is rarely
+// re-read while the vertex and solution rows around it are
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ TetRec ldtet(const TetRec *__restrict__ tets, int k) {
+  if constexpr (NT) {
+    const v4i_t *r = reinterpret_cast<const v4i_t *>(tets + k);
+    const v4i_t a = __builtin_nontemporal_load(r), b = __builtin_nontemporal_load(r + 1);
+    TetRec t;
+    t.v[0] = a.x; t.v[1] = a.y; t.v[2] = a.z; t.v[3] = a.w;
+    t.nb[0] = b.x; t.nb[1] = b.y; t.nb[2] = b.z; t.nb[3] = b.w;
+    return t;
+  } else {
+    return tets[k];
+  }
+}
+template <bool NT, class T>
+__device__ __forceinline__ void stw(T *p, T v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
 }
 
 // layout of the solutions for the walk kernel
@@ -183,7 +210,7 @@ static int walk_layout(const SolDesc &sd, int *S) {
 }
 
 
-template <int LAYOUT, int S>
+template <int LAYOUT, int S, bool NTS = false>
 __device__ __forceinline__ unsigned interp_layout(const double *__restrict__ sol, const SolDesc &sd,
                                                   const int *v, const double *phi,
                                                   double *__restrict__ out) {
@@ -231,7 +258,7 @@ __device__ __forceinline__ unsigned interp_layout(const double *__restrict__ sol
       for (int j = 0; j < S; j += 2) *reinterpret_cast<double2 *>(out + j) = make_double2(acc[j], acc[j + 1]);
     } else {
 #pragma unroll
-      for (int j = 0; j < S; j++) out[j] = acc[j];
+      for (int j = 0; j < S; j++) stw<NTS>(out + j, acc[j]);
     }
     return (1u << sd.nsol) - 1u;
   } else {
@@ -447,12 +474,13 @@ __device__ __forceinline__ double ddot(D3 a, D3 b) { return a.x * b.x + a.y * b.
 
 // one reference-order step decision (k_walk's): the first interior, not
 // recently visited neighbour in ascending-lambda order; 0 if none
-__device__ __forceinline__ int exact_next(const TetRec &t, const double lam[4], int ring[WALK_RING],
+template <int RG = WALK_RING>
+__device__ __forceinline__ int exact_next(const TetRec &t, const double lam[4], int ring[RG],
                                           int cur) {
   int rk[4];
   wranks(lam, rk);
 #pragma unroll
-  for (int r = WALK_RING - 1; r > 0; r--) ring[r] = ring[r - 1];
+  for (int r = RG - 1; r > 0; r--) ring[r] = ring[r - 1];
   ring[0] = cur;
   int next = 0;
 #pragma unroll
@@ -461,13 +489,13 @@ __device__ __forceinline__ int exact_next(const TetRec &t, const double lam[4], 
     int nb = pick4(t.nb, f);
     bool seen = false;
 #pragma unroll
-    for (int q = 0; q < WALK_RING; q++) seen |= (ring[q] == nb);
+    for (int q = 0; q < RG; q++) seen |= (ring[q] == nb);
     if (!next && nb && !seen) next = nb;
   }
   return next;
 }
 
-template <int LAYOUT, int S, bool TIES, bool DENSE>
+template <int LAYOUT, int S, bool TIES, bool DENSE, int RG = WALK_RING, int NT = 0>
 __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
   const int64_t b = walk_xcd_remap(blockIdx.x, gridDim.x);
   const int64_t j = b * blockDim.x + threadIdx.x;
@@ -490,12 +518,12 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
     const D3 p{A.qv[3 * j], A.qv[3 * j + 1], A.qv[3 * j + 2]};
     int cur = walk_hint(A.grid, A.g, p, A.grid64);
     if (A.rec_start) A.start[i] = cur;
-    int ring[WALK_RING];
+    int ring[RG];
 #pragma unroll
-    for (int r = 0; r < WALK_RING; r++) ring[r] = 0;
+    for (int r = 0; r < RG; r++) ring[r] = 0;
     int step = 0;
     bool found = false;
-    TetRec t = A.tets[cur];
+    TetRec t = ldtet<(NT & 1) != 0>(A.tets, cur);
     double lam[4];
     if (t.v[0] <= 0) step = 1;                        // !MG_EOK start: let the scan decide
     else {
@@ -520,7 +548,7 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
         if (!(vol > 0.0) || wmin > -(PMX_EPS + SLOT_GUARD) * vol) { cand = true; break; }
         if (step >= A.max_walk) break;
 #pragma unroll
-        for (int r = WALK_RING - 1; r > 0; r--) ring[r] = ring[r - 1];
+        for (int r = RG - 1; r > 0; r--) ring[r] = ring[r - 1];
         ring[0] = cur;
         // the admissible slot (interior, not recently visited neighbour) with
         // the smallest barycentric
@@ -531,14 +559,14 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
           const int nb = NB[k];
           bool seen = false;
 #pragma unroll
-          for (int q = 0; q < WALK_RING; q++) seen |= (ring[q] == nb);
+          for (int q = 0; q < RG; q++) seen |= (ring[q] == nb);
           const bool take = nb && !seen && (sb < 0 || w[k] < wb);
           sb = take ? k : sb;
           wb = take ? w[k] : wb;
         }
         if (sb < 0) break;
         const int next = pick4(NB, sb);
-        const TetRec u = A.tets[next];
+        const TetRec u = ldtet<(NT & 1) != 0>(A.tets, next);
         cur = next;
         t = u;
         if (u.v[0] <= 0) break;                            // !MG_EOK: let the scan decide
@@ -589,9 +617,9 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
           const double lmin = fmin(fmin(lam[0], lam[1]), fmin(lam[2], lam[3]));
           if (lmin > -PMX_EPS) { found = true; break; }    // src/barycoord_pmmg.c:102-107
           if (step >= A.max_walk) break;
-          const int next = exact_next(t, lam, ring, cur);
+          const int next = exact_next<RG>(t, lam, ring, cur);
           if (!next) break;
-          t = A.tets[next];
+          t = ldtet<(NT & 1) != 0>(A.tets, next);
           cur = next;
           if (t.v[0] <= 0) break;
           step++;
@@ -611,12 +639,13 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
       }
     }
     if (found) {
-      A.elem[i] = cur;
-      A.status[i] = 1;
-      A.steps[i] = step;
+      constexpr bool NTS = (NT & 2) != 0;
+      stw<NTS>(A.elem + i, cur);
+      stw<NTS>(A.status + i, 1);
+      stw<NTS>(A.steps + i, step);
       const int v[4] = {t.v[0], t.v[1], t.v[2], t.v[3]};
-      unsigned wm = interp_layout<LAYOUT, S>(A.sol, A.sd, v, lam, A.out + i * A.sd.S);
-      A.wmask[i] = (uint8_t)(wm | A.const_bit);
+      unsigned wm = interp_layout<LAYOUT, S, NTS>(A.sol, A.sd, v, lam, A.out + i * A.sd.S);
+      stw<NTS>(A.wmask + i, (uint8_t)(wm | A.const_bit));
       s_cnt = 1; s_sum = step; s_max = step; s_min = step;
     } else if (step >= 0) {
       unsigned slot = atomicAdd(A.stuck_count, 1u);
@@ -644,6 +673,14 @@ static void launch_walk_o(const VolArgs &a, int ties, hipStream_t s) {
     if (a.exp == 1) hipLaunchKernelGGL((k_walk<LAYOUT, S, true, OCC, BS, X ? 1 : 0>), dim3((unsigned)nb), dim3(BS), 0, s, a);
     else if (a.exp == 2) hipLaunchKernelGGL((k_walk<LAYOUT, S, true, OCC, BS, X ? 2 : 0>), dim3((unsigned)nb), dim3(BS), 0, s, a);
     else hipLaunchKernelGGL((k_walk<LAYOUT, S, true, OCC, BS, X ? 3 : 0>), dim3((unsigned)nb), dim3(BS), 0, s, a);
+  } else if (X && ties && a.exp == 4 && a.xyz && !a.ref_walk) {
+    // sensitivity experiment: a 2-entry visited ring in the slot walk
+    hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true, 2>), dim3((unsigned)nb), dim3(BS), 0, s, a);
+  } else if (X && ties && a.exp >= 5 && a.xyz && !a.ref_walk) {
+    // sensitivity experiments: non-temporal tet loads (5), output stores (6), both (7)
+    if (a.exp == 5) hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true, WALK_RING, 1>), dim3((unsigned)nb), dim3(BS), 0, s, a);
+    else if (a.exp == 6) hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true, WALK_RING, 2>), dim3((unsigned)nb), dim3(BS), 0, s, a);
+    else hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true, WALK_RING, 3>), dim3((unsigned)nb), dim3(BS), 0, s, a);
   } else if (X && !a.ref_walk) {
     // production: the slot walk, dense coordinates unless disabled
     if (a.xyz) {

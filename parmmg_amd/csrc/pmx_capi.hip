@@ -324,8 +324,10 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   // one record per wave of the largest k_walk block (1024 threads)
   if (!dgrow(ctx, ctx->d_vstat, (size_t)std::max<int64_t>((nv + 1023) / 1024 * 16 + 4, 1))) return 0;
   if (!dgrow(ctx, ctx->d_bstat, (size_t)std::max<int64_t>((nb + 63) / 64 + 4, 1))) return 0;
-  CK(hipMemcpyAsync(ctx->d_q.p, hq.data(), (size_t)n * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
-  CK(hipMemcpyAsync(ctx->d_kind.p, hk.data(), (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+  if (n) {   // no new vertex at all is a valid (empty) step
+    CK(hipMemcpyAsync(ctx->d_q.p, hq.data(), (size_t)n * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
+    CK(hipMemcpyAsync(ctx->d_kind.p, hk.data(), (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+  }
   if (nv) CK(hipMemcpyAsync(ctx->d_vollist.p, vl.data(), (size_t)nv * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
   // the volume points' coordinates once more, dense (24 B) and contiguous in
   // list order: the walks read them coalesced, without a list -> q gather
@@ -506,6 +508,7 @@ int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem, int *sta
   const int64_t n = ctx->nq;
   const int S = ctx->sd.S;
   CK(hipStreamSynchronize(ctx->stream));
+  if (n == 0) return 1;   // empty step: nothing to copy
   if (new_sols && S > 0) {
     std::vector<double> h((size_t)(n * S));
     std::vector<uint8_t> wm((size_t)std::max<int64_t>(n, 1));
@@ -530,6 +533,7 @@ int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem, int *sta
 int pmx_download_starts(pmx_ctx *ctx, int *start) {
   if (!ctx || !ctx->ran) return 0;
   CK(hipStreamSynchronize(ctx->stream));
+  if (ctx->nq == 0) return 1;
   CK(hipMemcpy(start, ctx->d_start.p, (size_t)ctx->nq * sizeof(int), hipMemcpyDeviceToHost));
   return 1;
 }
@@ -537,6 +541,7 @@ int pmx_download_starts(pmx_ctx *ctx, int *start) {
 int pmx_download_border(pmx_ctx *ctx, int *edge, int *vertex) {
   if (!ctx || !ctx->ran) return 0;
   CK(hipStreamSynchronize(ctx->stream));
+  if (ctx->nq == 0) return 1;
   if (edge) CK(hipMemcpy(edge, ctx->d_edge.p, (size_t)ctx->nq * sizeof(int), hipMemcpyDeviceToHost));
   if (vertex) CK(hipMemcpy(vertex, ctx->d_vertex.p, (size_t)ctx->nq * sizeof(int), hipMemcpyDeviceToHost));
   return 1;

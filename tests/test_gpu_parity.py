@@ -341,3 +341,71 @@ def test_large_size_properties(transfer):
                                             start_bdy=starts)
     bdy = np.nonzero(t == 16)[0]
     compare_exact((r.sols, r.elem, r.status, edge, vert), (outs, elem, sto, e, v), bdy, len(sols))
+
+
+DOUBLE_HINT, FLOAT_HINT = 0x10000000, 0x20000000   # hint centroids (default: fixed point)
+CENTRAL_HINT = 0x100000
+
+
+@pytest.mark.parametrize("metric", ["iso", "ani"])
+def test_hint_variants_agree(transfer, metric):
+    """The hint grid only chooses where a walk starts: fixed-point, single-
+    and double-precision centroids and the central-sample grid give the same
+    located tets and bit-identical fields (ties included)."""
+    m, x, t, sols = cube_case(14, metric=metric)
+    P = m.xyz[m.tet[1::89]]
+    x = np.concatenate([x, P[:, 0], 0.5 * (P[:, 0] + P[:, 2]), P[:, 1:].mean(1)])
+    t = np.concatenate([t, np.zeros(3 * len(P), np.uint16)])
+    a, *_ = run_gpu(transfer, m, x, t, sols, 0)
+    assert np.all(a.status != 0)
+    for tune in (DOUBLE_HINT, FLOAT_HINT, CENTRAL_HINT):
+        b, *_ = run_gpu(transfer, m, x, t, sols, 0, tune=tune)
+        vol = t == 0
+        assert np.array_equal(a.elem[vol], b.elem[vol]), hex(tune)
+        assert np.array_equal(a.status[vol], b.status[vol]), hex(tune)
+        for s in range(len(sols)):
+            assert bits_equal(a.sols[s][vol], b.sols[s][vol]).all(), hex(tune)
+
+
+def _shuffled(m, seed=7):
+    """Tets in a random order, local vertices rotated (orientation kept)."""
+    rng = np.random.default_rng(seed)
+    perm = rng.permutation(m.ne) + 1
+    tet = np.zeros_like(m.tet)
+    tet[1:] = m.tet[perm]
+    even = np.array([[0, 1, 2, 3], [1, 0, 3, 2], [2, 3, 0, 1], [3, 2, 1, 0]])
+    tet[1:] = np.take_along_axis(tet[1:], even[rng.integers(0, 4, m.ne)], axis=1)
+    return M.from_tets(m.xyz, tet)
+
+
+def test_shuffled_numbering_parity(transfer):
+    """A background with no numbering locality (random tet order, SURVEY.md
+    8(d) --shuffle-tets): same located tets and bit-exact fields as the oracle
+    (ties: the documented canonical rule)."""
+    m = _shuffled(M.kuhn_cube(10))
+    x, t = M.new_points(10, seed=12345, surface=False)
+    sols = [M.on_vertices(m, M.iso_metric), M.on_vertices(m, M.level_set),
+            M.on_vertices(m, M.velocity)]
+    r, *_ = run_gpu(transfer, m, x, t, sols, 0)
+    o = O.Oracle(m)
+    outs, elem, st, *_ = o.interp(x, t, sols, imet=0)
+    c = compare_volume(o, x, t, (r.sols, r.elem, r.status), (outs, elem, st), sols)
+    assert c["same"] >= c["nvol"] - max(3, c["nvol"] // 1000)
+    assert np.all(r.status == 1)
+
+
+def test_empty_and_single_point(transfer):
+    """Ragged edge cases: no new vertex at all, then exactly one (volume) and
+    one surface vertex."""
+    m, x, t, sols = cube_case(5, metric="iso")
+    r, *_ = run_gpu(transfer, m, x[:0], t[:0], sols, 0)
+    assert len(r.elem) == 0 and all(s.shape[0] == 0 for s in r.sols)
+    o = O.Oracle(m)
+    for i in (int(np.nonzero(t == 0)[0][7]), int(np.nonzero(t == 16)[0][3])):
+        xi, ti = x[i:i + 1], t[i:i + 1]
+        r, starts, e, v = run_gpu(transfer, m, xi, ti, sols, 0)
+        outs, elem, st, steps, e2, v2 = o.interp(xi, ti, sols, imet=0, fresh=True,
+                                                 start_vol=starts, start_bdy=starts)
+        assert r.elem[0] == elem[0] and r.status[0] == st[0]
+        for s in range(len(sols)):
+            assert bits_equal(r.sols[s], outs[s]).all()

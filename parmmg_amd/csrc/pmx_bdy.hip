@@ -564,19 +564,69 @@ __global__ __launch_bounds__(256) void k_exh_bdy(BdyArgs A) {
 }
 
 // tria hint grid: cell -> largest tria index whose centroid falls in it
+// (deterministic: the surface semantics depend on the start triangle)
+__device__ __forceinline__ void tria_hint_one(const TriRec *tris, const Pt4 *pts, int64_t k, int *grid,
+                                              const GridDesc &g) {
+  TriRec t = tris[k];
+  if (t.v[0] <= 0) return;
+  D3 a = ld3(pts, t.v[0]), b = ld3(pts, t.v[1]), c = ld3(pts, t.v[2]);
+  D3 m{(a.x + b.x + c.x) / 3.0, (a.y + b.y + c.y) / 3.0, (a.z + b.z + c.z) / 3.0};
+  int cx = (int)fmin(fmax((m.x - g.lo[0]) * g.inv[0], 0.0), (double)(g.dim[0] - 1));
+  int cy = (int)fmin(fmax((m.y - g.lo[1]) * g.inv[1], 0.0), (double)(g.dim[1] - 1));
+  int cz = (int)fmin(fmax((m.z - g.lo[2]) * g.inv[2], 0.0), (double)(g.dim[2] - 1));
+  atomicMax(&grid[(int64_t)cx + (int64_t)g.dim[0] * ((int64_t)cy + (int64_t)g.dim[1] * cz)], (int)k);
+}
+__device__ void tria_hint_part(const TriRec *tris, const Pt4 *pts, int64_t nt, int *grid,
+                               const GridDesc &g, int64_t b, int64_t nb) {
+  for (int64_t k = 1 + b * blockDim.x + threadIdx.x; k <= nt; k += nb * blockDim.x)
+    tria_hint_one(tris, pts, k, grid, g);
+}
+// the volume hint build (fixed-point centroids) and the tria hint build of
+// the surface path in ONE launch: blocks [0, nbt) sample tets, the rest walk
+// the boundary trias.  The latency-bound tria part then runs inside the
+// bandwidth-bound tet part instead of at the head of the surface path while
+// the volume walk saturates the memory system.
+__global__ __launch_bounds__(256) void k_hint_build_fused(const int4 *__restrict__ src, int64_t ne,
+                                                          int stride, int *__restrict__ grid, GridDesc g,
+                                                          const unsigned long long *__restrict__ xyzq,
+                                                          int64_t nbt, const TriRec *tris,
+                                                          const Pt4 *pts, int64_t nt, int *tgrid,
+                                                          GridDesc tg) {
+  if ((int64_t)blockIdx.x >= nbt) {
+    tria_hint_part(tris, pts, nt, tgrid, tg, blockIdx.x - nbt, gridDim.x - nbt);
+    return;
+  }
+  const int64_t n = (ne + stride - 1) / stride;
+  const int64_t t = xcd_remap(blockIdx.x, nbt) * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int4 v = src[t];
+  if (v.x <= 0) return;
+  const unsigned long long a = xyzq[v.x], b = xyzq[v.y], c = xyzq[v.z], d = xyzq[v.w];
+  const unsigned long long M = (1ull << 21) - 1;
+  int cq[3];
+#pragma unroll
+  for (int ax = 0; ax < 3; ax++) {
+    const int sh = 21 * ax;
+    const unsigned s4 = (unsigned)((a >> sh) & M) + (unsigned)((b >> sh) & M) +
+                        (unsigned)((c >> sh) & M) + (unsigned)((d >> sh) & M);
+    cq[ax] = min((int)(s4 >> (HINT_QF + 2)), g.dim[ax] - 1);
+  }
+  grid[(int64_t)cq[0] + (int64_t)g.dim[0] * ((int64_t)cq[1] + (int64_t)g.dim[1] * cq[2])] =
+      (int)(1 + t * stride);
+}
+void launch_hint_build_fused(const int4 *packed, int64_t ne, int stride, int *grid, GridDesc g,
+                             const unsigned long long *xyzq, const TriRec *tris, const Pt4 *pts,
+                             int64_t nt, int *tgrid, GridDesc tg, hipStream_t s) {
+  const int64_t n = (ne + stride - 1) / stride;
+  const int64_t nbt = std::max<int64_t>((n + 255) / 256, 1);
+  const int64_t nbr = std::min<int64_t>(std::max<int64_t>((nt + 255) / 256, 1), 4096);
+  hipLaunchKernelGGL(k_hint_build_fused, dim3((unsigned)(nbt + nbr)), dim3(256), 0, s, packed, ne,
+                     stride, grid, g, xyzq, nbt, tris, pts, nt, tgrid, tg);
+}
+
 __global__ __launch_bounds__(256) void k_tria_hint_build(const TriRec *tris, const Pt4 *pts,
                                                          int64_t nt, int *grid, GridDesc g) {
-  for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= nt;
-       k += (int64_t)gridDim.x * blockDim.x) {
-    TriRec t = tris[k];
-    if (t.v[0] <= 0) continue;
-    D3 a = ld3(pts, t.v[0]), b = ld3(pts, t.v[1]), c = ld3(pts, t.v[2]);
-    D3 m{(a.x + b.x + c.x) / 3.0, (a.y + b.y + c.y) / 3.0, (a.z + b.z + c.z) / 3.0};
-    int cx = (int)fmin(fmax((m.x - g.lo[0]) * g.inv[0], 0.0), (double)(g.dim[0] - 1));
-    int cy = (int)fmin(fmax((m.y - g.lo[1]) * g.inv[1], 0.0), (double)(g.dim[1] - 1));
-    int cz = (int)fmin(fmax((m.z - g.lo[2]) * g.inv[2], 0.0), (double)(g.dim[2] - 1));
-    atomicMax(&grid[(int64_t)cx + (int64_t)g.dim[0] * ((int64_t)cy + (int64_t)g.dim[1] * cz)], (int)k);
-  }
+  tria_hint_part(tris, pts, nt, grid, g, blockIdx.x, gridDim.x);
 }
 
 __device__ int tria_hint(const BdyArgs &A, D3 p) {
@@ -675,7 +725,7 @@ bool pmx_ctx::launch_bdy(const VolArgs &a, const pmx_run_opts &o, hipStream_t s)
   // tria hint grid: sized and allocated with the background
   // (pmx_ctx::size_tria_grid), zeroed by the step's prologue kernel
   const GridDesc tg = tgd;
-  {
+  if (!tria_hint_fused) {   // else built by k_hint_build_fused on the main stream
     int64_t nb = (nt + 255) / 256;
     if (nb > 4096) nb = 4096;
     hipLaunchKernelGGL(k_tria_hint_build, dim3((unsigned)std::max<int64_t>(nb, 1)), dim3(256), 0, s,

@@ -61,7 +61,10 @@ pmx_ctx *pmx_create(int device) {
     return nullptr;
   }
   ctx->stream = ctx->own;
-  if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess ||
+  int prio_lo = 0, prio_hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
+  if (hipStreamCreateWithPriority(&ctx->side_lo, hipStreamNonBlocking, prio_lo) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess) {
     pmx_destroy(ctx);
@@ -77,9 +80,11 @@ void pmx_destroy(pmx_ctx *ctx) {
   ctx->free_all();
   for (auto &e : ctx->events) hipEventDestroy(e);
   if (ctx->side) hipStreamSynchronize(ctx->side);
+  if (ctx->side_lo) hipStreamSynchronize(ctx->side_lo);
   if (ctx->ev_fork) hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) hipEventDestroy(ctx->ev_join);
   if (ctx->side) hipStreamDestroy(ctx->side);
+  if (ctx->side_lo) hipStreamDestroy(ctx->side_lo);
   if (ctx->own) hipStreamDestroy(ctx->own);
   delete ctx;
 }
@@ -406,6 +411,7 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   if (ev) CK(hipEventRecord(ev[0], st));
   // one prologue kernel zeroes the write masks, the counters and the hint grid
   const bool need_grid = !((opts.tune & 0x200) && !(opts.tune & 0x100));
+  ctx->tria_hint_fused = false;   // set below when the volume hint build also builds it
   launch_prologue(ctx->d_wmask.p, n, ctx->d_counts.p, need_grid ? ctx->d_grid.p : nullptr,
                   ctx->gcells, ctx->nq_bdy ? ctx->d_tgrid : nullptr, ctx->tcells, st);
   if (sd.metric_const)
@@ -447,6 +453,19 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
       // tune bit 13: strided reads of the connectivity stream (r01 A/B)
       const bool packed = stride == PMX_DEFAULT_HINT_STRIDE && !(opts.tune & 0x2000);
       if (A.grid64) launch_fill64(ctx->d_grid64.p, ctx->gcells, st);
+      // tune bit 31: the surface path's tria hint grid built in the same
+      // launch (k_hint_build_fused; r01: C2 +1.3 %, C3 +0.4 % step time --
+      // the latency-bound tria part lengthens the hint build more than it
+      // shortens the side stream)
+      ctx->tria_hint_fused = packed && !A.grid64 && !(opts.tune & 0x8000) &&
+                             !(opts.tune & (0x4000000 | 0x30000000)) &&
+                             ((unsigned)opts.tune & 0x80000000u) && ctx->nq_bdy &&
+                             bdy_mode == 2 && ctx->nt > 0;
+      if (ctx->tria_hint_fused)
+        launch_hint_build_fused(ctx->d_tets_s.p, ctx->ne, stride, ctx->d_grid.p, ctx->grid,
+                                ctx->d_xyzq.p, ctx->d_tris.p, ctx->d_pts.p, ctx->nt, ctx->d_tgrid,
+                                ctx->tgd, st);
+      else
       launch_hint_build(ctx->d_tetv.p, packed ? ctx->d_tets_s.p : nullptr, ctx->d_pts.p, ctx->ne,
                         stride, ctx->d_grid.p, ctx->grid, (opts.tune & 0x8000) ? 1 : 0, st,
                         const_cast<unsigned long long *>(A.grid64),
@@ -460,12 +479,15 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     if (ctx->nq_bdy && bdy_mode == 3) CK(hipStreamWaitEvent(st, ctx->ev_join, 0));
     if (ev) CK(hipEventRecord(ev[1], st));
     if (ctx->nq_bdy && bdy_mode == 2) {
+      // tune bit 30: the surface path on a lowest-priority stream (the
+      // volume walk's workgroups are dispatched first)
+      hipStream_t sd = (opts.tune & 0x40000000) ? ctx->side_lo : ctx->side;
       CK(hipEventRecord(ctx->ev_fork, st));
-      CK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-      if (ev) CK(hipEventRecord(ev[3], ctx->side));
-      if (!ctx->launch_bdy(A, opts, ctx->side)) return 0;
-      if (ev) CK(hipEventRecord(ev[5], ctx->side));
-      CK(hipEventRecord(ctx->ev_join, ctx->side));
+      CK(hipStreamWaitEvent(sd, ctx->ev_fork, 0));
+      if (ev) CK(hipEventRecord(ev[3], sd));
+      if (!ctx->launch_bdy(A, opts, sd)) return 0;
+      if (ev) CK(hipEventRecord(ev[5], sd));
+      CK(hipEventRecord(ctx->ev_join, sd));
     }
     if (ctx->tet_mode) {
       if (!ctx->launch_tet_locate(A, opts, st)) return 0;

@@ -201,3 +201,10 @@ __device__ __forceinline__ unsigned interp_bar(const double *__restrict__ sol, c
   return wm;
 }
 
+__device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nb) {
+  // blocks b and b+8 share an XCD (round-robin dispatch): give each XCD a
+  // contiguous range of the Morton-ordered queries so its L2 sees neighbours.
+  int64_t xcd = b & 7, r = b >> 3, q = nb >> 3, rem = nb & 7;
+  return (xcd < rem) ? xcd * (q + 1) + r : rem * (q + 1) + (xcd - rem) * q + r;
+}
+

@@ -17,6 +17,7 @@ struct pmx_ctx {
   // the surface path runs on `side`, forked after the prologue and joined
   // before the fallback: it overlaps the volume hint build and walk
   hipStream_t side = nullptr;
+  hipStream_t side_lo = nullptr;        // lowest-priority side stream (tune bit 30)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::string err;
 
@@ -71,6 +72,7 @@ struct pmx_ctx {
   int *d_tgrid = nullptr;
   size_t d_tgrid_cap = 0;
   GridDesc tgd{};
+  bool tria_hint_fused = false;         // this step's tria hint built with the volume hint
   int64_t tcells = 0;
 
   // statistics

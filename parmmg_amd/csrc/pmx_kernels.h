@@ -64,6 +64,9 @@ void launch_hint_build(const int4 *tetv, const int4 *packed, const Pt4 *pts, int
                        const float *xyzf = nullptr, const unsigned long long *xyzq = nullptr);
 // fraction bits of the fixed-point grid coordinates (dim <= 4096: 12 + 9 = 21 bits)
 #define HINT_QF 9
+void launch_hint_build_fused(const int4 *packed, int64_t ne, int stride, int *grid, GridDesc g,
+                             const unsigned long long *xyzq, const TriRec *tris, const Pt4 *pts,
+                             int64_t nt, int *tgrid, GridDesc tg, hipStream_t s);
 void launch_quant_xyz(const Pt4 *pts, int64_t n, GridDesc g, unsigned long long *q, hipStream_t s);
 void launch_fill64(unsigned long long *p, int64_t n, hipStream_t s);
 void launch_locate_vol(const VolArgs &a, hipStream_t s);

@@ -34,12 +34,6 @@ __device__ __forceinline__ void stable_ranks(const double l[4], int rk[4]) {
     }
 }
 
-__device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nb) {
-  // blocks b and b+8 share an XCD (round-robin dispatch): give each XCD a
-  // contiguous range of the Morton-ordered queries so its L2 sees neighbours.
-  int64_t xcd = b & 7, r = b >> 3, q = nb >> 3, rem = nb & 7;
-  return (xcd < rem) ? xcd * (q + 1) + r : rem * (q + 1) + (xcd - rem) * q + r;
-}
 
 __device__ __forceinline__ int clampi(double t, int n) {
   if (!(t > 0.0)) return 0;                 // also catches NaN

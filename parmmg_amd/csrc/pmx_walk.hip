@@ -495,8 +495,8 @@ __device__ __forceinline__ int exact_next(const TetRec &t, const double lam[4], 
   return next;
 }
 
-template <int LAYOUT, int S, bool TIES, bool DENSE, int RG = WALK_RING, int NT = 0>
-__global__ __launch_bounds__(256) void k_walks(VolArgs A) {
+template <int LAYOUT, int S, bool TIES, bool DENSE, int RG = WALK_RING, int NT = 0, int OCC = 1>
+__global__ __launch_bounds__(256, OCC) void k_walks(VolArgs A) {
   const int64_t b = walk_xcd_remap(blockIdx.x, gridDim.x);
   const int64_t j = b * blockDim.x + threadIdx.x;
   unsigned s_cnt = 0, s_sum = 0, s_max = 0, s_min = 0xffffffffu;
@@ -677,10 +677,12 @@ static void launch_walk_o(const VolArgs &a, int ties, hipStream_t s) {
     // sensitivity experiment: a 2-entry visited ring in the slot walk
     hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true, 2>), dim3((unsigned)nb), dim3(BS), 0, s, a);
   } else if (X && ties && a.exp >= 5 && a.xyz && !a.ref_walk) {
-    // sensitivity experiments: non-temporal tet loads (5), output stores (6), both (7)
+    // sensitivity experiments: non-temporal tet loads (5; r01: +25 % on C3,
+    // non-temporal output stores measured +4 % and removed); at least 5 (6)
+    // or 6 (7) waves per SIMD asked of the register allocator
     if (a.exp == 5) hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true, WALK_RING, 1>), dim3((unsigned)nb), dim3(BS), 0, s, a);
-    else if (a.exp == 6) hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true, WALK_RING, 2>), dim3((unsigned)nb), dim3(BS), 0, s, a);
-    else hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true, WALK_RING, 3>), dim3((unsigned)nb), dim3(BS), 0, s, a);
+    else if (a.exp == 6) hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true, WALK_RING, 0, 5>), dim3((unsigned)nb), dim3(BS), 0, s, a);
+    else hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true, WALK_RING, 0, 6>), dim3((unsigned)nb), dim3(BS), 0, s, a);
   } else if (X && !a.ref_walk) {
     // production: the slot walk, dense coordinates unless disabled
     if (a.xyz) {

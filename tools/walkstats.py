@@ -63,6 +63,16 @@ def main():
                                 "p99": float(np.percentile(d, 99)), "max": float(d.max())},
            "status": {int(k): int(v) for k, v in zip(*np.unique(r.status[vol], return_counts=True))},
            "stats": tr.locate_stats()}
+    # surface path: steps per point and per wave (64 consecutive list entries)
+    bdy = np.nonzero(t == 16)[0]
+    if len(bdy):
+        bs = np.abs(r.steps[bdy]).astype(np.int64)
+        pad = (-len(bs)) % 64
+        wmax = np.concatenate([bs, np.zeros(pad, np.int64)]).reshape(-1, 64).max(1)
+        out["bdy"] = {"n": int(len(bdy)), "steps_mean": float(bs.mean()),
+                      "steps_hist": {int(i): int(v) for i, v in enumerate(np.bincount(np.clip(bs, 0, 40))) if v},
+                      "wave_max_mean": float(wmax.mean()), "wave_max_max": int(wmax.max()),
+                      "status": {int(k): int(v) for k, v in zip(*np.unique(r.status[bdy], return_counts=True))}}
     print(json.dumps(out, indent=1))
 
 

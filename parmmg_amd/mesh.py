@@ -226,3 +226,60 @@ def read_medit_sol(path: str) -> list[np.ndarray]:
         out.append(a)
         off += s
     return out
+
+
+# ---- Medit writers (the wire format of ParMmg's
+# src/inout_pmmg.c via Mmg's MMG3D_saveMesh / MMG3D_saveSol) ----------------------
+
+_MEDIT_TYPE = {1: 1, 3: 2, 6: 3}     # solution size -> Medit type (scalar, vector, tensor)
+
+
+def write_medit(path: str, m: Mesh, required=None) -> None:
+    """ASCII Medit mesh: Vertices (ref 0), Tetrahedra (ref 0), the boundary
+    Triangles and, if given, RequiredVertices (1-based indices; the MG_REQ
+    points that the transfer copies instead of interpolating).  Coordinates
+    in %.17g, so read_medit(write_medit(m)) is bit-identical."""
+    with open(path, "w") as f:
+        f.write("MeshVersionFormatted 2\n\nDimension 3\n\n")
+        f.write(f"Vertices\n{m.np}\n")
+        f.writelines(f"{x:.17g} {y:.17g} {z:.17g} 0\n" for x, y, z in m.xyz[1:])
+        f.write(f"\nTetrahedra\n{m.ne}\n")
+        f.writelines(f"{a} {b} {c} {d} 0\n" for a, b, c, d in m.tet[1:])
+        if m.nt:
+            f.write(f"\nTriangles\n{m.nt}\n")
+            f.writelines(f"{a} {b} {c} 0\n" for a, b, c in m.tria[1:])
+        if required is not None and len(required):
+            f.write(f"\nRequiredVertices\n{len(required)}\n")
+            f.writelines(f"{int(i)}\n" for i in required)
+        f.write("\nEnd\n")
+
+
+def read_medit_required(path: str) -> np.ndarray:
+    """1-based indices listed under RequiredVertices (empty if none)."""
+    with open(path) as f:
+        tok = f.read().split()
+    if "RequiredVertices" not in tok:
+        return np.zeros(0, np.int64)
+    i = tok.index("RequiredVertices")
+    n = int(tok[i + 1])
+    return np.array(tok[i + 2: i + 2 + n], dtype=np.int64)
+
+
+def write_medit_sol(path: str, sols: list[np.ndarray]) -> None:
+    """ASCII SolAtVertices of (np+1, size) arrays (row 0 unused, like
+    read_medit_sol returns them); tensors from Mmg (11,12,13,22,23,33) to
+    Medit (11,12,22,13,23,33) order."""
+    n = sols[0].shape[0] - 1
+    cols = []
+    for s in sols:
+        a = np.asarray(s, np.float64)[1:]
+        if a.shape[1] == 6:
+            a = a[:, [0, 1, 3, 2, 4, 5]]
+        cols.append(a)
+    vals = np.concatenate(cols, axis=1) if cols else np.zeros((n, 0))
+    types = " ".join(str(_MEDIT_TYPE[s.shape[1]]) for s in sols)
+    with open(path, "w") as f:
+        f.write("MeshVersionFormatted 2\n\nDimension 3\n\n")
+        f.write(f"SolAtVertices\n{n}\n{len(sols)} {types}\n")
+        f.writelines(" ".join(f"{v:.17g}" for v in row) + "\n" for row in vals)
+        f.write("\nEnd\n")

@@ -725,7 +725,11 @@ bool pmx_ctx::launch_bdy(const VolArgs &a, const pmx_run_opts &o, hipStream_t s)
   // tria hint grid: sized and allocated with the background
   // (pmx_ctx::size_tria_grid), zeroed by the step's prologue kernel
   const GridDesc tg = tgd;
-  if (!tria_hint_fused) {   // else built by k_hint_build_fused on the main stream
+  if (!tria_hint_fused) {   // else zeroed + built on the main stream (k_hint_build_fused)
+    if (hipMemsetAsync(d_tgrid, 0, sizeof(int) * (size_t)tcells, s) != hipSuccess) {
+      err = "tria hint grid memset";
+      return false;
+    }
     int64_t nb = (nt + 255) / 256;
     if (nb > 4096) nb = 4096;
     hipLaunchKernelGGL(k_tria_hint_build, dim3((unsigned)std::max<int64_t>(nb, 1)), dim3(256), 0, s,

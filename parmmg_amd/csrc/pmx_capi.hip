@@ -412,8 +412,11 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   // one prologue kernel zeroes the write masks, the counters and the hint grid
   const bool need_grid = !((opts.tune & 0x200) && !(opts.tune & 0x100));
   ctx->tria_hint_fused = false;   // set below when the volume hint build also builds it
+  // the tria hint grid is zeroed at the head of the surface path (off the
+  // main stream), unless the volume hint launch builds it (tune bit 31)
+  const bool tgrid_here = ctx->nq_bdy && ((unsigned)opts.tune & 0x80000000u);
   launch_prologue(ctx->d_wmask.p, n, ctx->d_counts.p, need_grid ? ctx->d_grid.p : nullptr,
-                  ctx->gcells, ctx->nq_bdy ? ctx->d_tgrid : nullptr, ctx->tcells, st);
+                  ctx->gcells, tgrid_here ? ctx->d_tgrid : nullptr, ctx->tcells, st);
   if (sd.metric_const)
     launch_const_metric(ctx->d_kind.p, n, ctx->d_out.p, S, sd.off[sd.imet], sd.size[sd.imet],
                         opts.hsiz, ctx->d_wmask.p, sd.imet, st);

@@ -83,6 +83,7 @@ void launch_prologue(uint8_t *wmask, int64_t n, unsigned *counts, int *grid, int
 
 struct StatArgs {
   const Pt4 *pts;
+  const double *xyz;            // dense 24-B coordinates (k_build_xyz); null: pts
   const TetRec *tets;
   const int4 *tetv;             // connectivity stream (v only)
   int64_t ne;

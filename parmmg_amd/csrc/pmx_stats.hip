@@ -18,6 +18,7 @@
 // every length match the reference.
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 #include "pmx_internal.h"
 
@@ -90,9 +91,17 @@ struct QualPart {
   long long iel, ne, good, med, his[5];
 };
 
+__device__ __forceinline__ D3 sld3(const StatArgs &A, int i) {
+  if (A.xyz) {
+    const double *r = A.xyz + 3 * (int64_t)i;
+    return D3{r[0], r[1], r[2]};
+  }
+  return ld3(A.pts, i);
+}
+
 template <bool ANI>
 __device__ double tet_quality(const StatArgs &A, int64_t k, const TetRec &t) {
-  D3 a = ld3(A.pts, t.v[0]), b = ld3(A.pts, t.v[1]), c = ld3(A.pts, t.v[2]), d = ld3(A.pts, t.v[3]);
+  D3 a = sld3(A, t.v[0]), b = sld3(A, t.v[1]), c = sld3(A, t.v[2]), d = sld3(A, t.v[3]);
   if (ANI) {
     const double *m = A.sol;
     return caltet_ani(a, b, c, d, m + (int64_t)t.v[0] * A.S + A.moff, m + (int64_t)t.v[1] * A.S + A.moff,
@@ -236,7 +245,7 @@ __device__ __forceinline__ int loc_of(const TetRec &t, int p) {
 
 // MMG5_lenEdg_iso / lenEdg_ani (restated, unpinned)
 __device__ double edge_len(const StatArgs &A, int p1, int p2) {
-  D3 c1 = ld3(A.pts, p1), c2 = ld3(A.pts, p2);
+  D3 c1 = sld3(A, p1), c2 = sld3(A, p2);
   double ux = c2.x - c1.x, uy = c2.y - c1.y, uz = c2.z - c1.z;
   if (A.msize == 6) {
     const double *m1 = A.sol + (int64_t)p1 * A.S + A.moff, *m2 = A.sol + (int64_t)p2 * A.S + A.moff;
@@ -516,6 +525,10 @@ static int stat_blocks(int64_t ne) {
 static bool stat_args(pmx_ctx *ctx, StatArgs &A) {
   if (!ctx->have_bg) { ctx->err = "statistics: upload a group first"; return false; }
   A.pts = ctx->d_pts.p;
+  // vertex gathers from the dense 24-B stream (PMX_STATS_PT4=1: the 32-B
+  // Pt4 records, for A/B)
+  const char *pt4 = getenv("PMX_STATS_PT4");
+  A.xyz = (pt4 && pt4[0] == '1') ? nullptr : ctx->d_xyz.p;
   A.tets = ctx->d_tets.p;
   A.tetv = ctx->d_tetv.p;
   A.ne = ctx->ne;

@@ -118,6 +118,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N>1 process group backend (nccl = RCCL; gloo only to rehearse "
+                         "the multi-rank path, e.g. several ranks on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -127,8 +130,14 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
+        # PMX_BENCH_SAME_DEVICE=1 (rehearsal with gloo): every rank on GPU 0
+        if os.environ.get("PMX_BENCH_SAME_DEVICE") == "1":
+            local = 0
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     from parmmg_amd import build
     build.build_meshgen()

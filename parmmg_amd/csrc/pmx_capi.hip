@@ -40,6 +40,20 @@ static bool dgrow(pmx_ctx *ctx, DevBuf<T> &b, size_t n) {
   b.cap = n;
   return true;
 }
+// pinned staging of at least `bytes`, 25 % slack so that a slowly growing
+// ParMmg group does not re-pin every iteration
+static char *hstage(pmx_ctx *ctx, size_t bytes) {
+  if (bytes <= ctx->h_stage_cap && ctx->h_stage) return (char *)ctx->h_stage;
+  if (ctx->h_stage) hipHostFree(ctx->h_stage);
+  ctx->h_stage = nullptr;
+  ctx->h_stage_cap = 0;
+  const size_t cap = std::max<size_t>(bytes + bytes / 4, 1 << 20);
+  if (!ok(ctx, hipHostMalloc(&ctx->h_stage, cap, hipHostMallocDefault), "hipHostMalloc")) return nullptr;
+  ctx->h_stage_cap = cap;
+  return (char *)ctx->h_stage;
+}
+static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+
 template <class T> static void dfree(DevBuf<T> &b) {
   if (b.p) hipFree(b.p);
   b.p = nullptr;
@@ -287,28 +301,41 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   hipSetDevice(ctx->device);
   const int64_t n = pv->last - pv->first + 1;
   if (n < 0 || n >= (1LL << 31)) { ctx->err = "pmx_upload_points: bad range"; return 0; }
-  std::vector<Pt4> hq((size_t)std::max<int64_t>(n, 1));
-  std::vector<int8_t> hk((size_t)std::max<int64_t>(n, 1));
+  const size_t nn = (size_t)std::max<int64_t>(n, 1);
+  // staging layout (pinned): q | kind | vol list | bdy list | dense vol coords
+  const size_t o_q = 0, o_k = o_q + al256(nn * sizeof(Pt4)), o_vl = o_k + al256(nn),
+               o_bl = o_vl + al256(nn * sizeof(int)), o_qv = o_bl + al256(nn * sizeof(int)),
+               total = o_qv + al256(nn * 3 * sizeof(double));
+  CK(hipStreamSynchronize(ctx->stream));   // the arena may still feed an earlier copy
+  char *st = hstage(ctx, total);
+  if (!st) return 0;
+  Pt4 *hq = (Pt4 *)(st + o_q);
+  int8_t *hk = (int8_t *)(st + o_k);
+  int *vl = (int *)(st + o_vl), *bl = (int *)(st + o_bl);
+  double *hqv = (double *)(st + o_qv);
   const char *pc = (const char *)pv->c;
   const char *tg = (const char *)pv->tag;
-  int64_t nv = 0, nb = 0;
-  std::vector<int> vl, bl;           // per-path point lists, input order kept
-  vl.reserve((size_t)n);
+  int64_t nv = 0, nb = 0;            // per-path point lists, input order kept
   for (int64_t j = 0; j < n; j++) {
     const double *c = (const double *)(pc + (pv->first + j) * pv->stride);
-    hq[(size_t)j] = Pt4{c[0], c[1], c[2], 0.0};
+    hq[j] = Pt4{c[0], c[1], c[2], 0.0};
     unsigned tag = tg ? *(const uint16_t *)(tg + (pv->first + j) * pv->tag_stride) : 0u;
     int8_t kd;
     if (tag >= PMX_TAG_NUL) kd = KIND_NUL;
     else if (tag & PMX_TAG_REQ) kd = KIND_SKIP;
-    else if (tag & PMX_TAG_BDY) { kd = KIND_BDY; nb++; bl.push_back((int)j); }
-    else { kd = KIND_VOL; nv++; vl.push_back((int)j); }
-    hk[(size_t)j] = kd;
+    else if (tag & PMX_TAG_BDY) { kd = KIND_BDY; bl[nb++] = (int)j; }
+    else {
+      kd = KIND_VOL;
+      // the volume points' coordinates once more, dense (24 B) and contiguous
+      // in list order: the walks read them coalesced, without a list -> q gather
+      hqv[3 * nv] = c[0]; hqv[3 * nv + 1] = c[1]; hqv[3 * nv + 2] = c[2];
+      vl[nv++] = (int)j;
+    }
+    hk[j] = kd;
   }
   ctx->nq = n;
   ctx->nq_vol = nv;
   ctx->nq_bdy = nb;
-  const size_t nn = (size_t)std::max<int64_t>(n, 1);
   if (!dgrow(ctx, ctx->d_q, nn)) return 0;
   if (!dgrow(ctx, ctx->d_kind, nn)) return 0;
   if (!dgrow(ctx, ctx->d_wmask, nn)) return 0;
@@ -329,23 +356,14 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   // one record per wave of the largest k_walk block (1024 threads)
   if (!dgrow(ctx, ctx->d_vstat, (size_t)std::max<int64_t>((nv + 1023) / 1024 * 16 + 4, 1))) return 0;
   if (!dgrow(ctx, ctx->d_bstat, (size_t)std::max<int64_t>((nb + 63) / 64 + 4, 1))) return 0;
+  if (!dgrow(ctx, ctx->d_qv, (size_t)std::max<int64_t>(nv, 1) * 3)) return 0;
   if (n) {   // no new vertex at all is a valid (empty) step
-    CK(hipMemcpyAsync(ctx->d_q.p, hq.data(), (size_t)n * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
-    CK(hipMemcpyAsync(ctx->d_kind.p, hk.data(), (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+    CK(hipMemcpyAsync(ctx->d_q.p, hq, (size_t)n * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
+    CK(hipMemcpyAsync(ctx->d_kind.p, hk, (size_t)n, hipMemcpyHostToDevice, ctx->stream));
   }
-  if (nv) CK(hipMemcpyAsync(ctx->d_vollist.p, vl.data(), (size_t)nv * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
-  // the volume points' coordinates once more, dense (24 B) and contiguous in
-  // list order: the walks read them coalesced, without a list -> q gather
-  std::vector<double> hqv((size_t)std::max<int64_t>(nv, 1) * 3);
-  for (int64_t j = 0; j < nv; j++) {
-    const Pt4 &c = hq[(size_t)vl[(size_t)j]];
-    hqv[3 * (size_t)j] = c.x;
-    hqv[3 * (size_t)j + 1] = c.y;
-    hqv[3 * (size_t)j + 2] = c.z;
-  }
-  if (!dgrow(ctx, ctx->d_qv, hqv.size())) return 0;
-  if (nv) CK(hipMemcpyAsync(ctx->d_qv.p, hqv.data(), (size_t)nv * 3 * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-  if (nb) CK(hipMemcpyAsync(ctx->d_bdylist.p, bl.data(), (size_t)nb * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+  if (nv) CK(hipMemcpyAsync(ctx->d_vollist.p, vl, (size_t)nv * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+  if (nv) CK(hipMemcpyAsync(ctx->d_qv.p, hqv, (size_t)nv * 3 * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  if (nb) CK(hipMemcpyAsync(ctx->d_bdylist.p, bl, (size_t)nb * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
   ctx->have_pts = true;
   ctx->out_S = -1;
@@ -534,24 +552,38 @@ int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem, int *sta
   const int S = ctx->sd.S;
   CK(hipStreamSynchronize(ctx->stream));
   if (n == 0) return 1;   // empty step: nothing to copy
-  if (new_sols && S > 0) {
-    std::vector<double> h((size_t)(n * S));
-    std::vector<uint8_t> wm((size_t)std::max<int64_t>(n, 1));
-    CK(hipMemcpy(h.data(), ctx->d_out.p, (size_t)(n * S) * sizeof(double), hipMemcpyDeviceToHost));
-    CK(hipMemcpy(wm.data(), ctx->d_wmask.p, (size_t)n, hipMemcpyDeviceToHost));
+  // every device -> host copy lands in the pinned arena (async DMA, one sync),
+  // then the host scatters into the caller's (pageable, strided) arrays
+  const bool want_sol = new_sols && S > 0;
+  const size_t o_out = 0, o_wm = o_out + al256(want_sol ? (size_t)(n * S) * sizeof(double) : 0),
+               o_el = o_wm + al256(want_sol ? (size_t)n : 0), o_st = o_el + al256((size_t)n * sizeof(int)),
+               o_sp = o_st + al256((size_t)n * sizeof(int)), total = o_sp + al256((size_t)n * sizeof(int));
+  char *st = hstage(ctx, total);
+  if (!st) return 0;
+  const double *h = (const double *)(st + o_out);
+  const uint8_t *wm = (const uint8_t *)(st + o_wm);
+  if (want_sol) {
+    CK(hipMemcpyAsync(st + o_out, ctx->d_out.p, (size_t)(n * S) * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    CK(hipMemcpyAsync(st + o_wm, ctx->d_wmask.p, (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  if (elem) CK(hipMemcpyAsync(st + o_el, ctx->d_elem.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  if (status) CK(hipMemcpyAsync(st + o_st, ctx->d_status.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  if (steps) CK(hipMemcpyAsync(st + o_sp, ctx->d_steps.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  if (want_sol) {
     for (int s = 0; s < ctx->sd.nsol; s++) {
       double *dst = new_sols[s].m;
       const int sz = ctx->sd.size[s], off = ctx->sd.off[s];
       if (!dst) continue;
       for (int64_t i = 0; i < n; i++) {
-        if (!(wm[(size_t)i] & (1u << s))) continue;
+        if (!(wm[i] & (1u << s))) continue;
         for (int j = 0; j < sz; j++) dst[i * sz + j] = h[(size_t)(i * S + off + j)];
       }
     }
   }
-  if (elem) CK(hipMemcpy(elem, ctx->d_elem.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
-  if (status) CK(hipMemcpy(status, ctx->d_status.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
-  if (steps) CK(hipMemcpy(steps, ctx->d_steps.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
+  if (elem) memcpy(elem, st + o_el, (size_t)n * sizeof(int));
+  if (status) memcpy(status, st + o_st, (size_t)n * sizeof(int));
+  if (steps) memcpy(steps, st + o_sp, (size_t)n * sizeof(int));
   return 1;
 }
 
@@ -678,6 +710,9 @@ hipEvent_t *pmx_ctx::next_event_slot() {
 }
 
 void pmx_ctx::free_all() {
+  if (h_stage) hipHostFree(h_stage);
+  h_stage = nullptr;
+  h_stage_cap = 0;
   dfree(d_pts); dfree(d_tets); dfree(d_sol); dfree(d_xyz); dfree(d_xyzf); dfree(d_xyzq); dfree(d_tris); dfree(d_trn); dfree(d_grid); dfree(d_grid64);
   dfree(d_ntoff); dfree(d_ntlist);
   dfree(d_q); dfree(d_kind); dfree(d_wmask); dfree(d_out); dfree(d_elem); dfree(d_status);

@@ -20,6 +20,11 @@ struct pmx_ctx {
   hipStream_t side_lo = nullptr;        // lowest-priority side stream (tune bit 30)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::string err;
+  // pinned host staging arena (hipHostMalloc, grown on demand, reused across
+  // steps): point uploads and result downloads go through it as async DMA
+  // instead of pageable copies (PCIe-inclusive rate)
+  void *h_stage = nullptr;
+  size_t h_stage_cap = 0;
 
   // background group
   bool have_bg = false;

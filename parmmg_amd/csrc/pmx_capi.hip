@@ -153,10 +153,20 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     return 0;
   }
   const int64_t np = m->np, ne = m->ne, nt = m->nt;
+  int S0 = 0;
+  for (int s = 0; s < nsol; s++) S0 += sols[s].size;
+  S0 += (S0 >= 3 && (S0 & 1)) ? 1 : 0;   // room for PMX_SOL_PAD
+  // pinned staging: points | tets | solutions (async DMA, one sync at the end)
+  const size_t o_p = 0, o_t = o_p + al256((size_t)(np + 1) * sizeof(Pt4)),
+               o_s = o_t + al256((size_t)(ne + 1) * sizeof(TetRec)),
+               total = o_s + al256((size_t)(np + 1) * std::max(S0, 1) * sizeof(double));
+  CK(hipStreamSynchronize(ctx->stream));   // the arena may still feed an earlier copy
+  char *stg = hstage(ctx, total);
+  if (!stg) return 0;
   ctx->np = np; ctx->ne = ne; ctx->nt = nt; ctx->hausd = m->hausd;
 
   // points -> Pt4, bbox
-  std::vector<Pt4> hp((size_t)(np + 1));
+  Pt4 *hp = (Pt4 *)(stg + o_p);
   double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
   hp[0] = Pt4{0, 0, 0, 0};
   const char *pc = (const char *)m->point_c;
@@ -169,7 +179,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     }
   }
   // tets -> TetRec with neighbour tet index
-  std::vector<TetRec> ht((size_t)(ne + 1));
+  TetRec *ht = (TetRec *)(stg + o_t);
   memset(&ht[0], 0, sizeof(TetRec));
   const char *tc = (const char *)m->tetra_v;
   for (int64_t k = 1; k <= ne; k++) {
@@ -200,10 +210,14 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   // saved loads (k_walk 1.84 vs 1.78 ms, r01).
   const char *pad_env = getenv("PMX_SOL_PAD");
   const bool pad = pad_env && pad_env[0] == '1';
+  const int S_sum = S;
   S = (pad && S >= 3 && (S & 1)) ? S + 1 : S;
   sd.S = S;
   ctx->sd = sd;
-  std::vector<double> hs((size_t)(np + 1) * std::max(S, 1), 0.0);
+  const size_t hs_n = (size_t)(np + 1) * std::max(S, 1);
+  double *hs = (double *)(stg + o_s);
+  if (S != S_sum) memset(hs, 0, hs_n * sizeof(double));      // pad column (or no solution)
+  else memset(hs, 0, (size_t)std::max(S, 1) * sizeof(double));   // row 0 (unused slot)
   for (int s = 0; s < nsol; s++) {
     const int sz = sols[s].size;
     if (!sols[s].m) { ctx->err = "pmx_upload_background: null solution"; return 0; }
@@ -258,15 +272,15 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
 
   if (!dgrow(ctx, ctx->d_pts, (size_t)(np + 1))) return 0;
   if (!dgrow(ctx, ctx->d_tets, (size_t)(ne + 1))) return 0;
-  if (!dgrow(ctx, ctx->d_sol, hs.size())) return 0;
+  if (!dgrow(ctx, ctx->d_sol, hs_n)) return 0;
   if (!dgrow(ctx, ctx->d_tris, (size_t)(nt + 1))) return 0;
   if (!dgrow(ctx, ctx->d_grid, (size_t)cells)) return 0;
   if (!dgrow(ctx, ctx->d_grid64, (size_t)cells)) return 0;
   if (!dgrow(ctx, ctx->d_ntoff, ctx->h_ntoff.size())) return 0;
   if (!dgrow(ctx, ctx->d_ntlist, std::max<size_t>(ctx->h_ntlist.size(), 1))) return 0;
   if (!dgrow(ctx, ctx->d_trn, (size_t)(nt + 1))) return 0;
-  CK(hipMemcpyAsync(ctx->d_pts.p, hp.data(), hp.size() * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
-  CK(hipMemcpyAsync(ctx->d_tets.p, ht.data(), ht.size() * sizeof(TetRec), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemcpyAsync(ctx->d_pts.p, hp, (size_t)(np + 1) * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemcpyAsync(ctx->d_tets.p, ht, (size_t)(ne + 1) * sizeof(TetRec), hipMemcpyHostToDevice, ctx->stream));
   // connectivity-only stream for the tet-centric pass (16 of the 32 B)
   if (!dgrow(ctx, ctx->d_tetv, (size_t)(ne + 1))) return 0;
   launch_tet_conn(ctx->d_tets.p, 1, ne + 1, ctx->d_tetv.p, ctx->stream);
@@ -278,7 +292,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     if (!dgrow(ctx, ctx->d_tets_s, (size_t)std::max<int64_t>(ns, 1))) return 0;
     launch_tet_conn(ctx->d_tets.p + 1, PMX_DEFAULT_HINT_STRIDE, ns, ctx->d_tets_s.p, ctx->stream);
   }
-  CK(hipMemcpyAsync(ctx->d_sol.p, hs.data(), hs.size() * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemcpyAsync(ctx->d_sol.p, hs, hs_n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_tris.p, htr.data(), htr.size() * sizeof(TriRec), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_ntoff.p, ctx->h_ntoff.data(), ctx->h_ntoff.size() * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
   if (!ctx->h_ntlist.empty())

@@ -409,3 +409,24 @@ def test_empty_and_single_point(transfer):
         assert r.elem[0] == elem[0] and r.status[0] == st[0]
         for s in range(len(sols)):
             assert bits_equal(r.sols[s], outs[s]).all()
+
+
+def test_staging_arena_regrow_and_reuse(transfer):
+    """The pinned host staging arena (pmx_capi.hip hstage) is grown and reused
+    across uploads of different sizes: small -> large -> small background and
+    point sets on one context give the oracle's results each time, and the
+    last small step is bit-identical to the first."""
+    first = None
+    for n, metric in ((5, "iso"), (10, "ani"), (5, "iso")):
+        m, x, t, sols = cube_case(n, metric=metric, surface=False)
+        r, *_ = run_gpu(transfer, m, x, t, sols, 0)
+        o = O.Oracle(m)
+        outs, elem, st, steps, e, v = o.interp(x, t, sols, imet=0)
+        c = compare_volume(o, x, t, (r.sols, r.elem, r.status), (outs, elem, st), sols)
+        assert c["same"] >= c["nvol"] - max(3, c["nvol"] // 1000)
+        assert np.all(r.status[t == 0] == 1)
+        if first is None:
+            first = r
+    assert np.array_equal(first.elem, r.elem) and np.array_equal(first.status, r.status)
+    for a, b in zip(first.sols, r.sols):
+        assert bits_equal(a, b).all()

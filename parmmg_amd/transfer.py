@@ -130,18 +130,30 @@ class Transfer:
         o.hsiz, o.timing, o.max_walk, o.hint_stride, o.tune = hsiz, int(timing), max_walk, hint_stride, tune
         self._chk(self.lib.pmx_run(self.ctx, C.byref(o)), "pmx_run")
 
-    def download(self, init: list[np.ndarray] | None = None) -> Result:
+    def download(self, init: list[np.ndarray] | None = None, into: Result | None = None) -> Result:
+        """Results into new arrays (``init`` = values kept where a field is not
+        written), or in place into the arrays of ``into`` -- ParMmg's case, whose
+        ``met->m`` / ``field->m`` already exist (no allocation per step)."""
         n = self.npts
-        outs = []
+        if into is not None:
+            outs, elem, status, steps = into.sols, into.elem, into.status, into.steps
+            if (len(outs) != len(self.sizes) or any(
+                    a.dtype != np.float64 or not a.flags.c_contiguous or a.shape != (n, sz)
+                    for a, sz in zip(outs, self.sizes)) or any(
+                    a.dtype != np.int32 or not a.flags.c_contiguous or a.shape != (n,)
+                    for a in (elem, status, steps))):
+                raise ValueError("download(into=...): arrays do not match the uploaded step")
+        else:
+            outs = []
+            for i, sz in enumerate(self.sizes):
+                outs.append(np.array(init[i], np.float64, copy=True).reshape(n, sz) if init is not None
+                            else np.full((n, sz), np.nan))
+            elem = np.zeros(n, np.int32)
+            status = np.zeros(n, np.int32)
+            steps = np.zeros(n, np.int32)
         views = (N.SolView * max(len(self.sizes), 1))()
-        for i, sz in enumerate(self.sizes):
-            a = (np.array(init[i], np.float64, copy=True).reshape(n, sz) if init is not None
-                 else np.full((n, sz), np.nan))
-            outs.append(a)
+        for i, (a, sz) in enumerate(zip(outs, self.sizes)):
             views[i].size, views[i].m = sz, _dp(a)
-        elem = np.zeros(n, np.int32)
-        status = np.zeros(n, np.int32)
-        steps = np.zeros(n, np.int32)
         self._chk(self.lib.pmx_download(self.ctx, views, _ip(elem), _ip(status), _ip(steps)),
                   "pmx_download")
         return Result(outs, elem, status, steps)

@@ -430,3 +430,20 @@ def test_staging_arena_regrow_and_reuse(transfer):
     assert np.array_equal(first.elem, r.elem) and np.array_equal(first.status, r.status)
     for a, b in zip(first.sols, r.sols):
         assert bits_equal(a, b).all()
+
+
+def test_download_into_existing_arrays(transfer):
+    """download(into=...) writes the step's results in place (ParMmg's met->m /
+    field->m exist before the step): bit-identical to a fresh download."""
+    m, x, t, sols = cube_case(7, metric="ani")
+    r, *_ = run_gpu(transfer, m, x, t, sols, 0)
+    buf = transfer.download()
+    for a in buf.sols:
+        a.fill(np.nan)
+    buf.elem.fill(-7)
+    transfer.download(into=buf)
+    assert np.array_equal(buf.elem, r.elem) and np.array_equal(buf.status, r.status)
+    for a, b in zip(buf.sols, r.sols):
+        assert bits_equal(a, b).all()
+    with pytest.raises(ValueError):
+        transfer.download(into=type(buf)(buf.sols[:0], buf.elem, buf.status, buf.steps))

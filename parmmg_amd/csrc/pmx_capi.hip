@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pmx_transfer.h"
@@ -53,6 +54,30 @@ static char *hstage(pmx_ctx *ctx, size_t bytes) {
   return (char *)ctx->h_stage;
 }
 static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+// host gathers/scatters of large AoS arrays split over a few threads
+// (PMX_HOST_THREADS, default min(8, hardware threads)); small ranges stay serial
+static unsigned host_threads() {
+  static const unsigned T = [] {
+    const char *e = getenv("PMX_HOST_THREADS");
+    unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    unsigned t = e ? (unsigned)std::max(1, atoi(e)) : std::min(8u, hw);
+    return std::min(t, 64u);
+  }();
+  return T;
+}
+template <class F> static void par_for(int64_t lo, int64_t hi, F f) {
+  const unsigned T = host_threads();
+  const int64_t n = hi - lo;
+  if (T <= 1 || n < (1 << 18)) { f(lo, hi); return; }
+  std::vector<std::thread> th;
+  const int64_t chunk = (n + T - 1) / T;
+  for (unsigned i = 0; i < T; i++) {
+    const int64_t a = lo + (int64_t)i * chunk, b = std::min(hi, a + chunk);
+    if (a < b) th.emplace_back(f, a, b);
+  }
+  for (auto &x : th) x.join();
+}
 
 template <class T> static void dfree(DevBuf<T> &b) {
   if (b.p) hipFree(b.p);
@@ -182,14 +207,16 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   TetRec *ht = (TetRec *)(stg + o_t);
   memset(&ht[0], 0, sizeof(TetRec));
   const char *tc = (const char *)m->tetra_v;
-  for (int64_t k = 1; k <= ne; k++) {
-    const int *v = (const int *)(tc + k * m->tetra_stride);
-    TetRec &r = ht[(size_t)k];
-    for (int l = 0; l < 4; l++) {
-      r.v[l] = v[l];
-      r.nb[l] = adja_in[4 * (k - 1) + 1 + l] / 4;
+  par_for(1, ne + 1, [&](int64_t k0, int64_t k1) {
+    for (int64_t k = k0; k < k1; k++) {
+      const int *v = (const int *)(tc + k * m->tetra_stride);
+      TetRec &r = ht[(size_t)k];
+      for (int l = 0; l < 4; l++) {
+        r.v[l] = v[l];
+        r.nb[l] = adja_in[4 * (k - 1) + 1 + l] / 4;
+      }
     }
-  }
+  });
   // solutions -> interleaved [np+1][S]
   SolDesc sd{};
   sd.nsol = nsol;
@@ -221,8 +248,12 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   for (int s = 0; s < nsol; s++) {
     const int sz = sols[s].size;
     if (!sols[s].m) { ctx->err = "pmx_upload_background: null solution"; return 0; }
-    for (int64_t i = 1; i <= np; i++)
-      for (int j = 0; j < sz; j++) hs[(size_t)i * S + sd.off[s] + j] = sols[s].m[i * sz + j];
+    const double *src = sols[s].m;
+    const int off = sd.off[s];
+    par_for(1, np + 1, [&](int64_t i0, int64_t i1) {
+      for (int64_t i = i0; i < i1; i++)
+        for (int j = 0; j < sz; j++) hs[(size_t)i * S + off + j] = src[i * sz + j];
+    });
   }
   // boundary triangles
   std::vector<TriRec> htr((size_t)(nt + 1));
@@ -329,24 +360,49 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   double *hqv = (double *)(st + o_qv);
   const char *pc = (const char *)pv->c;
   const char *tg = (const char *)pv->tag;
-  int64_t nv = 0, nb = 0;            // per-path point lists, input order kept
-  for (int64_t j = 0; j < n; j++) {
-    const double *c = (const double *)(pc + (pv->first + j) * pv->stride);
-    hq[j] = Pt4{c[0], c[1], c[2], 0.0};
-    unsigned tag = tg ? *(const uint16_t *)(tg + (pv->first + j) * pv->tag_stride) : 0u;
-    int8_t kd;
-    if (tag >= PMX_TAG_NUL) kd = KIND_NUL;
-    else if (tag & PMX_TAG_REQ) kd = KIND_SKIP;
-    else if (tag & PMX_TAG_BDY) { kd = KIND_BDY; bl[nb++] = (int)j; }
-    else {
-      kd = KIND_VOL;
-      // the volume points' coordinates once more, dense (24 B) and contiguous
-      // in list order: the walks read them coalesced, without a list -> q gather
-      hqv[3 * nv] = c[0]; hqv[3 * nv + 1] = c[1]; hqv[3 * nv + 2] = c[2];
-      vl[nv++] = (int)j;
+  // two passes over fixed chunks (threads): classify + count, then fill the
+  // per-path point lists at the chunks' exclusive offsets (input order kept)
+  const int C = n >= (1 << 18) ? (int)host_threads() : 1;
+  const int64_t chunk = (n + C - 1) / std::max(C, 1);
+  std::vector<int64_t> cv((size_t)C + 1, 0), cb((size_t)C + 1, 0);
+  auto chunks = [&](auto body) {
+    if (C == 1) { body(0); return; }
+    std::vector<std::thread> th;
+    for (int i = 0; i < C; i++) th.emplace_back(body, i);
+    for (auto &x : th) x.join();
+  };
+  chunks([&](int ci) {
+    const int64_t j0 = ci * chunk, j1 = std::min<int64_t>(n, j0 + chunk);
+    int64_t a = 0, b = 0;
+    for (int64_t j = j0; j < j1; j++) {
+      const double *c = (const double *)(pc + (pv->first + j) * pv->stride);
+      hq[j] = Pt4{c[0], c[1], c[2], 0.0};
+      unsigned tag = tg ? *(const uint16_t *)(tg + (pv->first + j) * pv->tag_stride) : 0u;
+      int8_t kd;
+      if (tag >= PMX_TAG_NUL) kd = KIND_NUL;
+      else if (tag & PMX_TAG_REQ) kd = KIND_SKIP;
+      else if (tag & PMX_TAG_BDY) { kd = KIND_BDY; b++; }
+      else { kd = KIND_VOL; a++; }
+      hk[j] = kd;
     }
-    hk[j] = kd;
-  }
+    cv[(size_t)ci + 1] = a;
+    cb[(size_t)ci + 1] = b;
+  });
+  for (int i = 0; i < C; i++) { cv[(size_t)i + 1] += cv[(size_t)i]; cb[(size_t)i + 1] += cb[(size_t)i]; }
+  const int64_t nv = cv[(size_t)C], nb = cb[(size_t)C];
+  chunks([&](int ci) {
+    const int64_t j0 = ci * chunk, j1 = std::min<int64_t>(n, j0 + chunk);
+    int64_t a = cv[(size_t)ci], b = cb[(size_t)ci];
+    for (int64_t j = j0; j < j1; j++) {
+      if (hk[j] == KIND_BDY) bl[b++] = (int)j;
+      else if (hk[j] == KIND_VOL) {
+        // the volume points' coordinates once more, dense (24 B) and contiguous
+        // in list order: the walks read them coalesced, without a list -> q gather
+        hqv[3 * a] = hq[j].x; hqv[3 * a + 1] = hq[j].y; hqv[3 * a + 2] = hq[j].z;
+        vl[a++] = (int)j;
+      }
+    }
+  });
   ctx->nq = n;
   ctx->nq_vol = nv;
   ctx->nq_bdy = nb;
@@ -589,10 +645,12 @@ int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem, int *sta
       double *dst = new_sols[s].m;
       const int sz = ctx->sd.size[s], off = ctx->sd.off[s];
       if (!dst) continue;
-      for (int64_t i = 0; i < n; i++) {
-        if (!(wm[i] & (1u << s))) continue;
-        for (int j = 0; j < sz; j++) dst[i * sz + j] = h[(size_t)(i * S + off + j)];
-      }
+      par_for(0, n, [&](int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; i++) {
+          if (!(wm[i] & (1u << s))) continue;
+          for (int j = 0; j < sz; j++) dst[i * sz + j] = h[(size_t)(i * S + off + j)];
+        }
+      });
     }
   }
   if (elem) memcpy(elem, st + o_el, (size_t)n * sizeof(int));

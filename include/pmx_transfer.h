@@ -79,6 +79,11 @@ typedef struct {
 } pmx_locate_stats;
 
 /* ---- context ---------------------------------------------------------- */
+/* A context owns one stream's device buffers and a pinned host staging arena
+ * (hipHostMalloc, grown on demand, kept until pmx_destroy): about 64 B per
+ * background tet + (32 + 8*S) B per background vertex, or 65 B per new vertex,
+ * whichever upload is larger.  Host gathers/scatters use PMX_HOST_THREADS
+ * threads (default min(8, hardware threads)). */
 pmx_ctx    *pmx_create(int device);
 void        pmx_destroy(pmx_ctx *ctx);
 const char *pmx_last_error(pmx_ctx *ctx);

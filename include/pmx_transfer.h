@@ -60,11 +60,17 @@ typedef struct {
 } pmx_sol_view;
 
 /* New points to transfer onto: c[ip] at (const char*)c + ip*stride, ip=first..last;
- * tag as uint16_t at (const char*)tag + ip*tag_stride (MMG5_Point.tag). */
+ * tag as uint16_t at (const char*)tag + ip*tag_stride (MMG5_Point.tag).
+ * Optional new tets (tetra_v != NULL, entries 1..ne, stride in bytes, vertex
+ * indices in the same numbering as ip): only the points of valid tets
+ * (v[0] > 0) are located, as in the reference's vertex loop over the new tets
+ * (src/interpmesh_pmmg.c:535-541); the others are left untouched (a constant
+ * size metric is still written on every valid point).  NULL: every point. */
 typedef struct {
   int64_t         first, last;
   const double   *c;    int64_t stride;
   const uint16_t *tag;  int64_t tag_stride;
+  const int      *tetra_v;  int64_t tetra_stride;  int64_t ne;
 } pmx_points_view;
 
 /* Localisation statistics (reference PMMG_locateStats, src/locate_pmmg.h:45-50) */
@@ -74,16 +80,15 @@ typedef struct {
   int64_t nclosest;          /* not found -> closest element      */
   int64_t stepmin, stepmax;  /* walk steps                        */
   double  stepav;
-  int     tet_mode;          /* volume path ran tet-centric (no walk steps) */
-  double  tests_per_vertex;  /* tet-centric: containment tests per vertex   */
 } pmx_locate_stats;
 
 /* ---- context ---------------------------------------------------------- */
 /* A context owns one stream's device buffers and a pinned host staging arena
- * (hipHostMalloc, grown on demand, kept until pmx_destroy): about 64 B per
- * background tet + (32 + 8*S) B per background vertex, or 65 B per new vertex,
- * whichever upload is larger.  Host gathers/scatters use PMX_HOST_THREADS
- * threads (default min(8, hardware threads)). */
+ * (hipHostMalloc, grown on demand, kept until pmx_destroy): about 36 B per
+ * background tet + (24 + 8*S) B per background vertex, or 65 B per new vertex,
+ * whichever upload is larger.  Host gathers/scatters of 2^18 elements or more
+ * use PMX_HOST_THREADS threads (default min(8, hardware threads));
+ * PMX_HOST_THREADS_MIN overrides that threshold. */
 pmx_ctx    *pmx_create(int device);
 void        pmx_destroy(pmx_ctx *ctx);
 const char *pmx_last_error(pmx_ctx *ctx);
@@ -95,7 +100,9 @@ int         pmx_device_info(pmx_ctx *ctx, char *buf, int buflen);
 
 /* ---- background (old) group -------------------------------------------- */
 /* AoS -> SoA conversion on the host, then upload.  imet = index of the
- * metric in sols[] (or -1).  If adja is NULL it is rebuilt from tetra_v. */
+ * metric in sols[] (or -1).  If adja is NULL it is rebuilt from tetra_v.
+ * Every argument is checked before the context changes; on failure the
+ * context holds no background (pmx_run refuses until a good upload). */
 int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *old_mesh,
                           int nsol, const pmx_sol_view *old_sols, int imet);
 
@@ -110,11 +117,27 @@ typedef struct {
   double hsiz;                     /* >0: constant-size metric shortcut
                                       (src/interpmesh_pmmg.c:497-512)        */
   int    timing;                   /* record per-kernel HIP events           */
-  int    tune;                     /* kernel variant knobs (0 = defaults)    */
+  int    flags;                    /* PMX_RUN_* (0 = production defaults)    */
 } pmx_run_opts;
 
+/* pmx_run_opts.flags */
+#define PMX_RUN_REFERENCE_WALK   0x1  /* volume walk in the reference's order
+                                         (k_walk) instead of the slot walk    */
+#define PMX_RUN_NO_INLINE_TIES   0x2  /* every near-face point to the tie BFS */
+#define PMX_RUN_RECORD_STARTS    0x4  /* keep each volume walk's start tet    */
+#define PMX_RUN_SERIAL_SURFACE   0x8  /* surface path on the main stream      */
+#define PMX_RUN_FRESH_BACKGROUND 0x10 /* rebuild the background's derived data
+                                         (grid coordinates, tria normals) as
+                                         the first step after an upload does:
+                                         one ParMmg iteration per step        */
+#define PMX_RUN_DEBUG_BARRIER_TIMEOUT 0x100 /* test hook: the fallback's grid
+                                         barriers do not wait (the step must
+                                         then fail, never return silently)   */
+
 /* Locate every uploaded new point in the background group and interpolate all
- * background solutions onto it.  Results stay on the device. */
+ * background solutions onto it.  Results stay on the device.  Asynchronous:
+ * device-side failures (a fallback grid barrier that timed out) are reported
+ * by the next pmx_synchronize / pmx_download, which then return 0. */
 int pmx_run(pmx_ctx *ctx, const pmx_run_opts *opts);
 
 /* Copy results to the host.  new_sols[s].m receives size*(npts) doubles in
@@ -123,9 +146,8 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *opts);
 int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem,
                  int *status, int *steps);
 /* Per-point start element used by the device walk (debug/parity).  Volume
- * points' starts are recorded only by a pmx_run with tune bit 0x8000000
- * (PMX_TUNE_RECORD_STARTS); surface points' always. */
-#define PMX_TUNE_RECORD_STARTS 0x8000000
+ * points' starts are recorded only by a pmx_run with PMX_RUN_RECORD_STARTS;
+ * surface points' always. */
 int pmx_download_starts(pmx_ctx *ctx, int *start);
 /* Per-point reference-style extras for boundary points: edge/vertex (-1 unset). */
 int pmx_download_border(pmx_ctx *ctx, int *edge, int *vertex);

@@ -37,6 +37,7 @@ class PointsView(C.Structure):
         ("first", i64), ("last", i64),
         ("c", dptr), ("stride", i64),
         ("tag", u16ptr), ("tag_stride", i64),
+        ("tetra_v", iptr), ("tetra_stride", i64), ("ne", i64),
     ]
 
 
@@ -44,15 +45,23 @@ class LocateStats(C.Structure):
     _fields_ = [
         ("nvol", i64), ("nbdy", i64), ("nexhaust", i64), ("nclosest", i64),
         ("stepmin", i64), ("stepmax", i64), ("stepav", C.c_double),
-        ("tet_mode", C.c_int), ("tests_per_vertex", C.c_double),
     ]
 
 
 class RunOpts(C.Structure):
     _fields_ = [
         ("hint_stride", C.c_int), ("max_walk", C.c_int),
-        ("hsiz", C.c_double), ("timing", C.c_int), ("tune", C.c_int),
+        ("hsiz", C.c_double), ("timing", C.c_int), ("flags", C.c_int),
     ]
+
+
+# pmx_run_opts.flags (include/pmx_transfer.h)
+RUN_REFERENCE_WALK = 0x1
+RUN_NO_INLINE_TIES = 0x2
+RUN_RECORD_STARTS = 0x4
+RUN_SERIAL_SURFACE = 0x8
+RUN_FRESH_BACKGROUND = 0x10
+RUN_DEBUG_BARRIER_TIMEOUT = 0x100
 
 
 class Group(C.Structure):

@@ -25,7 +25,7 @@ TRANSFER_SO = os.path.join(PKG, "libpmx_transfer.so")
 MESHGEN_SO = os.path.join(PKG, "libpmx_meshgen.so")
 ORACLE_SO = os.path.join(ORACLE, "liboracle.so")
 
-HIP_SOURCES = ["pmx_capi.hip", "pmx_kernels.hip", "pmx_walk.hip", "pmx_tetloc.hip", "pmx_bdy.hip", "pmx_stats.hip",
+HIP_SOURCES = ["pmx_capi.hip", "pmx_kernels.hip", "pmx_walk.hip", "pmx_bdy.hip", "pmx_stats.hip",
                "pmx_groups.hip", "pmx_topo.hip"]
 HIPCC_FLAGS = [
     "-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-shared",

@@ -21,7 +21,7 @@
 __device__ __constant__ int NXT2d[6] = {1, 2, 0, 1, 2, 0};
 
 struct BdyArgs {
-  const Pt4 *pts;
+  const double *xyz;        // old vertices, 24 B
   const TriRec *tris;
   const Pt4 *trn;
   const int *ntoff, *ntlist;
@@ -175,7 +175,7 @@ __device__ __forceinline__ bool tria_eval_pre(const D3 P[3], D3 n, double area, 
 __device__ bool tria_eval(const BdyArgs &A, int g, int kn, D3 p, Bary &b) {
   const TriRec t = A.tris[g];
   const Pt4 nn = A.trn[kn];
-  const D3 P[3] = {ld3(A.pts, t.v[0]), ld3(A.pts, t.v[1]), ld3(A.pts, t.v[2])};
+  const D3 P[3] = {ld3(A.xyz, t.v[0]), ld3(A.xyz, t.v[1]), ld3(A.xyz, t.v[2])};
   return tria_eval_pre(P, D3{nn.x, nn.y, nn.z}, A.trn[g].w, p, b);
 }
 
@@ -200,7 +200,7 @@ __device__ __forceinline__ double centroid_dist_pre(const D3 P[3], D3 p) {
 }
 __device__ __forceinline__ double centroid_dist(const BdyArgs &A, int g, D3 p) {
   const TriRec t = A.tris[g];
-  const D3 P[3] = {ld3(A.pts, t.v[0]), ld3(A.pts, t.v[1]), ld3(A.pts, t.v[2])};
+  const D3 P[3] = {ld3(A.xyz, t.v[0]), ld3(A.xyz, t.v[1]), ld3(A.xyz, t.v[2])};
   return centroid_dist_pre(P, p);
 }
 
@@ -215,7 +215,7 @@ __device__ __forceinline__ bool in_tria(const BdyArgs &A, St &s, int g, int kn, 
   const TriRec t = A.tris[g];
   const Pt4 nn = A.trn[kn];
   const double area = A.trn[g].w;
-  const D3 P[3] = {ld3(A.pts, t.v[0]), ld3(A.pts, t.v[1]), ld3(A.pts, t.v[2])};
+  const D3 P[3] = {ld3(A.xyz, t.v[0]), ld3(A.xyz, t.v[1]), ld3(A.xyz, t.v[2])};
   const bool found = tria_eval_pre(P, D3{nn.x, nn.y, nn.z}, area, p, b);
   const double nrm = centroid_dist_pre(P, p);
   if (nrm < cdist) { cdist = nrm; ctria = kn; }
@@ -229,7 +229,7 @@ __device__ int in_wedge(const BdyArgs &A, St &s, int k, int l, D3 p, int base, B
   int i0 = NXT2d[l], i1 = NXT2d[l + 1];   // inxt2[l], iprv2[l]
   TriRec t = A.tris[k];
   int q0 = t.v[i0], q1 = t.v[i1];
-  D3 c0 = ld3(A.pts, q0), c1 = ld3(A.pts, q1);
+  D3 c0 = ld3(A.xyz, q0), c1 = ld3(A.xyz, q1);
   double pv[3] = {p.x - c0.x, p.y - c0.y, p.z - c0.z};
   double a[3] = {c1.x - c0.x, c1.y - c0.y, c1.z - c0.z};
   double n2 = 0.0, alpha = 0.0, dist = 0.0;
@@ -252,7 +252,7 @@ __device__ int in_wedge(const BdyArgs &A, St &s, int k, int l, D3 p, int base, B
 template <class St>
 __device__ bool in_cone(const BdyArgs &A, St &s, int k, int iloc, D3 p, int base) {
   int ip = A.tris[k].v[iloc];
-  D3 c0 = ld3(A.pts, ip);
+  D3 c0 = ld3(A.xyz, ip);
   set_flag(s, ip, base);
   double pv[3] = {p.x - c0.x, p.y - c0.y, p.z - c0.z};
   double dist = 0.0;
@@ -266,7 +266,7 @@ __device__ bool in_cone(const BdyArgs &A, St &s, int k, int iloc, D3 p, int base
       if (jp == ip) continue;
       if (get_flag(s, A, jp) == ip) continue;
       set_flag(s, jp, ip);
-      D3 cj = ld3(A.pts, jp);
+      D3 cj = ld3(A.xyz, jp);
       double a[3] = {cj.x - c0.x, cj.y - c0.y, cj.z - c0.z};
       if (dist > A.hausd) return false;
       double alpha = 0.0;
@@ -550,7 +550,7 @@ __global__ __launch_bounds__(256) void k_exh_bdy(BdyArgs A) {
           double bd = 0.0;
           int it = 0;
           for (int l = 0; l < 3; l++) {
-            D3 c = ld3(A.pts, t.v[l]);
+            D3 c = ld3(A.xyz, t.v[l]);
             double d = norm3(p.x - c.x, p.y - c.y, p.z - c.z);
             if (l == 0 || d < bd) { bd = d; it = l; }
           }
@@ -565,68 +565,25 @@ __global__ __launch_bounds__(256) void k_exh_bdy(BdyArgs A) {
 
 // tria hint grid: cell -> largest tria index whose centroid falls in it
 // (deterministic: the surface semantics depend on the start triangle)
-__device__ __forceinline__ void tria_hint_one(const TriRec *tris, const Pt4 *pts, int64_t k, int *grid,
+__device__ __forceinline__ void tria_hint_one(const TriRec *tris, const double *xyz, int64_t k, int *grid,
                                               const GridDesc &g) {
   TriRec t = tris[k];
   if (t.v[0] <= 0) return;
-  D3 a = ld3(pts, t.v[0]), b = ld3(pts, t.v[1]), c = ld3(pts, t.v[2]);
+  D3 a = ld3(xyz, t.v[0]), b = ld3(xyz, t.v[1]), c = ld3(xyz, t.v[2]);
   D3 m{(a.x + b.x + c.x) / 3.0, (a.y + b.y + c.y) / 3.0, (a.z + b.z + c.z) / 3.0};
   int cx = (int)fmin(fmax((m.x - g.lo[0]) * g.inv[0], 0.0), (double)(g.dim[0] - 1));
   int cy = (int)fmin(fmax((m.y - g.lo[1]) * g.inv[1], 0.0), (double)(g.dim[1] - 1));
   int cz = (int)fmin(fmax((m.z - g.lo[2]) * g.inv[2], 0.0), (double)(g.dim[2] - 1));
   atomicMax(&grid[(int64_t)cx + (int64_t)g.dim[0] * ((int64_t)cy + (int64_t)g.dim[1] * cz)], (int)k);
 }
-__device__ void tria_hint_part(const TriRec *tris, const Pt4 *pts, int64_t nt, int *grid,
-                               const GridDesc &g, int64_t b, int64_t nb) {
-  for (int64_t k = 1 + b * blockDim.x + threadIdx.x; k <= nt; k += nb * blockDim.x)
-    tria_hint_one(tris, pts, k, grid, g);
-}
-// the volume hint build (fixed-point centroids) and the tria hint build of
-// the surface path in ONE launch: blocks [0, nbt) sample tets, the rest walk
-// the boundary trias.  The latency-bound tria part then runs inside the
-// bandwidth-bound tet part instead of at the head of the surface path while
-// the volume walk saturates the memory system.
-__global__ __launch_bounds__(256) void k_hint_build_fused(const int4 *__restrict__ src, int64_t ne,
-                                                          int stride, int *__restrict__ grid, GridDesc g,
-                                                          const unsigned long long *__restrict__ xyzq,
-                                                          int64_t nbt, const TriRec *tris,
-                                                          const Pt4 *pts, int64_t nt, int *tgrid,
-                                                          GridDesc tg) {
-  if ((int64_t)blockIdx.x >= nbt) {
-    tria_hint_part(tris, pts, nt, tgrid, tg, blockIdx.x - nbt, gridDim.x - nbt);
-    return;
-  }
-  const int64_t n = (ne + stride - 1) / stride;
-  const int64_t t = xcd_remap(blockIdx.x, nbt) * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  const int4 v = src[t];
-  if (v.x <= 0) return;
-  const unsigned long long a = xyzq[v.x], b = xyzq[v.y], c = xyzq[v.z], d = xyzq[v.w];
-  const unsigned long long M = (1ull << 21) - 1;
-  int cq[3];
-#pragma unroll
-  for (int ax = 0; ax < 3; ax++) {
-    const int sh = 21 * ax;
-    const unsigned s4 = (unsigned)((a >> sh) & M) + (unsigned)((b >> sh) & M) +
-                        (unsigned)((c >> sh) & M) + (unsigned)((d >> sh) & M);
-    cq[ax] = min((int)(s4 >> (HINT_QF + 2)), g.dim[ax] - 1);
-  }
-  grid[(int64_t)cq[0] + (int64_t)g.dim[0] * ((int64_t)cq[1] + (int64_t)g.dim[1] * cq[2])] =
-      (int)(1 + t * stride);
-}
-void launch_hint_build_fused(const int4 *packed, int64_t ne, int stride, int *grid, GridDesc g,
-                             const unsigned long long *xyzq, const TriRec *tris, const Pt4 *pts,
-                             int64_t nt, int *tgrid, GridDesc tg, hipStream_t s) {
-  const int64_t n = (ne + stride - 1) / stride;
-  const int64_t nbt = std::max<int64_t>((n + 255) / 256, 1);
-  const int64_t nbr = std::min<int64_t>(std::max<int64_t>((nt + 255) / 256, 1), 4096);
-  hipLaunchKernelGGL(k_hint_build_fused, dim3((unsigned)(nbt + nbr)), dim3(256), 0, s, packed, ne,
-                     stride, grid, g, xyzq, nbt, tris, pts, nt, tgrid, tg);
-}
 
-__global__ __launch_bounds__(256) void k_tria_hint_build(const TriRec *tris, const Pt4 *pts,
+// tria hint grid: cell -> largest tria index whose centroid falls in it
+// (deterministic: the surface semantics depend on the start triangle)
+__global__ __launch_bounds__(256) void k_tria_hint_build(const TriRec *tris, const double *xyz,
                                                          int64_t nt, int *grid, GridDesc g) {
-  tria_hint_part(tris, pts, nt, grid, g, blockIdx.x, gridDim.x);
+  for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= nt;
+       k += (int64_t)gridDim.x * blockDim.x)
+    tria_hint_one(tris, xyz, k, grid, g);
 }
 
 __device__ int tria_hint(const BdyArgs &A, D3 p) {
@@ -648,27 +605,6 @@ __device__ int tria_hint(const BdyArgs &A, D3 p) {
           if (kk) return kk;
         }
   return 1;
-}
-
-// PMMG_precompute_triaNormals (src/locate_pmmg.c:68-90): unit normal + |n|
-__global__ __launch_bounds__(256) void k_tria_normals(const TriRec *tris, const Pt4 *pts,
-                                                      int64_t nt, Pt4 *trn) {
-  for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= nt;
-       k += (int64_t)gridDim.x * blockDim.x) {
-    TriRec t = tris[k];
-    if (t.v[0] <= 0) { trn[k] = Pt4{0, 0, 0, 0}; continue; }
-    D3 n = nonunit_normal(ld3(pts, t.v[0]), ld3(pts, t.v[1]), ld3(pts, t.v[2]));
-    double q = sqrt(n.x * n.x + n.y * n.y + n.z * n.z);
-    double dd = 1.0 / q;
-    trn[k] = Pt4{n.x * dd, n.y * dd, n.z * dd, q};
-  }
-}
-
-void launch_tria_normals(const TriRec *tris, const Pt4 *pts, int64_t nt, Pt4 *trn, hipStream_t s) {
-  int64_t nb = (nt + 255) / 256;
-  if (nb > 4096) nb = 4096;
-  if (nb < 1) nb = 1;
-  hipLaunchKernelGGL(k_tria_normals, dim3((unsigned)nb), dim3(256), 0, s, tris, pts, nt, trn);
 }
 
 // surface walks are short (1.5 steps on C2): 8 private slots, the rare longer
@@ -706,7 +642,7 @@ bool pmx_ctx::size_tria_grid() {
   return true;
 }
 
-bool pmx_ctx::launch_bdy(const VolArgs &a, const pmx_run_opts &o, hipStream_t s) {
+bool pmx_ctx::launch_bdy(const VolArgs &a, hipStream_t s) {
   if (nt < 1) { err = "surface points present but the background has no boundary trias"; return false; }
   // tria hint grid: a coarser grid over the same bbox (about 2 trias / cell
   // in each direction of the surface)
@@ -725,18 +661,19 @@ bool pmx_ctx::launch_bdy(const VolArgs &a, const pmx_run_opts &o, hipStream_t s)
   // tria hint grid: sized and allocated with the background
   // (pmx_ctx::size_tria_grid), zeroed by the step's prologue kernel
   const GridDesc tg = tgd;
-  if (!tria_hint_fused) {   // else zeroed + built on the main stream (k_hint_build_fused)
-    if (hipMemsetAsync(d_tgrid, 0, sizeof(int) * (size_t)tcells, s) != hipSuccess) {
-      err = "tria hint grid memset";
-      return false;
-    }
+  // zeroed and built at the head of the surface path (off the main stream)
+  if (hipMemsetAsync(d_tgrid, 0, sizeof(int) * (size_t)tcells, s) != hipSuccess) {
+    err = "tria hint grid memset";
+    return false;
+  }
+  {
     int64_t nb = (nt + 255) / 256;
     if (nb > 4096) nb = 4096;
     hipLaunchKernelGGL(k_tria_hint_build, dim3((unsigned)std::max<int64_t>(nb, 1)), dim3(256), 0, s,
-                       d_tris.p, d_pts.p, nt, d_tgrid, tg);
+                       d_tris.p, d_xyz.p, nt, d_tgrid, tg);
   }
   BdyArgs B{};
-  B.pts = d_pts.p; B.tris = d_tris.p; B.trn = d_trn.p; B.ntoff = d_ntoff.p; B.ntlist = d_ntlist.p;
+  B.xyz = d_xyz.p; B.tris = d_tris.p; B.trn = d_trn.p; B.ntoff = d_ntoff.p; B.ntlist = d_ntlist.p;
   B.sol = d_sol.p; B.sd = a.sd; B.q = d_q.p; B.kind = d_kind.p; B.nq = nq; B.nt = nt;
   B.hausd = hausd; B.grid = d_tgrid; B.g = tg;
   B.out = d_out.p; B.wmask = d_wmask.p; B.elem = d_elem.p; B.status = d_status.p;
@@ -748,6 +685,5 @@ bool pmx_ctx::launch_bdy(const VolArgs &a, const pmx_run_opts &o, hipStream_t s)
   hipLaunchKernelGGL(k_locate_bdy<BDY_CAP>, dim3((unsigned)nb), dim3(256), 0, s, B);
   hipLaunchKernelGGL(k_locate_bdy_ovf, dim3(OVF_THREADS / 64), dim3(64), 0, s, B, d_ows.p, OVF_CAP);
   hipLaunchKernelGGL(k_exh_bdy, dim3(256), dim3(256), 0, s, B);
-  (void)o;
   return hipGetLastError() == hipSuccess;
 }

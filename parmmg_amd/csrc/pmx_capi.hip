@@ -17,11 +17,9 @@
 #include "pmx_kernels.h"
 #include "pmx_internal.h"
 
-// hint grid from every 4th tet: 1/4 of the atomics and of the tet bytes of a
-// full build, at ~0.5 extra walk step (r01 measurements)
-#define PMX_DEFAULT_HINT_STRIDE 4
-#define PMX_DEFAULT_VOL_OCC 1
-#define PMX_EV_PER_RUN 7
+// events per recorded step: 0 start, 7 derived data built, 1 hint built,
+// 2 volume walk done, 3/5 surface path start/end (side stream), 6 joined, 4 end
+#define PMX_EV_PER_RUN 8
 
 static bool ok(pmx_ctx *c, hipError_t e, const char *what) {
   if (e == hipSuccess) return true;
@@ -30,20 +28,12 @@ static bool ok(pmx_ctx *c, hipError_t e, const char *what) {
 }
 #define CK(x) do { if (!ok(ctx, (x), #x)) return 0; } while (0)
 
-template <class T>
-static bool dgrow(pmx_ctx *ctx, DevBuf<T> &b, size_t n) {
-  if (n <= b.cap && b.p) return true;
-  if (b.p) hipFree(b.p);
-  b.p = nullptr;
-  b.cap = 0;
-  size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
-  if (!ok(ctx, hipMalloc((void **)&b.p, bytes), "hipMalloc")) return false;
-  b.cap = n;
-  return true;
+template <class T> static bool dgrow(pmx_ctx *ctx, DevBuf<T> &b, size_t n) {
+  return pmx_dgrow(ctx, b, n);
 }
 // pinned staging of at least `bytes`, 25 % slack so that a slowly growing
 // ParMmg group does not re-pin every iteration
-static char *hstage(pmx_ctx *ctx, size_t bytes) {
+char *pmx_hstage(pmx_ctx *ctx, size_t bytes) {
   if (bytes <= ctx->h_stage_cap && ctx->h_stage) return (char *)ctx->h_stage;
   if (ctx->h_stage) hipHostFree(ctx->h_stage);
   ctx->h_stage = nullptr;
@@ -53,10 +43,12 @@ static char *hstage(pmx_ctx *ctx, size_t bytes) {
   ctx->h_stage_cap = cap;
   return (char *)ctx->h_stage;
 }
+static char *hstage(pmx_ctx *ctx, size_t bytes) { return pmx_hstage(ctx, bytes); }
 static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 // host gathers/scatters of large AoS arrays split over a few threads
-// (PMX_HOST_THREADS, default min(8, hardware threads)); small ranges stay serial
+// (PMX_HOST_THREADS, default min(8, hardware threads)); ranges below
+// PMX_HOST_THREADS_MIN elements (default 2^18) stay serial
 static unsigned host_threads() {
   static const unsigned T = [] {
     const char *e = getenv("PMX_HOST_THREADS");
@@ -66,23 +58,50 @@ static unsigned host_threads() {
   }();
   return T;
 }
-template <class F> static void par_for(int64_t lo, int64_t hi, F f) {
-  const unsigned T = host_threads();
+static int64_t host_threads_min() {
+  static const int64_t M = [] {
+    const char *e = getenv("PMX_HOST_THREADS_MIN");
+    return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)(1 << 18);
+  }();
+  return M;
+}
+// f(chunk, lo, hi) over C contiguous chunks of [lo, hi); returns C
+template <class F> static int par_chunks(int64_t lo, int64_t hi, F f) {
   const int64_t n = hi - lo;
-  if (T <= 1 || n < (1 << 18)) { f(lo, hi); return; }
+  const int C = (host_threads() <= 1 || n < host_threads_min()) ? 1 : (int)host_threads();
+  if (C == 1) { f(0, lo, hi); return 1; }
   std::vector<std::thread> th;
-  const int64_t chunk = (n + T - 1) / T;
-  for (unsigned i = 0; i < T; i++) {
+  const int64_t chunk = (n + C - 1) / C;
+  for (int i = 0; i < C; i++) {
     const int64_t a = lo + (int64_t)i * chunk, b = std::min(hi, a + chunk);
-    if (a < b) th.emplace_back(f, a, b);
+    th.emplace_back(f, i, a, std::max(a, b));
   }
   for (auto &x : th) x.join();
+  return C;
+}
+template <class F> static void par_for(int64_t lo, int64_t hi, F f) {
+  par_chunks(lo, hi, [&](int, int64_t a, int64_t b) { if (a < b) f(a, b); });
 }
 
 template <class T> static void dfree(DevBuf<T> &b) {
   if (b.p) hipFree(b.p);
   b.p = nullptr;
   b.cap = 0;
+}
+
+bool pmx_ctx::check_device_errors() {
+  if (!ran || !d_counts.p) return true;
+  unsigned e = 0;
+  if (hipMemcpy(&e, d_counts.p + PMX_CNT_ERR, sizeof e, hipMemcpyDeviceToHost) != hipSuccess) {
+    err = "reading the step's device error word failed";
+    return false;
+  }
+  if (e & PMX_DERR_BARRIER) {
+    err = "k_fallback: a grid barrier timed out (workgroups not co-resident); the step's "
+          "results are invalid";
+    return false;
+  }
+  return true;
 }
 
 extern "C" {
@@ -100,12 +119,17 @@ pmx_ctx *pmx_create(int device) {
     return nullptr;
   }
   ctx->stream = ctx->own;
-  int prio_lo = 0, prio_hi = 0;
-  if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
-  if (hipStreamCreateWithPriority(&ctx->side_lo, hipStreamNonBlocking, prio_lo) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess ||
+  if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess) {
+    pmx_destroy(ctx);
+    return nullptr;
+  }
+  // the fallback's grid barrier needs every workgroup resident at once: size
+  // its grid from the occupancy query, leaving room for a second context's
+  // fallback on the same GPU (ParMmg groups of one rank, C4: 2 per GPU)
+  ctx->fallback_blocks = fallback_coresident_blocks(device, 2);
+  if (ctx->fallback_blocks < 1) {
     pmx_destroy(ctx);
     return nullptr;
   }
@@ -116,14 +140,12 @@ void pmx_destroy(pmx_ctx *ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
+  if (ctx->side) hipStreamSynchronize(ctx->side);
   ctx->free_all();
   for (auto &e : ctx->events) hipEventDestroy(e);
-  if (ctx->side) hipStreamSynchronize(ctx->side);
-  if (ctx->side_lo) hipStreamSynchronize(ctx->side_lo);
   if (ctx->ev_fork) hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) hipEventDestroy(ctx->ev_join);
   if (ctx->side) hipStreamDestroy(ctx->side);
-  if (ctx->side_lo) hipStreamDestroy(ctx->side_lo);
   if (ctx->own) hipStreamDestroy(ctx->own);
   delete ctx;
 }
@@ -138,8 +160,9 @@ int pmx_set_stream(pmx_ctx *ctx, void *s) {
 
 int pmx_synchronize(pmx_ctx *ctx) {
   if (!ctx) return 0;
+  hipSetDevice(ctx->device);
   CK(hipStreamSynchronize(ctx->stream));
-  return 1;
+  return ctx->check_device_errors() ? 1 : 0;
 }
 
 int pmx_device_info(pmx_ctx *ctx, char *buf, int buflen) {
@@ -153,18 +176,47 @@ int pmx_device_info(pmx_ctx *ctx, char *buf, int buflen) {
 
 // ---- background upload ------------------------------------------------------
 
+static bool check_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const pmx_sol_view *sols,
+                             int imet) {
+  if (m->np < 1 || m->ne < 1 || m->nt < 0 || m->np >= (1LL << 31) - 1 || 4 * m->ne >= (1LL << 31)) {
+    ctx->err = "pmx_upload_background: mesh sizes out of range";
+    return false;
+  }
+  if (!m->point_c || !m->tetra_v || m->point_stride < 24 || m->tetra_stride < 16) {
+    ctx->err = "pmx_upload_background: point_c / tetra_v missing or strides too small";
+    return false;
+  }
+  if (nsol < 0 || nsol > PMX_MAX_SOLS || imet < -1 || imet >= nsol || (nsol > 0 && !sols)) {
+    ctx->err = "pmx_upload_background: bad solution list";
+    return false;
+  }
+  for (int s = 0; s < nsol; s++) {
+    if (sols[s].size != 1 && sols[s].size != 3 && sols[s].size != 6) {
+      ctx->err = "pmx_upload_background: solution size must be 1, 3 or 6";
+      return false;
+    }
+    if (!sols[s].m) {
+      ctx->err = "pmx_upload_background: null solution";
+      return false;
+    }
+  }
+  if (m->nt > 0 && (!m->tria_v || !m->adjt || m->tria_stride < 12)) {
+    ctx->err = "pmx_upload_background: nt > 0 requires tria_v and adjt";
+    return false;
+  }
+  return true;
+}
+
 int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
                           const pmx_sol_view *sols, int imet) {
-  if (!ctx || !m) return 0;
+  if (!ctx) return 0;
+  // whatever happens below, the context holds no usable background until the
+  // upload has completed (a failed call must not leave sizes that disagree
+  // with the device buffers)
+  ctx->have_bg = ctx->ran = ctx->have_derived = ctx->have_tetv = ctx->have_qual = false;
+  if (!m) { ctx->err = "pmx_upload_background: null mesh"; return 0; }
   hipSetDevice(ctx->device);
-  if (m->np < 1 || m->ne < 1 || m->np >= (1LL << 31) || 4 * m->ne >= (1LL << 31)) {
-    ctx->err = "pmx_upload_background: mesh sizes out of range";
-    return 0;
-  }
-  if (!m->point_c || !m->tetra_v) {
-    ctx->err = "pmx_upload_background: point_c and tetra_v are required";
-    return 0;
-  }
+  if (!check_background(ctx, m, nsol, sols, imet)) return 0;
   // no adjacency given (MMG3D_hashTetra not run on the host): face matching on
   // the device (pmx_topo.hip)
   std::vector<int> built_adja;
@@ -173,81 +225,85 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     if (!pmx_ctx_build_adja_host(ctx, m, built_adja)) return 0;
     adja_in = built_adja.data();
   }
-  if (nsol < 0 || nsol > PMX_MAX_SOLS || imet >= nsol) {
-    ctx->err = "pmx_upload_background: bad solution list";
-    return 0;
-  }
   const int64_t np = m->np, ne = m->ne, nt = m->nt;
-  int S0 = 0;
-  for (int s = 0; s < nsol; s++) S0 += sols[s].size;
-  S0 += (S0 >= 3 && (S0 & 1)) ? 1 : 0;   // room for PMX_SOL_PAD
-  // pinned staging: points | tets | solutions (async DMA, one sync at the end)
-  const size_t o_p = 0, o_t = o_p + al256((size_t)(np + 1) * sizeof(Pt4)),
-               o_s = o_t + al256((size_t)(ne + 1) * sizeof(TetRec)),
-               total = o_s + al256((size_t)(np + 1) * std::max(S0, 1) * sizeof(double));
-  CK(hipStreamSynchronize(ctx->stream));   // the arena may still feed an earlier copy
-  char *stg = hstage(ctx, total);
-  if (!stg) return 0;
-  ctx->np = np; ctx->ne = ne; ctx->nt = nt; ctx->hausd = m->hausd;
-
-  // points -> Pt4, bbox
-  Pt4 *hp = (Pt4 *)(stg + o_p);
-  double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
-  hp[0] = Pt4{0, 0, 0, 0};
-  const char *pc = (const char *)m->point_c;
-  for (int64_t i = 1; i <= np; i++) {
-    const double *c = (const double *)(pc + i * m->point_stride);
-    hp[i] = Pt4{c[0], c[1], c[2], 0.0};
-    for (int a = 0; a < 3; a++) {
-      lo[a] = std::min(lo[a], c[a]);
-      hi[a] = std::max(hi[a], c[a]);
-    }
-  }
-  // tets -> TetRec with neighbour tet index
-  TetRec *ht = (TetRec *)(stg + o_t);
-  memset(&ht[0], 0, sizeof(TetRec));
-  const char *tc = (const char *)m->tetra_v;
-  par_for(1, ne + 1, [&](int64_t k0, int64_t k1) {
-    for (int64_t k = k0; k < k1; k++) {
-      const int *v = (const int *)(tc + k * m->tetra_stride);
-      TetRec &r = ht[(size_t)k];
-      for (int l = 0; l < 4; l++) {
-        r.v[l] = v[l];
-        r.nb[l] = adja_in[4 * (k - 1) + 1 + l] / 4;
-      }
-    }
-  });
-  // solutions -> interleaved [np+1][S]
   SolDesc sd{};
   sd.nsol = nsol;
   sd.imet = imet;
   int S = 0;
   for (int s = 0; s < nsol; s++) {
-    if (sols[s].size != 1 && sols[s].size != 3 && sols[s].size != 6) {
-      ctx->err = "pmx_upload_background: solution size must be 1, 3 or 6";
-      return 0;
-    }
     sd.size[s] = sols[s].size;
     sd.off[s] = S;
     S += sols[s].size;
   }
-  // PMX_SOL_PAD=1: odd S >= 3 padded to even so that every row is 16-B
-  // aligned and gathered with 16-B loads (C3, S = 5: 3 instead of 5 loads per
-  // vertex).  Off by default: on C3 the 20 % more row bytes cost more than the
-  // saved loads (k_walk 1.84 vs 1.78 ms, r01).
-  const char *pad_env = getenv("PMX_SOL_PAD");
-  const bool pad = pad_env && pad_env[0] == '1';
-  const int S_sum = S;
-  S = (pad && S >= 3 && (S & 1)) ? S + 1 : S;
   sd.S = S;
-  ctx->sd = sd;
+  const int64_t ns = (ne + PMX_HINT_STRIDE - 1) / PMX_HINT_STRIDE;
   const size_t hs_n = (size_t)(np + 1) * std::max(S, 1);
+  // pinned staging: xyz | tets | packed hint sample | solutions (async DMA,
+  // one sync at the end)
+  const size_t o_p = 0, o_t = o_p + al256((size_t)(np + 1) * 24),
+               o_h = o_t + al256((size_t)(ne + 1) * sizeof(TetRec)),
+               o_s = o_h + al256((size_t)ns * sizeof(int4)),
+               total = o_s + al256(hs_n * sizeof(double));
+  CK(hipStreamSynchronize(ctx->stream));   // the arena may still feed an earlier copy
+  char *stg = hstage(ctx, total);
+  if (!stg) return 0;
+
+  // points -> dense xyz (24 B), bounding box per chunk
+  double *hp = (double *)(stg + o_p);
+  hp[0] = hp[1] = hp[2] = 0.0;
+  const char *pc = (const char *)m->point_c;
+  double blo[64][3], bhi[64][3];
+  const int nch = par_chunks(1, np + 1, [&](int c, int64_t i0, int64_t i1) {
+    double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+    for (int64_t i = i0; i < i1; i++) {
+      const double *cc = (const double *)(pc + i * m->point_stride);
+      for (int a = 0; a < 3; a++) {
+        hp[3 * i + a] = cc[a];
+        lo[a] = std::min(lo[a], cc[a]);
+        hi[a] = std::max(hi[a], cc[a]);
+      }
+    }
+    for (int a = 0; a < 3; a++) { blo[c][a] = lo[a]; bhi[c][a] = hi[a]; }
+  });
+  double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+  for (int c = 0; c < nch; c++)
+    for (int a = 0; a < 3; a++) { lo[a] = std::min(lo[a], blo[c][a]); hi[a] = std::max(hi[a], bhi[c][a]); }
+  // tets -> TetRec with neighbour tet index, + the packed hint sample (the
+  // connectivity of every PMX_HINT_STRIDE-th tet, contiguous: the hint build
+  // streams ne/4 * 16 B instead of touching every line of the tet records)
+  TetRec *ht = (TetRec *)(stg + o_t);
+  int4 *hh = (int4 *)(stg + o_h);
+  memset(&ht[0], 0, sizeof(TetRec));
+  const char *tc = (const char *)m->tetra_v;
+  bool bad = false;
+  par_for(1, ne + 1, [&](int64_t k0, int64_t k1) {
+    bool b = false;
+    for (int64_t k = k0; k < k1; k++) {
+      const int *v = (const int *)(tc + k * m->tetra_stride);
+      TetRec &r = ht[(size_t)k];
+      // indices the kernels will gather through: a valid tet (v[0] > 0,
+      // MG_EOK) must name vertices 1..np and neighbours 0..ne
+      const bool valid = v[0] > 0;
+      for (int l = 0; l < 4; l++) {
+        r.v[l] = v[l];
+        const int a = adja_in[4 * (k - 1) + 1 + l];
+        r.nb[l] = a / 4;
+        if (valid && (v[l] < 1 || v[l] > np || a < 0 || a / 4 > ne)) b = true;
+      }
+      if ((k - 1) % PMX_HINT_STRIDE == 0) hh[(k - 1) / PMX_HINT_STRIDE] = make_int4(v[0], v[1], v[2], v[3]);
+    }
+    if (b) __atomic_store_n(&bad, true, __ATOMIC_RELAXED);
+  });
+  if (bad) {
+    ctx->err = "pmx_upload_background: tet vertex or adjacency index out of range";
+    return 0;
+  }
+  // solutions -> interleaved [np+1][S]
   double *hs = (double *)(stg + o_s);
-  if (S != S_sum) memset(hs, 0, hs_n * sizeof(double));      // pad column (or no solution)
-  else memset(hs, 0, (size_t)std::max(S, 1) * sizeof(double));   // row 0 (unused slot)
+  memset(hs, 0, (size_t)std::max(S, 1) * sizeof(double));   // row 0 (unused slot)
+  if (S == 0) memset(hs, 0, hs_n * sizeof(double));
   for (int s = 0; s < nsol; s++) {
     const int sz = sols[s].size;
-    if (!sols[s].m) { ctx->err = "pmx_upload_background: null solution"; return 0; }
     const double *src = sols[s].m;
     const int off = sd.off[s];
     par_for(1, np + 1, [&](int64_t i0, int64_t i1) {
@@ -259,20 +315,23 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   std::vector<TriRec> htr((size_t)(nt + 1));
   memset(&htr[0], 0, sizeof(TriRec));
   if (nt > 0) {
-    if (!m->tria_v || !m->adjt) {
-      ctx->err = "pmx_upload_background: nt > 0 requires tria_v and adjt";
-      return 0;
-    }
     const char *rc = (const char *)m->tria_v;
     for (int64_t k = 1; k <= nt; k++) {
       const int *v = (const int *)(rc + k * m->tria_stride);
       TriRec &r = htr[(size_t)k];
       for (int l = 0; l < 3; l++) {
         r.v[l] = v[l];
-        r.nb[l] = m->adjt[3 * (k - 1) + 1 + l] / 3;
+        const int a = m->adjt[3 * (k - 1) + 1 + l];
+        r.nb[l] = a / 3;
+        if (v[l] < 1 || v[l] > np || a < 0 || a / 3 > nt) {
+          ctx->err = "pmx_upload_background: tria vertex or adjacency index out of range";
+          return 0;
+        }
       }
     }
   }
+  ctx->np = np; ctx->ne = ne; ctx->nt = nt; ctx->hausd = m->hausd;
+  ctx->sd = sd;
   ctx->host_build_node_trias(htr);
 
   // hint grid over the background bbox: about one cell per 6 tets
@@ -301,51 +360,43 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   for (int a = 0; a < 3; a++) { ctx->bblo[a] = lo[a]; ctx->bbhi[a] = hi[a]; }
   if (!ctx->size_tria_grid()) return 0;
 
-  if (!dgrow(ctx, ctx->d_pts, (size_t)(np + 1))) return 0;
+  if (!dgrow(ctx, ctx->d_xyz, (size_t)(np + 1) * 3)) return 0;
   if (!dgrow(ctx, ctx->d_tets, (size_t)(ne + 1))) return 0;
+  if (!dgrow(ctx, ctx->d_tets_s, (size_t)std::max<int64_t>(ns, 1))) return 0;
   if (!dgrow(ctx, ctx->d_sol, hs_n)) return 0;
   if (!dgrow(ctx, ctx->d_tris, (size_t)(nt + 1))) return 0;
+  if (!dgrow(ctx, ctx->d_trn, (size_t)(nt + 1))) return 0;
   if (!dgrow(ctx, ctx->d_grid, (size_t)cells)) return 0;
-  if (!dgrow(ctx, ctx->d_grid64, (size_t)cells)) return 0;
+  if (!dgrow(ctx, ctx->d_xyzq, (size_t)(np + 1))) return 0;
   if (!dgrow(ctx, ctx->d_ntoff, ctx->h_ntoff.size())) return 0;
   if (!dgrow(ctx, ctx->d_ntlist, std::max<size_t>(ctx->h_ntlist.size(), 1))) return 0;
-  if (!dgrow(ctx, ctx->d_trn, (size_t)(nt + 1))) return 0;
-  CK(hipMemcpyAsync(ctx->d_pts.p, hp, (size_t)(np + 1) * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemcpyAsync(ctx->d_xyz.p, hp, (size_t)(np + 1) * 24, hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_tets.p, ht, (size_t)(ne + 1) * sizeof(TetRec), hipMemcpyHostToDevice, ctx->stream));
-  // connectivity-only stream for the tet-centric pass (16 of the 32 B)
-  if (!dgrow(ctx, ctx->d_tetv, (size_t)(ne + 1))) return 0;
-  launch_tet_conn(ctx->d_tets.p, 1, ne + 1, ctx->d_tetv.p, ctx->stream);
-  // packed hint sample (the connectivity of every PMX_DEFAULT_HINT_STRIDE-th
-  // tet, contiguous): the per-step hint build streams ne/4 * 16 B instead of
-  // touching every line of the connectivity stream
-  {
-    const int64_t ns = (ne + PMX_DEFAULT_HINT_STRIDE - 1) / PMX_DEFAULT_HINT_STRIDE;
-    if (!dgrow(ctx, ctx->d_tets_s, (size_t)std::max<int64_t>(ns, 1))) return 0;
-    launch_tet_conn(ctx->d_tets.p + 1, PMX_DEFAULT_HINT_STRIDE, ns, ctx->d_tets_s.p, ctx->stream);
-  }
+  CK(hipMemcpyAsync(ctx->d_tets_s.p, hh, (size_t)ns * sizeof(int4), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_sol.p, hs, hs_n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_tris.p, htr.data(), htr.size() * sizeof(TriRec), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_ntoff.p, ctx->h_ntoff.data(), ctx->h_ntoff.size() * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
   if (!ctx->h_ntlist.empty())
     CK(hipMemcpyAsync(ctx->d_ntlist.p, ctx->h_ntlist.data(), ctx->h_ntlist.size() * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
-  if (nt > 0) launch_tria_normals(ctx->d_tris.p, ctx->d_pts.p, nt, ctx->d_trn.p, ctx->stream);
-  // dense coordinates for the walk: the uploaded vertices in a second layout
-  if (!dgrow(ctx, ctx->d_xyz, (size_t)(np + 1) * 3)) return 0;
-  if (!dgrow(ctx, ctx->d_xyzf, (size_t)(np + 1) * 3)) return 0;
-  launch_build_xyz(ctx->d_pts.p, np + 1, ctx->d_xyz.p, ctx->d_xyzf.p, ctx->stream);
-  if (!dgrow(ctx, ctx->d_xyzq, (size_t)(np + 1))) return 0;
-  launch_quant_xyz(ctx->d_pts.p, np + 1, ctx->grid, ctx->d_xyzq.p, ctx->stream);
-  CK(hipGetLastError());
   CK(hipStreamSynchronize(ctx->stream));   // host staging vectors die here
   ctx->have_bg = true;
   return 1;
 }
 
 int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
-  if (!ctx || !pv) return 0;
+  if (!ctx) return 0;
+  ctx->have_pts = ctx->ran = false;
+  if (!pv) { ctx->err = "pmx_upload_points: null view"; return 0; }
   hipSetDevice(ctx->device);
   const int64_t n = pv->last - pv->first + 1;
-  if (n < 0 || n >= (1LL << 31)) { ctx->err = "pmx_upload_points: bad range"; return 0; }
+  if (n < 0 || n >= (1LL << 31) || pv->first < 0 || (n > 0 && (!pv->c || pv->stride < 24))) {
+    ctx->err = "pmx_upload_points: bad range or coordinates";
+    return 0;
+  }
+  if (pv->tetra_v && (pv->ne < 0 || pv->tetra_stride < 16)) {
+    ctx->err = "pmx_upload_points: bad new-tet view";
+    return 0;
+  }
   const size_t nn = (size_t)std::max<int64_t>(n, 1);
   // staging layout (pinned): q | kind | vol list | bdy list | dense vol coords
   const size_t o_q = 0, o_k = o_q + al256(nn * sizeof(Pt4)), o_vl = o_k + al256(nn),
@@ -360,26 +411,43 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   double *hqv = (double *)(st + o_qv);
   const char *pc = (const char *)pv->c;
   const char *tg = (const char *)pv->tag;
+  // points referenced by a valid new tet (the reference visits only those,
+  // src/interpmesh_pmmg.c:535-541); marked into the kind array first
+  if (pv->tetra_v) {
+    memset(hk, 0, (size_t)n);
+    const char *tc = (const char *)pv->tetra_v;
+    bool bad = false;
+    par_for(1, pv->ne + 1, [&](int64_t k0, int64_t k1) {
+      bool b = false;
+      for (int64_t k = k0; k < k1; k++) {
+        const int *v = (const int *)(tc + k * pv->tetra_stride);
+        if (v[0] <= 0) continue;                     // !MG_EOK
+        for (int l = 0; l < 4; l++) {
+          const int64_t j = (int64_t)v[l] - pv->first;
+          if (j < 0 || j >= n) { b = true; continue; }
+          __atomic_store_n(&hk[j], (int8_t)1, __ATOMIC_RELAXED);
+        }
+      }
+      if (b) __atomic_store_n(&bad, true, __ATOMIC_RELAXED);
+    });
+    if (bad) {
+      ctx->err = "pmx_upload_points: new tet vertex outside [first, last]";
+      return 0;
+    }
+  }
+  const bool use_mark = pv->tetra_v != nullptr;
   // two passes over fixed chunks (threads): classify + count, then fill the
   // per-path point lists at the chunks' exclusive offsets (input order kept)
-  const int C = n >= (1 << 18) ? (int)host_threads() : 1;
-  const int64_t chunk = (n + C - 1) / std::max(C, 1);
-  std::vector<int64_t> cv((size_t)C + 1, 0), cb((size_t)C + 1, 0);
-  auto chunks = [&](auto body) {
-    if (C == 1) { body(0); return; }
-    std::vector<std::thread> th;
-    for (int i = 0; i < C; i++) th.emplace_back(body, i);
-    for (auto &x : th) x.join();
-  };
-  chunks([&](int ci) {
-    const int64_t j0 = ci * chunk, j1 = std::min<int64_t>(n, j0 + chunk);
+  std::vector<int64_t> cv(65, 0), cb(65, 0);
+  const int C = par_chunks(0, n, [&](int ci, int64_t j0, int64_t j1) {
     int64_t a = 0, b = 0;
     for (int64_t j = j0; j < j1; j++) {
       const double *c = (const double *)(pc + (pv->first + j) * pv->stride);
       hq[j] = Pt4{c[0], c[1], c[2], 0.0};
       unsigned tag = tg ? *(const uint16_t *)(tg + (pv->first + j) * pv->tag_stride) : 0u;
       int8_t kd;
-      if (tag >= PMX_TAG_NUL) kd = KIND_NUL;
+      if (tag >= PMX_TAG_NUL) kd = KIND_NUL;                 // !MG_VOK
+      else if (use_mark && !hk[j]) kd = KIND_ORPH;           // in no valid new tet
       else if (tag & PMX_TAG_REQ) kd = KIND_SKIP;
       else if (tag & PMX_TAG_BDY) { kd = KIND_BDY; b++; }
       else { kd = KIND_VOL; a++; }
@@ -390,8 +458,7 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   });
   for (int i = 0; i < C; i++) { cv[(size_t)i + 1] += cv[(size_t)i]; cb[(size_t)i + 1] += cb[(size_t)i]; }
   const int64_t nv = cv[(size_t)C], nb = cb[(size_t)C];
-  chunks([&](int ci) {
-    const int64_t j0 = ci * chunk, j1 = std::min<int64_t>(n, j0 + chunk);
+  par_chunks(0, n, [&](int ci, int64_t j0, int64_t j1) {
     int64_t a = cv[(size_t)ci], b = cb[(size_t)ci];
     for (int64_t j = j0; j < j1; j++) {
       if (hk[j] == KIND_BDY) bl[b++] = (int)j;
@@ -420,12 +487,12 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   if (!dgrow(ctx, ctx->d_bestk, nn)) return 0;
   if (!dgrow(ctx, ctx->d_best, nn)) return 0;
   if (!dgrow(ctx, ctx->d_ties, nn)) return 0;
-  if (!dgrow(ctx, ctx->d_counts, 32)) return 0;   // [0..7] counters, [16..31] 8 x u64 chunk counters
+  if (!dgrow(ctx, ctx->d_counts, 32)) return 0;
   if (!dgrow(ctx, ctx->d_vollist, (size_t)std::max<int64_t>(nv, 1))) return 0;
   if (!dgrow(ctx, ctx->d_bdylist, (size_t)std::max<int64_t>(nb, 1))) return 0;
-  // one record per wave of the largest k_walk block (1024 threads)
-  if (!dgrow(ctx, ctx->d_vstat, (size_t)std::max<int64_t>((nv + 1023) / 1024 * 16 + 4, 1))) return 0;
-  if (!dgrow(ctx, ctx->d_bstat, (size_t)std::max<int64_t>((nb + 63) / 64 + 4, 1))) return 0;
+  // one record per wave
+  if (!dgrow(ctx, ctx->d_vstat, (size_t)std::max<int64_t>((nv + 255) / 256 * 4 + 4, 1))) return 0;
+  if (!dgrow(ctx, ctx->d_bstat, (size_t)std::max<int64_t>((nb + 255) / 256 * 4 + 4, 1))) return 0;
   if (!dgrow(ctx, ctx->d_qv, (size_t)std::max<int64_t>(nv, 1) * 3)) return 0;
   if (n) {   // no new vertex at all is a valid (empty) step
     CK(hipMemcpyAsync(ctx->d_q.p, hq, (size_t)n * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
@@ -436,14 +503,13 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   if (nb) CK(hipMemcpyAsync(ctx->d_bdylist.p, bl, (size_t)nb * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
   ctx->have_pts = true;
-  ctx->out_S = -1;
   return 1;
 }
 
 // ---- the step ---------------------------------------------------------------
 
 static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &opts, VolArgs &A) {
-  A.pts = ctx->d_pts.p; A.tets = ctx->d_tets.p; A.sol = ctx->d_sol.p; A.sd = sd;
+  A.xyz = ctx->d_xyz.p; A.tets = ctx->d_tets.p; A.sol = ctx->d_sol.p; A.sd = sd;
   A.q = ctx->d_q.p; A.kind = ctx->d_kind.p; A.nq = ctx->nq; A.ne = ctx->ne;
   A.grid = ctx->d_grid.p; A.g = ctx->grid;
   A.out = ctx->d_out.p; A.wmask = ctx->d_wmask.p;
@@ -455,40 +521,23 @@ static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &o
   A.list = ctx->d_vollist.p; A.nlist = ctx->nq_vol; A.wstats = ctx->d_vstat.p;
   A.max_walk = opts.max_walk > 0 ? opts.max_walk : 512;
   A.const_bit = sd.metric_const ? (1u << sd.imet) : 0u;
-  A.occ = (opts.tune & 0xF) ? (opts.tune & 0xF) : PMX_DEFAULT_VOL_OCC;
-  A.xcd_swizzle = 1;
-  A.inline_ties = (opts.tune & 0x4000) ? 0 : 1;   // tune bit 14: all ties to k_fallback
+  A.inline_ties = (opts.flags & PMX_RUN_NO_INLINE_TIES) ? 0 : 1;
   A.qv = ctx->d_qv.p;
-  A.wctr = reinterpret_cast<unsigned long long *>(ctx->d_counts.p + 16);
-  A.region = ((ctx->nq_vol + 7) / 8 + 63) / 64 * 64;
-  // tune bits 17/18: 512 / 1024 threads per k_walk block
-  A.block = (opts.tune & 0x40000) ? 1024 : (opts.tune & 0x20000) ? 512 : 256;
-  // tune bit 20: central hint (per cell, the sample closest to the centre)
-  A.grid64 = (opts.tune & 0x100000) ? ctx->d_grid64.p : nullptr;
-  // tune bits 21-23: k_walk sensitivity experiments (results unchanged):
-  // 1 = every step's f64 face arithmetic done twice, 2 = an extra 32-B tet
-  // record gather per step, 3 = an extra 32-B vertex gather per step
-  A.exp = (opts.tune >> 21) & 7;
-  // tune bit 24: the reference-order walk k_walk instead of the slot walk;
-  // tune bit 25: the slot walk on the 32-B Pt4 records instead of the dense
-  // 24-B coordinates
-  A.ref_walk = (opts.tune & 0x1000000) ? 1 : 0;
-  // tune bit 27: record the volume walks' start tets (pmx_download_starts;
-  // diagnostics and tests -- not an output of the reference)
-  A.rec_start = (opts.tune & 0x8000000) ? 1 : 0;
-  A.xyz = (opts.tune & 0x2000000) ? nullptr : ctx->d_xyz.p;
+  A.ref_walk = (opts.flags & PMX_RUN_REFERENCE_WALK) ? 1 : 0;
+  A.rec_start = (opts.flags & PMX_RUN_RECORD_STARTS) ? 1 : 0;
 }
 
 int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   if (!ctx) return 0;
+  ctx->ran = false;
   if (!ctx->have_bg || !ctx->have_pts) { ctx->err = "pmx_run: upload background and points first"; return 0; }
   hipSetDevice(ctx->device);
   pmx_run_opts opts{};
   if (o) opts = *o;
+  if (opts.hint_stride < 0 || opts.max_walk < 0) { ctx->err = "pmx_run: bad options"; return 0; }
   const int64_t n = ctx->nq;
   const int S = ctx->sd.S;
   if (!dgrow(ctx, ctx->d_out, (size_t)std::max<int64_t>(n * S, 1))) return 0;
-  ctx->out_S = S;
   SolDesc sd = ctx->sd;
   sd.metric_const = (opts.hsiz > 0.0 && sd.imet >= 0) ? 1 : 0;
 
@@ -498,129 +547,89 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   hipStream_t st = ctx->stream;
   if (ev) CK(hipEventRecord(ev[0], st));
   // one prologue kernel zeroes the write masks, the counters and the hint grid
-  const bool need_grid = !((opts.tune & 0x200) && !(opts.tune & 0x100));
-  ctx->tria_hint_fused = false;   // set below when the volume hint build also builds it
-  // the tria hint grid is zeroed at the head of the surface path (off the
-  // main stream), unless the volume hint launch builds it (tune bit 31)
-  const bool tgrid_here = ctx->nq_bdy && ((unsigned)opts.tune & 0x80000000u);
-  launch_prologue(ctx->d_wmask.p, n, ctx->d_counts.p, need_grid ? ctx->d_grid.p : nullptr,
-                  ctx->gcells, tgrid_here ? ctx->d_tgrid : nullptr, ctx->tcells, st);
+  launch_prologue(ctx->d_wmask.p, n, ctx->d_counts.p, ctx->d_grid.p, ctx->gcells, st);
+  // per-background derived data: after an upload, or every step when the
+  // caller times whole iterations (PMX_RUN_FRESH_BACKGROUND)
+  if (!ctx->have_derived || (opts.flags & PMX_RUN_FRESH_BACKGROUND)) {
+    launch_bg_derive(ctx->d_xyz.p, ctx->np, ctx->grid, ctx->d_xyzq.p, ctx->d_tris.p, ctx->nt,
+                     ctx->d_trn.p, st);
+    ctx->have_derived = true;
+  }
+  if (ev) CK(hipEventRecord(ev[7], st));
   if (sd.metric_const)
     launch_const_metric(ctx->d_kind.p, n, ctx->d_out.p, S, sd.off[sd.imet], sd.size[sd.imet],
                         opts.hsiz, ctx->d_wmask.p, sd.imet, st);
   bool any_interp = false;
   for (int s = 0; s < sd.nsol; s++)
     if (!(s == sd.imet && sd.metric_const)) any_interp = true;
-  // reference early exit (src/interpmesh_pmmg.c:509-512): nothing to locate
+  // reference early exit (src/interpmesh_pmmg.c:508-512): nothing to locate
   if (any_interp) {
-    // volume path: tet-centric stream when the new vertices are a sizeable
-    // fraction of the old tets (remesh iterations), adjacency walk otherwise
-    // (tune bit 8 forces the walk, bit 9 the stream)
-    const bool force_walk = (opts.tune & 0x100) != 0, force_tet = (opts.tune & 0x200) != 0;
-    ctx->tet_mode = ctx->nq_vol > 0 && force_tet && !force_walk;
-    (void)force_walk;
-    // surface path placement (tune bits 11/12): default = forked after the
-    // volume hint build (overlaps the walk, which is latency-bound and leaves
-    // issue slots; forking before the bandwidth-bound hint build slowed it by
-    // 40%: r01 sweep), 0x800 = serial on the main stream, 0x1000 = forked
-    // right after the prologue
-    // 0x80000 = forked after the prologue and joined before the volume walk
-    // (overlaps the hint build only)
-    const int bdy_mode = (opts.tune & 0x800) ? 1 : (opts.tune & 0x1000) ? 0 : (opts.tune & 0x80000) ? 3 : 2;
     VolArgs A{};
     fill_vol_args(ctx, sd, opts, A);
-    if (ctx->nq_bdy && (bdy_mode == 0 || bdy_mode == 3)) {
-      // fork: the surface locate (its own hint grid, walk, fallbacks) shares
-      // nothing with the volume path but the zeroed counters and masks
+    const int stride = opts.hint_stride > 0 ? opts.hint_stride : PMX_HINT_STRIDE;
+    launch_hint_build(stride == PMX_HINT_STRIDE ? ctx->d_tets_s.p : nullptr, ctx->d_tets.p, ctx->ne,
+                      stride, ctx->d_grid.p, ctx->grid, ctx->d_xyzq.p, st);
+    if (ev) CK(hipEventRecord(ev[1], st));
+    // surface path on the side stream, forked after the bandwidth-bound hint
+    // build (forking before it slowed that by 40 %, r01 sweep): it is
+    // latency-bound and overlaps the volume walk
+    const bool serial = (opts.flags & PMX_RUN_SERIAL_SURFACE) != 0;
+    if (ctx->nq_bdy && !serial) {
       CK(hipEventRecord(ctx->ev_fork, st));
       CK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
       if (ev) CK(hipEventRecord(ev[3], ctx->side));
-      if (!ctx->launch_bdy(A, opts, ctx->side)) return 0;
+      if (!ctx->launch_bdy(A, ctx->side)) return 0;
       if (ev) CK(hipEventRecord(ev[5], ctx->side));
       CK(hipEventRecord(ctx->ev_join, ctx->side));
     }
-    if (!ctx->tet_mode) {
-      const int stride = opts.hint_stride > 0 ? opts.hint_stride : PMX_DEFAULT_HINT_STRIDE;
-      // tune bit 13: strided reads of the connectivity stream (r01 A/B)
-      const bool packed = stride == PMX_DEFAULT_HINT_STRIDE && !(opts.tune & 0x2000);
-      if (A.grid64) launch_fill64(ctx->d_grid64.p, ctx->gcells, st);
-      // tune bit 31: the surface path's tria hint grid built in the same
-      // launch (k_hint_build_fused; r01: C2 +1.3 %, C3 +0.4 % step time --
-      // the latency-bound tria part lengthens the hint build more than it
-      // shortens the side stream)
-      ctx->tria_hint_fused = packed && !A.grid64 && !(opts.tune & 0x8000) &&
-                             !(opts.tune & (0x4000000 | 0x30000000)) &&
-                             ((unsigned)opts.tune & 0x80000000u) && ctx->nq_bdy &&
-                             bdy_mode == 2 && ctx->nt > 0;
-      if (ctx->tria_hint_fused)
-        launch_hint_build_fused(ctx->d_tets_s.p, ctx->ne, stride, ctx->d_grid.p, ctx->grid,
-                                ctx->d_xyzq.p, ctx->d_tris.p, ctx->d_pts.p, ctx->nt, ctx->d_tgrid,
-                                ctx->tgd, st);
-      else
-      launch_hint_build(ctx->d_tetv.p, packed ? ctx->d_tets_s.p : nullptr, ctx->d_pts.p, ctx->ne,
-                        stride, ctx->d_grid.p, ctx->grid, (opts.tune & 0x8000) ? 1 : 0, st,
-                        const_cast<unsigned long long *>(A.grid64),
-                        (opts.tune & 0x4000000) ? nullptr : ctx->d_xyz.p,    // bit 26: Pt4 reads
-                        // centroids: default fixed-point grid coordinates (r01
-                        // C3 hint: double 0.295, float 0.217, fixed 0.197 ms);
-                        // bit 28: double, bit 29: single precision
-                        (opts.tune & 0x30000000) == 0x20000000 ? ctx->d_xyzf.p : nullptr,
-                        (opts.tune & 0x30000000) ? nullptr : ctx->d_xyzq.p);
-    }
-    if (ctx->nq_bdy && bdy_mode == 3) CK(hipStreamWaitEvent(st, ctx->ev_join, 0));
-    if (ev) CK(hipEventRecord(ev[1], st));
-    if (ctx->nq_bdy && bdy_mode == 2) {
-      // tune bit 30: the surface path on a lowest-priority stream (the
-      // volume walk's workgroups are dispatched first)
-      hipStream_t sd = (opts.tune & 0x40000000) ? ctx->side_lo : ctx->side;
-      CK(hipEventRecord(ctx->ev_fork, st));
-      CK(hipStreamWaitEvent(sd, ctx->ev_fork, 0));
-      if (ev) CK(hipEventRecord(ev[3], sd));
-      if (!ctx->launch_bdy(A, opts, sd)) return 0;
-      if (ev) CK(hipEventRecord(ev[5], sd));
-      CK(hipEventRecord(ctx->ev_join, sd));
-    }
-    if (ctx->tet_mode) {
-      if (!ctx->launch_tet_locate(A, opts, st)) return 0;
-    } else if (ctx->nq_vol) {
-      // tune bit 10: the r01 kernel k_locate_vol (A/B reference)
-      // tune bit 16: the persistent-lane k_walkp (r01: 2.7x slower at 2 waves/SIMD)
-      if (opts.tune & 0x400) launch_locate_vol(A, st);
-      else if (opts.tune & 0x10000) launch_walkp(A, st);
-      else launch_walk(A, st);
-    }
+    if (ctx->nq_vol) launch_walk(A, st);
     if (ev) CK(hipEventRecord(ev[2], st));
-    if (ctx->nq_bdy && (bdy_mode == 0 || bdy_mode == 2)) {
+    if (ctx->nq_bdy && !serial) {
       CK(hipStreamWaitEvent(st, ctx->ev_join, 0));     // surface path done
-    } else if (ctx->nq_bdy && bdy_mode == 1) {
+    } else if (ctx->nq_bdy) {
       if (ev) CK(hipEventRecord(ev[3], st));
-      if (!ctx->launch_bdy(A, opts, st)) return 0;
+      if (!ctx->launch_bdy(A, st)) return 0;
       if (ev) CK(hipEventRecord(ev[5], st));
-    } else if (ev && !ctx->nq_bdy) {
+    } else if (ev) {
       CK(hipEventRecord(ev[3], st));
       CK(hipEventRecord(ev[5], st));
     }
     if (ev) CK(hipEventRecord(ev[6], st));
     ExhArgs E{};
-    E.pts = ctx->d_pts.p; E.tets = ctx->d_tets.p; E.ne = ctx->ne; E.q = ctx->d_q.p;
+    E.xyz = ctx->d_xyz.p; E.tets = ctx->d_tets.p; E.ne = ctx->ne; E.q = ctx->d_q.p;
     E.list = ctx->d_list.p; E.count = ctx->d_counts.p; E.found = ctx->d_found.p;
     E.best = ctx->d_best.p; E.bestk = ctx->d_bestk.p;
-    if (ctx->nq_vol) launch_exhaustive(E, A, st);
+    E.spin_limit = (opts.flags & PMX_RUN_DEBUG_BARRIER_TIMEOUT) ? 0L : (1L << 26);
+    if (ctx->nq_vol) launch_exhaustive(E, A, ctx->fallback_blocks, st);
     if (ev) CK(hipEventRecord(ev[4], st));
   } else if (ev) {
-    for (int k = 1; k < PMX_EV_PER_RUN; k++) CK(hipEventRecord(ev[k], st));
+    for (int k = 1; k < PMX_EV_PER_RUN; k++)
+      if (k != 7) CK(hipEventRecord(ev[k], st));
   }
   CK(hipGetLastError());
+  ctx->out_S = S;
+  ctx->out_n = n;
   ctx->ran = true;
   return 1;
 }
 
+// results of the last step, consistent with the current uploads
+static bool results_ready(pmx_ctx *ctx, const char *who) {
+  if (!ctx->ran || !ctx->have_pts || !ctx->have_bg || ctx->out_n != ctx->nq || ctx->out_S != ctx->sd.S) {
+    ctx->err = std::string(who) + ": no step has run on the current uploads";
+    return false;
+  }
+  return true;
+}
+
 int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem, int *status, int *steps) {
-  if (!ctx || !ctx->ran) { if (ctx) ctx->err = "pmx_download: nothing ran"; return 0; }
+  if (!ctx) return 0;
+  if (!results_ready(ctx, "pmx_download")) return 0;
   hipSetDevice(ctx->device);
   const int64_t n = ctx->nq;
   const int S = ctx->sd.S;
   CK(hipStreamSynchronize(ctx->stream));
+  if (!ctx->check_device_errors()) return 0;
   if (n == 0) return 1;   // empty step: nothing to copy
   // every device -> host copy lands in the pinned arena (async DMA, one sync),
   // then the host scatters into the caller's (pageable, strided) arrays
@@ -660,16 +669,20 @@ int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem, int *sta
 }
 
 int pmx_download_starts(pmx_ctx *ctx, int *start) {
-  if (!ctx || !ctx->ran) return 0;
+  if (!ctx || !start) return 0;
+  if (!results_ready(ctx, "pmx_download_starts")) return 0;
   CK(hipStreamSynchronize(ctx->stream));
+  if (!ctx->check_device_errors()) return 0;
   if (ctx->nq == 0) return 1;
   CK(hipMemcpy(start, ctx->d_start.p, (size_t)ctx->nq * sizeof(int), hipMemcpyDeviceToHost));
   return 1;
 }
 
 int pmx_download_border(pmx_ctx *ctx, int *edge, int *vertex) {
-  if (!ctx || !ctx->ran) return 0;
+  if (!ctx) return 0;
+  if (!results_ready(ctx, "pmx_download_border")) return 0;
   CK(hipStreamSynchronize(ctx->stream));
+  if (!ctx->check_device_errors()) return 0;
   if (ctx->nq == 0) return 1;
   if (edge) CK(hipMemcpy(edge, ctx->d_edge.p, (size_t)ctx->nq * sizeof(int), hipMemcpyDeviceToHost));
   if (vertex) CK(hipMemcpy(vertex, ctx->d_vertex.p, (size_t)ctx->nq * sizeof(int), hipMemcpyDeviceToHost));
@@ -677,9 +690,11 @@ int pmx_download_border(pmx_ctx *ctx, int *edge, int *vertex) {
 }
 
 int pmx_locate_stats_get(pmx_ctx *ctx, pmx_locate_stats *st) {
-  if (!ctx || !ctx->ran || !st) return 0;
+  if (!ctx || !st) return 0;
+  if (!results_ready(ctx, "pmx_locate_stats_get")) return 0;
   unsigned cnt[8];
   CK(hipStreamSynchronize(ctx->stream));
+  if (!ctx->check_device_errors()) return 0;
   CK(hipMemcpy(cnt, ctx->d_counts.p, sizeof cnt, hipMemcpyDeviceToHost));
   memset(st, 0, sizeof *st);
   st->nvol = ctx->nq_vol;
@@ -688,18 +703,10 @@ int pmx_locate_stats_get(pmx_ctx *ctx, pmx_locate_stats *st) {
   // reduce the per-wave records of both walks
   unsigned long long located = 0, sum = 0;
   unsigned mx = 0, mn = 0xffffffffu;
-  st->tet_mode = ctx->tet_mode ? 1 : 0;
-  if (ctx->tet_mode && ctx->tests_blocks > 0 && ctx->nq_vol > 0) {
-    std::vector<unsigned long long> tp((size_t)ctx->tests_blocks);
-    CK(hipMemcpy(tp.data(), ctx->d_tests.p, tp.size() * 8, hipMemcpyDeviceToHost));
-    unsigned long long tot = 0;
-    for (auto x : tp) tot += x;
-    st->tests_per_vertex = (double)tot / (double)ctx->nq_vol;
-  }
   for (int path = 0; path < 2; path++) {
     int64_t npath = path ? ctx->nq_bdy : ctx->nq_vol;
-    if (!npath || (path == 0 && ctx->tet_mode)) continue;
-    std::vector<uint4> w((size_t)((npath + 63) / 64));
+    if (!npath) continue;
+    std::vector<uint4> w((size_t)((npath + 255) / 256 * 4));
     CK(hipMemcpy(w.data(), path ? ctx->d_bstat.p : ctx->d_vstat.p, w.size() * sizeof(uint4),
                  hipMemcpyDeviceToHost));
     for (const uint4 &r : w) {
@@ -750,15 +757,15 @@ int pmx_timing_reset(pmx_ctx *ctx) {
 }
 
 double pmx_kernel_ms(pmx_ctx *ctx, int which) {
-  if (!ctx || ctx->ev_used == 0 || which < 0 || which > 4) return -1.0;
+  if (!ctx || ctx->ev_used == 0 || which < 0 || which > 5) return -1.0;
   hipStreamSynchronize(ctx->stream);
   double tot = 0.0;
   for (int r = 0; r < ctx->ev_used; r++) {
     hipEvent_t *e = &ctx->events[(size_t)r * PMX_EV_PER_RUN];
     float ms = 0.f;
-    // events: 0 start, 1 hint built, 2 volume walk done, 3/5 surface path
-    // start/end (side stream), 6 joined, 4 end
-    static const int from[5] = {0, 1, 3, 6, 0}, to[5] = {1, 2, 5, 4, 4};
+    // 0 hint (prologue + derived data + hint build), 1 volume walk, 2 surface
+    // path, 3 fallback, 4 total, 5 derived data (prologue included)
+    static const int from[6] = {0, 1, 3, 6, 0, 0}, to[6] = {1, 2, 5, 4, 4, 7};
     hipEventElapsedTime(&ms, e[from[which]], e[to[which]]);
     tot += ms;
   }
@@ -785,18 +792,20 @@ void pmx_ctx::free_all() {
   if (h_stage) hipHostFree(h_stage);
   h_stage = nullptr;
   h_stage_cap = 0;
-  dfree(d_pts); dfree(d_tets); dfree(d_sol); dfree(d_xyz); dfree(d_xyzf); dfree(d_xyzq); dfree(d_tris); dfree(d_trn); dfree(d_grid); dfree(d_grid64);
-  dfree(d_ntoff); dfree(d_ntlist);
+  dfree(d_xyz); dfree(d_tets); dfree(d_sol); dfree(d_tets_s); dfree(d_tris); dfree(d_ntoff);
+  dfree(d_ntlist); dfree(d_xyzq); dfree(d_trn); dfree(d_grid); dfree(d_tetv);
   dfree(d_q); dfree(d_kind); dfree(d_wmask); dfree(d_out); dfree(d_elem); dfree(d_status);
   dfree(d_steps); dfree(d_start); dfree(d_edge); dfree(d_vertex); dfree(d_list); dfree(d_found);
   dfree(d_bestk); dfree(d_best); dfree(d_ties); dfree(d_counts); dfree(d_vollist); dfree(d_bdylist);
-  dfree(d_vstat); dfree(d_bstat);
-  dfree(d_tetv); dfree(d_qcnt); dfree(d_qstart); dfree(d_qcell); dfree(d_qslot); dfree(d_tbest);
-  dfree(d_qs); dfree(d_tests); dfree(d_scan_tmp);
-  dfree(d_qual); dfree(d_red); dfree(d_emask); dfree(d_elist); dfree(d_bcount); dfree(d_blist); dfree(d_olist); dfree(d_ows);
+  dfree(d_vstat); dfree(d_bstat); dfree(d_qv);
+  dfree(d_qual); dfree(d_red); dfree(d_emask); dfree(d_elist); dfree(d_bcount); dfree(d_blist);
+  dfree(d_olist); dfree(d_ows);
+  dfree(d_cmet); dfree(d_ctag); dfree(d_cperm); dfree(d_cdst); dfree(d_ccnt); dfree(d_cold);
+  dfree(d_cvals);
   if (d_tgrid) hipFree(d_tgrid);
   d_tgrid = nullptr;
   d_tgrid_cap = 0;
+  have_bg = have_pts = ran = have_derived = have_tetv = have_qual = false;
 }
 
 // node -> trias graph: offsets[np+2] (0-based CSR) + list of incident trias

@@ -1,7 +1,7 @@
 // pmx_device.h -- device-side data layout and geometry for the gfx950 kernels.
 //
 // HBM layout (all 1-based like Mmg, slot 0 unused):
-//   Pt4     pts[np+1]     32 B  {x,y,z,0}          one aligned 32-B gather / vertex
+//   double  xyz[3*(np+1)] 24 B  x, y, z            uploaded as is (no padding)
 //   TetRec  tets[ne+1]    32 B  {v[4], nb[4]}      nb[f] = adja/4 (0 = boundary face)
 //   double  sol[(np+1)*S]        all background solutions interleaved per vertex
 //   TriRec  tris[nt+1]    32 B  {v[3], -, nb[3], -} nb[e] = adjt/3
@@ -25,7 +25,9 @@ struct __align__(32) TriRec { int v[3]; int pad0; int nb[3]; int pad1; };
 
 struct D3 { double x, y, z; };
 
-enum : int8_t { KIND_VOL = 0, KIND_BDY = 1, KIND_SKIP = 2, KIND_NUL = 3 };
+// KIND_SKIP: MG_REQ (copied by PMMG_copyMetricsAndFields_point); KIND_NUL:
+// !MG_VOK; KIND_ORPH: in no valid new tet (never visited by the reference)
+enum : int8_t { KIND_VOL = 0, KIND_BDY = 1, KIND_SKIP = 2, KIND_NUL = 3, KIND_ORPH = 4 };
 
 struct SolDesc {
   int nsol;
@@ -39,6 +41,11 @@ struct SolDesc {
 __device__ __forceinline__ D3 ld3(const Pt4 *p, int i) {
   Pt4 t = p[i];
   return D3{t.x, t.y, t.z};
+}
+// old-mesh vertices: dense x, y, z (24 B, 5.3 vertices per 128-B line)
+__device__ __forceinline__ D3 ld3(const double *__restrict__ xyz, int i) {
+  const double *r = xyz + 3 * (int64_t)i;
+  return D3{r[0], r[1], r[2]};
 }
 
 // MMG5_nonUnitNorPts (restated): (b-a) x (c-a)

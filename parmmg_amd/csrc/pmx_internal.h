@@ -1,6 +1,7 @@
 // pmx_internal.h -- the context object behind the C ABI (host only).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <string>
 #include <vector>
 #include "pmx_transfer.h"
@@ -11,22 +12,25 @@ template <class T> struct DevBuf {
   size_t cap = 0;
 };
 
+// hint grid from every 4th tet: 1/4 of the stores and of the tet bytes of a
+// full build, at ~0.5 extra walk step (r01 measurements)
+#define PMX_HINT_STRIDE 4
+
 struct pmx_ctx {
   int device = 0;
   hipStream_t own = nullptr, stream = nullptr;
-  // the surface path runs on `side`, forked after the prologue and joined
-  // before the fallback: it overlaps the volume hint build and walk
+  // the surface path runs on `side`, forked after the volume hint build and
+  // joined before the fallback: it overlaps the volume walk
   hipStream_t side = nullptr;
-  hipStream_t side_lo = nullptr;        // lowest-priority side stream (tune bit 30)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::string err;
+  int fallback_blocks = 0;              // co-resident k_fallback workgroups
   // pinned host staging arena (hipHostMalloc, grown on demand, reused across
-  // steps): point uploads and result downloads go through it as async DMA
-  // instead of pageable copies (PCIe-inclusive rate)
+  // steps): uploads and downloads go through it as async DMA
   void *h_stage = nullptr;
   size_t h_stage_cap = 0;
 
-  // background group
+  // background group (raw uploads)
   bool have_bg = false;
   int64_t np = 0, ne = 0, nt = 0;
   double hausd = 0.0;
@@ -34,23 +38,28 @@ struct pmx_ctx {
   GridDesc grid{};
   int64_t gcells = 0;
   double bblo[3]{}, bbhi[3]{};
-  DevBuf<Pt4> d_pts;
+  DevBuf<double> d_xyz;                 // old vertices, x y z (24 B), slot 0 unused
   DevBuf<TetRec> d_tets;
   DevBuf<double> d_sol;
-  DevBuf<double> d_xyz;                 // dense coordinates, 3 doubles per vertex
-  DevBuf<float> d_xyzf;                 // the same in single precision (hint centroids)
-  DevBuf<unsigned long long> d_xyzq;    // fixed-point grid coordinates (hint centroids)
+  DevBuf<int4> d_tets_s;                // host-packed hint sample: tets 1, 1+4, 1+8, ...
   DevBuf<TriRec> d_tris;
-  DevBuf<Pt4> d_trn;
-  DevBuf<int> d_grid;
-  DevBuf<unsigned long long> d_grid64;    // central-hint grid: (dist2 f32 bits << 32 | tet) minima
   DevBuf<int> d_ntoff, d_ntlist;
   std::vector<int> h_ntoff, h_ntlist;
+  // derived from the raw uploads on the device (k_bg_derive), by the first
+  // step after an upload or by every step with PMX_RUN_FRESH_BACKGROUND
+  bool have_derived = false;
+  DevBuf<unsigned long long> d_xyzq;    // fixed-point grid coordinates (hint centroids)
+  DevBuf<Pt4> d_trn;                    // tria unit normals + areas
+  DevBuf<int> d_grid;
+  // statistics only: 16-B connectivity stream, derived on first use
+  bool have_tetv = false;
+  DevBuf<int4> d_tetv;
 
   // new points and results
   bool have_pts = false, ran = false;
   int64_t nq = 0, nq_vol = 0, nq_bdy = 0;
-  int out_S = -1;
+  int out_S = -1;                       // solution width the results were computed for
+  int64_t out_n = -1;                   // point count the results were computed for
   DevBuf<Pt4> d_q;
   DevBuf<int8_t> d_kind;
   DevBuf<uint8_t> d_wmask;
@@ -58,18 +67,8 @@ struct pmx_ctx {
   DevBuf<int> d_elem, d_status, d_steps, d_start, d_edge, d_vertex;
   DevBuf<int> d_list, d_found, d_bestk;
   DevBuf<int2> d_ties;
-  // tet-centric volume path
-  DevBuf<int4> d_tetv;                  // connectivity stream (16 B / tet)
-  DevBuf<int4> d_tets_s;                // packed sample: tets 1, 1+S, 1+2S.. (S = hint stride)
-  DevBuf<unsigned> d_qcnt, d_qstart;
-  DevBuf<int> d_qcell, d_qslot, d_tbest;
-  DevBuf<Pt4> d_qs;
-  DevBuf<unsigned long long> d_tests;
-  DevBuf<char> d_scan_tmp;
-  int tests_blocks = 0;
-  bool tet_mode = false;
   DevBuf<unsigned long long> d_best;
-  DevBuf<unsigned> d_counts;            // [0] vol stuck, [1] bdy stuck, [2] bdy overflow
+  DevBuf<unsigned> d_counts;            // step counters, see pmx_kernels.h
   DevBuf<int> d_vollist, d_bdylist;     // compacted point lists per path
   DevBuf<double> d_qv;                  // volume points, dense xyz in list order
   DevBuf<uint4> d_vstat, d_bstat;       // per-wave walk statistics
@@ -77,8 +76,14 @@ struct pmx_ctx {
   int *d_tgrid = nullptr;
   size_t d_tgrid_cap = 0;
   GridDesc tgd{};
-  bool tria_hint_fused = false;         // this step's tria hint built with the volume hint
   int64_t tcells = 0;
+
+  // group seams (pmx_groups.hip): constant-size metric of a step without a
+  // background, and the frozen-point copy (buffers reused across calls)
+  DevBuf<double> d_cmet;
+  DevBuf<uint16_t> d_ctag;
+  DevBuf<int> d_cperm, d_cdst, d_ccnt;
+  DevBuf<double> d_cold, d_cvals;
 
   // statistics
   DevBuf<double> d_qual;
@@ -96,11 +101,29 @@ struct pmx_ctx {
   hipEvent_t *next_event_slot();
   void free_all();
   void host_build_node_trias(const std::vector<TriRec> &tr);
-  bool launch_bdy(const VolArgs &a, const pmx_run_opts &o, hipStream_t s);
+  bool launch_bdy(const VolArgs &a, hipStream_t s);
   bool size_tria_grid();
-  bool launch_tet_locate(const VolArgs &a, const pmx_run_opts &o, hipStream_t s);
+  // device error word of the last step (after a stream sync): 0 = none
+  bool check_device_errors();
 };
 
+// grow-only device buffer (contents not kept); false + ctx->err on failure
+template <class T> inline bool pmx_dgrow(pmx_ctx *ctx, DevBuf<T> &b, size_t n) {
+  if (n <= b.cap && b.p) return true;
+  if (b.p) hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  const hipError_t e = hipMalloc((void **)&b.p, std::max<size_t>(n, 1) * sizeof(T));
+  if (e != hipSuccess) {
+    ctx->err = std::string("hipMalloc: ") + hipGetErrorString(e);
+    b.p = nullptr;
+    return false;
+  }
+  b.cap = n;
+  return true;
+}
+// the context's pinned staging arena, at least `bytes` (pmx_capi.hip)
+char *pmx_hstage(pmx_ctx *ctx, size_t bytes);
+
 bool pmx_ctx_build_adja_host(pmx_ctx *ctx, const pmx_mesh_view *m, std::vector<int> &adja);
-void launch_tria_normals(const TriRec *tris, const Pt4 *pts, int64_t nt, Pt4 *trn, hipStream_t s);
 extern "C" int pmx_timing_reset(pmx_ctx *ctx);

@@ -1,39 +1,21 @@
 // pmx_kernels.hip -- gfx950 kernels of the transfer path (volume part).
 //
-// k_hint_build       uniform grid over the background bbox, cell -> largest
-//                    tet index whose centroid falls in it (deterministic)
-// k_locate_vol       one thread per new vertex: adjacency walk from the hint
-//                    (PMMG_locatePointVol, reference src/locate_pmmg.c:786-883)
-//                    fused with PMMG_interp4bar_{iso,ani}
-//                    (src/interpmesh_pmmg.c:206-270); stuck lanes are
-//                    compacted into a list (wave-aggregated atomic)
-// k_exh_find         LDS-staged exhaustive scan for the stuck list: smallest
-//                    containing tet index == the reference's first hit in
-//                    index order (src/locate_pmmg.c:737-770)
-// k_exh_closest[_idx] argmin of |lambda_min|*vol over all tets for points
-//                    contained nowhere, then the reference's closest-vertex
-//                    barycentrics (src/barycoord_pmmg.c:371-404)
-// k_exh_finish       interpolation for the stuck list
+// k_bg_derive        per-background derived data, one launch: fixed-point grid
+//                    coordinates of the old vertices (hint centroids) and the
+//                    unit normals of the boundary trias
+//                    (PMMG_precompute_triaNormals, src/locate_pmmg.c:68-90)
+// k_hint_build       uniform grid over the background bbox, cell -> a sampled
+//                    tet whose centroid falls in it (the walk start)
+// k_fallback         ties, LDS-staged exhaustive scan (smallest containing tet
+//                    index == the reference's first hit in index order,
+//                    src/locate_pmmg.c:737-770), closest tet (argmin of
+//                    |lambda_min|*vol, src/barycoord_pmmg.c:371-404) and the
+//                    interpolation of the scanned points, phases separated by
+//                    a grid barrier that reports a timeout instead of hiding it
+// The production walk itself is pmx_walk.hip.
 #include <algorithm>
 #include "pmx_device.h"
 #include "pmx_kernels.h"
-
-#define WALK_RING 4
-
-// rank of each value in the stable ascending order (ties: lower index first)
-__device__ __forceinline__ void stable_ranks(const double l[4], int rk[4]) {
-  rk[0] = rk[1] = rk[2] = rk[3] = 0;
-#pragma unroll
-  for (int a = 0; a < 4; a++)
-#pragma unroll
-    for (int b = a + 1; b < 4; b++) {
-      // b after a unless l[b] < l[a]
-      bool bfirst = l[b] < l[a];
-      rk[a] += bfirst ? 1 : 0;
-      rk[b] += bfirst ? 0 : 1;
-    }
-}
-
 
 __device__ __forceinline__ int clampi(double t, int n) {
   if (!(t > 0.0)) return 0;                 // also catches NaN
@@ -41,120 +23,18 @@ __device__ __forceinline__ int clampi(double t, int n) {
   return (int)t;
 }
 
-__device__ __forceinline__ int64_t cell_of(const GridDesc &g, D3 p, int *c) {
-  c[0] = clampi((p.x - g.lo[0]) * g.inv[0], g.dim[0]);
-  c[1] = clampi((p.y - g.lo[1]) * g.inv[1], g.dim[1]);
-  c[2] = clampi((p.z - g.lo[2]) * g.inv[2], g.dim[2]);
-  return (int64_t)c[0] + (int64_t)g.dim[0] * ((int64_t)c[1] + (int64_t)g.dim[1] * c[2]);
-}
+// ---- per-background derived data -----------------------------------------------
 
-__device__ int hint_lookup(const int *grid, const GridDesc &g, D3 p) {
-  int c[3];
-  int k = grid[cell_of(g, p, c)];
-  if (k) return k;
-  for (int r = 1; r <= 3; r++) {
-    for (int dz = -r; dz <= r; dz++)
-      for (int dy = -r; dy <= r; dy++)
-        for (int dx = -r; dx <= r; dx++) {
-          if (max(abs(dx), max(abs(dy), abs(dz))) != r) continue;
-          int x = c[0] + dx, y = c[1] + dy, z = c[2] + dz;
-          if (x < 0 || y < 0 || z < 0 || x >= g.dim[0] || y >= g.dim[1] || z >= g.dim[2]) continue;
-          int kk = grid[(int64_t)x + (int64_t)g.dim[0] * ((int64_t)y + (int64_t)g.dim[1] * z)];
-          if (kk) return kk;
-        }
-  }
-  return 1;
-}
-
-template <bool MID, bool CENTRAL, bool DX = false, bool FX = false, bool QX = false>
-__global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ src, int64_t sstride,
-                                                    const Pt4 *__restrict__ pts, int64_t ne,
-                                                    int stride, int *__restrict__ grid,
-                                                    GridDesc g,
-                                                    unsigned long long *__restrict__ grid64,
-                                                    const double *__restrict__ xyz = nullptr,
-                                                    const float *__restrict__ xyzf = nullptr,
-                                                    const unsigned long long *__restrict__ xyzq = nullptr) {
-  // one sample per thread; XCD-aware block order: each XCD's L2 serves a
-  // contiguous range of samples, i.e. neighbouring tets sharing vertices
-  const int64_t n = (ne + stride - 1) / stride;
-  const int64_t t = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  const int64_t k = 1 + t * stride;
-  // sampled tet k: from the packed sample stream (sstride 1, coalesced) or
-  // from every stride-th record of the 16-B connectivity stream
-  const int4 v = src[t * sstride];
-  if (v.x <= 0) return;
-  D3 m;
-  if constexpr (QX) {
-    // QX: the vertices' grid coordinates in 21-bit fixed point (HINT_QF
-    // fraction bits, packed x | y << 21 | z << 42 at upload): one 8-B gather
-    // per vertex, the centroid's cell by integer sums and a shift
-    const unsigned long long a = xyzq[v.x], b = xyzq[v.y], c = xyzq[v.z], d = xyzq[v.w];
-    const unsigned long long M = (1ull << 21) - 1;
-    int cq[3];
-#pragma unroll
-    for (int ax = 0; ax < 3; ax++) {
-      const int sh = 21 * ax;
-      const unsigned s4 = (unsigned)((a >> sh) & M) + (unsigned)((b >> sh) & M) +
-                          (unsigned)((c >> sh) & M) + (unsigned)((d >> sh) & M);
-      cq[ax] = min((int)(s4 >> (HINT_QF + 2)), g.dim[ax] - 1);
-    }
-    grid[(int64_t)cq[0] + (int64_t)g.dim[0] * ((int64_t)cq[1] + (int64_t)g.dim[1] * cq[2])] = (int)k;
-    return;
-  } else if constexpr (FX) {
-    // FX: centroid from the 12-B single-precision copy of the coordinates (one
-    // 12-B gather per vertex instead of 24 B in two loads).  The cell only
-    // picks a start tet, and the located tet does not depend on the start.
-    auto ldf = [&](int i) -> float3 {
-      const float *r = xyzf + 3 * (int64_t)i;
-      return make_float3(r[0], r[1], r[2]);
-    };
-    const float3 a = ldf(v.x), b = ldf(v.y), c = ldf(v.z), d = ldf(v.w);
-    m = D3{(double)((a.x + b.x + c.x + d.x) * 0.25f), (double)((a.y + b.y + c.y + d.y) * 0.25f),
-           (double)((a.z + b.z + c.z + d.z) * 0.25f)};
-  } else if (MID) {
-    // midpoint of edge v0-v1: a point of the tet's closure, 2 gathers
-    const D3 a = ld3(pts, v.x), b = ld3(pts, v.y);
-    m = D3{(a.x + b.x) * 0.5, (a.y + b.y) * 0.5, (a.z + b.z) * 0.5};
-  } else {
-    // DX: from the dense 24-B coordinates (VolArgs::xyz)
-    auto ldp = [&](int i) -> D3 {
-      if constexpr (DX) return D3{xyz[3 * (int64_t)i], xyz[3 * (int64_t)i + 1], xyz[3 * (int64_t)i + 2]};
-      else return ld3(pts, i);
-    };
-    const D3 a = ldp(v.x), b = ldp(v.y), c = ldp(v.z), d = ldp(v.w);
-    m = D3{(a.x + b.x + c.x + d.x) * 0.25, (a.y + b.y + c.y + d.y) * 0.25,
-           (a.z + b.z + c.z + d.z) * 0.25};
-  }
-  int cc[3];
-  const int64_t cell = cell_of(g, m, cc);
-  if (CENTRAL) {
-    // the sample whose centroid is closest to the cell centre (ties: lowest
-    // tet index): deterministic, and a shorter walk from anywhere in the cell
-    const double dx = m.x - (g.lo[0] + (cc[0] + 0.5) / g.inv[0]);
-    const double dy = m.y - (g.lo[1] + (cc[1] + 0.5) / g.inv[1]);
-    const double dz = m.z - (g.lo[2] + (cc[2] + 0.5) / g.inv[2]);
-    const float d2 = (float)(dx * dx + dy * dy + dz * dz);
-    const unsigned long long key =
-        ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned long long)(unsigned)k;
-    atomicMin(grid64 + cell, key);
-  } else {
-    // plain store: any sampled tet of the cell is a valid start; the located
-    // tet does not depend on the start (unique containing tet, or the
-    // canonical min-index tet of a tie, see canonical_tet)
-    grid[cell] = (int)k;
-  }
-}
-
-// grid coordinates of the vertices in fixed point for k_hint_build<QX>:
-// q = (x - lo) * inv * 2^HINT_QF, clamped to [0, dim * 2^HINT_QF - 1]
-__global__ __launch_bounds__(256) void k_quant_xyz(const Pt4 *__restrict__ pts, int64_t n, GridDesc g,
-                                                   unsigned long long *__restrict__ q) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const Pt4 p = pts[i];
-    const double c[3] = {p.x, p.y, p.z};
+// grid coordinates of the vertices in fixed point for k_hint_build:
+// q = (x - lo) * inv * 2^HINT_QF, clamped to [0, dim * 2^HINT_QF - 1], packed
+// x | y << 21 | z << 42; and the tria normals + areas
+__global__ __launch_bounds__(256) void k_bg_derive(const double *__restrict__ xyz, int64_t np, GridDesc g,
+                                                   unsigned long long *__restrict__ q,
+                                                   const TriRec *__restrict__ tris, int64_t nt,
+                                                   Pt4 *__restrict__ trn) {
+  const int64_t st = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= np; i += st) {
+    const double c[3] = {xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]};
     unsigned long long r = 0;
 #pragma unroll
     for (int a = 0; a < 3; a++) {
@@ -165,35 +45,77 @@ __global__ __launch_bounds__(256) void k_quant_xyz(const Pt4 *__restrict__ pts, 
     }
     q[i] = r;
   }
-}
-void launch_quant_xyz(const Pt4 *pts, int64_t n, GridDesc g, unsigned long long *q, hipStream_t s) {
-  const int64_t nb = std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), 65536);
-  hipLaunchKernelGGL(k_quant_xyz, dim3((unsigned)nb), dim3(256), 0, s, pts, n, g, q);
-}
-
-__global__ __launch_bounds__(256) void k_fill64(unsigned long long *p, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    p[i] = ~0ull;
-}
-void launch_fill64(unsigned long long *p, int64_t n, hipStream_t s) {
-  const int64_t nb = std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), 4096);
-  hipLaunchKernelGGL(k_fill64, dim3((unsigned)nb), dim3(256), 0, s, p, n);
-}
-
-// connectivity stream out of the tet records: dst[i] = src[i * stride].v
-// (a kernel rather than a pitched 2-D copy: no row-count limits at 1e8 tets)
-__global__ __launch_bounds__(256) void k_tet_conn(const TetRec *__restrict__ src, int64_t stride,
-                                                  int64_t n, int4 *__restrict__ dst) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int4 *r = reinterpret_cast<const int4 *>(src + i * stride);
-    dst[i] = r[0];
+  for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= nt; k += st) {
+    const TriRec t = tris[k];
+    if (t.v[0] <= 0) { trn[k] = Pt4{0, 0, 0, 0}; continue; }
+    const D3 n = nonunit_normal(ld3(xyz, t.v[0]), ld3(xyz, t.v[1]), ld3(xyz, t.v[2]));
+    const double a = sqrt(n.x * n.x + n.y * n.y + n.z * n.z);
+    const double dd = 1.0 / a;
+    trn[k] = Pt4{n.x * dd, n.y * dd, n.z * dd, a};
   }
 }
-void launch_tet_conn(const TetRec *src, int64_t stride, int64_t n, int4 *dst, hipStream_t s) {
+void launch_bg_derive(const double *xyz, int64_t np, GridDesc g, unsigned long long *xyzq,
+                      const TriRec *tris, int64_t nt, Pt4 *trn, hipStream_t s) {
+  const int64_t n = std::max(np + 1, nt);
+  const int64_t nb = std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), 65536);
+  hipLaunchKernelGGL(k_bg_derive, dim3((unsigned)nb), dim3(256), 0, s, xyz, np, g, xyzq, tris, nt, trn);
+}
+
+// ---- hint grid ---------------------------------------------------------------------
+
+// One sample per thread; XCD-aware block order: each XCD's L2 serves a
+// contiguous range of samples, i.e. neighbouring tets sharing vertices.  The
+// centroid's cell comes from the vertices' fixed-point grid coordinates (one
+// 8-B gather per vertex, integer sums and a shift, no FP; r01 same-box A/B on
+// C3: 0.197 ms against 0.295 ms from the double coordinates).  Plain store:
+// any sampled tet of the cell is a valid start, the located tet does not
+// depend on the start (unique containing tet, or the canonical min-index tet
+// of a tie, see canonical_tet).
+template <bool PACKED>
+__global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ packed,
+                                                    const TetRec *__restrict__ tets, int64_t ne,
+                                                    int stride, int *__restrict__ grid, GridDesc g,
+                                                    const unsigned long long *__restrict__ xyzq) {
+  const int64_t n = (ne + stride - 1) / stride;
+  const int64_t t = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int64_t k = 1 + t * stride;
+  const int4 v = PACKED ? packed[t] : *reinterpret_cast<const int4 *>(tets + k);
+  if (v.x <= 0) return;
+  const unsigned long long a = xyzq[v.x], b = xyzq[v.y], c = xyzq[v.z], d = xyzq[v.w];
+  const unsigned long long M = (1ull << 21) - 1;
+  int cq[3];
+#pragma unroll
+  for (int ax = 0; ax < 3; ax++) {
+    const int sh = 21 * ax;
+    const unsigned s4 = (unsigned)((a >> sh) & M) + (unsigned)((b >> sh) & M) +
+                        (unsigned)((c >> sh) & M) + (unsigned)((d >> sh) & M);
+    cq[ax] = min((int)(s4 >> (HINT_QF + 2)), g.dim[ax] - 1);
+  }
+  grid[(int64_t)cq[0] + (int64_t)g.dim[0] * ((int64_t)cq[1] + (int64_t)g.dim[1] * cq[2])] = (int)k;
+}
+void launch_hint_build(const int4 *packed, const TetRec *tets, int64_t ne, int stride, int *grid,
+                       GridDesc g, const unsigned long long *xyzq, hipStream_t s) {
+  const int64_t n = (ne + stride - 1) / stride;
+  const int64_t nb = std::max<int64_t>((n + 255) / 256, 1);
+  if (packed)
+    hipLaunchKernelGGL(k_hint_build<true>, dim3((unsigned)nb), dim3(256), 0, s, packed, tets, ne, stride,
+                       grid, g, xyzq);
+  else
+    hipLaunchKernelGGL(k_hint_build<false>, dim3((unsigned)nb), dim3(256), 0, s, packed, tets, ne, stride,
+                       grid, g, xyzq);
+}
+
+// connectivity stream out of the tet records (statistics pass, built on demand)
+__global__ __launch_bounds__(256) void k_tet_conn(const TetRec *__restrict__ src, int64_t n,
+                                                  int4 *__restrict__ dst) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = *reinterpret_cast<const int4 *>(src + i);
+}
+void launch_tet_conn(const TetRec *src, int64_t n, int4 *dst, hipStream_t s) {
   int64_t nb = std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), 16384);
-  hipLaunchKernelGGL(k_tet_conn, dim3((unsigned)nb), dim3(256), 0, s, src, stride, n, dst);
+  hipLaunchKernelGGL(k_tet_conn, dim3((unsigned)nb), dim3(256), 0, s, src, n, dst);
 }
 
 // ---- ties -----------------------------------------------------------------------
@@ -208,7 +130,7 @@ void launch_tet_conn(const TetRec *src, int64_t stride, int64_t n, int4 *dst, hi
 // across a sharper size jump is still a containing tet, only not canonical
 #define TIE_NEAR 1.e-5
 #define TIE_CAP 48
-__device__ __noinline__ int canonical_tet(const TetRec *tets, const Pt4 *pts, int k0, D3 p) {
+__device__ __noinline__ int canonical_tet(const TetRec *tets, const double *xyz, int k0, D3 p) {
   int vis[TIE_CAP], inq[TIE_CAP];
   int nv = 0, nq = 0, head = 0, best = k0;
   vis[nv++] = k0;
@@ -216,7 +138,7 @@ __device__ __noinline__ int canonical_tet(const TetRec *tets, const Pt4 *pts, in
   while (head < nq) {
     int k = inq[head++];
     TetRec t = tets[k];
-    D3 P[4] = {ld3(pts, t.v[0]), ld3(pts, t.v[1]), ld3(pts, t.v[2]), ld3(pts, t.v[3])};
+    D3 P[4] = {ld3(xyz, t.v[0]), ld3(xyz, t.v[1]), ld3(xyz, t.v[2]), ld3(xyz, t.v[3])};
     double lam[4], vol;
     tet_lambda(P, p, lam, &vol);
     for (int f = 0; f < 4; f++) {
@@ -229,7 +151,7 @@ __device__ __noinline__ int canonical_tet(const TetRec *tets, const Pt4 *pts, in
       vis[nv++] = nb;
       TetRec u = tets[nb];
       if (u.v[0] <= 0) continue;
-      D3 Q[4] = {ld3(pts, u.v[0]), ld3(pts, u.v[1]), ld3(pts, u.v[2]), ld3(pts, u.v[3])};
+      D3 Q[4] = {ld3(xyz, u.v[0]), ld3(xyz, u.v[1]), ld3(xyz, u.v[2]), ld3(xyz, u.v[3])};
       double mu[4], vu;
       tet_lambda(Q, p, mu, &vu);
       if (fmin(fmin(mu[0], mu[1]), fmin(mu[2], mu[3])) > -PMX_EPS) {
@@ -242,121 +164,6 @@ __device__ __noinline__ int canonical_tet(const TetRec *tets, const Pt4 *pts, in
   return best;
 }
 
-// ---- volume locate + interpolate ------------------------------------------
-
-__device__ __forceinline__ bool in_ring(const int r[WALK_RING], int k) {
-  bool h = false;
-#pragma unroll
-  for (int i = 0; i < WALK_RING; i++) h |= (r[i] == k);
-  return h;
-}
-
-// Walk statistics: one 4-word record per wavefront (no same-address atomics;
-// reduced on demand by pmx_locate_stats_get).  v0 profile: 4 contended
-// atomics per wave serialised the whole launch.
-__device__ __forceinline__ void wave_stats(uint4 *rec, unsigned cnt, unsigned sum, unsigned mx,
-                                           unsigned mn) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    cnt += __shfl_xor(cnt, o, 64);
-    sum += __shfl_xor(sum, o, 64);
-    unsigned a = __shfl_xor(mx, o, 64), b = __shfl_xor(mn, o, 64);
-    mx = a > mx ? a : mx;
-    mn = b < mn ? b : mn;
-  }
-  if ((threadIdx.x & 63) == 0) *rec = make_uint4(cnt, sum, mx, mn);
-}
-
-// OCC = minimum waves per SIMD requested from the register allocator
-// (1 = unconstrained); selected at run time by pmx_run_opts.tune
-template <int OCC>
-__global__ __launch_bounds__(256, OCC) void k_locate_vol(VolArgs A) {
-  int64_t b = A.xcd_swizzle ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
-  int64_t j = b * blockDim.x + threadIdx.x;
-  unsigned s_cnt = 0, s_sum = 0, s_max = 0, s_min = 0xffffffffu;
-
-  if (j < A.nlist) {
-    const int64_t i = A.list[j];
-    Pt4 qq = A.q[i];
-    D3 p{qq.x, qq.y, qq.z};
-    int cur = hint_lookup(A.grid, A.g, p);
-    if (A.start) A.start[i] = cur;
-    int ring[WALK_RING];
-#pragma unroll
-    for (int r = 0; r < WALK_RING; r++) ring[r] = 0;
-    int step = 0;
-    bool found = false;
-    int v[4];
-    double lam[4];
-    for (;;) {
-      step++;
-      TetRec t = A.tets[cur];
-      if (t.v[0] <= 0) break;                       // !MG_EOK: let the scan decide
-      v[0] = t.v[0]; v[1] = t.v[1]; v[2] = t.v[2]; v[3] = t.v[3];
-      D3 P[4] = {ld3(A.pts, v[0]), ld3(A.pts, v[1]), ld3(A.pts, v[2]), ld3(A.pts, v[3])};
-      double vol;
-      tet_lambda(P, p, lam, &vol);
-      // position of face f in the reference's stable ascending order of the
-      // barycentrics (glibc qsort, src/barycoord_pmmg.c:306) as ranks: no
-      // sorted copy of the doubles is kept live
-      int rk[4];
-      stable_ranks(lam, rk);
-      double lmin = lam[0];
-      lmin = (rk[1] == 0) ? lam[1] : lmin;
-      lmin = (rk[2] == 0) ? lam[2] : lmin;
-      lmin = (rk[3] == 0) ? lam[3] : lmin;
-      if (lmin > -PMX_EPS) { found = true; break; }   // src/barycoord_pmmg.c:102-107
-      if (step >= A.max_walk) break;
-#pragma unroll
-      for (int r = WALK_RING - 1; r > 0; r--) ring[r] = ring[r - 1];
-      ring[0] = cur;
-      // first interior, not recently visited neighbour in ascending-lambda
-      // order (src/locate_pmmg.c:819-833)
-      int next = 0;
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        int f = (rk[0] == r) ? 0 : (rk[1] == r) ? 1 : (rk[2] == r) ? 2 : 3;
-        int nb = sel4(t.nb, f);
-        if (!next && nb && !in_ring(ring, nb)) next = nb;
-      }
-      if (!next) break;
-      cur = next;
-    }
-    if (found) {
-      // a point within the tolerance of a face/edge/vertex is contained by
-      // several tets: take the smallest index among them (start-independent)
-      // (resolved by k_ties: keeps the BFS out of this kernel's registers)
-      double lmn = fmin(fmin(lam[0], lam[1]), fmin(lam[2], lam[3]));
-      if (lmn < TIE_NEAR) {
-        unsigned slot = atomicAdd(A.tie_count, 1u);
-        A.tie_list[slot] = make_int2((int)i, cur);
-        A.steps[i] = step;
-        found = false;
-        step = -1;                                  // neither found nor stuck
-      }
-    }
-    if (found) {
-      A.elem[i] = cur;
-      A.status[i] = 1;
-      A.steps[i] = step;
-      double *out = A.out + i * A.sd.S;
-      unsigned wm = interp_bar<4>(A.sol, A.sd, v, lam, out);
-      A.wmask[i] = (uint8_t)(wm | A.const_bit);
-      s_cnt = 1; s_sum = step; s_max = step; s_min = step;
-    } else if (step >= 0) {
-      unsigned slot = atomicAdd(A.stuck_count, 1u);
-      A.stuck_list[slot] = (int)i;
-      A.found[slot] = 0x7fffffff;
-      A.bestk[slot] = 0x7fffffff;
-      A.best[slot] = ~0ull;
-      A.steps[i] = -step;
-    }
-  }
-  wave_stats(A.wstats + (b * blockDim.x + threadIdx.x) / 64, s_cnt, s_sum, s_max, s_min);
-}
-
-// ---- tie resolution ----------------------------------------------------------
-
 __device__ void d_ties(const VolArgs &A, unsigned bid, unsigned nblk) {
   const unsigned n = *A.tie_count;
   for (unsigned j = bid * blockDim.x + threadIdx.x; j < n; j += nblk * blockDim.x) {
@@ -364,7 +171,7 @@ __device__ void d_ties(const VolArgs &A, unsigned bid, unsigned nblk) {
     const int64_t i = e.x;
     Pt4 qq = A.q[i];
     D3 p{qq.x, qq.y, qq.z};
-    int kc = canonical_tet(A.tets, A.pts, e.y, p);
+    int kc = canonical_tet(A.tets, A.xyz, e.y, p);
     if (kc < 0) {                                   // tie set too large: scan
       unsigned slot = atomicAdd(A.stuck_count, 1u);
       A.stuck_list[slot] = (int)i;
@@ -376,7 +183,7 @@ __device__ void d_ties(const VolArgs &A, unsigned bid, unsigned nblk) {
     }
     TetRec t = A.tets[kc];
     int v[4] = {t.v[0], t.v[1], t.v[2], t.v[3]};
-    D3 P[4] = {ld3(A.pts, v[0]), ld3(A.pts, v[1]), ld3(A.pts, v[2]), ld3(A.pts, v[3])};
+    D3 P[4] = {ld3(A.xyz, v[0]), ld3(A.xyz, v[1]), ld3(A.xyz, v[2]), ld3(A.xyz, v[3])};
     double lam[4], vol;
     tet_lambda(P, p, lam, &vol);
     A.elem[i] = kc;
@@ -406,7 +213,7 @@ __device__ void d_exh_find(const ExhArgs &A, unsigned bid, unsigned nblk) {
          k += (int64_t)nblk * blockDim.x) {
       TetRec t = A.tets[k];
       if (t.v[0] <= 0) continue;
-      D3 P[4] = {ld3(A.pts, t.v[0]), ld3(A.pts, t.v[1]), ld3(A.pts, t.v[2]), ld3(A.pts, t.v[3])};
+      D3 P[4] = {ld3(A.xyz, t.v[0]), ld3(A.xyz, t.v[1]), ld3(A.xyz, t.v[2]), ld3(A.xyz, t.v[3])};
       double lo[3] = {P[0].x, P[0].y, P[0].z}, hi[3] = {P[0].x, P[0].y, P[0].z};
 #pragma unroll
       for (int l = 1; l < 4; l++) {
@@ -450,7 +257,7 @@ __device__ void d_exh_closest(const ExhArgs &A, int pass, unsigned bid, unsigned
          k += (int64_t)nblk * blockDim.x) {
       TetRec t = A.tets[k];
       if (t.v[0] <= 0) continue;
-      D3 P[4] = {ld3(A.pts, t.v[0]), ld3(A.pts, t.v[1]), ld3(A.pts, t.v[2]), ld3(A.pts, t.v[3])};
+      D3 P[4] = {ld3(A.xyz, t.v[0]), ld3(A.xyz, t.v[1]), ld3(A.xyz, t.v[2]), ld3(A.xyz, t.v[3])};
       for (unsigned j = 0; j < m; j++) {
         if (!act[j]) continue;
         double lam[4], vol;
@@ -478,9 +285,14 @@ __device__ void d_exh_finish(const ExhArgs &A, const VolArgs &V, unsigned bid, u
       k = A.bestk[j];
       st = 0;
     }
+    if (k == 0x7fffffff) {                          // no valid tet at all: left untouched
+      V.elem[i] = 0;
+      V.status[i] = 0;
+      continue;
+    }
     TetRec t = A.tets[k];
     int v[4] = {t.v[0], t.v[1], t.v[2], t.v[3]};
-    D3 P[4] = {ld3(A.pts, v[0]), ld3(A.pts, v[1]), ld3(A.pts, v[2]), ld3(A.pts, v[3])};
+    D3 P[4] = {ld3(A.xyz, v[0]), ld3(A.xyz, v[1]), ld3(A.xyz, v[2]), ld3(A.xyz, v[3])};
     if (st) {
       double vol;
       tet_lambda(P, p, phi, &vol);
@@ -508,45 +320,73 @@ __device__ void d_exh_finish(const ExhArgs &A, const VolArgs &V, unsigned bid, u
 // ---- fused fallback -------------------------------------------------------------
 //
 // Ties, exhaustive scan (find, closest value, closest index) and the final
-// interpolation of the scanned points used to be five launches that almost
-// always found nothing to do (~4.5 us each).  One launch of FALLBACK_BLOCKS
-// co-resident workgroups (1 per CU at most; the kernel admits 4) now reads the
+// interpolation of the scanned points in ONE launch (five launches that almost
+// always found nothing to do cost ~4.5 us each).  The launch reads the
 // counters and leaves, or runs the phases separated by a grid barrier
 // (MI355X_MICROARCH.md "barrier-counter": release fence + waitcnt before the
-// arrive, relaxed agent-scope poll, acquire fence after; bounded spin).
-#define FALLBACK_BLOCKS 256
+// arrive, relaxed agent-scope poll, acquire fence after).  Its grid is sized
+// on the host from the occupancy query so that every workgroup is co-resident
+// even beside another context's fallback (fallback_coresident_blocks); should
+// a barrier still time out, the workgroup records PMX_DERR_BARRIER in the
+// step's error word and every later phase is skipped, and the host turns that
+// into a failed call (pmx_synchronize / pmx_download) -- never a silent result.
 
 __device__ __forceinline__ unsigned ld_agent(const unsigned *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ void grid_barrier(unsigned *bar, unsigned target) {
+// false when the wait gave up (the error word is set then)
+__device__ bool grid_barrier(unsigned *bar, unsigned target, unsigned *err, long spin_limit) {
+  __shared__ int s_ok;
   __syncthreads();
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     atomicAdd(bar, 1u);
-    for (long it = 0; ld_agent(bar) < target && it < (1L << 26); it++) __builtin_amdgcn_s_sleep(2);
+    long it = 0;
+    while (ld_agent(bar) < target && ld_agent(err) == 0u && it < spin_limit) {
+      __builtin_amdgcn_s_sleep(2);
+      it++;
+    }
+    const bool ok = ld_agent(bar) >= target && ld_agent(err) == 0u;
+    if (!ok) atomicOr(err, PMX_DERR_BARRIER);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_ok = ok ? 1 : 0;
   }
   __syncthreads();
+  return s_ok != 0;
 }
 
 __global__ __launch_bounds__(256) void k_fallback(ExhArgs E, VolArgs V) {
   const unsigned nb = gridDim.x, b = blockIdx.x;
-  unsigned *bar = V.stuck_count + 4;           // counts[4], zeroed by k_run_init
+  unsigned *bar = V.stuck_count + 4;           // counts[4], zeroed by the prologue
+  unsigned *err = V.stuck_count + PMX_CNT_ERR;
   if (ld_agent(V.tie_count) == 0 && ld_agent(V.stuck_count) == 0) return;
   d_ties(V, b, nb);
-  grid_barrier(bar, nb);
+  if (!grid_barrier(bar, nb, err, E.spin_limit)) return;
   if (ld_agent(V.stuck_count) == 0) return;
   d_exh_find(E, b, nb);
-  grid_barrier(bar, 2 * nb);
+  if (!grid_barrier(bar, 2 * nb, err, E.spin_limit)) return;
   d_exh_closest(E, 0, b, nb);
-  grid_barrier(bar, 3 * nb);
+  if (!grid_barrier(bar, 3 * nb, err, E.spin_limit)) return;
   d_exh_closest(E, 1, b, nb);
-  grid_barrier(bar, 4 * nb);
+  if (!grid_barrier(bar, 4 * nb, err, E.spin_limit)) return;
   d_exh_finish(E, V, b, nb);
+}
+
+int fallback_coresident_blocks(int device, int share) {
+  int cus = 0, per_cu = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(k_fallback),
+                                                   256, 0) != hipSuccess)
+    return 0;
+  const long cap = (long)cus * per_cu / std::max(1, share);
+  return (int)std::min<long>(256, cap);
+}
+
+void launch_exhaustive(const ExhArgs &e, const VolArgs &v, int blocks, hipStream_t s) {
+  hipLaunchKernelGGL(k_fallback, dim3((unsigned)std::max(1, blocks)), dim3(256), 0, s, e, v);
 }
 
 // constant-size metric (MMG3D_Set_constantSize restated): all valid points
@@ -567,85 +407,6 @@ __global__ __launch_bounds__(256) void k_const_metric(const int8_t *__restrict__
     wmask[i] |= (uint8_t)(1u << imet);
   }
 }
-
-// counts[0] volume stuck, [1] surface stuck, [2] surface overflow
-__global__ void k_run_init(unsigned *counts) {
-  if (threadIdx.x < 8) counts[threadIdx.x] = 0;
-}
-void launch_run_init(unsigned *counts, hipStream_t s) {
-  hipLaunchKernelGGL(k_run_init, dim3(1), dim3(64), 0, s, counts);
-}
-
-__global__ __launch_bounds__(256) void k_prologue(uint8_t *wmask, int64_t n, unsigned *counts,
-                                                  int *grid, int64_t gcells, int *tgrid,
-                                                  int64_t tcells) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
-  if (t < 32) counts[t] = 0;
-  const int64_t n16 = n / 16;
-  for (int64_t i = t; i < n16; i += st) reinterpret_cast<uint4 *>(wmask)[i] = make_uint4(0, 0, 0, 0);
-  for (int64_t i = n16 * 16 + t; i < n; i += st) wmask[i] = 0;
-  int *gs[2] = {grid, tgrid};
-  const int64_t cs[2] = {gcells, tcells};
-#pragma unroll
-  for (int k = 0; k < 2; k++) {
-    int *g = gs[k];
-    if (!g) continue;
-    const int64_t g4 = cs[k] / 4;
-    for (int64_t i = t; i < g4; i += st) reinterpret_cast<int4 *>(g)[i] = make_int4(0, 0, 0, 0);
-    for (int64_t i = g4 * 4 + t; i < cs[k]; i += st) g[i] = 0;
-  }
-}
-void launch_prologue(uint8_t *wmask, int64_t n, unsigned *counts, int *grid, int64_t gcells,
-                     int *tgrid, int64_t tcells, hipStream_t s) {
-  int64_t work = std::max<int64_t>(n / 16, std::max<int64_t>(grid ? gcells / 4 : 0, tgrid ? tcells / 4 : 0));
-  int64_t nb = std::min<int64_t>(std::max<int64_t>((work + 255) / 256, 1), 4096);
-  hipLaunchKernelGGL(k_prologue, dim3((unsigned)nb), dim3(256), 0, s, wmask, n, counts, grid, gcells,
-                     tgrid, tcells);
-}
-
-void launch_hint_build(const int4 *tetv, const int4 *packed, const Pt4 *pts, int64_t ne,
-                       int stride, int *grid, GridDesc g, int mid, hipStream_t s,
-                       unsigned long long *grid64, const double *xyz, const float *xyzf,
-                       const unsigned long long *xyzq) {
-  const int64_t n = (ne + stride - 1) / stride;
-  const int64_t nb = std::max<int64_t>((n + 255) / 256, 1);
-  const int4 *src = packed ? packed : tetv + 1;
-  const int64_t sstride = packed ? 1 : stride;
-  if (grid64)
-    hipLaunchKernelGGL((k_hint_build<false, true>), dim3((unsigned)nb), dim3(256), 0, s, src, sstride,
-                       pts, ne, stride, grid, g, grid64, nullptr);
-  else if (xyzq)
-    hipLaunchKernelGGL((k_hint_build<false, false, false, false, true>), dim3((unsigned)nb), dim3(256), 0,
-                       s, src, sstride, pts, ne, stride, grid, g, grid64, nullptr, nullptr, xyzq);
-  else if (xyzf)
-    hipLaunchKernelGGL((k_hint_build<false, false, false, true>), dim3((unsigned)nb), dim3(256), 0, s,
-                       src, sstride, pts, ne, stride, grid, g, grid64, nullptr, xyzf);
-  else if (mid)
-    hipLaunchKernelGGL((k_hint_build<true, false>), dim3((unsigned)nb), dim3(256), 0, s, src, sstride,
-                       pts, ne, stride, grid, g, grid64, nullptr);
-  else if (xyz)
-    hipLaunchKernelGGL((k_hint_build<false, false, true>), dim3((unsigned)nb), dim3(256), 0, s, src,
-                       sstride, pts, ne, stride, grid, g, grid64, xyz);
-  else
-    hipLaunchKernelGGL((k_hint_build<false, false>), dim3((unsigned)nb), dim3(256), 0, s, src, sstride,
-                       pts, ne, stride, grid, g, grid64, nullptr);
-}
-void launch_locate_vol(const VolArgs &a, hipStream_t s) {
-  int64_t nb = (a.nlist + 255) / 256;
-  if (nb < 1) return;
-  switch (a.occ) {
-    case 6: hipLaunchKernelGGL(k_locate_vol<6>, dim3((unsigned)nb), dim3(256), 0, s, a); break;
-    case 8: hipLaunchKernelGGL(k_locate_vol<8>, dim3((unsigned)nb), dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL(k_locate_vol<1>, dim3((unsigned)nb), dim3(256), 0, s, a); break;
-  }
-}
-void launch_exhaustive(const ExhArgs &e, const VolArgs &v, hipStream_t s) {
-  int64_t nb = (e.ne + 255) / 256;
-  if (nb > 2048) nb = 2048;
-  if (nb < 1) nb = 1;
-  (void)nb;
-  hipLaunchKernelGGL(k_fallback, dim3(FALLBACK_BLOCKS), dim3(256), 0, s, e, v);
-}
 void launch_const_metric(const int8_t *kind, int64_t nq, double *out, int S, int off, int size,
                          double hsiz, uint8_t *wmask, int imet, hipStream_t s) {
   int64_t nb = (nq + 255) / 256;
@@ -653,4 +414,24 @@ void launch_const_metric(const int8_t *kind, int64_t nq, double *out, int S, int
   if (nb < 1) return;
   hipLaunchKernelGGL(k_const_metric, dim3((unsigned)nb), dim3(256), 0, s, kind, nq, out, S, off,
                      size, hsiz, wmask, imet);
+}
+
+// zero the write masks, the step's counters and the hint grid (one launch)
+__global__ __launch_bounds__(256) void k_prologue(uint8_t *wmask, int64_t n, unsigned *counts,
+                                                  int *grid, int64_t gcells) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
+  if (t < 32) counts[t] = 0;
+  const int64_t n16 = n / 16;
+  for (int64_t i = t; i < n16; i += st) reinterpret_cast<uint4 *>(wmask)[i] = make_uint4(0, 0, 0, 0);
+  for (int64_t i = n16 * 16 + t; i < n; i += st) wmask[i] = 0;
+  if (!grid) return;
+  const int64_t g4 = gcells / 4;
+  for (int64_t i = t; i < g4; i += st) reinterpret_cast<int4 *>(grid)[i] = make_int4(0, 0, 0, 0);
+  for (int64_t i = g4 * 4 + t; i < gcells; i += st) grid[i] = 0;
+}
+void launch_prologue(uint8_t *wmask, int64_t n, unsigned *counts, int *grid, int64_t gcells,
+                     hipStream_t s) {
+  int64_t work = std::max<int64_t>(n / 16, grid ? gcells / 4 : 0);
+  int64_t nb = std::min<int64_t>(std::max<int64_t>((work + 255) / 256, 1), 4096);
+  hipLaunchKernelGGL(k_prologue, dim3((unsigned)nb), dim3(256), 0, s, wmask, n, counts, grid, gcells);
 }

@@ -91,13 +91,7 @@ struct QualPart {
   long long iel, ne, good, med, his[5];
 };
 
-__device__ __forceinline__ D3 sld3(const StatArgs &A, int i) {
-  if (A.xyz) {
-    const double *r = A.xyz + 3 * (int64_t)i;
-    return D3{r[0], r[1], r[2]};
-  }
-  return ld3(A.pts, i);
-}
+__device__ __forceinline__ D3 sld3(const StatArgs &A, int i) { return ld3(A.xyz, i); }
 
 template <bool ANI>
 __device__ double tet_quality(const StatArgs &A, int64_t k, const TetRec &t) {
@@ -524,11 +518,24 @@ static int stat_blocks(int64_t ne) {
 
 static bool stat_args(pmx_ctx *ctx, StatArgs &A) {
   if (!ctx->have_bg) { ctx->err = "statistics: upload a group first"; return false; }
-  A.pts = ctx->d_pts.p;
-  // vertex gathers from the dense 24-B stream (PMX_STATS_PT4=1: the 32-B
-  // Pt4 records, for A/B)
-  const char *pt4 = getenv("PMX_STATS_PT4");
-  A.xyz = (pt4 && pt4[0] == '1') ? nullptr : ctx->d_xyz.p;
+  // the 16-B connectivity stream of the quality pass, derived from the tet
+  // records on the first statistics call after an upload (the transfer step
+  // itself does not need it)
+  if (!ctx->have_tetv) {
+    if (ctx->d_tetv.cap < (size_t)(ctx->ne + 1)) {
+      if (ctx->d_tetv.p) hipFree(ctx->d_tetv.p);
+      ctx->d_tetv.p = nullptr;
+      ctx->d_tetv.cap = 0;
+      if (hipMalloc((void **)&ctx->d_tetv.p, sizeof(int4) * (size_t)(ctx->ne + 1)) != hipSuccess) {
+        ctx->err = "statistics: hipMalloc tetv";
+        return false;
+      }
+      ctx->d_tetv.cap = (size_t)(ctx->ne + 1);
+    }
+    launch_tet_conn(ctx->d_tets.p, ctx->ne + 1, ctx->d_tetv.p, ctx->stream);
+    ctx->have_tetv = true;
+  }
+  A.xyz = ctx->d_xyz.p;
   A.tets = ctx->d_tets.p;
   A.tetv = ctx->d_tetv.p;
   A.ne = ctx->ne;

@@ -108,26 +108,37 @@ class Transfer:
                                                  imet if arr else -1), "pmx_upload_background")
         self.sizes = [v.size for v in views[: len(arr)]]
 
-    def upload_points(self, xyz: np.ndarray, tags: np.ndarray | None = None):
+    def upload_points(self, xyz: np.ndarray, tags: np.ndarray | None = None,
+                      tets: np.ndarray | None = None):
+        """xyz: (n, 3) new points (0-based list); tags: MMG5_Point.tag values;
+        tets: optional (ne+1, 4) new tets with 0-based point indices in rows
+        1..ne -- only points of valid tets (v[0] >= 0 here) are located."""
         xyz = np.ascontiguousarray(xyz, np.float64)
         pv = N.PointsView()
         pv.first, pv.last = 0, xyz.shape[0] - 1
         pv.c, pv.stride = _dp(xyz), 24
+        self._keep = []
         if tags is not None:
             t = np.ascontiguousarray(tags, np.uint16)
-            self._keep = [t]
+            self._keep.append(t)
             pv.tag, pv.tag_stride = t.ctypes.data_as(N.u16ptr), 2
+        if tets is not None:
+            tv = np.ascontiguousarray(tets, np.int32)
+            self._keep.append(tv)
+            pv.tetra_v, pv.tetra_stride, pv.ne = _ip(tv), 16, tv.shape[0] - 1
         self._chk(self.lib.pmx_upload_points(self.ctx, C.byref(pv)), "pmx_upload_points")
         self.npts = xyz.shape[0]
 
     def run(self, hsiz: float = 0.0, timing: bool = False, max_walk: int = 0, hint_stride: int = 0,
-            tune: int = 0, record_starts: bool = False):
-        """One step.  record_starts: keep every volume point's walk start tet
-        for starts() (diagnostics; the production step does not write it)."""
+            flags: int = 0, record_starts: bool = False):
+        """One step (asynchronous; device-side failures surface in
+        synchronize()/download()).  flags: ``_native.RUN_*``.  record_starts:
+        keep every volume point's walk start tet for starts() (diagnostics;
+        the production step does not write it)."""
         if record_starts:
-            tune |= 0x8000000
+            flags |= N.RUN_RECORD_STARTS
         o = N.RunOpts()
-        o.hsiz, o.timing, o.max_walk, o.hint_stride, o.tune = hsiz, int(timing), max_walk, hint_stride, tune
+        o.hsiz, o.timing, o.max_walk, o.hint_stride, o.flags = hsiz, int(timing), max_walk, hint_stride, flags
         self._chk(self.lib.pmx_run(self.ctx, C.byref(o)), "pmx_run")
 
     def download(self, init: list[np.ndarray] | None = None, into: Result | None = None) -> Result:

@@ -1,0 +1,219 @@
+"""The BASELINE.json configurations on one GPU, against the oracle.
+
+* C2 / C3 at their full benchmark sizes (the meshes bench.py builds): every
+  volume point bit-exact vs the carry-over oracle or a documented tie; a
+  sample of the surface points bit-exact vs the oracle in device semantics;
+  every surface point that differs from the reference's SEQUENTIAL run falls
+  in a documented class (a containing tria, or a shadow wedge/cone acceptance
+  within hausd of the returned edge/vertex).
+* C4 per-GPU share: two ParMmg groups in two contexts whose steps -- and
+  whose fallback grid barriers -- run concurrently on the GPU.
+* C5 per-GPU share (n = 275, 124.8M tets): the statistics counts against the
+  analytic Kuhn-cube counts, and the device partials of two groups reduced
+  across two ranks (gloo) against the oracle on the union.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import bench
+from helpers import bits_equal, compare_exact, compare_volume, lin_field
+from oracle import oracle as O
+from parmmg_amd import mesh as M
+from parmmg_amd.transfer import Transfer
+
+pytestmark = pytest.mark.gpu
+
+
+def _tria_dist_classes(m, x, idx, elem, edge, vert):
+    """Distance of x[i] to the returned edge (edge >= 0) / vertex (vert >= 0)."""
+    out = np.full(len(idx), np.inf)
+    for j, i in enumerate(idx):
+        tr = m.tria[elem[i]]
+        p = x[i]
+        if vert[i] >= 0:
+            out[j] = np.linalg.norm(p - m.xyz[tr[vert[i]]])
+        elif edge[i] >= 0:
+            a, b = m.xyz[tr[(edge[i] + 1) % 3]], m.xyz[tr[(edge[i] + 2) % 3]]
+            ab = b - a
+            s = np.clip(np.dot(p - a, ab) / np.dot(ab, ab), 0.0, 1.0)
+            out[j] = np.linalg.norm(p - (a + s * ab))
+    return out
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("cfg", ["C2", "C3"])
+def test_full_size_parity(cfg):
+    m, x, t, sols = bench.build_case(bench.CONFIGS[cfg], 0)
+    tr = Transfer(0)
+    tr.upload_background(m, sols, 0)
+    tr.upload_points(x, t)
+    tr.run(record_starts=True)
+    r = tr.download()
+    starts = tr.starts()
+    edge, vert = tr.border()
+    tr.close()
+    o = O.Oracle(m)
+    vol = np.nonzero(t == 0)[0]
+    bdy = np.nonzero(t == M.TAG_BDY)[0]
+    # volume: the reference's carry-over walk over the Morton-ordered points
+    outs, elem, st, *_ = o.interp(x, t, sols, imet=0, order=vol)
+    c = compare_volume(o, x, t, (r.sols, r.elem, r.status), (outs, elem, st), sols)
+    print(f"\n{cfg}: {c['nvol']} volume points, {c['same']} identical elements, {c['ties']} ties")
+    assert c["same"] >= c["nvol"] - max(3, c["nvol"] // 1000)
+    assert np.all(r.status[vol] == 1)
+    # surface, device semantics, on a sample (the oracle's per-query flag reset
+    # is O(np))
+    rng = np.random.default_rng(1)
+    sample = np.sort(rng.choice(bdy, min(len(bdy), 600 if cfg == "C2" else 200), replace=False))
+    so, se, ss, _, sed, sve = o.interp(x, t, sols, imet=0, order=sample, fresh=True,
+                                       start_vol=starts, start_bdy=starts)
+    compare_exact((r.sols, r.elem, r.status, edge, vert), (so, se, ss, sed, sve), sample, len(sols))
+    # surface, the reference's sequential run: differences are path classes
+    qo, qe, qs, _, qed, qve = o.interp(x, t, sols, imet=0, order=bdy)
+    diff = bdy[(r.elem[bdy] != qe[bdy]) | (edge[bdy] != qed[bdy]) | (vert[bdy] != qve[bdy])]
+    inside = np.array([edge[i] < 0 and vert[i] < 0 and r.status[i] == 1 and
+                       o.tria_contains(int(r.elem[i]), x[i]) for i in diff], bool)
+    d = _tria_dist_classes(m, x, diff, r.elem, edge, vert)
+    shadow = d <= m.hausd * (1 + 1e-12)
+    print(f"{cfg}: {len(bdy)} surface points, {len(diff)} differ from the sequential run "
+          f"({int(inside.sum())} containing tria, {int(shadow.sum())} wedge/cone within hausd)")
+    assert np.all(inside | shadow), diff[~(inside | shadow)][:10]
+    assert len(diff) <= 0.05 * len(bdy)
+
+
+def l_shaped(n, cut=(0.5, 0.5, 0.5)):
+    m = M.kuhn_cube(n)
+    c = m.centroids()
+    keep = ~np.all(c > np.array(cut), axis=1)
+    tet = np.concatenate([m.tet[:1], m.tet[1:][keep]])
+    return M.from_tets(m.xyz, tet)
+
+
+def test_c4_two_groups_concurrent_fallbacks():
+    """C4's per-GPU share is two groups in two contexts on one GPU.  With the
+    walk capped at one step and non-convex groups, both contexts' fallbacks
+    (tie BFS, exhaustive scan, closest -- phases behind grid barriers) run at
+    the same time; each group must still match the oracle."""
+    rng = np.random.default_rng(17)
+    cases = []
+    for n, cut in ((8, (0.5, 0.5, 0.5)), (9, (0.4, 0.6, 0.3))):
+        m = l_shaped(n, cut)
+        x = rng.uniform(-0.05, 1.05, size=(2500, 3))
+        t = np.zeros(len(x), np.uint16)
+        sols = [M.on_vertices(m, M.shock_metric), M.on_vertices(m, lin_field)]
+        cases.append((m, x, t, sols))
+    trs = [Transfer(0), Transfer(0)]
+    for tr, (m, x, t, sols) in zip(trs, cases):
+        tr.upload_background(m, sols, 0)
+        tr.upload_points(x, t)
+    for _ in range(3):
+        for tr in trs:                  # both steps enqueued before any sync
+            tr.run(max_walk=1)
+        res = [tr.download() for tr in trs]
+        for r, (m, x, t, sols) in zip(res, cases):
+            o = O.Oracle(m)
+            outs, elem, st, *_ = o.interp(x, t, sols, imet=0)
+            assert (r.status == -1).sum() > 500 and (r.status == 0).sum() > 50
+            compare_volume(o, x, t, (r.sols, r.elem, r.status), (outs, elem, st), sols)
+            closest = np.nonzero(st == 0)[0]
+            assert np.array_equal(r.elem[closest], elem[closest])
+    for tr in trs:
+        tr.close()
+
+
+def kuhn_edges(n):
+    """Unique edges of the Kuhn cube: axis edges, one diagonal per square
+    face, one body diagonal per cube."""
+    return 3 * n * (n + 1) ** 2 + 3 * n * n * (n + 1) + n ** 3
+
+
+@pytest.mark.timeout(900)
+def test_c5_share_stats_counts():
+    """C5's per-GPU share (1B tets over 8 GPUs, Kuhn n = 275 = 124.8M tets):
+    element and edge counts are exact against the analytic Kuhn-cube counts."""
+    n = 275
+    m = M.kuhn_cube(n)
+    tr = Transfer(0)
+    tr.upload_background(m, [M.on_vertices(m, M.iso_metric)], 0)
+    q = tr.qualhisto()
+    assert q["ne"] == 6 * n ** 3 and sum(q["his"]) == q["ne"]
+    assert 0 < q["min"] <= q["max"] <= 1.0 + 1e-12
+    L = tr.prilen()
+    assert L["ned"] + L["nullEdge"] == kuhn_edges(n)
+    assert sum(L["hl"]) == L["ned"]
+    tr.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _stats_rank(rank, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    from parmmg_amd import mesh as Mm
+    from parmmg_amd import shard
+    from parmmg_amd.transfer import Transfer as T
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    m = Mm.kuhn_cube(6 + 3 * rank, seed=300 + rank)
+    met = Mm.on_vertices(m, Mm.iso_metric)
+    tr = T(0)
+    tr.upload_background(m, [met], 0)
+    dq = torch.zeros(12, dtype=torch.float64, device="cuda:0")
+    dl = torch.zeros(16, dtype=torch.float64, device="cuda:0")
+    tr.qualhisto_device(dq.data_ptr())
+    tr.prilen_device(dl.data_ptr())
+    tr.synchronize()
+    rq = shard.reduce_qual(dq.cpu(), rank, 0, dist)
+    rl = shard.reduce_len(dl.cpu(), rank, dist)
+    tr.close()
+    q.put((rank, rq, rl))
+    dist.destroy_process_group()
+
+
+def test_c5_device_partials_reduced_across_two_ranks():
+    """Two ranks (one GPU, gloo on CPU tensors) reduce their groups' device
+    partials; the result equals the oracle's statistics of the union."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_stats_rank, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = sorted([q.get(timeout=300) for _ in ps], key=lambda e: e[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, rq0, rl0), (_, rq1, rl1) = out
+    assert rq0 == rq1 and rl0 == rl1
+    qs, ls = [], []
+    for rank in range(2):
+        m = M.kuhn_cube(6 + 3 * rank, seed=300 + rank)
+        met = M.on_vertices(m, M.iso_metric)
+        qo = O.tetra_qual(m)
+        qs.append(O.qualhisto(m, qo))
+        ls.append(O.prilen(m, met))
+    assert rq0["ne"] == qs[0]["ne"] + qs[1]["ne"]
+    assert rq0["his"] == [a + b for a, b in zip(qs[0]["his"], qs[1]["his"])]
+    assert rq0["good"] == qs[0]["good"] + qs[1]["good"] and rq0["med"] == qs[0]["med"] + qs[1]["med"]
+    assert rq0["max"] == max(qs[0]["max"], qs[1]["max"])
+    w = 0 if qs[0]["min"] <= qs[1]["min"] else 1
+    assert rq0["min"] == qs[w]["min"] and rq0["min_rank"] == w and rq0["iel"] == qs[w]["iel"]
+    assert abs(rq0["avg"] - (qs[0]["avg"] + qs[1]["avg"])) <= 1e-12 * abs(rq0["avg"])
+    assert rl0["ned"] == ls[0]["ned"] + ls[1]["ned"]
+    assert sum(abs(a - b - c) for a, b, c in zip(rl0["hl"], ls[0]["hl"], ls[1]["hl"])) <= 4
+    assert abs(rl0["lmin"] - min(ls[0]["lmin"], ls[1]["lmin"])) <= 1e-14 * rl0["lmin"]
+    assert abs(rl0["lmax"] - max(ls[0]["lmax"], ls[1]["lmax"])) <= 1e-14 * rl0["lmax"]

@@ -1,0 +1,240 @@
+"""GPU edge cases of the reference's transfer path, against the oracle.
+
+* MG_NUL new points (``!MG_VOK``): never touched (src/interpmesh_pmmg.c:541).
+* New points referenced by no valid new tet: never visited by the reference's
+  vertex loop over the new tets (:535-541), left untouched here too; a
+  constant-size metric is still written on them (MMG3D_Set_constantSize).
+* Deleted background tets (``v[0] = 0``, !MG_EOK) carving a hole: stuck
+  walks, exhaustive scan, closest element for points in the hole.
+* A singular background metric: ``MMG5_invmat`` fails, the anisotropic
+  interpolation returns 0 and leaves the output untouched (:258-267).
+* Failure handling of the C ABI: a failed upload leaves no usable context,
+  results of an earlier step are refused after new uploads, a fallback grid
+  barrier that gives up makes the step fail instead of returning garbage.
+* The threaded host gathers/scatters (PMX_HOST_THREADS_MIN) give the same
+  bytes as the serial path.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from helpers import bits_equal, compare_volume, cube_case, lin_field
+from oracle import oracle as O
+from parmmg_amd import _native as N
+from parmmg_amd import mesh as M
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(tr, m, x, t, sols, init=None, imet=0, flags=0, tets=None, max_walk=0):
+    tr.upload_background(m, sols, imet)
+    tr.upload_points(x, t, tets)
+    tr.run(flags=flags, max_walk=max_walk)
+    return tr.download(init=init)
+
+
+def test_nul_points_untouched(transfer):
+    m, x, t, sols = cube_case(7, metric="ani")
+    t = t.copy()
+    t[::13] = M.TAG_NUL
+    init = [np.full((len(x), s.shape[1]), -7.0) for s in sols]
+    transfer.upload_background(m, sols, 0)
+    transfer.upload_points(x, t)
+    transfer.run()
+    r = transfer.download(init=init)
+    nul = t == M.TAG_NUL
+    for s in range(len(sols)):
+        assert np.all(r.sols[s][nul] == -7.0)
+    o = O.Oracle(m)
+    outs, elem, st, *_ = o.interp(x, t, sols, imet=0, init=init)
+    vol = t == 0
+    assert np.all(r.elem[nul] == 0)
+    c = compare_volume(o, x, t, (r.sols, r.elem, r.status), (outs, elem, st), sols)
+    assert c["same"] >= c["nvol"] - max(3, c["nvol"] // 1000)
+    assert vol.sum() > 0
+
+
+def test_orphan_points_untouched_and_constant_size(transfer):
+    """Points outside every valid new tet are not located; with -hsiz the
+    constant metric is still set on them."""
+    m, x, t, sols = cube_case(6, metric="iso", surface=False)
+    n = len(x)
+    # new tets over the first 80 % of the points (0-based point indices)
+    rng = np.random.default_rng(4)
+    used = np.zeros(n, bool)
+    used[: int(0.8 * n)] = True
+    pool = np.nonzero(used)[0]
+    ntet = len(pool)
+    tets = np.zeros((ntet + 2, 4), np.int32)
+    tets[1:ntet + 1] = rng.choice(pool, size=(ntet, 4))
+    tets[1:ntet + 1, 0] = pool          # every pooled point in at least one tet
+    orph = np.nonzero(~used)[0]
+    tets[ntet + 1] = [-1, orph[0], orph[1], orph[2]]   # a deleted new tet (!MG_EOK) is ignored
+    init = [np.full((n, s.shape[1]), -7.0) for s in sols]
+    r = _run(transfer, m, x, t, sols, init, tets=tets)
+    ref_t = t.copy()
+    ref_t[~used] = M.TAG_NUL            # the oracle skips them too
+    o = O.Oracle(m)
+    outs, elem, st, *_ = o.interp(x, ref_t, sols, imet=0, init=init)
+    for s in range(len(sols)):
+        assert np.all(r.sols[s][~used] == -7.0)
+    c = compare_volume(o, x, ref_t, (r.sols, r.elem, r.status), (outs, elem, st), sols)
+    assert c["same"] >= c["nvol"] - max(3, c["nvol"] // 1000)
+    # constant size: every valid point gets the metric, orphans included
+    transfer.run(hsiz=0.05)
+    r2 = transfer.download(init=init)
+    assert np.all(r2.sols[0][:, 0] == 0.05)
+    for s in range(1, len(sols)):
+        assert np.all(r2.sols[s][~used] == -7.0)
+
+
+def delete_tets(m, dead):
+    """Mark tets `dead` as deleted (v[0] = 0, the rest of the record kept) and
+    cut the adjacency to and from them: Mmg's state of a hole."""
+    tet = m.tet.copy()
+    adja = m.adja.copy()
+    dead = np.asarray(sorted(set(int(k) for k in dead)))
+    isdead = np.zeros(m.ne + 1, bool)
+    isdead[dead] = True
+    a = adja[1:4 * m.ne + 1].reshape(m.ne, 4)
+    a[isdead[1:]] = 0
+    nb = a // 4
+    a[isdead[nb] & (nb > 0)] = 0
+    tet[dead, 0] = 0
+    return M.Mesh(m.xyz, tet, adja, m.tria, m.adjt, m.hausd)
+
+
+def test_deleted_background_tets(transfer):
+    m = M.kuhn_cube(8)
+    c = m.centroids()
+    hole = 1 + np.nonzero(np.linalg.norm(c - np.array([0.6, 0.45, 0.5]), axis=1) < 0.17)[0]
+    hole = hole[hole > 1]
+    md = delete_tets(m, hole)
+    rng = np.random.default_rng(9)
+    x = rng.uniform(0.02, 0.98, size=(3000, 3))
+    t = np.zeros(len(x), np.uint16)
+    sols = [M.on_vertices(md, M.shock_metric), M.on_vertices(md, lin_field)]
+    r = _run(transfer, md, x, t, sols)
+    o = O.Oracle(md)
+    outs, elem, st, *_ = o.interp(x, t, sols, imet=0)
+    assert (st == 0).sum() > 20, "points in the hole must fall back to the closest tet"
+    assert np.all(md.tet[r.elem, 0] > 0), "a deleted tet was returned"
+    cmp = compare_volume(o, x, t, (r.sols, r.elem, r.status), (outs, elem, st), sols)
+    closest = np.nonzero(st == 0)[0]
+    assert np.array_equal(r.elem[closest], elem[closest])
+    assert cmp["ties"] <= 5
+
+
+def test_singular_metric_leaves_output_untouched(transfer):
+    m, x, t, sols = cube_case(6, metric="ani", surface=False, fields=False)
+    met = sols[0].copy()
+    # vertices with a singular, non-diagonal metric: MMG5_invmat fails
+    bad = np.arange(1, m.np + 1, 17)
+    met[bad] = [1.0, 1.0, 0.0, 1.0, 0.0, 1.0]
+    sols = [met, M.on_vertices(m, lin_field)]
+    init = [np.full((len(x), s.shape[1]), -7.0) for s in sols]
+    r = _run(transfer, m, x, t, sols, init)
+    o = O.Oracle(m)
+    outs, elem, st, *_ = o.interp(x, t, sols, imet=0, init=init)
+    untouched = np.all(r.sols[0] == -7.0, axis=1)
+    assert untouched.sum() > 50, "some points must touch a singular vertex"
+    # the linear field is interpolated regardless
+    assert np.abs(r.sols[1][:, 0] - lin_field(x)[:, 0]).max() < 1e-12
+    cmp = compare_volume(o, x, t, (r.sols, r.elem, r.status), (outs, elem, st), sols)
+    assert cmp["same"] >= cmp["nvol"] - max(3, cmp["nvol"] // 1000)
+    same = r.elem == elem
+    assert np.array_equal(untouched[same], np.all(outs[0][same] == -7.0, axis=1))
+
+
+def test_failed_upload_leaves_no_usable_context(transfer):
+    """a good upload then a bad one must not leave sizes that
+    disagree with the device buffers -- the next step is refused cleanly."""
+    m, x, t, sols = cube_case(5, metric="iso")
+    transfer.upload_background(m, sols, 0)
+    transfer.upload_points(x, t)
+    transfer.run()
+    big = M.kuhn_cube(9)
+    bad = M.Mesh(big.xyz, big.tet.copy(), big.adja, big.tria, big.adjt)
+    bad.tet[3, 2] = big.np + 5                      # vertex index out of range
+    with pytest.raises(RuntimeError, match="out of range"):
+        transfer.upload_background(bad, [M.on_vertices(big, M.iso_metric)], 0)
+    with pytest.raises(RuntimeError, match="upload background"):
+        transfer.run()
+    with pytest.raises(RuntimeError):
+        transfer.download()
+    # a good upload makes the context usable again
+    r = _run(transfer, m, x, t, sols)
+    assert np.all(r.status != 0)
+
+
+def test_stale_results_refused_after_new_points(transfer):
+    """results of a step are not downloadable once the points or
+    the background changed (sizes would disagree)."""
+    m, x, t, sols = cube_case(5, metric="iso")
+    transfer.upload_background(m, sols, 0)
+    transfer.upload_points(x[:10], t[:10])
+    transfer.run()
+    transfer.upload_points(x, t)                    # more points, no step yet
+    with pytest.raises(RuntimeError, match="no step has run"):
+        transfer.download()
+    transfer.run()
+    r = transfer.download()
+    assert len(r.elem) == len(x) and np.all(r.status != 0)
+
+
+def test_fallback_barrier_timeout_fails_loudly(transfer):
+    """The fused fallback's grid barrier reports a timeout instead of
+    proceeding: with the debug hook the barriers do not wait, and the step
+    must fail (pmx_synchronize / pmx_download return 0)."""
+    m, x, t, sols = cube_case(6, metric="ani", surface=False)
+    transfer.upload_background(m, sols, 0)
+    transfer.upload_points(x, t)
+    transfer.run(max_walk=1, flags=N.RUN_DEBUG_BARRIER_TIMEOUT)   # stuck points: the fallback runs
+    with pytest.raises(RuntimeError, match="grid barrier"):
+        transfer.synchronize()
+    with pytest.raises(RuntimeError, match="grid barrier"):
+        transfer.download()
+    # the next normal step is fine
+    transfer.run(max_walk=1)
+    r = transfer.download()
+    o = O.Oracle(m)
+    outs, elem, st, *_ = o.interp(x, t, sols, imet=0)
+    compare_volume(o, x, t, (r.sols, r.elem, r.status), (outs, elem, st), sols)
+
+
+_THREADED = r"""
+import sys, numpy as np
+sys.path.insert(0, {root!r})
+sys.path.insert(0, {tests!r})
+from helpers import cube_case
+from parmmg_amd.transfer import Transfer
+m, x, t, sols = cube_case(12, metric="ani")
+tr = Transfer(0)
+tr.upload_background(m, sols, 0)
+tr.upload_points(x, t)
+tr.run()
+r = tr.download()
+np.savez({out!r}, elem=r.elem, status=r.status, steps=r.steps, *[s for s in r.sols])
+"""
+
+
+def test_threaded_host_paths_bit_identical(tmp_path):
+    """The host gathers/scatters split over threads (forced on a small case
+    with PMX_HOST_THREADS_MIN=1) give the bytes of the serial path."""
+    outs = []
+    for mode, env in (("serial", {"PMX_HOST_THREADS": "1"}),
+                      ("threaded", {"PMX_HOST_THREADS": "8", "PMX_HOST_THREADS_MIN": "1"})):
+        out = str(tmp_path / f"{mode}.npz")
+        code = _THREADED.format(root=ROOT, tests=os.path.join(ROOT, "tests"), out=out)
+        e = dict(os.environ, **env)
+        p = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True,
+                           timeout=300)
+        assert p.returncode == 0, p.stdout + p.stderr
+        outs.append(np.load(out))
+    a, b = outs
+    for k in a.files:
+        assert np.array_equal(a[k].view(np.uint8), b[k].view(np.uint8)), k

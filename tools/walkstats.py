@@ -2,7 +2,7 @@
 """Walk diagnostics on a bench config (GPU): histogram of walk steps, distance
 from the hint start, ties / stuck counts.
 
-  python tools/walkstats.py --config C2 [--tune T] [--hint-stride S]
+  python tools/walkstats.py --config C2 [--flags F] [--hint-stride S]
 """
 import argparse
 import json
@@ -18,7 +18,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C2")
-    ap.add_argument("--tune", type=int, default=0)
+    ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--hint-stride", type=int, default=0)
     args = ap.parse_args()
     import bench
@@ -31,7 +31,7 @@ def main():
     tr = Transfer(0)
     tr.upload_background(m, sols, 0)
     tr.upload_points(x, t)
-    tr.run(tune=args.tune, hint_stride=args.hint_stride, record_starts=True)
+    tr.run(flags=args.flags, hint_stride=args.hint_stride, record_starts=True)
     r = tr.download()
     st = tr.starts()
     vol = t == 0

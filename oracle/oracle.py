@@ -111,7 +111,9 @@ class Oracle:
         od = np.ascontiguousarray(order, np.int64) if order is not None else None
         sv = np.ascontiguousarray(start_vol, np.int32) if start_vol is not None else None
         sb = np.ascontiguousarray(start_bdy, np.int32) if start_bdy is not None else None
-        self.lib.orc_interp_points(self.ctx, n, _p(xyz), _p(tags), _p(od), len(sols), _p(sizes),
+        # order: the points to process, in that order (a subset is allowed)
+        cnt = len(od) if od is not None else n
+        self.lib.orc_interp_points(self.ctx, cnt, _p(xyz), _p(tags), _p(od), len(sols), _p(sizes),
                                    oldp, newp, imet if sols else -1, _p(sv), _p(sb), int(fresh),
                                    _p(elem), _p(status), _p(steps), _p(edge), _p(vertex))
         return outs, elem, status, steps, edge, vertex

@@ -50,8 +50,9 @@ def build_dropin_demo() -> str:
     library (plain C, as ParMmg's own sources would be)."""
     import subprocess
     os.makedirs(os.path.dirname(DEMO_BIN), exist_ok=True)
+    deps = [DEMO_SRC, os.path.join(ROOT, "include", "pmx_transfer.h"), _native.LIB_PATH]
     if (not os.path.exists(DEMO_BIN)
-            or os.path.getmtime(DEMO_BIN) < os.path.getmtime(DEMO_SRC)):
+            or any(os.path.getmtime(DEMO_BIN) < os.path.getmtime(d) for d in deps if os.path.exists(d))):
         subprocess.run(["gcc", "-O2", "-Wall", "-Werror", "-std=c99", "-I",
                         os.path.join(ROOT, "include"), DEMO_SRC, "-o", DEMO_BIN, "-L",
                         os.path.dirname(_native.LIB_PATH), "-lpmx_transfer",

@@ -613,14 +613,17 @@ __device__ int tria_hint(const BdyArgs &A, D3 p) {
 #define OVF_CAP 2048
 #define OVF_THREADS (64 * 64)
 
-// the coarser tria hint grid over the background bbox (about 2 trias per
-// cell in each direction of the surface)
+// the coarser tria hint grid over the background bbox: cells of about 8
+// boundary trias.  The grid is 3-D but only its surface cells are used, so it
+// is zeroed and rebuilt every step for mostly empty cells; at 2 trias per
+// cell it was a 66-MB memset per C3 step beside the volume walk (r02 profile),
+// at 8 it is 8.4 MB (surface walks of ~1 more step, latency on the side stream)
 bool pmx_ctx::size_tria_grid() {
   double ext[3];
   int64_t cells = 1;
   for (int ax = 0; ax < 3; ax++) ext[ax] = std::max(bbhi[ax] - bblo[ax], 1e-300);
   const double area = 2.0 * (ext[0] * ext[1] + ext[1] * ext[2] + ext[0] * ext[2]);
-  const double h = std::sqrt(area / std::max(1.0, (double)nt / 2.0));
+  const double h = std::sqrt(area / std::max(1.0, (double)nt / 8.0));
   for (int ax = 0; ax < 3; ax++) {
     // 1e-9 slack: libm cbrt/sqrt are not correctly rounded and a cell count
     // of exactly n must not become n+1 (misaligned with a lattice-like mesh)
@@ -644,8 +647,6 @@ bool pmx_ctx::size_tria_grid() {
 
 bool pmx_ctx::launch_bdy(const VolArgs &a, hipStream_t s) {
   if (nt < 1) { err = "surface points present but the background has no boundary trias"; return false; }
-  // tria hint grid: a coarser grid over the same bbox (about 2 trias / cell
-  // in each direction of the surface)
   if (!d_blist.p || d_blist.cap < (size_t)nq) {
     if (d_blist.p) hipFree(d_blist.p);
     if (hipMalloc((void **)&d_blist.p, sizeof(int) * (size_t)std::max<int64_t>(nq, 1)) != hipSuccess) { err = "hipMalloc blist"; return false; }

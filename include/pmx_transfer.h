@@ -217,12 +217,37 @@ int PMX_copyMetricsAndFields_point(pmx_ctx *ctx, pmx_group *grp,
                                    const int *permNodGlob, int renum, int inputMet);
 
 /* ---- statistics ---------------------------------------------------------- */
+/* Reference: PMMG_tetraQual / PMMG_qualhisto / PMMG_prilen (src/parmmg.h:564-566,
+ * def src/quality_pmmg.c:156-733).  The per-element arithmetic is Mmg's,
+ * restated (MMG5_caltet_iso / caltet33_ani, MMG5_lenEdg*; unpinned). */
+#define PMX_INQUA  0          /* PMMG_INQUA : before the remesh                */
+#define PMX_OUTQUA 1          /* PMMG_OUTQUA: after it (counts nrid, below)    */
+#define PMX_TAG_GEO    2      /* MG_GEO  */
+#define PMX_TAG_PARBDY 8192   /* MG_PARBDY */
+
+/* Per-group partials as written to device memory by the *_device functions:
+ * plain 8-byte fields, no padding (all-gathered as int64 words). */
+typedef struct {
+  double  avg, max, min;       /* alpha*q: SUM, max, min                     */
+  int64_t iel, ne, np, good, med, nrid;
+  int64_t his[5];
+  int64_t iel_grp;             /* filled by the host fold                    */
+} pmx_qual_part;               /* 15 x 8 B */
+typedef struct {
+  double  avlen, lmin, lmax;   /* avlen is the SUM over edges                */
+  int64_t amin, bmin, amax, bmax, ned, nullEdge;
+  int64_t hl[9];
+} pmx_len_part;                /* 18 x 8 B */
+
+/* Results (one group, or reduced over groups and ranks). */
 typedef struct {
   int64_t ne, np;
   double  max, min, avg;       /* alpha*q, avg is the SUM (reference avg_cur) */
-  int64_t iel;                 /* element realising min (1-based)            */
+  int64_t iel;                 /* element realising min (1-based, in its group) */
   int64_t good, med;
   int64_t his[5];
+  int64_t nrid;                /* OUTQUA: tets whose 4 vertices are ridge points */
+  int     iel_grp, cpu;        /* group and rank of iel                      */
 } pmx_qual_stats;
 
 typedef struct {
@@ -230,27 +255,89 @@ typedef struct {
   double  avlen, lmin, lmax;   /* avlen is the SUM over edges                */
   int64_t amin, bmin, amax, bmax;
   int64_t hl[9];
+  int     cpu_min, cpu_max;
 } pmx_len_stats;
+
+/* Point tags of the uploaded background (MMG5_Point.tag through a stride):
+ * ridge points for the length loop's filter (src/quality_pmmg.c:509-517) and
+ * OUTQUA's nrid.  NULL: no tags.  Kept until the next background upload. */
+int pmx_upload_point_tags(pmx_ctx *ctx, const uint16_t *tag, int64_t tag_stride);
 
 /* Quality of every background tet in the uploaded metric (MMG3D_tetraQual).
  * Result stays on the device; qual (ne+1 doubles) may be NULL. */
 int pmx_tetra_qual(pmx_ctx *ctx, double *qual);
-/* PMMG_qualhisto on the uploaded group (per-group part, before the reduce). */
-int pmx_qualhisto(pmx_ctx *ctx, pmx_qual_stats *st);
-/* PMMG_prilen / MMG3D_computePrilen on the uploaded group.  point_tag may be
- * NULL (no ridges).  metRidTyp as in the reference. */
-int pmx_prilen(pmx_ctx *ctx, const uint16_t *point_tag, int64_t tag_stride,
-               int metRidTyp, pmx_len_stats *st);
 
-/* Device-resident variants for the multi-GPU reduction (RCCL all-reduce of the
- * partials, see parmmg_amd/shard.py): the per-group partial is written, on the
- * context stream, to dev_result (device memory):
- *   qualhisto: 12 x 8 B = {double avg,max,min; int64 iel,ne,good,med,his[5]}
- *   prilen:    16 x 8 B = {double avlen,lmin,lmax; int64 kmin,kmax,ned,
- *                          nullEdge,hl[9]}  (k = 6*tet+edge of first occurrence)
- * dev_tag: device uint16 point tags (np+1) or NULL. */
-int pmx_qualhisto_device(pmx_ctx *ctx, int use_stored, void *dev_result);
-int pmx_prilen_device(pmx_ctx *ctx, const uint16_t *dev_tag, void *dev_result);
+/* PMMG_count_nodes_par (src/quality_pmmg.c:33-80) for the uploaded group:
+ * the group's points in the internal node communicator (idx_ip[i] -> slot
+ * idx_comm[i], nitem_grp entries) count when they claim their slot
+ * (intvalues[slot] == 0 -> base; intvalues is the rank's array of nitem
+ * slots, in/out, pre-marked by the caller for nodes a higher rank counts,
+ * :196-209); every other point counts when a valid tet touches it.  The
+ * count is the group's np in the next qualhisto partial. */
+int pmx_count_nodes(pmx_ctx *ctx, const int *idx_ip, const int *idx_comm, int64_t nitem_grp,
+                    int *intvalues, int64_t nitem, int base, int64_t *np);
+
+/* The per-group part of PMMG_qualhisto (src/quality_pmmg.c:216-261) on the
+ * uploaded group: opt PMX_INQUA / PMX_OUTQUA; use_stored: the qualities of the
+ * last pmx_tetra_qual.  Partial written to dev_result (pmx_qual_part, device
+ * memory) on the context stream. */
+int pmx_qualhisto_device(pmx_ctx *ctx, int opt, int use_stored, void *dev_result);
+int pmx_qualhisto(pmx_ctx *ctx, int opt, pmx_qual_stats *st);
+
+/* Parallel (interface) edges of the group for the distributed PMMG_prilen
+ * (src/quality_pmmg.c:398-502): edge i joins a[i] -> b[i] (mesh->edge
+ * orientation) and is owned by rank owner[i] (the lowest rank sharing it).
+ * The owned edges are measured first, in list order, each once; the rank's
+ * tet loop then measures every other edge -- the non-owned parallel edges
+ * too, as the reference does (its warning at :585-586: interface edges are
+ * counted by every rank holding them) unless exact_once is set. */
+typedef struct {
+  int64_t         n;
+  const int      *a, *b, *owner;
+  int             myrank;
+  int             exact_once;
+} pmx_par_edges;
+
+/* PMMG_prilen on the uploaded group: centralized (par == NULL, the
+ * MMG3D_computePrilen branch) or distributed (PMMG_computePrilen).  Tets whose
+ * 4 vertices are ridge points (pmx_upload_point_tags) are skipped.  metRidTyp:
+ * classic metric storage only (size 1, or 6 on every point). */
+int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, void *dev_result);
+int pmx_prilen(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, pmx_len_stats *st);
+
+/* PMMG_tetraQual on the NEW mesh right after the interpolation
+ * (src/libparmmg1.c:845): the new tets (1-based records through a stride,
+ * vertex indices in the last points view's numbering) are uploaded; the
+ * coordinates and the interpolated metric are the step's device-resident
+ * points and results.  qual (ne+1 doubles, host) and/or dev_result (the
+ * qualhisto partial of the new mesh, opt as above; np = the points) may be
+ * NULL.  Needs a pmx_run on those points. */
+int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, int64_t ne, int opt,
+                      double *qual, void *dev_result);
+
+/* The reduction across groups and ranks (the reference's MPI_Reduce with its
+ * custom operators, src/quality_pmmg.c:82-144, :265-307, :661-676), as host
+ * folds in (rank, group) order -- deterministic; ties go to the first:
+ *   pmx_qual_fold: parts[i] of rank[i] (nondecreasing; NULL = one group per
+ *     rank), groups folded as PMMG_qualhisto's loop, then ranks;
+ *   pmx_len_fold:  one part per rank, with the reference's operator
+ *     (a smaller lmin also takes the other rank's amax/bmax, :125-131). */
+int pmx_qual_fold(const pmx_qual_part *parts, const int *rank, int n, pmx_qual_stats *out);
+int pmx_len_fold(const pmx_len_part *parts, int n, pmx_len_stats *out);
+
+/* RCCL: one all-gather of the ranks' device partials on the context stream,
+ * then the fold.  comm is an ncclComm_t (void *): pmx_comm_unique_id on one
+ * rank (broadcast the bytes, e.g. MPI_Bcast on parmesh->comm), pmx_comm_init
+ * on every rank. */
+int pmx_comm_unique_id(char *id, int len);
+int pmx_comm_init(pmx_ctx *ctx, void **comm, int nranks, const char *id, int rank);
+int pmx_comm_destroy(void *comm);
+/* dev_parts: this rank's ngrp group partials (pmx_qual_part, contiguous in
+ * device memory), merged on the host before the all-gather. */
+int pmx_qualhisto_allreduce(pmx_ctx *ctx, void *comm, int nranks, const void *dev_parts, int ngrp,
+                            pmx_qual_stats *out);
+int pmx_prilen_allreduce(pmx_ctx *ctx, void *comm, int nranks, const void *dev_part,
+                         pmx_len_stats *out);
 
 #ifdef __cplusplus
 }

@@ -21,7 +21,7 @@ vp, i64 = C.c_void_p, C.c_int64
 
 class QualStats(C.Structure):
     _fields_ = [("ne", i64), ("max", C.c_double), ("min", C.c_double), ("avg", C.c_double),
-                ("iel", i64), ("good", i64), ("med", i64), ("his", i64 * 5)]
+                ("iel", i64), ("good", i64), ("med", i64), ("his", i64 * 5), ("nrid", i64)]
 
 
 class LenStats(C.Structure):
@@ -53,8 +53,12 @@ def load():
         lib.orc_constant_size.argtypes = [i64, C.c_int, C.c_double, vp]
         lib.orc_tetra_qual.argtypes = [i64, vp, vp, vp, C.c_int, vp]
         lib.orc_qualhisto.argtypes = [i64, vp, vp, C.POINTER(QualStats)]
+        lib.orc_qualhisto_tags.argtypes = [i64, vp, vp, vp, C.POINTER(QualStats)]
         lib.orc_prilen.restype = C.c_int
         lib.orc_prilen.argtypes = [i64, i64, vp, vp, vp, C.c_int, C.POINTER(LenStats)]
+        lib.orc_prilen_dist.restype = C.c_int
+        lib.orc_prilen_dist.argtypes = [i64, i64, vp, vp, vp, C.c_int, vp, i64, vp, vp, vp, C.c_int,
+                                        C.c_int, C.POINTER(LenStats)]
         _lib = lib
     return _lib
 
@@ -136,20 +140,55 @@ def tetra_qual(mesh, met=None):
     return q
 
 
-def qualhisto(mesh, qual):
+def qualhisto(mesh, qual, tags=None):
+    """MMG3D_computeInqua statistics; with point tags, MMG3D_computeOutqua's nrid."""
     lib = load()
     st = QualStats()
-    lib.orc_qualhisto(mesh.ne, _p(mesh.tet), _p(np.ascontiguousarray(qual)), C.byref(st))
+    t = None if tags is None else np.ascontiguousarray(tags, np.uint16)
+    lib.orc_qualhisto_tags(mesh.ne, _p(mesh.tet), _p(np.ascontiguousarray(qual)), _p(t), C.byref(st))
     d = {f: getattr(st, f) for f, _ in QualStats._fields_}
     d["his"] = list(st.his)
     return d
 
 
-def prilen(mesh, met):
+def prilen(mesh, met, tags=None, par=None):
+    """PMMG_prilen: centralized (par None) or PMMG_computePrilen with parallel
+    edges par = {"a", "b", "owner", "myrank", "exact_once"}."""
     lib = load()
     st = LenStats()
     m = np.ascontiguousarray(met, np.float64)
-    lib.orc_prilen(mesh.np, mesh.ne, _p(mesh.xyz), _p(mesh.tet), _p(m), m.shape[1], C.byref(st))
+    t = None if tags is None else np.ascontiguousarray(tags, np.uint16)
+    if par is None:
+        pa = pb = po = None
+        npar, myrank, once = 0, 0, 0
+    else:
+        pa = np.ascontiguousarray(par["a"], np.int32)
+        pb = np.ascontiguousarray(par["b"], np.int32)
+        po = np.ascontiguousarray(par["owner"], np.int32)
+        npar, myrank, once = len(pa), int(par.get("myrank", 0)), int(par.get("exact_once", 0))
+    lib.orc_prilen_dist(mesh.np, mesh.ne, _p(mesh.xyz), _p(mesh.tet), _p(m), m.shape[1], _p(t), npar,
+                        _p(pa), _p(pb), _p(po), myrank, once, C.byref(st))
     d = {f: getattr(st, f) for f, _ in LenStats._fields_}
     d["hl"] = list(st.hl)
     return d
+
+
+def count_nodes(mesh, idx_ip, idx_comm, intvalues, base=1):
+    """PMMG_count_nodes_par (reference src/quality_pmmg.c:33-80), restated in
+    Python for small cases: intvalues updated in place; returns np."""
+    flag = np.zeros(mesh.np + 1, bool)
+    n = 0
+    for ip, idx in zip(idx_ip, idx_comm):
+        if not intvalues[idx]:
+            intvalues[idx] = base
+            n += 1
+        flag[ip] = True
+    for k in range(1, mesh.ne + 1):
+        v = mesh.tet[k]
+        if v[0] <= 0:
+            continue
+        for ip in v:
+            if not flag[ip]:
+                flag[ip] = True
+                n += 1
+    return n

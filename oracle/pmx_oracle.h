@@ -91,13 +91,17 @@ typedef struct {
   int64_t iel;           /* first element realising min (1-based) */
   int64_t good, med;
   int64_t his[5];
+  int64_t nrid;          /* OUTQUA: elements with 4 ridge vertices */
 } orc_qualstats;
 
 /* per-tet quality (MMG3D_tetraQual -> MMG5_caltet_iso / caltet33_ani) */
 void orc_tetra_qual(int64_t ne, const double *xyz, const int *tet,
                     const double *met, int msize, double *qual /* ne+1 */);
-/* histogram of MMG3D_computeInqua-style statistics over qual[1..ne] */
+/* histogram of MMG3D_computeInqua-style statistics over qual[1..ne]; with
+ * point tags (np+1, or NULL), MMG3D_computeOutqua's nrid */
 void orc_qualhisto(int64_t ne, const int *tet, const double *qual, orc_qualstats *st);
+void orc_qualhisto_tags(int64_t ne, const int *tet, const double *qual, const uint16_t *tag,
+                        orc_qualstats *st);
 
 typedef struct {
   int64_t ned, nullEdge;
@@ -108,6 +112,15 @@ typedef struct {
 /* unique-edge length histogram (MMG3D_computePrilen, centralized) */
 int orc_prilen(int64_t np, int64_t ne, const double *xyz, const int *tet,
                const double *met, int msize, orc_lenstats *st);
+/* PMMG_computePrilen (src/quality_pmmg.c:370-574): point tags (np+1 or NULL:
+ * tets with 4 ridge vertices skipped, :509-517) and npar parallel edges
+ * pa[i] -> pb[i] owned by rank powner[i]: owned ones first in list order,
+ * then every other edge in (k, ia) order; exact_once: the non-owned parallel
+ * edges are not counted (the reference counts them, its warning :585-586). */
+int orc_prilen_dist(int64_t np, int64_t ne, const double *xyz, const int *tet,
+                    const double *met, int msize, const uint16_t *tag, int64_t npar,
+                    const int *pa, const int *pb, const int *powner, int myrank, int exact_once,
+                    orc_lenstats *st);
 
 #ifdef __cplusplus
 }

@@ -97,6 +97,27 @@ void orc_tetra_qual(int64_t ne, const double *xyz, const int *tet, const double 
   }
 }
 
+/* a non-singular ridge point: !(MG_SIN || MG_NOM) && MG_GEO (MG_SIN = CRN|REQ) */
+static int ridge_pt(unsigned tg) {
+  int sin = (tg & TAG_CRN) || (tg & TAG_REQ);
+  return !(sin || (TAG_NOM & tg)) && (tg & TAG_GEO);
+}
+static int tet_4ridge(const int *v, const uint16_t *tag) {
+  int i;
+  if (!tag) return 0;
+  for (i = 0; i < 4; i++)
+    if (!ridge_pt(tag[v[i]])) return 0;
+  return 1;
+}
+
+void orc_qualhisto_tags(int64_t ne, const int *tet, const double *qual, const uint16_t *tag,
+                        orc_qualstats *st) {
+  int64_t k;
+  orc_qualhisto(ne, tet, qual, st);
+  for (k = 1; k <= ne; k++)
+    if (tet[4*k] > 0 && tet_4ridge(&tet[4*k], tag)) st->nrid++;
+}
+
 void orc_qualhisto(int64_t ne, const int *tet, const double *qual, orc_qualstats *st) {
   int64_t k;
   int i;
@@ -123,8 +144,6 @@ void orc_qualhisto(int64_t ne, const int *tet, const double *qual, orc_qualstats
 
 /* ---- edge lengths -------------------------------------------------------- */
 
-typedef struct { int a, b; int used; } hedge;
-
 static uint64_t hkey(int a, int b) { return ((uint64_t)(uint32_t)a << 32) | (uint32_t)b; }
 
 static double len_iso(const double *xyz, const double *met, int p1, int p2) {
@@ -145,50 +164,91 @@ static double len_ani(const double *xyz, const double *met, int p1, int p2) {
   return (sqrt(dd1) + sqrt(dd2) + 4.0*sqrt(0.5*(dd1 + dd2))) / 6.0;
 }
 
-int orc_prilen(int64_t np, int64_t ne, const double *xyz, const int *tet, const double *met,
-               int msize, orc_lenstats *st) {
+/* open-addressing set of unordered edges (key = min << 32 | max) */
+typedef struct { uint64_t cap, mask, *tab; uint8_t *popped; } eset;
+static int eset_init(eset *e, int64_t nmax) {
+  e->cap = 1;
+  while (e->cap < (uint64_t)(2 * nmax + 16)) e->cap <<= 1;
+  e->mask = e->cap - 1;
+  e->tab = (uint64_t *)calloc(e->cap, sizeof(uint64_t));
+  e->popped = (uint8_t *)calloc(e->cap, 1);
+  return e->tab && e->popped;
+}
+static void eset_free(eset *e) { free(e->tab); free(e->popped); }
+/* slot of the edge (inserted if absent and ins); -1 if absent */
+static int64_t eset_slot(eset *e, int a, int b, int ins) {
+  int lo = a < b ? a : b, hi = a < b ? b : a;
+  uint64_t key = hkey(lo, hi), h = (key * 0x9e3779b97f4a7c15ULL) >> 20;
+  while (e->tab[h & e->mask] && e->tab[h & e->mask] != key) h++;
+  if (!e->tab[h & e->mask]) {
+    if (!ins) return -1;
+    e->tab[h & e->mask] = key;
+  }
+  return (int64_t)(h & e->mask);
+}
+
+static void len_count(orc_lenstats *st, double len, int np_, int nq_) {
   static const double bd[9] = {0.0, 0.3, 0.6, 0.7071, 0.9, 1.3, 1.4142, 2.0, 5.0};
-  /* open-addressing set of unordered edges */
-  uint64_t cap = 1, mask, *tab;
-  uint8_t *popped;
-  int64_t k;
+  int i;
+  if (!len) { st->nullEdge++; return; }
+  st->avlen += len;
+  st->ned++;
+  if (len < st->lmin) { st->lmin = len; st->amin = np_; st->bmin = nq_; }
+  if (len > st->lmax) { st->lmax = len; st->amax = np_; st->bmax = nq_; }
+  for (i = 0; i < 8; i++)
+    if (bd[i] <= len && len < bd[i+1]) { st->hl[i]++; break; }
+  if (i == 8) st->hl[8]++;
+}
+
+int orc_prilen_dist(int64_t np, int64_t ne, const double *xyz, const int *tet,
+                    const double *met, int msize, const uint16_t *tag, int64_t npar,
+                    const int *pa, const int *pb, const int *powner, int myrank, int exact_once,
+                    orc_lenstats *st) {
+  eset e;
+  int64_t k, i;
   (void)np;
-  while (cap < (uint64_t)(16 * ne + 16)) cap <<= 1;
-  mask = cap - 1;
-  tab = (uint64_t *)calloc(cap, sizeof(uint64_t));
-  popped = (uint8_t *)calloc(cap, 1);
-  if (!tab || !popped) { free(tab); free(popped); return 0; }
+  if (!eset_init(&e, 6 * ne)) { eset_free(&e); return 0; }
   memset(st, 0, sizeof *st);
   st->lmin = 1.e30;
   st->lmax = 0.0;
-  /* the admissibility filter needs point tags; the oracle takes none (all
-   * tets admissible), matching pmx_prilen with point_tag == NULL */
+  /* MMG5_hashEdge of every edge of every valid tet (:421-440) */
   for (k = 1; k <= ne; k++) {
     const int *v = &tet[4*k];
     int ia;
     if (v[0] <= 0) continue;
+    for (ia = 0; ia < 6; ia++) eset_slot(&e, v[IARE[ia][0]], v[IARE[ia][1]], 1);
+  }
+  /* 1) owned parallel edges, in communicator order (:445-502) */
+  for (i = 0; i < npar; i++) {
+    int64_t s = eset_slot(&e, pa[i], pb[i], 0);
+    if (powner[i] != myrank) {
+      if (exact_once && s >= 0) e.popped[s] = 1;    /* not ours: never counted here */
+      continue;
+    }
+    if (s < 0 || e.popped[s]) continue;            /* MMG5_hashPop failed */
+    e.popped[s] = 1;
+    len_count(st, (msize == 6) ? len_ani(xyz, met, pa[i], pb[i]) : len_iso(xyz, met, pa[i], pb[i]),
+              pa[i], pb[i]);
+  }
+  /* 2) the other edges, (k, ia) order, ridge-only tets skipped (:505-564) */
+  for (k = 1; k <= ne; k++) {
+    const int *v = &tet[4*k];
+    int ia;
+    if (v[0] <= 0) continue;
+    if (tet_4ridge(v, tag)) continue;
     for (ia = 0; ia < 6; ia++) {
       int np_ = v[IARE[ia][0]], nq_ = v[IARE[ia][1]];
-      int a = np_ < nq_ ? np_ : nq_, b = np_ < nq_ ? nq_ : np_;
-      uint64_t key = hkey(a, b), h = (key * 0x9e3779b97f4a7c15ULL) >> 20;
-      double len;
-      int i;
-      while (tab[h & mask] && tab[h & mask] != key) h++;
-      if (!tab[h & mask]) tab[h & mask] = key;
-      if (popped[h & mask]) continue;          /* MMG5_hashPop returned 0 */
-      popped[h & mask] = 1;
-      len = (msize == 6) ? len_ani(xyz, met, np_, nq_) : len_iso(xyz, met, np_, nq_);
-      if (!len) { st->nullEdge++; continue; }
-      st->avlen += len;
-      st->ned++;
-      if (len < st->lmin) { st->lmin = len; st->amin = np_; st->bmin = nq_; }
-      if (len > st->lmax) { st->lmax = len; st->amax = np_; st->bmax = nq_; }
-      for (i = 0; i < 8; i++)
-        if (bd[i] <= len && len < bd[i+1]) { st->hl[i]++; break; }
-      if (i == 8) st->hl[8]++;
+      int64_t s = eset_slot(&e, np_, nq_, 0);
+      if (e.popped[s]) continue;                    /* MMG5_hashPop returned 0 */
+      e.popped[s] = 1;
+      len_count(st, (msize == 6) ? len_ani(xyz, met, np_, nq_) : len_iso(xyz, met, np_, nq_), np_, nq_);
     }
   }
-  free(tab);
-  free(popped);
+  eset_free(&e);
   return 1;
+}
+
+int orc_prilen(int64_t np, int64_t ne, const double *xyz, const int *tet, const double *met,
+               int msize, orc_lenstats *st) {
+  return orc_prilen_dist(np, ne, xyz, tet, met, msize, NULL, 0, NULL, NULL, NULL, 0, 0, st);
 }

@@ -76,7 +76,8 @@ class Group(C.Structure):
 class QualStats(C.Structure):
     _fields_ = [
         ("ne", i64), ("np", i64), ("max", C.c_double), ("min", C.c_double), ("avg", C.c_double),
-        ("iel", i64), ("good", i64), ("med", i64), ("his", i64 * 5),
+        ("iel", i64), ("good", i64), ("med", i64), ("his", i64 * 5), ("nrid", i64),
+        ("iel_grp", C.c_int), ("cpu", C.c_int),
     ]
 
 
@@ -84,8 +85,36 @@ class LenStats(C.Structure):
     _fields_ = [
         ("ned", i64), ("nullEdge", i64), ("avlen", C.c_double), ("lmin", C.c_double),
         ("lmax", C.c_double), ("amin", i64), ("bmin", i64), ("amax", i64), ("bmax", i64),
-        ("hl", i64 * 9),
+        ("hl", i64 * 9), ("cpu_min", C.c_int), ("cpu_max", C.c_int),
     ]
+
+
+class QualPart(C.Structure):
+    """pmx_qual_part: the device partial of one group (15 x 8 B)."""
+    _fields_ = [
+        ("avg", C.c_double), ("max", C.c_double), ("min", C.c_double),
+        ("iel", i64), ("ne", i64), ("np", i64), ("good", i64), ("med", i64), ("nrid", i64),
+        ("his", i64 * 5), ("iel_grp", i64),
+    ]
+
+
+class LenPart(C.Structure):
+    """pmx_len_part: the device partial of one group (18 x 8 B)."""
+    _fields_ = [
+        ("avlen", C.c_double), ("lmin", C.c_double), ("lmax", C.c_double),
+        ("amin", i64), ("bmin", i64), ("amax", i64), ("bmax", i64), ("ned", i64),
+        ("nullEdge", i64), ("hl", i64 * 9),
+    ]
+
+
+class ParEdges(C.Structure):
+    _fields_ = [
+        ("n", i64), ("a", iptr), ("b", iptr), ("owner", iptr), ("myrank", C.c_int),
+        ("exact_once", C.c_int),
+    ]
+
+
+INQUA, OUTQUA = 0, 1
 
 
 # symbol -> (restype, argtypes); every function declared in include/pmx_transfer.h
@@ -115,10 +144,21 @@ SIGNATURES = {
     "PMX_interpMetricsAndFields": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(Group), iptr, C.c_int]),
     "PMX_copyMetricsAndFields_point": (C.c_int, [C.c_void_p, C.POINTER(Group), u16ptr, i64, iptr, C.c_int, C.c_int]),
     "pmx_tetra_qual": (C.c_int, [C.c_void_p, dptr]),
-    "pmx_qualhisto": (C.c_int, [C.c_void_p, C.POINTER(QualStats)]),
-    "pmx_prilen": (C.c_int, [C.c_void_p, u16ptr, i64, C.c_int, C.POINTER(LenStats)]),
-    "pmx_qualhisto_device": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
-    "pmx_prilen_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "pmx_upload_point_tags": (C.c_int, [C.c_void_p, u16ptr, i64]),
+    "pmx_count_nodes": (C.c_int, [C.c_void_p, iptr, iptr, i64, iptr, i64, C.c_int, C.POINTER(i64)]),
+    "pmx_qualhisto_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    "pmx_qualhisto": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(QualStats)]),
+    "pmx_prilen_device": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(ParEdges), C.c_void_p]),
+    "pmx_prilen": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(ParEdges), C.POINTER(LenStats)]),
+    "pmx_new_mesh_qual": (C.c_int, [C.c_void_p, iptr, i64, i64, C.c_int, dptr, C.c_void_p]),
+    "pmx_qual_fold": (C.c_int, [C.POINTER(QualPart), iptr, C.c_int, C.POINTER(QualStats)]),
+    "pmx_len_fold": (C.c_int, [C.POINTER(LenPart), C.c_int, C.POINTER(LenStats)]),
+    "pmx_comm_unique_id": (C.c_int, [C.c_char_p, C.c_int]),
+    "pmx_comm_init": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int, C.c_char_p, C.c_int]),
+    "pmx_comm_destroy": (C.c_int, [C.c_void_p]),
+    "pmx_qualhisto_allreduce": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
+                                          C.POINTER(QualStats)]),
+    "pmx_prilen_allreduce": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.POINTER(LenStats)]),
 }
 
 _lib = None

@@ -30,6 +30,7 @@ HIP_SOURCES = ["pmx_capi.hip", "pmx_kernels.hip", "pmx_walk.hip", "pmx_bdy.hip",
 HIPCC_FLAGS = [
     "-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-shared",
     "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
+    "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib",
 ]
 
 

@@ -214,6 +214,8 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   // upload has completed (a failed call must not leave sizes that disagree
   // with the device buffers)
   ctx->have_bg = ctx->ran = ctx->have_derived = ctx->have_tetv = ctx->have_qual = false;
+  ctx->have_ptag = false;
+  ctx->stat_np = -1;
   if (!m) { ctx->err = "pmx_upload_background: null mesh"; return 0; }
   hipSetDevice(ctx->device);
   if (!check_background(ctx, m, nsol, sols, imet)) return 0;
@@ -399,9 +401,11 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   }
   const size_t nn = (size_t)std::max<int64_t>(n, 1);
   // staging layout (pinned): q | kind | vol list | bdy list | dense vol coords
+  // | raw tags (statistics of the new mesh)
   const size_t o_q = 0, o_k = o_q + al256(nn * sizeof(Pt4)), o_vl = o_k + al256(nn),
                o_bl = o_vl + al256(nn * sizeof(int)), o_qv = o_bl + al256(nn * sizeof(int)),
-               total = o_qv + al256(nn * 3 * sizeof(double));
+               o_tg = o_qv + al256(nn * 3 * sizeof(double)),
+               total = o_tg + al256(pv->tag ? nn * 2 : 0);
   CK(hipStreamSynchronize(ctx->stream));   // the arena may still feed an earlier copy
   char *st = hstage(ctx, total);
   if (!st) return 0;
@@ -409,6 +413,7 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   int8_t *hk = (int8_t *)(st + o_k);
   int *vl = (int *)(st + o_vl), *bl = (int *)(st + o_bl);
   double *hqv = (double *)(st + o_qv);
+  uint16_t *htg = (uint16_t *)(st + o_tg);
   const char *pc = (const char *)pv->c;
   const char *tg = (const char *)pv->tag;
   // points referenced by a valid new tet (the reference visits only those,
@@ -445,6 +450,7 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
       const double *c = (const double *)(pc + (pv->first + j) * pv->stride);
       hq[j] = Pt4{c[0], c[1], c[2], 0.0};
       unsigned tag = tg ? *(const uint16_t *)(tg + (pv->first + j) * pv->tag_stride) : 0u;
+      if (tg) htg[j] = (uint16_t)tag;
       int8_t kd;
       if (tag >= PMX_TAG_NUL) kd = KIND_NUL;                 // !MG_VOK
       else if (use_mark && !hk[j]) kd = KIND_ORPH;           // in no valid new tet
@@ -501,7 +507,14 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   if (nv) CK(hipMemcpyAsync(ctx->d_vollist.p, vl, (size_t)nv * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
   if (nv) CK(hipMemcpyAsync(ctx->d_qv.p, hqv, (size_t)nv * 3 * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
   if (nb) CK(hipMemcpyAsync(ctx->d_bdylist.p, bl, (size_t)nb * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+  ctx->have_qtag = false;
+  if (tg && n) {
+    if (!dgrow(ctx, ctx->d_qtag, nn)) return 0;
+    CK(hipMemcpyAsync(ctx->d_qtag.p, htg, (size_t)n * 2, hipMemcpyHostToDevice, ctx->stream));
+  }
   CK(hipStreamSynchronize(ctx->stream));
+  ctx->have_qtag = tg && n;
+  ctx->pts_first = pv->first;
   ctx->have_pts = true;
   return 1;
 }
@@ -798,14 +811,16 @@ void pmx_ctx::free_all() {
   dfree(d_steps); dfree(d_start); dfree(d_edge); dfree(d_vertex); dfree(d_list); dfree(d_found);
   dfree(d_bestk); dfree(d_best); dfree(d_ties); dfree(d_counts); dfree(d_vollist); dfree(d_bdylist);
   dfree(d_vstat); dfree(d_bstat); dfree(d_qv);
-  dfree(d_qual); dfree(d_red); dfree(d_emask); dfree(d_elist); dfree(d_bcount); dfree(d_blist);
-  dfree(d_olist); dfree(d_ows);
+  dfree(d_qual); dfree(d_red); dfree(d_blist); dfree(d_olist); dfree(d_ows);
+  dfree(d_ptag); dfree(d_touch); dfree(d_cidx); dfree(d_intv); dfree(d_pub); dfree(d_pkey);
+  dfree(d_ppt); dfree(d_pedge); dfree(d_ntetv); dfree(d_nqual); dfree(d_qtag); dfree(d_gather);
   dfree(d_cmet); dfree(d_ctag); dfree(d_cperm); dfree(d_cdst); dfree(d_ccnt); dfree(d_cold);
   dfree(d_cvals);
   if (d_tgrid) hipFree(d_tgrid);
   d_tgrid = nullptr;
   d_tgrid_cap = 0;
-  have_bg = have_pts = ran = have_derived = have_tetv = have_qual = false;
+  have_bg = have_pts = ran = have_derived = have_tetv = have_qual = have_ptag = have_qtag = false;
+  stat_np = -1;
 }
 
 // node -> trias graph: offsets[np+2] (0-based CSR) + list of incident trias

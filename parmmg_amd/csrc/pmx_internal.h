@@ -88,10 +88,22 @@ struct pmx_ctx {
   // statistics
   DevBuf<double> d_qual;
   DevBuf<unsigned long long> d_red;
-  DevBuf<uint8_t> d_emask;              // prilen: per-tet mask of edges whose shell is rotated
-  DevBuf<uint32_t> d_elist;             // prilen: compacted (tet*8 + edge) list
-  DevBuf<unsigned> d_bcount;            // prilen: per-block counts -> offsets, [nb] total
   bool have_qual = false;
+  bool have_ptag = false;               // background point tags (pmx_upload_point_tags)
+  DevBuf<uint16_t> d_ptag;
+  int64_t stat_np = -1;                 // node count of pmx_count_nodes (-1: np)
+  DevBuf<uint8_t> d_touch;
+  DevBuf<int> d_cidx, d_intv;
+  DevBuf<double> d_pub;                 // public partial records of the host wrappers
+  DevBuf<unsigned long long> d_pkey;    // prilen: excluded parallel edges (sorted keys)
+  DevBuf<uint8_t> d_ppt;
+  DevBuf<int2> d_pedge;                 // prilen: owned parallel edges (step 1)
+  DevBuf<int4> d_ntetv;                 // new-mesh quality: the new tets
+  DevBuf<double> d_nqual;
+  bool have_qtag = false;               // raw tags of the new points
+  DevBuf<uint16_t> d_qtag;
+  int64_t pts_first = 0;                // points view's first index
+  DevBuf<double> d_gather;              // all-gathered partials
 
   // timing
   double topo_ms = 0.0;                 // device time of the last topology build

@@ -81,11 +81,20 @@ void launch_tet_conn(const TetRec *src, int64_t n, int4 *dst, hipStream_t s);
 int fallback_coresident_blocks(int device, int share);
 
 struct StatArgs {
-  const double *xyz;            // dense 24-B coordinates
-  const TetRec *tets;
+  // vertex v at xyz[xstride * (v - vbase)] (background: dense xyz, stride 3,
+  // base 0; new mesh: the uploaded Pt4 points, stride 4, base = first index);
+  // its metric at sol[S * (v - vbase) + moff], its tag at ptag[v - vbase]
+  const double *xyz;
+  int xstride, vbase;
+  const TetRec *tets;           // records with neighbours (background only)
   const int4 *tetv;             // connectivity stream (v only)
   int64_t ne;
   const double *sol;
   int S, msize, moff;
-  const uint16_t *ptag;
+  const uint16_t *ptag;         // point tags or null (no ridge points)
+  // distributed prilen: sorted (min << 32 | max) keys of the parallel edges
+  // the tet loop must skip, and a per-point prefilter
+  const unsigned long long *par_key;
+  int64_t npar;
+  const uint8_t *par_pt;
 };

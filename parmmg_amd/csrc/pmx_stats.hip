@@ -1,24 +1,38 @@
 // pmx_stats.hip -- quality and edge-length statistics on gfx950.
 //
-// pmx_tetra_qual  <- PMMG_tetraQual -> MMG3D_tetraQual (reference
-//                    src/quality_pmmg.c:720-733; per-tet kernels restated from
-//                    Mmg MMG5_caltet_iso / MMG5_caltet33_ani, unpinned)
-// pmx_qualhisto   <- PMMG_qualhisto per-group part (src/quality_pmmg.c:156-261)
-//                    with MMG3D_computeInqua's histogram (5 bins)
-// pmx_prilen      <- PMMG_prilen / MMG3D_computePrilen (src/quality_pmmg.c:370-709)
+// pmx_tetra_qual       <- PMMG_tetraQual -> MMG3D_tetraQual (reference
+//                         src/quality_pmmg.c:720-733; per-tet kernels restated
+//                         from Mmg MMG5_caltet_iso / MMG5_caltet33_ani, unpinned)
+// pmx_qualhisto[_device] <- the per-group part of PMMG_qualhisto
+//                         (src/quality_pmmg.c:156-261): MMG3D_computeInqua /
+//                         computeOutqua statistics (5 bins, min + location,
+//                         max, sum, good, med; OUTQUA: nrid) and the group's
+//                         node count (PMMG_count_nodes_par, :33-80)
+// pmx_prilen[_device]  <- PMMG_prilen / PMMG_computePrilen (src/quality_pmmg.c:
+//                         370-709): owned parallel edges first, then every
+//                         other unique edge in (k, ia) hash-pop order
+// pmx_new_mesh_qual    <- PMMG_tetraQual on the new mesh right after the
+//                         interpolation (src/libparmmg1.c:845), in the
+//                         device-resident interpolated metric (no re-upload)
+// pmx_qual_fold / pmx_len_fold, pmx_*_allreduce <- the reference's MPI_Reduce
+//                         with its custom ops (:82-144, :265-307, :661-676):
+//                         one RCCL all-gather of the per-rank partials, then
+//                         the reference's operators folded in rank order
 //
-// Both histograms are one pass over the mesh: per-thread accumulation, a
-// wavefront/LDS tree per workgroup, one partial record per workgroup, and a
-// two-level final reduction in workgroup order (deterministic sums).
-// Unique edges are enumerated without a hash table: tet k owns its local edge
-// ia iff k is the smallest admissible tet index in the edge shell, found by
-// rotating around the edge through the adjacency (early exit on the first
-// smaller index) -- this is the first occurrence in the reference's
-// (k ascending, ia ascending) hash-pop order, so endpoints and orientation of
-// every length match the reference.
+// Histograms are one pass over the mesh: per-thread accumulation, a wavefront
+// reduction, one partial record per workgroup, and a two-level final
+// reduction in workgroup order (deterministic sums).  Unique edges are
+// enumerated without a hash table: tet k owns its local edge ia iff k is the
+// smallest admissible tet index in the edge shell, found by rotating around
+// the edge through the adjacency (early exit on the first smaller index) --
+// the first occurrence in the reference's (k ascending, ia ascending)
+// hash-pop order, so endpoints and orientation of every length match it.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
+#include <unordered_set>
 #include <vector>
 #include "pmx_internal.h"
 
@@ -27,6 +41,7 @@
 #define TAG_REQ 4
 #define TAG_NOM 8
 #define TAG_CRN 32
+#define LEN_STEP2 (1LL << 40)      // keys of tet edges: LEN_STEP2 + 6*k + ia
 
 __constant__ int IARE[6][2] = {{0, 1}, {0, 2}, {0, 3}, {1, 2}, {1, 3}, {2, 3}};
 
@@ -86,28 +101,64 @@ __device__ double caltet_ani(D3 a, D3 b, D3 c, D3 d, const double *ma, const dou
   return det / num;
 }
 
-struct QualPart {
-  double avg, max, min;
-  long long iel, ne, good, med, his[5];
-};
+// vertex v of the statistics' mesh (the background: dense xyz; the new mesh:
+// the uploaded Pt4 points, shifted by the first point index)
+__device__ __forceinline__ D3 sld3(const StatArgs &A, int v) {
+  const double *r = A.xyz + (int64_t)A.xstride * (v - A.vbase);
+  return D3{r[0], r[1], r[2]};
+}
+__device__ __forceinline__ const double *smet(const StatArgs &A, int v) {
+  return A.sol + (int64_t)(v - A.vbase) * A.S + A.moff;
+}
+__device__ __forceinline__ unsigned stag(const StatArgs &A, int v) { return A.ptag[v - A.vbase]; }
 
-__device__ __forceinline__ D3 sld3(const StatArgs &A, int i) { return ld3(A.xyz, i); }
+// a vertex that is a non-singular ridge point: !(MG_SIN || MG_NOM) && MG_GEO
+__device__ __forceinline__ bool ridge_pt(unsigned tg) {
+  const bool sin = (tg & TAG_CRN) || (tg & TAG_REQ);
+  return !(sin || (TAG_NOM & tg)) && (tg & TAG_GEO);
+}
+// all 4 vertices are non-singular ridge points: skipped by the length loop
+// (reference src/quality_pmmg.c:509-517), counted by MMG3D_computeOutqua's nrid
+__device__ __forceinline__ bool tet_4ridge(const StatArgs &A, const int v[4]) {
+  if (!A.ptag) return false;
+  bool all = true;
+#pragma unroll
+  for (int i = 0; i < 4; i++) all = all && ridge_pt(stag(A, v[i]));
+  return all;
+}
 
 template <bool ANI>
-__device__ double tet_quality(const StatArgs &A, int64_t k, const TetRec &t) {
-  D3 a = sld3(A, t.v[0]), b = sld3(A, t.v[1]), c = sld3(A, t.v[2]), d = sld3(A, t.v[3]);
-  if (ANI) {
-    const double *m = A.sol;
-    return caltet_ani(a, b, c, d, m + (int64_t)t.v[0] * A.S + A.moff, m + (int64_t)t.v[1] * A.S + A.moff,
-                      m + (int64_t)t.v[2] * A.S + A.moff, m + (int64_t)t.v[3] * A.S + A.moff);
-  }
+__device__ double tet_quality(const StatArgs &A, const int v[4]) {
+  D3 a = sld3(A, v[0]), b = sld3(A, v[1]), c = sld3(A, v[2]), d = sld3(A, v[3]);
+  if (ANI) return caltet_ani(a, b, c, d, smet(A, v[0]), smet(A, v[1]), smet(A, v[2]), smet(A, v[3]));
   return caltet_iso(a, b, c, d);
 }
 
-// quality of every tet (+ optional histogram partials in the same pass)
+// ---- quality histogram ------------------------------------------------------------
+
+struct QualPart {
+  double avg, max, min;
+  long long iel, ne, good, med, his[5], nrid;
+};
+
+__device__ __forceinline__ void qual_merge(QualPart &x, const QualPart &y) {
+  x.avg += y.avg;
+  x.max = fmax(x.max, y.max);
+  if (y.min < x.min || (y.min == x.min && y.iel < x.iel)) { x.min = y.min; x.iel = y.iel; }
+  x.ne += y.ne; x.good += y.good; x.med += y.med; x.nrid += y.nrid;
+  for (int i = 0; i < 5; i++) x.his[i] += y.his[i];
+}
+__device__ __forceinline__ void qual_init(QualPart &p) {
+  p.avg = 0.0; p.max = 0.0; p.min = 2.0; p.iel = 0x7fffffffffffffffLL;
+  p.ne = 0; p.good = 0; p.med = 0; p.nrid = 0;
+  for (int i = 0; i < 5; i++) p.his[i] = 0;
+}
+
+// quality of every tet (+ optional histogram partials in the same pass).
 // ANI: the metric is a 6-component tensor (compiled apart: the iso variant
-// does not carry the tensor path's registers)
-template <bool ANI>
+// does not carry the tensor path's registers).  OUT: MMG3D_computeOutqua's
+// count of tets with 4 ridge vertices.
+template <bool ANI, bool OUT>
 __global__ __launch_bounds__(256) void k_qual(StatArgs A, double *qual, QualPart *parts,
                                               int use_stored) {
   __shared__ QualPart sh[256];
@@ -115,20 +166,26 @@ __global__ __launch_bounds__(256) void k_qual(StatArgs A, double *qual, QualPart
   // half the registers of QualPart's 64-bit fields
   double avg = 0.0, qmax = 0.0, qmin = 2.0;
   long long iel = 0x7fffffffffffffffLL;
-  unsigned cne = 0, cgood = 0, cmed = 0, chis[5] = {0, 0, 0, 0, 0};
-  const int64_t per = (A.ne + gridDim.x - 1) / gridDim.x;       // contiguous chunk per block
-  const int64_t k0 = 1 + (int64_t)blockIdx.x * per, k1 = min(A.ne, k0 + per - 1);
+  unsigned cne = 0, cgood = 0, cmed = 0, cnrid = 0, chis[5] = {0, 0, 0, 0, 0};
+  // contiguous chunk per block; each XCD gets a contiguous run of chunks so
+  // the next z-layer's points (another chunk) are in its own L2
+  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t per = (A.ne + gridDim.x - 1) / gridDim.x;
+  const int64_t k0 = 1 + lb * per, k1 = min(A.ne, k0 + per - 1);
   for (int64_t k = k0 + threadIdx.x; k <= k1; k += blockDim.x) {
     // 16-B connectivity stream: the neighbours are not needed here
     const int4 cv = A.tetv[k];
-    TetRec t;
-    t.v[0] = cv.x; t.v[1] = cv.y; t.v[2] = cv.z; t.v[3] = cv.w;
-    if (t.v[0] <= 0) continue;
-    double q = use_stored ? qual[k] : tet_quality<ANI>(A, k, t);
+    const int v[4] = {cv.x, cv.y, cv.z, cv.w};
+    if (v[0] <= 0) {                      // !MG_EOK: no quality (0, not a stale value)
+      if (!use_stored && qual) qual[k] = 0.0;
+      continue;
+    }
+    double q = use_stored ? qual[k] : tet_quality<ANI>(A, v);
     if (!use_stored && qual) qual[k] = q;
     if (!parts) continue;
     double rap = ALPHAD * q;
     cne++;
+    if (OUT && tet_4ridge(A, v)) cnrid++;
     if (rap < qmin || (rap == qmin && k < iel)) { qmin = rap; iel = k; }
     if (rap > 0.5) cmed++;
     if (rap > 0.12) cgood++;
@@ -143,82 +200,87 @@ __global__ __launch_bounds__(256) void k_qual(StatArgs A, double *qual, QualPart
   if (!parts) return;
   QualPart p;
   p.avg = avg; p.max = qmax; p.min = qmin; p.iel = iel;
-  p.ne = cne; p.good = cgood; p.med = cmed;
+  p.ne = cne; p.good = cgood; p.med = cmed; p.nrid = cnrid;
 #pragma unroll
   for (int i = 0; i < 5; i++) p.his[i] = chis[i];
   sh[threadIdx.x] = p;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) {
-      QualPart &x = sh[threadIdx.x];
-      const QualPart &y = sh[threadIdx.x + o];
-      x.avg += y.avg;
-      x.max = fmax(x.max, y.max);
-      if (y.min < x.min || (y.min == x.min && y.iel < x.iel)) { x.min = y.min; x.iel = y.iel; }
-      x.ne += y.ne; x.good += y.good; x.med += y.med;
-      for (int i = 0; i < 5; i++) x.his[i] += y.his[i];
-    }
+    if ((int)threadIdx.x < o) qual_merge(sh[threadIdx.x], sh[threadIdx.x + o]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) parts[blockIdx.x] = sh[0];
+  if (threadIdx.x == 0) parts[lb] = sh[0];
 }
 
-__global__ __launch_bounds__(256) void k_qual_final(const QualPart *parts, int n, QualPart *res) {
+// fixed-order reduction of n partials (launched twice: FINAL_GRID blocks, then
+// one); the last level writes the public pmx_qual_part (np from the node count)
+__global__ __launch_bounds__(256) void k_qual_final(const QualPart *parts, int n, QualPart *res,
+                                                    pmx_qual_part *pub, long long np) {
   __shared__ QualPart sh[256];
   QualPart p;
-  p.avg = 0.0; p.max = 0.0; p.min = 2.0; p.iel = 0x7fffffffffffffffLL; p.ne = 0; p.good = 0; p.med = 0;
-  for (int i = 0; i < 5; i++) p.his[i] = 0;
-  // this block's contiguous range, contiguous sub-ranges per thread: the
-  // summation order is fixed (launched twice: FINAL_GRID blocks, then one)
+  qual_init(p);
   const int pb = (n + gridDim.x - 1) / gridDim.x;
   const int lo = blockIdx.x * pb, hi = min(n, lo + pb);
   int per = (hi - lo + 255) / 256;
-  for (int b = lo + threadIdx.x * per; b < min(hi, lo + (int)(threadIdx.x + 1) * per); b++) {
-    const QualPart &y = parts[b];
-    p.avg += y.avg;
-    p.max = fmax(p.max, y.max);
-    if (y.min < p.min || (y.min == p.min && y.iel < p.iel)) { p.min = y.min; p.iel = y.iel; }
-    p.ne += y.ne; p.good += y.good; p.med += y.med;
-    for (int i = 0; i < 5; i++) p.his[i] += y.his[i];
-  }
+  for (int b = lo + threadIdx.x * per; b < min(hi, lo + (int)(threadIdx.x + 1) * per); b++)
+    qual_merge(p, parts[b]);
   sh[threadIdx.x] = p;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) {
-      QualPart &x = sh[threadIdx.x];
-      const QualPart &y = sh[threadIdx.x + o];
-      x.avg += y.avg;
-      x.max = fmax(x.max, y.max);
-      if (y.min < x.min || (y.min == x.min && y.iel < x.iel)) { x.min = y.min; x.iel = y.iel; }
-      x.ne += y.ne; x.good += y.good; x.med += y.med;
-      for (int i = 0; i < 5; i++) x.his[i] += y.his[i];
-    }
+    if ((int)threadIdx.x < o) qual_merge(sh[threadIdx.x], sh[threadIdx.x + o]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) res[blockIdx.x] = sh[0];
+  if (threadIdx.x != 0) return;
+  if (res) res[blockIdx.x] = sh[0];
+  if (pub) {
+    const QualPart &r = sh[0];
+    pmx_qual_part o;
+    o.avg = r.avg; o.max = r.max; o.min = r.min;
+    o.iel = r.ne ? r.iel : 0;
+    o.ne = r.ne; o.np = np; o.good = r.good; o.med = r.med; o.nrid = r.nrid;
+    for (int i = 0; i < 5; i++) o.his[i] = r.his[i];
+    o.iel_grp = 0;
+    *pub = o;
+  }
+}
+
+// ---- node count (PMMG_count_nodes_par, src/quality_pmmg.c:33-80) ------------------
+
+// points touched by a valid tet
+__global__ __launch_bounds__(256) void k_touch(const int4 *__restrict__ tv, int64_t ne,
+                                               uint8_t *__restrict__ touched) {
+  for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= ne;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int4 v = tv[k];
+    if (v.x <= 0) continue;
+    touched[v.x] = 1; touched[v.y] = 1; touched[v.z] = 1; touched[v.w] = 1;
+  }
+}
+// points of the internal node communicator count when they claim their slot
+// (intvalues[idx] == 0 -> base); the other points when a valid tet touches them
+__global__ __launch_bounds__(256) void k_count_nodes(const uint8_t *__restrict__ touched, int64_t np,
+                                                     const int *__restrict__ comm_idx,
+                                                     int *__restrict__ intvalues, int base,
+                                                     unsigned long long *__restrict__ count) {
+  unsigned c = 0;
+  for (int64_t ip = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ip <= np;
+       ip += (int64_t)gridDim.x * blockDim.x) {
+    const int idx = comm_idx ? comm_idx[ip] : -1;
+    if (idx >= 0) c += atomicCAS(&intvalues[idx], 0, base) == 0 ? 1u : 0u;
+    else c += touched[ip] ? 1u : 0u;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, (unsigned long long)c);
 }
 
 // ---- edge lengths ---------------------------------------------------------------
 
 struct LenPart {
   double avlen, lmin, lmax;
-  long long kmin, kmax;          // first-occurrence key 6*k+ia of the extremal edges
+  long long kmin, kmax;          // first-occurrence keys of the extremal edges
   long long ned, nul, hl[9];
 };
-
-// a tet is skipped when all 4 vertices are non-singular ridge points
-// (reference src/quality_pmmg.c:509-517)
-__device__ __forceinline__ bool tet_admissible(const StatArgs &A, const TetRec &t) {
-  if (!A.ptag) return true;
-  int n = 0;
-  for (int i = 0; i < 4; i++) {
-    unsigned tg = A.ptag[t.v[i]];
-    bool sin = (tg & TAG_CRN) || (tg & TAG_REQ);
-    if (!(sin || (TAG_NOM & tg)) && (tg & TAG_GEO)) continue;
-    n++;
-  }
-  return n > 0;
-}
 
 __device__ __forceinline__ int pick_v(const TetRec &t, int l) {
   return (t.v[0] & -(int)(l == 0)) | (t.v[1] & -(int)(l == 1)) | (t.v[2] & -(int)(l == 2)) |
@@ -237,23 +299,29 @@ __device__ __forceinline__ int loc_of(const TetRec &t, int p) {
   return l;
 }
 
-// MMG5_lenEdg_iso / lenEdg_ani (restated, unpinned)
-__device__ double edge_len(const StatArgs &A, int p1, int p2) {
+// MMG5_lenEdg_iso / lenEdg33_ani (restated, unpinned; the surface lengths
+// MMG5_lenSurfEdg_iso / lenSurfEdg33_ani of the parallel edges take the same
+// formulas in classic metric storage)
+template <bool ANI>
+__device__ __forceinline__ double edge_len_t(const StatArgs &A, int p1, int p2) {
   D3 c1 = sld3(A, p1), c2 = sld3(A, p2);
   double ux = c2.x - c1.x, uy = c2.y - c1.y, uz = c2.z - c1.z;
-  if (A.msize == 6) {
-    const double *m1 = A.sol + (int64_t)p1 * A.S + A.moff, *m2 = A.sol + (int64_t)p2 * A.S + A.moff;
+  if (ANI) {
+    const double *m1 = smet(A, p1), *m2 = smet(A, p2);
     double dd1 = mlen2(m1, ux, uy, uz);
     double dd2 = mlen2(m2, ux, uy, uz);
     if (dd1 <= 0.0) dd1 = 0.0;
     if (dd2 <= 0.0) dd2 = 0.0;
     return (sqrt(dd1) + sqrt(dd2) + 4.0 * sqrt(0.5 * (dd1 + dd2))) / 6.0;
   }
-  double h1 = A.sol[(int64_t)p1 * A.S + A.moff], h2 = A.sol[(int64_t)p2 * A.S + A.moff];
+  double h1 = smet(A, p1)[0], h2 = smet(A, p2)[0];
   double l = ux * ux + uy * uy + uz * uz;
   l = sqrt(l);
   double r = h2 / h1 - 1.0;
   return (fabs(r) < PMX_EPS) ? (l / h1) : (l / (h2 - h1) * log1p(r));
+}
+__device__ double edge_len(const StatArgs &A, int p1, int p2) {
+  return A.msize == 6 ? edge_len_t<true>(A, p1, p2) : edge_len_t<false>(A, p1, p2);
 }
 
 __device__ __forceinline__ void len_merge(LenPart &x, const LenPart &y) {
@@ -273,222 +341,309 @@ __device__ __forceinline__ void len_init(LenPart &p) {
 
 __constant__ double BD[9] = {0.0, 0.3, 0.6, 0.7071, 0.9, 1.3, 1.4142, 2.0, 5.0};
 
-// ---- prilen: unique edges by shell ownership, compacted ------------------------
-//
-// Tet k owns its local edge ia iff no admissible tet of smaller index shares
-// it (the first occurrence in the reference's (k, ia) hash-pop order).  A
-// per-thread loop over tets rotating each shell in turn left ~1 lane in 6
-// with a shell to rotate on a lattice-ordered mesh (r01: 40 ms at 125M tets),
-// so the shells to rotate are compacted first:
-//  1. k_len_mark: per tet, edges decided without a load -- disowned by a
-//     smaller face neighbour (no point tags), or owned because both faces
-//     around the edge are boundary faces (shell = {k}, measured right away) --
-//     and a 6-bit mask of the edges whose shell must be rotated;
-//  2. k_len_scan + k_len_compact: those (tet, edge) pairs, in (k, ia) order,
-//     into a list (deterministic positions: block counts + exclusive scan);
-//  3. k_len_rotate: one list entry per thread, every lane rotating a shell.
-// Sums are reduced in a fixed order (phase-1 partials, then phase-3 partials,
-// two-level final reduction): the result does not depend on the schedule.
-
-__device__ __forceinline__ void edge_others(int ia, int &o0, int &o1) {
-  const int i0 = IARE[ia][0], i1 = IARE[ia][1];
-  o0 = (i0 != 0 && i1 != 0) ? 0 : (i0 != 1 && i1 != 1) ? 1 : 2;
-  o1 = 6 - i0 - i1 - o0;
+// the edge (a, b) is measured elsewhere: an owned parallel edge of step 1 (or,
+// exact_once, a parallel edge of another rank).  Sorted (min, max) keys,
+// prefiltered by a per-point flag.
+__device__ __forceinline__ bool par_excluded(const StatArgs &A, int a, int b) {
+  if (!A.npar || !A.par_pt[a] || !A.par_pt[b]) return false;
+  const unsigned long long key = ((unsigned long long)(unsigned)min(a, b) << 32) | (unsigned)max(a, b);
+  int64_t lo = 0, hi = A.npar;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (A.par_key[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < A.npar && A.par_key[lo] == key;
 }
 
+// Edge-length accumulator.  add() is called by every lane of a wave in
+// converged control flow ("on" = this lane has an edge).  The histogram and
+// the null-edge count are workgroup counters in LDS (one ds_add per edge);
+// the sum and the extrema are per lane, reduced in a fixed tree at store().
+// (Wave-uniform counters in scalar registers spilled to VGPR lanes: ~900
+// readlane/writelane VALU instructions in the loop.)
 struct LenAcc {
+  unsigned *cnt;                       // LDS [10]: hl[0..8], null edges
   double avlen = 0.0, lmin = 1.e30, lmax = 0.0;
   long long kmin = 0x7fffffffffffffffLL, kmax = 0x7fffffffffffffffLL;
-  unsigned ned = 0, nul = 0, hl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  __device__ void add(const StatArgs &A, const TetRec &t, int64_t k, int ia) {
-    const int np_ = pick_v(t, IARE[ia][0]), nq_ = pick_v(t, IARE[ia][1]);
-    const double len = edge_len(A, np_, nq_);
-    if (!(len != 0.0)) { if (len == 0.0) { nul++; return; } }
-    const long long key = 6 * k + ia;
-    avlen += len;
-    ned++;
-    if (len < lmin || (len == lmin && key < kmin)) { lmin = len; kmin = key; }
-    if (len > lmax || (len == lmax && key < kmax)) { lmax = len; kmax = key; }
+  __device__ explicit LenAcc(unsigned *lds) : cnt(lds) {
+    if (threadIdx.x < 10) cnt[threadIdx.x] = 0u;
+    __syncthreads();
+  }
+  __device__ void add(bool on, double len, long long key) {
+    if (!on) return;
+    if (len == 0.0) { atomicAdd(&cnt[9], 1u); return; }
     int bin = 8;
 #pragma unroll
     for (int i = 7; i >= 0; i--) bin = (BD[i] <= len && len < BD[i + 1]) ? i : bin;
-#pragma unroll
-    for (int i = 0; i < 9; i++) hl[i] += (i == bin) ? 1u : 0u;
+    atomicAdd(&cnt[bin], 1u);
+    avlen += len;
+    if (len < lmin || (len == lmin && key < kmin)) { lmin = len; kmin = key; }
+    if (len > lmax || (len == lmax && key < kmax)) { lmax = len; kmax = key; }
   }
-  __device__ void store(LenPart *sh, LenPart *out) const {
-    LenPart p;
-    p.avlen = avlen; p.lmin = lmin; p.lmax = lmax; p.kmin = kmin; p.kmax = kmax;
-    p.ned = ned; p.nul = nul;
+  // one LenPart per workgroup: wave shuffles of the per-lane fields, the 4
+  // wave results in order, the LDS counters
+  __device__ void store(LenPart *out) const {
+    __shared__ LenPart wsh[4];
+    double s = avlen, lo = lmin, hi = lmax;
+    long long klo = kmin, khi = kmax;
 #pragma unroll
-    for (int i = 0; i < 9; i++) p.hl[i] = hl[i];
-    sh[threadIdx.x] = p;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if ((int)threadIdx.x < o) len_merge(sh[threadIdx.x], sh[threadIdx.x + o]);
-      __syncthreads();
+    for (int o = 1; o < 64; o <<= 1) {
+      const double ys = __shfl_xor(s, o, 64), ylo = __shfl_xor(lo, o, 64), yhi = __shfl_xor(hi, o, 64);
+      const long long yklo = __shfl_xor(klo, o, 64), ykhi = __shfl_xor(khi, o, 64);
+      // the same tree on every lane: the lower lane's value first, so all
+      // lanes agree bitwise
+      const bool low = (threadIdx.x & o) == 0;
+      s = low ? s + ys : ys + s;
+      if (ylo < lo || (ylo == lo && yklo < klo)) { lo = ylo; klo = yklo; }
+      if (yhi > hi || (yhi == hi && ykhi < khi)) { hi = yhi; khi = ykhi; }
     }
-    if (threadIdx.x == 0) *out = sh[0];
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+      LenPart p;
+      p.avlen = s; p.lmin = lo; p.lmax = hi; p.kmin = klo; p.kmax = khi;
+      p.ned = 0; p.nul = 0;
+      for (int i = 0; i < 9; i++) p.hl[i] = 0;
+      wsh[threadIdx.x >> 6] = p;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      LenPart r = wsh[0];
+      for (int w = 1; w < (int)(blockDim.x >> 6); w++) len_merge(r, wsh[w]);
+      r.ned = 0;
+      for (int i = 0; i < 9; i++) { r.hl[i] = cnt[i]; r.ned += cnt[i]; }   // every non-null length has a bin
+      r.nul = cnt[9];
+      *out = r;
+    }
   }
 };
 
-__device__ __forceinline__ unsigned block_sum(unsigned v, unsigned *sh) {
+// IARE and the two other local vertices of edge ia, as nibble tables (no
+// constant-memory load for a per-lane index)
+__device__ __forceinline__ int iare0(int ia) { return (0x211000 >> (4 * ia)) & 15; }
+__device__ __forceinline__ int iare1(int ia) { return (0x323321 >> (4 * ia)) & 15; }
+__device__ __forceinline__ int oth0(int ia) { return (0x000112 >> (4 * ia)) & 15; }
+__device__ __forceinline__ int oth1(int ia) { return (0x123233 >> (4 * ia)) & 15; }
+
+__device__ __forceinline__ bool rec_4ridge(const StatArgs &A, const TetRec &t) {
+  const int v[4] = {t.v[0], t.v[1], t.v[2], t.v[3]};
+  return tet_4ridge(A, v);
+}
+
+// the vertex of t that is none of a, b, keep
+__device__ __forceinline__ int other_vertex(const TetRec &t, int a, int b, int keep) {
+  int nk = 0;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
-  __syncthreads();
-  return sh[0] + sh[1] + sh[2] + sh[3];
-}
-
-__global__ __launch_bounds__(256) void k_len_mark(StatArgs A, LenPart *parts, uint8_t *emask,
-                                                  unsigned *bcount) {
-  __shared__ LenPart sh[256];
-  __shared__ unsigned shc[4];
-  LenAcc acc;
-  unsigned cnt = 0;
-  const int64_t per = (A.ne + gridDim.x - 1) / gridDim.x;
-  const int64_t k0 = 1 + (int64_t)blockIdx.x * per, k1 = min(A.ne, k0 + per - 1);
-  for (int64_t k = k0 + threadIdx.x; k <= k1; k += blockDim.x) {
-    const TetRec t = A.tets[k];
-    unsigned m = 0;
-    if (t.v[0] > 0 && tet_admissible(A, t)) {
-      for (int ia = 0; ia < 6; ia++) {
-        int o0, o1;
-        edge_others(ia, o0, o1);
-        const int n0 = pick_nb(t, o0), n1 = pick_nb(t, o1);
-        if (!A.ptag && ((n0 && n0 < k) || (n1 && n1 < k))) continue;   // disowned
-        if (!n0 && !n1) { acc.add(A, t, k, ia); continue; }             // shell = {k}
-        m |= 1u << ia;
-      }
-    }
-    emask[k] = (uint8_t)m;
-    cnt += __popc(m);
+  for (int l = 0; l < 4; l++) {
+    const int w = t.v[l];
+    nk = (w != a && w != b && w != keep) ? w : nk;
   }
-  const unsigned tot = block_sum(cnt, shc);
-  if (threadIdx.x == 0) bcount[blockIdx.x] = tot;
-  acc.store(sh, parts + blockIdx.x);
+  return nk;
 }
 
-// exclusive scan of the per-block counts (one workgroup; n <= 16384)
-__global__ __launch_bounds__(256) void k_len_scan(unsigned *bcount, int n, unsigned *total) {
-  __shared__ unsigned sh[256];
-  const int per = (n + 255) / 256;
-  const int b0 = threadIdx.x * per, b1 = min(n, b0 + per);
-  unsigned s = 0;
-  for (int b = b0; b < b1; b++) s += bcount[b];
-  sh[threadIdx.x] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned run = 0;
-    for (int i = 0; i < 256; i++) { unsigned v = sh[i]; sh[i] = run; run += v; }
-    *total = run;
-  }
-  __syncthreads();
-  unsigned run = sh[threadIdx.x];
-  for (int b = b0; b < b1; b++) { unsigned v = bcount[b]; bcount[b] = run; run += v; }
-}
-
-__global__ __launch_bounds__(256) void k_len_compact(const uint8_t *emask, int64_t ne,
-                                                     const unsigned *boff, uint32_t *list) {
-  __shared__ unsigned sh[256];
-  const int64_t per = (ne + gridDim.x - 1) / gridDim.x;
-  const int64_t k0 = 1 + (int64_t)blockIdx.x * per, k1 = min(ne, k0 + per - 1);
-  unsigned base = boff[blockIdx.x];
-  for (int64_t kb = k0; kb <= k1; kb += blockDim.x) {
-    const int64_t k = kb + threadIdx.x;
-    const unsigned m = (k <= k1) ? emask[k] : 0u;
-    const unsigned c = __popc(m);
-    // block-wide exclusive scan of c (Hillis-Steele in LDS)
-    sh[threadIdx.x] = c;
-    __syncthreads();
-    for (int o = 1; o < 256; o <<= 1) {
-      const unsigned v = (int)threadIdx.x >= o ? sh[threadIdx.x - o] : 0u;
-      __syncthreads();
-      sh[threadIdx.x] += v;
-      __syncthreads();
-    }
-    unsigned pos = base + sh[threadIdx.x] - c;
-    const unsigned stot = sh[255];
-    for (int ia = 0; ia < 6; ia++)
-      if ((m >> ia) & 1u) list[pos++] = (uint32_t)(k * 8 + ia);
-    base += stot;
-    __syncthreads();
-  }
-}
-
-// True iff no admissible tet with index < k contains edge ia of tet k.  The
-// shell is rotated from k through the two faces of k that contain the edge,
-// both directions advanced together (two independent loads in flight): a
-// smaller index is met after min(d0, d1) steps, and a closed shell is covered
-// when the two cursors meet, in half the dependent steps.
-__device__ bool owns_edge_bidir(const StatArgs &A, int64_t k, const TetRec &t0, int ia) {
-  const int i0 = IARE[ia][0], i1 = IARE[ia][1];
-  const int a = pick_v(t0, i0), b = pick_v(t0, i1);
-  int o0, o1;
-  edge_others(ia, o0, o1);
-  int c0 = pick_nb(t0, o0), c1 = pick_nb(t0, o1);
-  int keep0 = pick_v(t0, o1), keep1 = pick_v(t0, o0);
+// True iff no admissible tet with index < k contains the edge (a, b) of tet
+// k.  The shell is rotated from k through the two faces of k that contain the
+// edge (cursors c0, c1; keep0/keep1 = the vertex of the face just crossed),
+// both directions advanced together: a smaller index is met after min(d0, d1)
+// steps, and a closed shell is covered when the cursors meet.  r0/r1 are the
+// records of c0/c1, loaded by the caller (with the edge's points, in one
+// round trip) and then one step ahead; without point tags an index alone
+// decides, so a record is only loaded when the rotation goes on through it.
+template <bool TAGS>
+__device__ bool owns_edge(const StatArgs &A, int64_t k, int a, int b, int c0, int c1, int keep0,
+                          int keep1, TetRec r0, TetRec r1) {
   for (int guard = 0; guard < 4096; guard++) {
     if (c0 == (int)k) c0 = 0;                    // a direction that wrapped around
     if (c1 == (int)k) c1 = 0;
     if (!c0 && !c1) return true;                 // both ends reached: every tet seen
-    if (!A.ptag && ((c0 && c0 < k) || (c1 && c1 < k))) return false;
+    if (!TAGS && ((c0 && c0 < k) || (c1 && c1 < k))) return false;
     if (c0 && c0 == c1) {                        // the cursors meet on one tet
-      const TetRec t = A.tets[c0];
-      return !(c0 < k && tet_admissible(A, t));
+      if (!TAGS) return true;                  // its index was checked above
+      return !(c0 < k && !rec_4ridge(A, r0));
     }
-    TetRec t0r, t1r;
-    if (c0) t0r = A.tets[c0];
-    if (c1) t1r = A.tets[c1];
     int n0 = 0, n1 = 0;
     if (c0) {
-      if (c0 < k && tet_admissible(A, t0r)) return false;
-      n0 = pick_nb(t0r, loc_of(t0r, keep0));
-      int nk = 0;
-#pragma unroll
-      for (int l = 0; l < 4; l++) {
-        const int v = t0r.v[l];
-        nk = (v != a && v != b && v != keep0) ? v : nk;
-      }
-      keep0 = nk;
+      if (TAGS && c0 < k && !rec_4ridge(A, r0)) return false;
+      n0 = pick_nb(r0, loc_of(r0, keep0));
+      keep0 = other_vertex(r0, a, b, keep0);
     }
     if (c1) {
-      if (c1 < k && tet_admissible(A, t1r)) return false;
-      n1 = pick_nb(t1r, loc_of(t1r, keep1));
-      int nk = 0;
-#pragma unroll
-      for (int l = 0; l < 4; l++) {
-        const int v = t1r.v[l];
-        nk = (v != a && v != b && v != keep1) ? v : nk;
-      }
-      keep1 = nk;
+      if (TAGS && c1 < k && !rec_4ridge(A, r1)) return false;
+      n1 = pick_nb(r1, loc_of(r1, keep1));
+      keep1 = other_vertex(r1, a, b, keep1);
     }
     // closed shell: the next tet of one direction is the one the other just saw
     if (c0 && c1 && (n0 == c1 || n1 == c0)) return true;
     c0 = c0 ? n0 : 0;
     c1 = c1 ? n1 : 0;
+    const bool need0 = c0 && c0 != (int)k, need1 = c1 && c1 != (int)k;
+    if (!TAGS) {                               // decided by the indices: no load
+      if ((need0 && c0 < k) || (need1 && c1 < k)) return false;
+      if (need0 && c0 == c1) return true;
+    }
+    if (need0) r0 = A.tets[c0];
+    if (need1) r1 = A.tets[c1];
   }
   return true;
 }
 
-__global__ __launch_bounds__(256) void k_len_rotate(StatArgs A, const uint32_t *list,
-                                                    const unsigned *total, LenPart *parts) {
-  __shared__ LenPart sh[256];
-  LenAcc acc;
-  const int64_t n = *total;
-  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
-  const int64_t e0 = (int64_t)blockIdx.x * per, e1 = min(n, e0 + per);
-  for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
-    const uint32_t it = list[e];
-    const int64_t k = it >> 3;
-    const int ia = (int)(it & 7u);
-    const TetRec t = A.tets[k];
-    if (owns_edge_bidir(A, k, t, ia)) acc.add(A, t, k, ia);
+// ---- prilen: unique edges by shell ownership, one pass ------------------------
+//
+// Each workgroup walks a contiguous range of tets, 256 records per batch:
+//  1. every thread reads its tet record (prefetched one batch ahead, kept in a
+//     double-buffered LDS array), drops the edges a smaller face neighbour
+//     owns (no point tags) and queues the others, in (k, ia) order, in an LDS
+//     ring;
+//  2. the ring is consumed in full rounds of 256 edges -- one per thread:
+//     the edge's points and the first shell step's records are loaded in one
+//     round trip, the length is computed, the shell rotation decides whether
+//     it counts.  Fewer than 256 left over wait for the next batch, unless
+//     they belong to the previous batch, whose LDS records are about to be
+//     overwritten (then a partial round).
+// (r01 ran the phases as separate launches through a global list: 6.25 ms at
+// 125M tets; a fused version with one round trip per dependent load and
+// partial rounds after every batch: 7.2 ms.)
+#define LEN_QCAP 2048                 // > 255 left over + 6 * 256 queued
+template <bool ANI, bool TAGS, bool PAR>
+__global__ __launch_bounds__(256) void k_prilen(StatArgs A, LenPart *parts) {
+  __shared__ TetRec srec[2][256];
+  __shared__ unsigned short q[LEN_QCAP];
+  __shared__ unsigned wcnt[4];
+  __shared__ long long kbase[2];                 // first tet of each LDS buffer
+  __shared__ unsigned lcnt[10];
+  LenAcc acc(lcnt);
+  // XCD-contiguous chunks: the shells and points of the next z-layer of
+  // cells are another chunk's, read by the same L2
+  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t per = (A.ne + gridDim.x - 1) / gridDim.x;
+  const int64_t k0 = 1 + lb * per, k1 = min(A.ne, k0 + per - 1);
+  const unsigned tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  unsigned head = 0, tail = 0;                   // ring positions (uniform)
+  // each batch's records go to an LDS buffer; the next batch's are loaded at
+  // the start of the batch and written to the other buffer after its rounds,
+  // so the load is in flight during them (loaded from a clamped index: no
+  // merge copy that would wait for it; records past k1 are never used)
+  const int4 *recs = reinterpret_cast<const int4 *>(A.tets);
+  {
+    const int64_t kn = min(k0 + (int64_t)tid, A.ne);
+    int4 *srow = reinterpret_cast<int4 *>(&srec[0][tid]);
+    srow[0] = recs[2 * kn];
+    srow[1] = recs[2 * kn + 1];
+    if (tid == 0) kbase[0] = k0;
+    __syncthreads();
   }
-  acc.store(sh, parts + blockIdx.x);
+
+  int buf = 0;
+  for (int64_t kb = k0;; kb += 256, buf ^= 1) {
+    const bool more = kb <= k1;
+    if (!more && head == tail) break;
+    const unsigned prev_end = tail;              // entries before it: the previous batch
+    const int64_t kn = min(kb + 256 + (int64_t)tid, A.ne);
+    const int4 pv = recs[2 * kn], pn = recs[2 * kn + 1];
+    if (more) {
+      const int64_t k = kb + tid;
+      const TetRec t = srec[buf][tid];
+      unsigned m = 0;
+      if (k <= k1) {
+        const int v[4] = {t.v[0], t.v[1], t.v[2], t.v[3]};
+        if (t.v[0] > 0 && !(TAGS && tet_4ridge(A, v))) {
+#pragma unroll
+          for (int ia = 0; ia < 6; ia++) {
+            const int n0 = pick_nb(t, oth0(ia)), n1 = pick_nb(t, oth1(ia));
+            if (!TAGS && ((n0 && n0 < k) || (n1 && n1 < k))) continue;   // disowned
+            m |= 1u << ia;
+          }
+        }
+      }
+      // ring positions in (thread, ia) order: wave prefix + wave offsets
+      const unsigned c = __popc(m);
+      unsigned pre = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned y = __shfl_up(pre, o, 64);
+        if ((int)lane >= o) pre += y;
+      }
+      if (lane == 63) wcnt[wv] = pre;
+      __syncthreads();
+      unsigned base = 0, total = 0;
+      for (unsigned w = 0; w < 4; w++) {
+        base += (w < wv) ? wcnt[w] : 0u;
+        total += wcnt[w];
+      }
+      total = __builtin_amdgcn_readfirstlane(total);
+      unsigned pos = tail + base + pre - c;
+#pragma unroll
+      for (int ia = 0; ia < 6; ia++)
+        if ((m >> ia) & 1u) q[(pos++) & (LEN_QCAP - 1)] = (unsigned short)((buf << 11) | (tid << 3) | ia);
+      __syncthreads();
+      tail += total;
+    }
+    // full rounds; a partial one while entries of the previous batch remain
+    // (their LDS records are rewritten next); everything once the tets ran out
+    const unsigned avail = tail - head;
+    unsigned nr = avail >> 8;
+    if (!more) nr = (avail + 255u) >> 8;
+    else if (head + (nr << 8) < prev_end) nr++;
+    for (unsigned r = 0; r < nr; r++) {
+      const unsigned cnt = min(256u, tail - head);
+      bool on = false;
+      double len = 0.0;
+      long long key = 0;
+      if (tid < cnt) {
+        const unsigned it = q[(head + tid) & (LEN_QCAP - 1)];
+        const int eb = (int)(it >> 11), slot = (int)((it >> 3) & 255u), ia = (int)(it & 7u);
+        const TetRec t = srec[eb][slot];
+        const int64_t kk = kbase[eb] + slot;
+        const int a = pick_v(t, iare0(ia)), b = pick_v(t, iare1(ia));
+        const int o0 = oth0(ia), o1 = oth1(ia);
+        const int c0 = pick_nb(t, o0), c1 = pick_nb(t, o1);
+        // the first rotation step's records, issued with the points' loads
+        TetRec r0{}, r1{};
+        if (c0) r0 = A.tets[c0];
+        if (c1) r1 = A.tets[c1];
+        len = edge_len_t<ANI>(A, a, b);
+        on = owns_edge<TAGS>(A, kk, a, b, c0, c1, pick_v(t, o1), pick_v(t, o0), r0, r1) &&
+             !(PAR && par_excluded(A, a, b));
+        key = LEN_STEP2 + 6 * kk + ia;
+      }
+      acc.add(on, len, key);
+      head += cnt;
+    }
+    if (more) {                                  // no entry of the previous batch is left
+      int4 *srow = reinterpret_cast<int4 *>(&srec[buf ^ 1][tid]);
+      srow[0] = pv;
+      srow[1] = pn;
+      if (tid == 0) kbase[buf ^ 1] = kb + 256;
+    }
+    __syncthreads();                             // srec, wcnt, kbase rewritten next
+  }
+  acc.store(parts + lb);
 }
 
-__global__ __launch_bounds__(256) void k_prilen_final(const LenPart *parts, int n, LenPart *res) {
+// step 1 of the distributed prilen: the owned parallel edges, in list order,
+// each once (src/quality_pmmg.c:445-502); one workgroup
+__global__ __launch_bounds__(256) void k_prilen_par(StatArgs A, const int2 *edges, int64_t n,
+                                                    LenPart *part) {
+  __shared__ unsigned lcnt[10];
+  LenAcc acc(lcnt);
+  for (int64_t base = 0; base < n; base += blockDim.x) {
+    const int64_t i = base + threadIdx.x;
+    const bool on = i < n;
+    double len = 0.0;
+    if (on) {
+      const int2 e = edges[i];
+      len = edge_len(A, e.x, e.y);
+    }
+    acc.add(on, len, i);
+  }
+  acc.store(part);
+}
+
+// fixed-order reduction; the last level resolves the extremal edges' endpoints
+// (step-1 keys: the list entry; step-2 keys: the tet's local edge)
+__global__ __launch_bounds__(256) void k_prilen_final(const LenPart *parts, int n, LenPart *res,
+                                                      pmx_len_part *pub, const TetRec *tets,
+                                                      const int2 *par_edges) {
   __shared__ LenPart sh[256];
   LenPart p;
   len_init(p);
@@ -503,10 +658,45 @@ __global__ __launch_bounds__(256) void k_prilen_final(const LenPart *parts, int 
     if ((int)threadIdx.x < o) len_merge(sh[threadIdx.x], sh[threadIdx.x + o]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) res[blockIdx.x] = sh[0];
+  if (threadIdx.x != 0) return;
+  if (res) res[blockIdx.x] = sh[0];
+  if (pub) {
+    const LenPart &r = sh[0];
+    pmx_len_part o;
+    o.avlen = r.avlen; o.lmin = r.ned ? r.lmin : 1.e30; o.lmax = r.lmax;
+    o.ned = r.ned; o.nullEdge = r.nul;
+    for (int i = 0; i < 9; i++) o.hl[i] = r.hl[i];
+    o.amin = o.bmin = o.amax = o.bmax = 0;
+    long long keys[2] = {r.kmin, r.kmax};
+    long long ab[2][2] = {{0, 0}, {0, 0}};
+    for (int j = 0; j < 2 && r.ned; j++) {
+      const long long key = keys[j];
+      if (key >= LEN_STEP2) {
+        const long long kk = (key - LEN_STEP2) / 6;
+        const int ia = (int)((key - LEN_STEP2) % 6);
+        const TetRec t = tets[kk];
+        ab[j][0] = pick_v(t, IARE[ia][0]);
+        ab[j][1] = pick_v(t, IARE[ia][1]);
+      } else {
+        ab[j][0] = par_edges[key].x;
+        ab[j][1] = par_edges[key].y;
+      }
+    }
+    o.amin = ab[0][0]; o.bmin = ab[0][1]; o.amax = ab[1][0]; o.bmax = ab[1][1];
+    *pub = o;
+  }
 }
 
-// ---- C ABI ----------------------------------------------------------------------
+// ---- the new mesh (PMMG_tetraQual after the interpolation) ----------------------
+
+__global__ __launch_bounds__(256) void k_conn_from_host(const int4 *__restrict__ src, int64_t n,
+                                                       int4 *__restrict__ dst) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
+// ---- host side ------------------------------------------------------------------
 
 // partial records per pass: a function of ne only (the fixed-order final
 // reduction then gives the same sums on every run); enough workgroups to fill
@@ -516,26 +706,25 @@ static int stat_blocks(int64_t ne) {
   return (int)std::max<int64_t>(256, std::min<int64_t>(16384, ne / 2048));
 }
 
+static bool ensure_tetv(pmx_ctx *ctx) {
+  if (ctx->have_tetv) return true;
+  if (!pmx_dgrow(ctx, ctx->d_tetv, (size_t)(ctx->ne + 1))) return false;
+  launch_tet_conn(ctx->d_tets.p, ctx->ne + 1, ctx->d_tetv.p, ctx->stream);
+  ctx->have_tetv = true;
+  return true;
+}
+
+// the statistics' view of the background group
 static bool stat_args(pmx_ctx *ctx, StatArgs &A) {
   if (!ctx->have_bg) { ctx->err = "statistics: upload a group first"; return false; }
   // the 16-B connectivity stream of the quality pass, derived from the tet
   // records on the first statistics call after an upload (the transfer step
   // itself does not need it)
-  if (!ctx->have_tetv) {
-    if (ctx->d_tetv.cap < (size_t)(ctx->ne + 1)) {
-      if (ctx->d_tetv.p) hipFree(ctx->d_tetv.p);
-      ctx->d_tetv.p = nullptr;
-      ctx->d_tetv.cap = 0;
-      if (hipMalloc((void **)&ctx->d_tetv.p, sizeof(int4) * (size_t)(ctx->ne + 1)) != hipSuccess) {
-        ctx->err = "statistics: hipMalloc tetv";
-        return false;
-      }
-      ctx->d_tetv.cap = (size_t)(ctx->ne + 1);
-    }
-    launch_tet_conn(ctx->d_tets.p, ctx->ne + 1, ctx->d_tetv.p, ctx->stream);
-    ctx->have_tetv = true;
-  }
+  if (!ensure_tetv(ctx)) return false;
+  A = StatArgs{};
   A.xyz = ctx->d_xyz.p;
+  A.xstride = 3;
+  A.vbase = 0;
   A.tets = ctx->d_tets.p;
   A.tetv = ctx->d_tetv.p;
   A.ne = ctx->ne;
@@ -543,53 +732,86 @@ static bool stat_args(pmx_ctx *ctx, StatArgs &A) {
   A.S = ctx->sd.S;
   A.msize = ctx->sd.imet >= 0 ? ctx->sd.size[ctx->sd.imet] : 0;
   A.moff = ctx->sd.imet >= 0 ? ctx->sd.off[ctx->sd.imet] : 0;
-  A.ptag = nullptr;
+  A.ptag = ctx->have_ptag ? ctx->d_ptag.p : nullptr;
   return true;
 }
-
-template <class T> static bool dgrow_t(pmx_ctx *ctx, DevBuf<T> &b, size_t n) {
-  if (b.p && b.cap >= n) return true;
-  if (b.p) hipFree(b.p);
-  b.p = nullptr;
-  b.cap = 0;
-  if (hipMalloc((void **)&b.p, n * sizeof(T)) != hipSuccess) { ctx->err = "hipMalloc prilen"; return false; }
-  b.cap = n;
-  return true;
-}
-static bool dgrow_u8(pmx_ctx *ctx, DevBuf<uint8_t> &b, size_t n) { return dgrow_t(ctx, b, n); }
-static bool dgrow_u32(pmx_ctx *ctx, DevBuf<uint32_t> &b, size_t n) { return dgrow_t(ctx, b, n); }
-static bool dgrow_u32(pmx_ctx *ctx, DevBuf<unsigned> &b, size_t n, int) { return dgrow_t(ctx, b, n); }
 
 static bool ensure_red(pmx_ctx *ctx, size_t bytes) {
-  size_t n = (bytes + 7) / 8;
-  if (ctx->d_red.cap >= n && ctx->d_red.p) return true;
-  if (ctx->d_red.p) hipFree(ctx->d_red.p);
-  ctx->d_red.p = nullptr;
-  if (hipMalloc((void **)&ctx->d_red.p, n * 8) != hipSuccess) { ctx->err = "hipMalloc stats"; return false; }
-  ctx->d_red.cap = n;
-  return true;
+  return pmx_dgrow(ctx, ctx->d_red, (bytes + 7) / 8);
+}
+
+// qualhisto partial of the mesh described by A (background or new mesh)
+static int qual_partial(pmx_ctx *ctx, const StatArgs &A, int opt, double *qual_dev, int use_stored,
+                        pmx_qual_part *pub, long long np) {
+  const int nb = stat_blocks(A.ne);
+  if (!ensure_red(ctx, sizeof(QualPart) * (nb + FINAL_GRID + 1))) return 0;
+  QualPart *parts = (QualPart *)ctx->d_red.p;
+  hipStream_t s = ctx->stream;
+  const bool ani = A.msize == 6, out = opt == PMX_OUTQUA && A.ptag;
+  double *q = use_stored ? qual_dev : nullptr;
+  if (ani && out) hipLaunchKernelGGL((k_qual<true, true>), dim3(nb), dim3(256), 0, s, A, q, parts, use_stored);
+  else if (ani) hipLaunchKernelGGL((k_qual<true, false>), dim3(nb), dim3(256), 0, s, A, q, parts, use_stored);
+  else if (out) hipLaunchKernelGGL((k_qual<false, true>), dim3(nb), dim3(256), 0, s, A, q, parts, use_stored);
+  else hipLaunchKernelGGL((k_qual<false, false>), dim3(nb), dim3(256), 0, s, A, q, parts, use_stored);
+  QualPart *mid = parts + nb;
+  hipLaunchKernelGGL(k_qual_final, dim3(FINAL_GRID), dim3(256), 0, s, parts, nb, mid,
+                     (pmx_qual_part *)nullptr, 0LL);
+  hipLaunchKernelGGL(k_qual_final, dim3(1), dim3(256), 0, s, mid, FINAL_GRID, (QualPart *)nullptr, pub, np);
+  if (hipGetLastError() != hipSuccess) { ctx->err = "qualhisto: launch failed"; return 0; }
+  return 1;
+}
+
+static void qual_to_stats(const pmx_qual_part &r, pmx_qual_stats *st) {
+  memset(st, 0, sizeof *st);
+  st->ne = r.ne; st->np = r.np; st->max = r.max; st->min = r.min; st->avg = r.avg;
+  st->iel = r.iel; st->good = r.good; st->med = r.med; st->nrid = r.nrid;
+  for (int i = 0; i < 5; i++) st->his[i] = r.his[i];
+  st->iel_grp = (int)r.iel_grp;
+  st->cpu = 0;
+}
+static void len_to_stats(const pmx_len_part &r, pmx_len_stats *st) {
+  memset(st, 0, sizeof *st);
+  st->ned = r.ned; st->nullEdge = r.nullEdge; st->avlen = r.avlen; st->lmin = r.lmin; st->lmax = r.lmax;
+  st->amin = r.amin; st->bmin = r.bmin; st->amax = r.amax; st->bmax = r.bmax;
+  for (int i = 0; i < 9; i++) st->hl[i] = r.hl[i];
+  st->cpu_min = st->cpu_max = 0;
 }
 
 extern "C" {
 
+int pmx_upload_point_tags(pmx_ctx *ctx, const uint16_t *tag, int64_t stride) {
+  if (!ctx) return 0;
+  ctx->have_ptag = false;
+  if (!ctx->have_bg) { ctx->err = "pmx_upload_point_tags: upload a background first"; return 0; }
+  if (!tag) return 1;                       // no tags: no ridge points
+  hipSetDevice(ctx->device);
+  const int64_t np = ctx->np;
+  char *st = pmx_hstage(ctx, (size_t)(np + 1) * 2);
+  if (!st) return 0;
+  uint16_t *h = (uint16_t *)st;
+  h[0] = 0;
+  for (int64_t i = 1; i <= np; i++) h[i] = *(const uint16_t *)((const char *)tag + i * stride);
+  if (!pmx_dgrow(ctx, ctx->d_ptag, (size_t)(np + 1))) return 0;
+  if (hipMemcpyAsync(ctx->d_ptag.p, h, (size_t)(np + 1) * 2, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    ctx->err = "pmx_upload_point_tags: copy";
+    return 0;
+  }
+  ctx->have_ptag = true;
+  return 1;
+}
+
 int pmx_tetra_qual(pmx_ctx *ctx, double *qual) {
   if (!ctx) return 0;
   hipSetDevice(ctx->device);
-  StatArgs A{};
+  StatArgs A;
   if (!stat_args(ctx, A)) return 0;
-  if (ctx->d_qual.cap < (size_t)(ctx->ne + 1)) {
-    if (ctx->d_qual.p) hipFree(ctx->d_qual.p);
-    if (hipMalloc((void **)&ctx->d_qual.p, sizeof(double) * (size_t)(ctx->ne + 1)) != hipSuccess) {
-      ctx->err = "hipMalloc qual";
-      return 0;
-    }
-    ctx->d_qual.cap = (size_t)(ctx->ne + 1);
-  }
+  if (!pmx_dgrow(ctx, ctx->d_qual, (size_t)(ctx->ne + 1))) return 0;
   if (A.msize == 6)
-    hipLaunchKernelGGL(k_qual<true>, dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
+    hipLaunchKernelGGL((k_qual<true, false>), dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
                        ctx->d_qual.p, (QualPart *)nullptr, 0);
   else
-    hipLaunchKernelGGL(k_qual<false>, dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
+    hipLaunchKernelGGL((k_qual<false, false>), dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
                        ctx->d_qual.p, (QualPart *)nullptr, 0);
   if (hipGetLastError() != hipSuccess) { ctx->err = "k_qual launch"; return 0; }
   ctx->have_qual = true;
@@ -601,119 +823,388 @@ int pmx_tetra_qual(pmx_ctx *ctx, double *qual) {
   return 1;
 }
 
-int pmx_qualhisto_device(pmx_ctx *ctx, int use_stored, void *dev_result) {
-  StatArgs A{};
-  if (!stat_args(ctx, A)) return 0;
-  if (use_stored && !ctx->have_qual) { ctx->err = "pmx_qualhisto: no stored quality"; return 0; }
-  if (!ensure_red(ctx, sizeof(QualPart) * (stat_blocks(ctx->ne) + FINAL_GRID + 1))) return 0;
-  QualPart *parts = (QualPart *)ctx->d_red.p;
-  if (A.msize == 6)
-    hipLaunchKernelGGL(k_qual<true>, dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
-                       use_stored ? ctx->d_qual.p : (double *)nullptr, parts, use_stored);
-  else
-    hipLaunchKernelGGL(k_qual<false>, dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
-                       use_stored ? ctx->d_qual.p : (double *)nullptr, parts, use_stored);
-  QualPart *mid = parts + stat_blocks(ctx->ne);
-  QualPart *res = dev_result ? (QualPart *)dev_result : mid + FINAL_GRID;
-  hipLaunchKernelGGL(k_qual_final, dim3(FINAL_GRID), dim3(256), 0, ctx->stream, parts,
-                     stat_blocks(ctx->ne), mid);
-  hipLaunchKernelGGL(k_qual_final, dim3(1), dim3(256), 0, ctx->stream, mid, FINAL_GRID, res);
-  return hipGetLastError() == hipSuccess;
-}
-
-int pmx_qualhisto(pmx_ctx *ctx, pmx_qual_stats *st) {
-  if (!ctx || !st) return 0;
+int pmx_count_nodes(pmx_ctx *ctx, const int *idx_ip, const int *idx_comm, int64_t nitem_grp,
+                    int *intvalues, int64_t nitem, int base, int64_t *np_out) {
+  if (!ctx || !np_out) return 0;
   hipSetDevice(ctx->device);
-  if (!pmx_qualhisto_device(ctx, 0, nullptr)) return 0;
-  QualPart r;
-  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return 0;
-  if (hipMemcpy(&r, (QualPart *)ctx->d_red.p + stat_blocks(ctx->ne) + FINAL_GRID, sizeof r, hipMemcpyDeviceToHost) != hipSuccess) return 0;
-  st->ne = r.ne;
-  st->np = ctx->np;
-  st->max = r.max;
-  st->min = r.min;
-  st->avg = r.avg;
-  st->iel = r.ne ? r.iel : 0;
-  st->good = r.good;
-  st->med = r.med;
-  for (int i = 0; i < 5; i++) st->his[i] = r.his[i];
+  StatArgs A;
+  if (!stat_args(ctx, A)) return 0;
+  if (nitem_grp < 0 || nitem < 0 || (nitem_grp > 0 && (!idx_ip || !idx_comm || !intvalues))) {
+    ctx->err = "pmx_count_nodes: bad communicator arrays";
+    return 0;
+  }
+  const int64_t np = ctx->np;
+  hipStream_t s = ctx->stream;
+  // point -> communicator slot (-1: not in the internal communicator)
+  std::vector<int> cidx;
+  if (nitem_grp > 0) {
+    cidx.assign((size_t)(np + 1), -1);
+    for (int64_t i = 0; i < nitem_grp; i++) {
+      if (idx_ip[i] < 1 || idx_ip[i] > np || idx_comm[i] < 0 || idx_comm[i] >= nitem) {
+        ctx->err = "pmx_count_nodes: communicator index out of range";
+        return 0;
+      }
+      cidx[(size_t)idx_ip[i]] = idx_comm[i];
+    }
+  }
+  if (!pmx_dgrow(ctx, ctx->d_touch, (size_t)(np + 1)) || !pmx_dgrow(ctx, ctx->d_cidx, cidx.size() + 1) ||
+      !pmx_dgrow(ctx, ctx->d_intv, (size_t)std::max<int64_t>(nitem, 1)) || !ensure_red(ctx, 64))
+    return 0;
+  unsigned long long *cnt = ctx->d_red.p;
+  bool okk = hipMemsetAsync(ctx->d_touch.p, 0, (size_t)(np + 1), s) == hipSuccess &&
+             hipMemsetAsync(cnt, 0, 8, s) == hipSuccess;
+  if (okk && nitem_grp > 0)
+    okk = hipMemcpyAsync(ctx->d_cidx.p, cidx.data(), cidx.size() * 4, hipMemcpyHostToDevice, s) == hipSuccess &&
+          hipMemcpyAsync(ctx->d_intv.p, intvalues, (size_t)nitem * 4, hipMemcpyHostToDevice, s) == hipSuccess;
+  if (!okk) { ctx->err = "pmx_count_nodes: copy"; return 0; }
+  const int64_t nbt = std::min<int64_t>((ctx->ne + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_touch, dim3((unsigned)std::max<int64_t>(nbt, 1)), dim3(256), 0, s, A.tetv, ctx->ne,
+                     ctx->d_touch.p);
+  const int64_t nbp = std::min<int64_t>((np + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_count_nodes, dim3((unsigned)std::max<int64_t>(nbp, 1)), dim3(256), 0, s,
+                     ctx->d_touch.p, np, nitem_grp > 0 ? ctx->d_cidx.p : nullptr, ctx->d_intv.p, base, cnt);
+  unsigned long long c = 0;
+  okk = hipMemcpyAsync(&c, cnt, 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
+        (nitem_grp == 0 || hipMemcpyAsync(intvalues, ctx->d_intv.p, (size_t)nitem * 4, hipMemcpyDeviceToHost, s) == hipSuccess) &&
+        hipStreamSynchronize(s) == hipSuccess;
+  if (!okk) { ctx->err = "pmx_count_nodes: launch"; return 0; }
+  *np_out = (int64_t)c;
+  ctx->stat_np = (int64_t)c;
   return 1;
 }
 
-// result slot of the prilen reduction in d_red (after both partial arrays)
-static int64_t len_res_slot(pmx_ctx *ctx) { return 2 * (int64_t)stat_blocks(ctx->ne) + FINAL_GRID; }
+int pmx_qualhisto_device(pmx_ctx *ctx, int opt, int use_stored, void *dev_result) {
+  if (!ctx || !dev_result) return 0;
+  hipSetDevice(ctx->device);
+  StatArgs A;
+  if (!stat_args(ctx, A)) return 0;
+  if (use_stored && !ctx->have_qual) { ctx->err = "pmx_qualhisto: no stored quality"; return 0; }
+  const long long np = ctx->stat_np >= 0 ? ctx->stat_np : ctx->np;
+  return qual_partial(ctx, A, opt, ctx->d_qual.p, use_stored, (pmx_qual_part *)dev_result, np);
+}
 
-int pmx_prilen_device(pmx_ctx *ctx, const uint16_t *dtag, void *dev_result) {
-  StatArgs A{};
+int pmx_qualhisto(pmx_ctx *ctx, int opt, pmx_qual_stats *st) {
+  if (!ctx || !st) return 0;
+  hipSetDevice(ctx->device);
+  if (!pmx_dgrow(ctx, ctx->d_pub, 32)) return 0;
+  if (!pmx_qualhisto_device(ctx, opt, 0, ctx->d_pub.p)) return 0;
+  pmx_qual_part r;
+  if (hipMemcpyAsync(&r, ctx->d_pub.p, sizeof r, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    ctx->err = "pmx_qualhisto: download";
+    return 0;
+  }
+  qual_to_stats(r, st);
+  return 1;
+}
+
+int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, void *dev_result) {
+  (void)metRidTyp;   // classic metric storage (size 1 or 6 on every point), see the header
+  if (!ctx || !dev_result) return 0;
+  hipSetDevice(ctx->device);
+  StatArgs A;
   if (!stat_args(ctx, A)) return 0;
   if (ctx->sd.imet < 0) { ctx->err = "pmx_prilen: no metric"; return 0; }
   if (ctx->ne >= (1LL << 29)) { ctx->err = "pmx_prilen: ne >= 2^29 per group"; return 0; }
-  A.ptag = dtag;
+  hipStream_t s = ctx->stream;
+  // parallel edges (host): step-1 list (owned, first occurrence, list order)
+  // and the sorted keys of the edges step 2 must not count
+  std::vector<int2> own;
+  std::vector<unsigned long long> excl;
+  std::vector<uint8_t> ppt;
+  if (par && par->n > 0) {
+    if (!par->a || !par->b || !par->owner) { ctx->err = "pmx_prilen: bad parallel edges"; return 0; }
+    std::unordered_set<unsigned long long> popped;
+    for (int64_t i = 0; i < par->n; i++) {
+      const int a = par->a[i], b = par->b[i];
+      if (a < 1 || b < 1 || a > ctx->np || b > ctx->np || a == b) {
+        ctx->err = "pmx_prilen: parallel edge vertex out of range";
+        return 0;
+      }
+      const unsigned long long key = ((unsigned long long)(unsigned)std::min(a, b) << 32) | (unsigned)std::max(a, b);
+      if (par->owner[i] == par->myrank) {
+        // MMG5_hashPop succeeds once per edge: a repeated entry is not counted
+        if (popped.insert(key).second) own.push_back(make_int2(a, b));
+        excl.push_back(key);
+      } else if (par->exact_once) {
+        excl.push_back(key);
+      }
+    }
+    std::sort(excl.begin(), excl.end());
+    excl.erase(std::unique(excl.begin(), excl.end()), excl.end());
+    ppt.assign((size_t)(ctx->np + 1), 0);
+    for (unsigned long long key : excl) {
+      ppt[(size_t)(key >> 32)] = 1;
+      ppt[(size_t)(key & 0xffffffffu)] = 1;
+    }
+  }
   const int nb = stat_blocks(ctx->ne);
-  if (!ensure_red(ctx, sizeof(LenPart) * (2 * (size_t)nb + FINAL_GRID + 1))) return 0;
+  if (!ensure_red(ctx, sizeof(LenPart) * ((size_t)nb + 1 + FINAL_GRID + 1))) return 0;
   LenPart *parts = (LenPart *)ctx->d_red.p;
-  LenPart *res = dev_result ? (LenPart *)dev_result : parts + len_res_slot(ctx);
-  if (!dgrow_u8(ctx, ctx->d_emask, (size_t)(ctx->ne + 1)) ||
-      !dgrow_u32(ctx, ctx->d_elist, (size_t)(6 * ctx->ne + 1)) ||
-      !dgrow_u32(ctx, ctx->d_bcount, (size_t)nb + 1))
-    return 0;
-  unsigned *bc = ctx->d_bcount.p, *total = ctx->d_bcount.p + nb;
-  hipLaunchKernelGGL(k_len_mark, dim3(nb), dim3(256), 0, ctx->stream, A, parts, ctx->d_emask.p, bc);
-  hipLaunchKernelGGL(k_len_scan, dim3(1), dim3(256), 0, ctx->stream, bc, nb, total);
-  hipLaunchKernelGGL(k_len_compact, dim3(nb), dim3(256), 0, ctx->stream, ctx->d_emask.p, ctx->ne, bc,
-                     ctx->d_elist.p);
-  hipLaunchKernelGGL(k_len_rotate, dim3(nb), dim3(256), 0, ctx->stream, A, ctx->d_elist.p, total,
-                     parts + nb);
-  LenPart *mid = parts + 2 * nb;
-  hipLaunchKernelGGL(k_prilen_final, dim3(FINAL_GRID), dim3(256), 0, ctx->stream, parts, 2 * nb, mid);
-  hipLaunchKernelGGL(k_prilen_final, dim3(1), dim3(256), 0, ctx->stream, mid, FINAL_GRID, res);
-  return hipGetLastError() == hipSuccess;
+  A.npar = (int64_t)excl.size();
+  if (A.npar) {
+    if (!pmx_dgrow(ctx, ctx->d_pkey, excl.size()) || !pmx_dgrow(ctx, ctx->d_ppt, ppt.size()) ||
+        !pmx_dgrow(ctx, ctx->d_pedge, std::max<size_t>(own.size(), 1)))
+      return 0;
+    if (hipMemcpyAsync(ctx->d_pkey.p, excl.data(), excl.size() * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(ctx->d_ppt.p, ppt.data(), ppt.size(), hipMemcpyHostToDevice, s) != hipSuccess ||
+        (!own.empty() && hipMemcpyAsync(ctx->d_pedge.p, own.data(), own.size() * sizeof(int2), hipMemcpyHostToDevice, s) != hipSuccess)) {
+      ctx->err = "pmx_prilen: parallel edge upload";
+      return 0;
+    }
+    A.par_key = ctx->d_pkey.p;
+    A.par_pt = ctx->d_ppt.p;
+  }
+  // partials: [0] step 1 (owned parallel edges), [1..nb] step 2 (tet edges)
+  if (!own.empty())
+    hipLaunchKernelGGL(k_prilen_par, dim3(1), dim3(256), 0, s, A, ctx->d_pedge.p, (int64_t)own.size(), parts);
+  else
+    hipLaunchKernelGGL(k_prilen_par, dim3(1), dim3(256), 0, s, A, (const int2 *)nullptr, (int64_t)0, parts);
+  {
+    // variants: metric kind x point tags x parallel edges (each drops the
+    // other paths' registers and branches)
+    using KFn = void (*)(StatArgs, LenPart *);
+    static const KFn kfn[8] = {k_prilen<false, false, false>, k_prilen<false, false, true>,
+                               k_prilen<false, true, false>,  k_prilen<false, true, true>,
+                               k_prilen<true, false, false>,  k_prilen<true, false, true>,
+                               k_prilen<true, true, false>,   k_prilen<true, true, true>};
+    const int sel = (A.msize == 6 ? 4 : 0) | (A.ptag ? 2 : 0) | (A.npar ? 1 : 0);
+    hipLaunchKernelGGL(kfn[sel], dim3(nb), dim3(256), 0, s, A, parts + 1);
+  }
+  LenPart *mid = parts + 1 + nb;
+  hipLaunchKernelGGL(k_prilen_final, dim3(FINAL_GRID), dim3(256), 0, s, parts, nb + 1, mid,
+                     (pmx_len_part *)nullptr, ctx->d_tets.p, (const int2 *)ctx->d_pedge.p);
+  hipLaunchKernelGGL(k_prilen_final, dim3(1), dim3(256), 0, s, mid, FINAL_GRID, (LenPart *)nullptr,
+                     (pmx_len_part *)dev_result, ctx->d_tets.p, (const int2 *)ctx->d_pedge.p);
+  if (hipGetLastError() != hipSuccess) { ctx->err = "pmx_prilen: launch failed"; return 0; }
+  return 1;
 }
 
-int pmx_prilen(pmx_ctx *ctx, const uint16_t *point_tag, int64_t tag_stride, int metRidTyp,
-               pmx_len_stats *st) {
-  (void)metRidTyp;   // classic storage only: met->size 1 or 6 on every point
+int pmx_prilen(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, pmx_len_stats *st) {
   if (!ctx || !st) return 0;
   hipSetDevice(ctx->device);
-  uint16_t *dtag = nullptr;
-  if (point_tag) {
-    std::vector<uint16_t> h((size_t)(ctx->np + 1), 0);
-    for (int64_t i = 1; i <= ctx->np; i++)
-      h[(size_t)i] = *(const uint16_t *)((const char *)point_tag + i * tag_stride);
-    if (hipMalloc((void **)&dtag, h.size() * 2) != hipSuccess) return 0;
-    hipMemcpy(dtag, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+  if (!pmx_dgrow(ctx, ctx->d_pub, 32)) return 0;
+  if (!pmx_prilen_device(ctx, metRidTyp, par, ctx->d_pub.p)) return 0;
+  pmx_len_part r;
+  if (hipMemcpyAsync(&r, ctx->d_pub.p, sizeof r, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    ctx->err = "pmx_prilen: download";
+    return 0;
   }
-  int r = pmx_prilen_device(ctx, dtag, nullptr);
-  LenPart res;
-  if (r) {
-    r = hipStreamSynchronize(ctx->stream) == hipSuccess &&
-        hipMemcpy(&res, (LenPart *)ctx->d_red.p + len_res_slot(ctx), sizeof res, hipMemcpyDeviceToHost) == hipSuccess;
-  }
-  if (dtag) hipFree(dtag);
-  if (!r) return 0;
-  st->ned = res.ned;
-  st->nullEdge = res.nul;
-  st->avlen = res.avlen;
-  st->lmin = res.ned ? res.lmin : 1.e30;
-  st->lmax = res.lmax;
-  st->amin = st->bmin = st->amax = st->bmax = 0;
-  // endpoints from the first-occurrence keys
-  if (res.ned) {
-    TetRec t;
-    int64_t k = res.kmin / 6;
-    int ia = (int)(res.kmin % 6);
-    static const int ia0[6] = {0, 0, 0, 1, 1, 2}, ia1[6] = {1, 2, 3, 2, 3, 3};
-    hipMemcpy(&t, ctx->d_tets.p + k, sizeof t, hipMemcpyDeviceToHost);
-    st->amin = t.v[ia0[ia]];
-    st->bmin = t.v[ia1[ia]];
-    k = res.kmax / 6;
-    ia = (int)(res.kmax % 6);
-    hipMemcpy(&t, ctx->d_tets.p + k, sizeof t, hipMemcpyDeviceToHost);
-    st->amax = t.v[ia0[ia]];
-    st->bmax = t.v[ia1[ia]];
-  }
-  for (int i = 0; i < 9; i++) st->hl[i] = res.hl[i];
+  len_to_stats(r, st);
   return 1;
+}
+
+int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, int64_t ne, int opt,
+                      double *qual, void *dev_result) {
+  if (!ctx) return 0;
+  hipSetDevice(ctx->device);
+  if (!ctx->ran || !ctx->have_pts || ctx->out_n != ctx->nq) {
+    ctx->err = "pmx_new_mesh_qual: run a step on the new points first";
+    return 0;
+  }
+  if (!tetra_v || ne < 1 || tetra_stride < 16 || ne >= (1LL << 31)) {
+    ctx->err = "pmx_new_mesh_qual: bad new tets";
+    return 0;
+  }
+  // the new tets, 1-based, vertex indices in the points view's numbering
+  const int64_t first = ctx->pts_first, n = ctx->nq;
+  char *st = pmx_hstage(ctx, (size_t)(ne + 1) * 16);
+  if (!st) return 0;
+  int4 *h = (int4 *)st;
+  h[0] = make_int4(0, 0, 0, 0);
+  for (int64_t k = 1; k <= ne; k++) {
+    const int *v = (const int *)((const char *)tetra_v + k * tetra_stride);
+    h[k] = make_int4(v[0], v[1], v[2], v[3]);
+    if (v[0] <= 0) continue;
+    for (int l = 0; l < 4; l++)
+      if (v[l] < first || v[l] >= first + n) {
+        ctx->err = "pmx_new_mesh_qual: tet vertex outside the uploaded points";
+        return 0;
+      }
+  }
+  hipStream_t s = ctx->stream;
+  if (!pmx_dgrow(ctx, ctx->d_ntetv, (size_t)(ne + 1)) || !pmx_dgrow(ctx, ctx->d_nqual, (size_t)(ne + 1))) return 0;
+  if (hipMemcpyAsync(ctx->d_ntetv.p, h, (size_t)(ne + 1) * 16, hipMemcpyHostToDevice, s) != hipSuccess) {
+    ctx->err = "pmx_new_mesh_qual: upload";
+    return 0;
+  }
+  StatArgs A{};
+  A.xyz = reinterpret_cast<const double *>(ctx->d_q.p);   // Pt4 {x, y, z, 0}
+  A.xstride = 4;
+  A.vbase = (int)first;
+  A.tetv = ctx->d_ntetv.p;
+  A.ne = ne;
+  // the interpolated metric, in the step's output rows (a constant-size
+  // metric of the step is there too)
+  A.sol = ctx->d_out.p;
+  A.S = ctx->sd.S;
+  A.msize = ctx->sd.imet >= 0 ? ctx->sd.size[ctx->sd.imet] : 0;
+  A.moff = ctx->sd.imet >= 0 ? ctx->sd.off[ctx->sd.imet] : 0;
+  A.ptag = (opt == PMX_OUTQUA && ctx->have_qtag) ? ctx->d_qtag.p : nullptr;
+  const int nb = stat_blocks(ne);
+  if (A.msize == 6)
+    hipLaunchKernelGGL((k_qual<true, false>), dim3(nb), dim3(256), 0, s, A, ctx->d_nqual.p, (QualPart *)nullptr, 0);
+  else
+    hipLaunchKernelGGL((k_qual<false, false>), dim3(nb), dim3(256), 0, s, A, ctx->d_nqual.p, (QualPart *)nullptr, 0);
+  if (dev_result && !qual_partial(ctx, A, opt, ctx->d_nqual.p, 1, (pmx_qual_part *)dev_result, n)) return 0;
+  if (hipGetLastError() != hipSuccess) { ctx->err = "pmx_new_mesh_qual: launch"; return 0; }
+  if (qual) {
+    if (hipMemcpyAsync(qual, ctx->d_nqual.p, (size_t)(ne + 1) * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      ctx->err = "pmx_new_mesh_qual: download";
+      return 0;
+    }
+    qual[0] = 0.0;
+  }
+  return 1;
+}
+
+// ---- the reduction across ranks (host folds + RCCL) --------------------------------
+
+int pmx_qual_fold(const pmx_qual_part *parts, const int *rank, int n, pmx_qual_stats *out) {
+  if (!parts || !out || n < 1) return 0;
+  // per rank: the groups in order (PMMG_qualhisto's loop, :216-261: sums,
+  // strict max, strict min -> first group on ties); then the ranks in order
+  // with the reduce operators (:275-306, custom op :82-98: strict min ->
+  // lowest rank on ties)
+  memset(out, 0, sizeof *out);
+  bool first_rank = true;
+  int i = 0;
+  while (i < n) {
+    const int r = rank ? rank[i] : i;
+    pmx_qual_stats g;
+    memset(&g, 0, sizeof g);
+    g.max = 0.0;          // reference max = DBL_MIN; every partial's max is >= 0
+    g.min = 1.e300;       // DBL_MAX
+    int grp = 0;
+    const int i0 = i;
+    while (i < n && (rank ? rank[i] : i) == r) i++;
+    const bool single = i - i0 == 1;          // an already merged rank partial
+    for (int j = i0; j < i; j++, grp++) {
+      const pmx_qual_part &p = parts[j];
+      g.np += p.np; g.ne += p.ne; g.avg += p.avg; g.med += p.med; g.good += p.good; g.nrid += p.nrid;
+      if (p.max > g.max) g.max = p.max;
+      if (p.ne && p.min < g.min) { g.min = p.min; g.iel = p.iel; g.iel_grp = single ? (int)p.iel_grp : grp; }
+      for (int h = 0; h < 5; h++) g.his[h] += p.his[h];
+    }
+    g.cpu = r;
+    if (first_rank) {
+      *out = g;
+      first_rank = false;
+      continue;
+    }
+    out->np += g.np; out->ne += g.ne; out->avg += g.avg; out->med += g.med; out->good += g.good;
+    out->nrid += g.nrid;
+    if (g.max > out->max) out->max = g.max;
+    if (g.min < out->min) { out->min = g.min; out->iel = g.iel; out->iel_grp = g.iel_grp; out->cpu = g.cpu; }
+    for (int h = 0; h < 5; h++) out->his[h] += g.his[h];
+  }
+  return 1;
+}
+
+int pmx_len_fold(const pmx_len_part *parts, int n, pmx_len_stats *out) {
+  if (!parts || !out || n < 1) return 0;
+  // PMMG_compute_lenStats (:106-144) applied in rank order: sums; a strictly
+  // smaller lmin takes lmin, amin/bmin AND amax/bmax (the reference's quirk)
+  // and cpu_min; a strictly larger lmax takes lmax, amax/bmax and cpu_max
+  len_to_stats(parts[0], out);
+  out->cpu_min = out->cpu_max = 0;
+  for (int r = 1; r < n; r++) {
+    const pmx_len_part &in = parts[r];
+    out->avlen += in.avlen;
+    out->ned += in.ned;
+    out->nullEdge += in.nullEdge;
+    for (int j = 0; j < 9; j++) out->hl[j] += in.hl[j];
+    if (in.lmin < out->lmin) {
+      out->lmin = in.lmin; out->amin = in.amin; out->bmin = in.bmin;
+      out->amax = in.amax; out->bmax = in.bmax; out->cpu_min = r;
+    }
+    if (in.lmax > out->lmax) {
+      out->lmax = in.lmax; out->amax = in.amax; out->bmax = in.bmax; out->cpu_max = r;
+    }
+  }
+  return 1;
+}
+
+int pmx_comm_unique_id(char *id, int len) {
+  if (!id || len < (int)sizeof(ncclUniqueId)) return 0;
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return 0;
+  memcpy(id, &u, sizeof u);
+  return (int)sizeof u;
+}
+
+int pmx_comm_init(pmx_ctx *ctx, void **comm, int nranks, const char *id, int rank) {
+  if (!ctx || !comm || !id || nranks < 1 || rank < 0 || rank >= nranks) return 0;
+  hipSetDevice(ctx->device);
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof u);
+  ncclComm_t c;
+  const ncclResult_t r = ncclCommInitRank(&c, nranks, u, rank);
+  if (r != ncclSuccess) { ctx->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r); return 0; }
+  *comm = (void *)c;
+  return 1;
+}
+
+int pmx_comm_destroy(void *comm) {
+  if (!comm) return 0;
+  return ncclCommDestroy((ncclComm_t)comm) == ncclSuccess ? 1 : 0;
+}
+
+// one all-gather of each rank's partial (records of `bytes`), on the context stream
+static bool gather_parts(pmx_ctx *ctx, void *comm, int nranks, const void *dev_part, size_t bytes,
+                         std::vector<char> &host) {
+  hipStream_t s = ctx->stream;
+  if (!pmx_dgrow(ctx, ctx->d_gather, (size_t)nranks * bytes / 8 + 1)) return false;
+  const ncclResult_t r = ncclAllGather(dev_part, ctx->d_gather.p, bytes / 8, ncclInt64, (ncclComm_t)comm, s);
+  if (r != ncclSuccess) { ctx->err = std::string("ncclAllGather: ") + ncclGetErrorString(r); return false; }
+  host.resize((size_t)nranks * bytes);
+  if (hipMemcpyAsync(host.data(), ctx->d_gather.p, host.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    ctx->err = "stats all-gather: download";
+    return false;
+  }
+  return true;
+}
+
+int pmx_qualhisto_allreduce(pmx_ctx *ctx, void *comm, int nranks, const void *dev_parts, int ngrp,
+                            pmx_qual_stats *out) {
+  if (!ctx || !comm || !dev_parts || !out || nranks < 1 || ngrp < 1) return 0;
+  hipSetDevice(ctx->device);
+  hipStream_t s = ctx->stream;
+  // the rank's groups merged first (PMMG_qualhisto's group loop), then one
+  // record per rank all-gathered
+  std::vector<pmx_qual_part> g((size_t)ngrp);
+  if (hipMemcpyAsync(g.data(), dev_parts, g.size() * sizeof(pmx_qual_part), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    ctx->err = "pmx_qualhisto_allreduce: download";
+    return 0;
+  }
+  pmx_qual_stats m;
+  std::vector<int> zero((size_t)ngrp, 0);
+  pmx_qual_fold(g.data(), zero.data(), ngrp, &m);
+  pmx_qual_part mine;
+  mine.avg = m.avg; mine.max = m.max; mine.min = m.min; mine.iel = m.iel; mine.ne = m.ne; mine.np = m.np;
+  mine.good = m.good; mine.med = m.med; mine.nrid = m.nrid;
+  for (int h = 0; h < 5; h++) mine.his[h] = m.his[h];
+  mine.iel_grp = m.iel_grp;
+  if (!pmx_dgrow(ctx, ctx->d_pub, 32) ||
+      hipMemcpyAsync(ctx->d_pub.p, &mine, sizeof mine, hipMemcpyHostToDevice, s) != hipSuccess) {
+    ctx->err = "pmx_qualhisto_allreduce: upload";
+    return 0;
+  }
+  std::vector<char> h;
+  if (!gather_parts(ctx, comm, nranks, ctx->d_pub.p, sizeof(pmx_qual_part), h)) return 0;
+  return pmx_qual_fold((const pmx_qual_part *)h.data(), nullptr, nranks, out);
+}
+
+int pmx_prilen_allreduce(pmx_ctx *ctx, void *comm, int nranks, const void *dev_part, pmx_len_stats *out) {
+  if (!ctx || !comm || !dev_part || !out || nranks < 1) return 0;
+  hipSetDevice(ctx->device);
+  std::vector<char> h;
+  if (!gather_parts(ctx, comm, nranks, dev_part, sizeof(pmx_len_part), h)) return 0;
+  return pmx_len_fold((const pmx_len_part *)h.data(), nranks, out);
 }
 
 }  // extern "C"

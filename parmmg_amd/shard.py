@@ -4,26 +4,27 @@ ParMmg groups are interpolated independently (reference
 src/interpmesh_pmmg.c:690-730), so the data path has no collective: each rank
 (= one MPI rank of ParMmg, one GPU) transfers its own groups.  The only
 exchange is the statistics reduction that PMMG_qualhisto / PMMG_prilen do with
-MPI_Reduce and custom ops (src/quality_pmmg.c:82-144, :275-306, :664-675);
-here it is an all-reduce over RCCL (``torch.distributed`` backend "nccl") of
-device-resident partials -- or gloo on CPU tensors in the tests.
-
-RCCL has no user-defined ops, so "min with location" is two reductions: MIN of
-the value, then MIN of a packed (rank, group, element) key over the ranks
-whose value equals the global minimum.
+MPI_Reduce and custom operators (src/quality_pmmg.c:82-144, :265-307,
+:661-676).  RCCL has no user-defined operators, so the reduction is ONE
+all-gather of the per-rank partial records (a few hundred bytes) followed by
+the reference's operators folded in rank order by the library's host folds
+(pmx_qual_fold / pmx_len_fold, the same code the C ABI's RCCL path runs):
+deterministic, ties to the lowest rank, the prilen operator's quirk kept.
+Here the all-gather is ``torch.distributed`` (backend "nccl" = RCCL on device
+tensors, or gloo on CPU tensors in the tests); C callers use
+pmx_qualhisto_allreduce / pmx_prilen_allreduce on an ncclComm_t directly.
 """
 from __future__ import annotations
 
+import ctypes as C
+
+import numpy as np
 import torch
 
-KEY_MAX = (1 << 63) - 1
+from . import _native as N
 
-# layout of the device partial written by pmx_qualhisto_device (12 x 8 bytes)
-QUAL_F64 = ("avg", "max", "min")
-QUAL_I64 = ("iel", "ne", "good", "med", "his0", "his1", "his2", "his3", "his4")
-# layout of the device partial written by pmx_prilen_device (16 x 8 bytes)
-LEN_F64 = ("avlen", "lmin", "lmax")
-LEN_I64 = ("kmin", "kmax", "ned", "nullEdge") + tuple(f"hl{i}" for i in range(9))
+QUAL_WORDS = C.sizeof(N.QualPart) // 8     # 15
+LEN_WORDS = C.sizeof(N.LenPart) // 8       # 18
 
 
 def groups_for_rank(ngrp: int, rank: int, world: int) -> list[int]:
@@ -33,75 +34,94 @@ def groups_for_rank(ngrp: int, rank: int, world: int) -> list[int]:
     return list(range(lo, lo + per + (1 if rank < rem else 0)))
 
 
-def pack_key(rank: int, grp: int, iel: int) -> int:
-    return (rank << 48) | (grp << 36) | iel
+def _gather(part: torch.Tensor, dist) -> np.ndarray:
+    """All-gather of one float64 record per rank -> (world, words) host array."""
+    world = dist.get_world_size()
+    out = [torch.empty_like(part) for _ in range(world)]
+    dist.all_gather(out, part.contiguous())
+    return torch.stack(out).cpu().numpy().astype(np.float64, copy=False)
 
 
-def unpack_key(k: int) -> tuple[int, int, int]:
-    return k >> 48, (k >> 36) & 0xFFF, k & ((1 << 36) - 1)
+def _qdict(st) -> dict:
+    d = {f: getattr(st, f) for f, _ in N.QualStats._fields_}
+    d["his"] = list(st.his)
+    return d
 
 
-def _minloc(val: torch.Tensor, key: torch.Tensor, dist, op_min) -> tuple[float, int]:
-    v = val.clone()
-    dist.all_reduce(v, op=op_min)
-    k = torch.where(val == v, key, torch.full_like(key, KEY_MAX))
-    dist.all_reduce(k, op=op_min)
-    return float(v.item()), int(k.item())
+def _ldict(st) -> dict:
+    d = {f: getattr(st, f) for f, _ in N.LenStats._fields_}
+    d["hl"] = list(st.hl)
+    return d
 
 
-def reduce_qual(part: torch.Tensor, rank: int, grp: int, dist) -> dict:
-    """part: float64 tensor of 12 entries laid out as QUAL_F64 + QUAL_I64
-    (device or CPU).  Returns the global statistics on every rank."""
-    f = part[:3].clone()
-    i = part.view(torch.int64)[3:].clone()
-    R = dist.ReduceOp
-    sums = i[1:].clone()                      # ne, good, med, his[5]
-    dist.all_reduce(sums, op=R.SUM)
-    avg = f[0:1].clone()
-    dist.all_reduce(avg, op=R.SUM)
-    mx = f[1:2].clone()
-    dist.all_reduce(mx, op=R.MAX)
-    key = torch.tensor([pack_key(rank, grp, int(i[0].item()))], dtype=torch.int64, device=part.device)
-    mn, k = _minloc(f[2:3], key, dist, R.MIN)
-    s = sums.cpu().tolist()
-    r, g, iel = unpack_key(k)
-    return {"ne": s[0], "good": s[1], "med": s[2], "his": s[3:8], "avg": float(avg.item()),
-            "max": float(mx.item()), "min": mn, "min_rank": r, "min_grp": g, "iel": iel}
+def fold_qual(parts: np.ndarray, ranks=None) -> dict:
+    """parts: (n, 15) float64 words of pmx_qual_part records (groups of a rank
+    consecutive, ranks nondecreasing in ``ranks``; None = one record per rank)."""
+    a = np.ascontiguousarray(parts, np.float64).reshape(-1, QUAL_WORDS)
+    r = None if ranks is None else np.ascontiguousarray(ranks, np.int32)
+    st = N.QualStats()
+    lib = N.load()
+    if not lib.pmx_qual_fold(a.ctypes.data_as(C.POINTER(N.QualPart)),
+                             r.ctypes.data_as(N.iptr) if r is not None else None, a.shape[0],
+                             C.byref(st)):
+        raise RuntimeError("pmx_qual_fold failed")
+    return _qdict(st)
 
 
-def reduce_len(part: torch.Tensor, rank: int, dist) -> dict:
-    """part: float64 tensor of 16 entries laid out as LEN_F64 + LEN_I64."""
-    f = part[:3].clone()
-    i = part.view(torch.int64)[3:].clone()
-    R = dist.ReduceOp
-    sums = i[2:].clone()                      # ned, nullEdge, hl[9]
-    dist.all_reduce(sums, op=R.SUM)
-    av = f[0:1].clone()
-    dist.all_reduce(av, op=R.SUM)
-    kmin = torch.tensor([(rank << 40) | int(i[0].item())], dtype=torch.int64, device=part.device)
-    lmin, kmn = _minloc(f[1:2], kmin, dist, R.MIN)
-    # lmax: MAX of value, then MIN key among the maximisers
-    v = f[2:3].clone()
-    dist.all_reduce(v, op=R.MAX)
-    kmax = torch.tensor([(rank << 40) | int(i[1].item())], dtype=torch.int64, device=part.device)
-    kk = torch.where(f[2:3] == v, kmax, torch.full_like(kmax, KEY_MAX))
-    dist.all_reduce(kk, op=R.MIN)
-    s = sums.cpu().tolist()
-    return {"ned": s[0], "nullEdge": s[1], "hl": s[2:11], "avlen": float(av.item()),
-            "lmin": lmin, "lmin_rank": kmn >> 40, "lmax": float(v.item()),
-            "lmax_rank": int(kk.item()) >> 40}
+def fold_len(parts: np.ndarray) -> dict:
+    """parts: (nranks, 18) float64 words of pmx_len_part records, rank order."""
+    a = np.ascontiguousarray(parts, np.float64).reshape(-1, LEN_WORDS)
+    st = N.LenStats()
+    if not N.load().pmx_len_fold(a.ctypes.data_as(C.POINTER(N.LenPart)), a.shape[0], C.byref(st)):
+        raise RuntimeError("pmx_len_fold failed")
+    return _ldict(st)
 
 
-def qualhisto_allreduce(tr, dist, local: int, grp: int = 0) -> dict:
-    """Device partial of the uploaded group -> RCCL all-reduce."""
+def merge_groups(parts: np.ndarray) -> np.ndarray:
+    """The rank's group partials merged into one record (PMMG_qualhisto's group
+    loop, :216-261), iel_grp = the group of the minimum."""
+    d = fold_qual(parts, np.zeros(len(parts), np.int32))
+    rec = N.QualPart()
+    for f, _ in N.QualPart._fields_:
+        if f == "his":
+            for i in range(5):
+                rec.his[i] = d["his"][i]
+        elif f == "iel_grp":
+            rec.iel_grp = d["iel_grp"]
+        else:
+            setattr(rec, f, d[f])
+    return np.frombuffer(bytes(rec), np.float64).copy()
+
+
+def reduce_qual(group_parts, dist) -> dict:
+    """group_parts: (ngrp, 15) records of this rank's groups (torch tensor on
+    the device or the CPU, or numpy).  Returns the global statistics on every
+    rank: PMMG_qualhisto's reduction (cpu = the rank of the minimum)."""
+    p = group_parts.detach().cpu().numpy() if isinstance(group_parts, torch.Tensor) else group_parts
+    mine = torch.from_numpy(merge_groups(np.asarray(p, np.float64).reshape(-1, QUAL_WORDS)))
+    dev = group_parts.device if isinstance(group_parts, torch.Tensor) else torch.device("cpu")
+    if dist.get_backend() == "nccl":
+        mine = mine.to(dev)
+    return fold_qual(_gather(mine, dist))
+
+
+def reduce_len(part, dist) -> dict:
+    """part: this rank's pmx_len_part record (one group per rank, as
+    PMMG_prilen requires, :623-627)."""
+    t = part if isinstance(part, torch.Tensor) else torch.from_numpy(np.asarray(part, np.float64))
+    return fold_len(_gather(t.reshape(-1), dist))
+
+
+def qualhisto_allreduce(tr, dist, local: int) -> dict:
+    """Device partial of the uploaded group -> all-gather over the process group."""
+    import time
     dev = torch.device("cuda", local)
-    part = torch.zeros(12, dtype=torch.float64, device=dev)
+    part = torch.zeros(QUAL_WORDS, dtype=torch.float64, device=dev)
     tr.qualhisto_device(part.data_ptr())
     tr.synchronize()
-    import time
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    res = reduce_qual(part, dist.get_rank(), grp, dist)
+    res = reduce_qual(part.reshape(1, -1), dist)
     torch.cuda.synchronize()
     res["allreduce_ms"] = (time.perf_counter() - t0) * 1e3
     return res

@@ -34,6 +34,20 @@ def _ip(a):
     return a.ctypes.data_as(N.iptr) if a is not None else None
 
 
+def _shift(a, rec: int, ctype):
+    """Pointer to record -1 of a 0-based array: a 1-based view (the library
+    only dereferences records first..last >= 1)."""
+    return C.cast(C.c_void_p(a.ctypes.data - rec), C.POINTER(ctype))
+
+
+def _tets_1based(tets) -> np.ndarray:
+    """0-based new tets (v[0] < 0: deleted) -> Mmg's 1-based records (v[0] = 0)."""
+    tv = np.ascontiguousarray(tets, np.int32) + 1
+    tv[tv[:, 0] < 0, 0] = 0
+    tv[0] = 0
+    return tv
+
+
 def mesh_view(m: Mesh) -> N.MeshView:
     v = N.MeshView()
     v.np, v.ne, v.nt = m.np, m.ne, m.nt
@@ -112,18 +126,20 @@ class Transfer:
                       tets: np.ndarray | None = None):
         """xyz: (n, 3) new points (0-based list); tags: MMG5_Point.tag values;
         tets: optional (ne+1, 4) new tets with 0-based point indices in rows
-        1..ne -- only points of valid tets (v[0] >= 0 here) are located."""
+        1..ne -- only points of valid tets (v[0] >= 0 here) are located.
+        The C view is Mmg's 1-based one (points 1..n, a tet valid when
+        v[0] > 0), so the pointers are shifted by one record."""
         xyz = np.ascontiguousarray(xyz, np.float64)
         pv = N.PointsView()
-        pv.first, pv.last = 0, xyz.shape[0] - 1
-        pv.c, pv.stride = _dp(xyz), 24
+        pv.first, pv.last = 1, xyz.shape[0]
+        pv.c, pv.stride = _shift(xyz, 24, C.c_double), 24
         self._keep = []
         if tags is not None:
             t = np.ascontiguousarray(tags, np.uint16)
             self._keep.append(t)
-            pv.tag, pv.tag_stride = t.ctypes.data_as(N.u16ptr), 2
+            pv.tag, pv.tag_stride = _shift(t, 2, C.c_uint16), 2
         if tets is not None:
-            tv = np.ascontiguousarray(tets, np.int32)
+            tv = _tets_1based(tets)
             self._keep.append(tv)
             pv.tetra_v, pv.tetra_stride, pv.ne = _ip(tv), 16, tv.shape[0] - 1
         self._chk(self.lib.pmx_upload_points(self.ctx, C.byref(pv)), "pmx_upload_points")
@@ -266,33 +282,115 @@ class Transfer:
         return self.lib.PMX_interpMetricsAndFields(self.ctx, len(groups), G, _ip(perm), input_met)
 
     # ---- statistics -----------------------------------------------------------
+    def upload_point_tags(self, tags: np.ndarray | None):
+        """MMG5_Point.tag of the uploaded background, (np+1,) (ridge points for
+        the length filter and OUTQUA's nrid)."""
+        t = None if tags is None else np.ascontiguousarray(tags, np.uint16)
+        self._keep_tags = t
+        self._chk(self.lib.pmx_upload_point_tags(self.ctx, t.ctypes.data_as(N.u16ptr) if t is not None
+                                                 else None, 2), "pmx_upload_point_tags")
+
     def tetra_qual(self, ne: int) -> np.ndarray:
         q = np.zeros(ne + 1)
         self._chk(self.lib.pmx_tetra_qual(self.ctx, _dp(q)), "pmx_tetra_qual")
         return q
 
-    def qualhisto(self) -> dict:
-        st = N.QualStats()
-        self._chk(self.lib.pmx_qualhisto(self.ctx, C.byref(st)), "pmx_qualhisto")
+    def count_nodes(self, idx_ip=None, idx_comm=None, intvalues=None, base: int = 1) -> int:
+        """PMMG_count_nodes_par on the uploaded group; intvalues is updated in place."""
+        n_grp = 0 if idx_ip is None else len(idx_ip)
+        ip = np.ascontiguousarray(idx_ip if idx_ip is not None else [], np.int32)
+        ic = np.ascontiguousarray(idx_comm if idx_comm is not None else [], np.int32)
+        iv = intvalues if intvalues is not None else np.zeros(0, np.int32)
+        assert iv.dtype == np.int32 and iv.flags.c_contiguous
+        out = C.c_int64()
+        self._chk(self.lib.pmx_count_nodes(self.ctx, _ip(ip), _ip(ic), n_grp, _ip(iv), len(iv), base,
+                                           C.byref(out)), "pmx_count_nodes")
+        return out.value
+
+    @staticmethod
+    def _qdict(st) -> dict:
         d = {f: getattr(st, f) for f, _ in N.QualStats._fields_}
         d["his"] = list(st.his)
         return d
 
-    def qualhisto_device(self, dev_ptr: int, use_stored: bool = False):
-        self._chk(self.lib.pmx_qualhisto_device(self.ctx, int(use_stored), C.c_void_p(dev_ptr)),
-                  "pmx_qualhisto_device")
-
-    def prilen_device(self, dev_ptr: int, dev_tag_ptr: int = 0):
-        self._chk(self.lib.pmx_prilen_device(self.ctx, C.c_void_p(dev_tag_ptr or None),
-                                             C.c_void_p(dev_ptr)), "pmx_prilen_device")
-
-    def prilen(self, tags: np.ndarray | None = None, met_rid_typ: int = 0) -> dict:
-        st = N.LenStats()
-        t = None
-        if tags is not None:
-            t = np.ascontiguousarray(tags, np.uint16)
-        self._chk(self.lib.pmx_prilen(self.ctx, t.ctypes.data_as(N.u16ptr) if t is not None else None,
-                                      2, met_rid_typ, C.byref(st)), "pmx_prilen")
+    @staticmethod
+    def _ldict(st) -> dict:
         d = {f: getattr(st, f) for f, _ in N.LenStats._fields_}
         d["hl"] = list(st.hl)
         return d
+
+    def qualhisto(self, opt: int = N.INQUA) -> dict:
+        st = N.QualStats()
+        self._chk(self.lib.pmx_qualhisto(self.ctx, opt, C.byref(st)), "pmx_qualhisto")
+        return self._qdict(st)
+
+    def qualhisto_device(self, dev_ptr: int, opt: int = N.INQUA, use_stored: bool = False):
+        self._chk(self.lib.pmx_qualhisto_device(self.ctx, opt, int(use_stored), C.c_void_p(dev_ptr)),
+                  "pmx_qualhisto_device")
+
+    @staticmethod
+    def _par(par: dict | None):
+        if par is None:
+            return None, []
+        a = np.ascontiguousarray(par["a"], np.int32)
+        b = np.ascontiguousarray(par["b"], np.int32)
+        o = np.ascontiguousarray(par["owner"], np.int32)
+        pe = N.ParEdges()
+        pe.n, pe.a, pe.b, pe.owner = len(a), _ip(a), _ip(b), _ip(o)
+        pe.myrank, pe.exact_once = int(par.get("myrank", 0)), int(par.get("exact_once", 0))
+        return C.byref(pe), [a, b, o, pe]
+
+    def prilen(self, met_rid_typ: int = 0, par: dict | None = None) -> dict:
+        """par: {"a", "b", "owner", "myrank", "exact_once"} (distributed PMMG_prilen)."""
+        st = N.LenStats()
+        pp, keep = self._par(par)
+        self._chk(self.lib.pmx_prilen(self.ctx, met_rid_typ, pp, C.byref(st)), "pmx_prilen")
+        del keep
+        return self._ldict(st)
+
+    def prilen_device(self, dev_ptr: int, met_rid_typ: int = 0, par: dict | None = None):
+        pp, keep = self._par(par)
+        self._chk(self.lib.pmx_prilen_device(self.ctx, met_rid_typ, pp, C.c_void_p(dev_ptr)),
+                  "pmx_prilen_device")
+        del keep
+
+    def new_mesh_qual(self, tets: np.ndarray, opt: int = N.INQUA, dev_ptr: int = 0) -> np.ndarray:
+        """PMMG_tetraQual on the new mesh after the last step: tets (ne+1, 4)
+        with indices of the uploaded points (0-based here, v[0] < 0: deleted)."""
+        tv = _tets_1based(tets)
+        q = np.zeros(tv.shape[0])
+        self._chk(self.lib.pmx_new_mesh_qual(self.ctx, _ip(tv), 16, tv.shape[0] - 1, opt, _dp(q),
+                                             C.c_void_p(dev_ptr or None)), "pmx_new_mesh_qual")
+        return q
+
+    def comm_init(self, nranks: int, uid: bytes, rank: int) -> int:
+        c = C.c_void_p()
+        self._chk(self.lib.pmx_comm_init(self.ctx, C.byref(c), nranks, uid, rank), "pmx_comm_init")
+        return c.value
+
+    @staticmethod
+    def comm_destroy(comm: int):
+        if comm and not N.load().pmx_comm_destroy(C.c_void_p(comm)):
+            raise RuntimeError("pmx_comm_destroy failed")
+
+    def qualhisto_allreduce(self, comm: int, nranks: int, dev_ptr: int, ngrp: int = 1) -> dict:
+        st = N.QualStats()
+        self._chk(self.lib.pmx_qualhisto_allreduce(self.ctx, C.c_void_p(comm), nranks,
+                                                   C.c_void_p(dev_ptr), ngrp, C.byref(st)),
+                  "pmx_qualhisto_allreduce")
+        return self._qdict(st)
+
+    def prilen_allreduce(self, comm: int, nranks: int, dev_ptr: int) -> dict:
+        st = N.LenStats()
+        self._chk(self.lib.pmx_prilen_allreduce(self.ctx, C.c_void_p(comm), nranks, C.c_void_p(dev_ptr),
+                                                C.byref(st)), "pmx_prilen_allreduce")
+        return self._ldict(st)
+
+
+def comm_unique_id() -> bytes:
+    lib = N.load()
+    buf = C.create_string_buffer(256)
+    n = lib.pmx_comm_unique_id(buf, 256)
+    if not n:
+        raise RuntimeError("pmx_comm_unique_id failed")
+    return buf.raw[:n]

@@ -33,6 +33,38 @@ def cube_case(n: int, metric: str = "iso", surface: bool = True, fields: bool = 
     return m, x, t, sols
 
 
+def split_partitions(m, cut: float = 0.5):
+    """Two ParMmg partitions of a mesh (tets with centroid x < cut, the rest),
+    each renumbered locally, and their parallel (interface) edges in local
+    numbering: [(mesh_r, glob_r, par_r)] with par_r = {"a", "b", "owner"},
+    owner = the lowest rank sharing the edge (0), orientation (min, max) of
+    the global ids (the same edge on both sides)."""
+    IARE = [(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)]
+    c = m.centroids()
+    sides = [np.nonzero(c[:, 0] < cut)[0] + 1, np.nonzero(c[:, 0] >= cut)[0] + 1]
+    edges = []
+    for ks in sides:
+        t = m.tet[ks]
+        e = np.concatenate([np.sort(t[:, [i, j]], axis=1) for i, j in IARE])
+        edges.append(set(map(tuple, e)))
+    shared = sorted(edges[0] & edges[1])
+    out = []
+    for r, ks in enumerate(sides):
+        glob = np.unique(m.tet[ks].ravel())                  # local ip -> global, 0-based
+        loc = np.zeros(m.np + 1, np.int32)
+        loc[glob] = np.arange(1, len(glob) + 1)
+        xyz = np.zeros((len(glob) + 1, 3))
+        xyz[1:] = m.xyz[glob]
+        tet = np.zeros((len(ks) + 1, 4), np.int32)
+        tet[1:] = loc[m.tet[ks]]
+        mr = M.from_tets(xyz, tet)
+        par = {"a": np.array([loc[a] for a, b in shared], np.int32),
+               "b": np.array([loc[b] for a, b in shared], np.int32),
+               "owner": np.zeros(len(shared), np.int32), "myrank": r}
+        out.append((mr, np.concatenate([[0], glob]), par))
+    return out, len(shared)
+
+
 def bits_equal(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     """Row-wise bitwise equality of float64 arrays (NaN == NaN)."""
     a = np.ascontiguousarray(a, np.float64).view(np.int64)

@@ -171,13 +171,13 @@ def _stats_rank(rank, port, q):
     met = Mm.on_vertices(m, Mm.iso_metric)
     tr = T(0)
     tr.upload_background(m, [met], 0)
-    dq = torch.zeros(12, dtype=torch.float64, device="cuda:0")
-    dl = torch.zeros(16, dtype=torch.float64, device="cuda:0")
+    dq = torch.zeros(shard.QUAL_WORDS, dtype=torch.float64, device="cuda:0")
+    dl = torch.zeros(shard.LEN_WORDS, dtype=torch.float64, device="cuda:0")
     tr.qualhisto_device(dq.data_ptr())
     tr.prilen_device(dl.data_ptr())
     tr.synchronize()
-    rq = shard.reduce_qual(dq.cpu(), rank, 0, dist)
-    rl = shard.reduce_len(dl.cpu(), rank, dist)
+    rq = shard.reduce_qual(dq.cpu().reshape(1, -1), dist)
+    rl = shard.reduce_len(dl.cpu(), dist)
     tr.close()
     q.put((rank, rq, rl))
     dist.destroy_process_group()
@@ -211,7 +211,7 @@ def test_c5_device_partials_reduced_across_two_ranks():
     assert rq0["good"] == qs[0]["good"] + qs[1]["good"] and rq0["med"] == qs[0]["med"] + qs[1]["med"]
     assert rq0["max"] == max(qs[0]["max"], qs[1]["max"])
     w = 0 if qs[0]["min"] <= qs[1]["min"] else 1
-    assert rq0["min"] == qs[w]["min"] and rq0["min_rank"] == w and rq0["iel"] == qs[w]["iel"]
+    assert rq0["min"] == qs[w]["min"] and rq0["cpu"] == w and rq0["iel"] == qs[w]["iel"]
     assert abs(rq0["avg"] - (qs[0]["avg"] + qs[1]["avg"])) <= 1e-12 * abs(rq0["avg"])
     assert rl0["ned"] == ls[0]["ned"] + ls[1]["ned"]
     assert sum(abs(a - b - c) for a, b, c in zip(rl0["hl"], ls[0]["hl"], ls[1]["hl"])) <= 4

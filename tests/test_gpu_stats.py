@@ -1,0 +1,221 @@
+"""GPU statistics (PMMG_qualhisto / PMMG_prilen / PMMG_tetraQual) against the oracle.
+
+* ridge points (MMG5_Point.tag): the length loop's 4-ridge filter
+  (reference src/quality_pmmg.c:509-517) and MMG3D_computeOutqua's nrid;
+* PMMG_count_nodes_par (:33-80) against the oracle's restatement;
+* the distributed prilen of a partition with parallel edges (:398-502), in the
+  reference's semantics (interface edges counted by both ranks, :585-586) and
+  exactly once;
+* the quality of the NEW mesh right after the interpolation
+  (src/libparmmg1.c:845): per-tet qualities bit-exact against the oracle's
+  MMG3D_tetraQual on the new mesh with the same metric;
+* the RCCL reduction with one rank equals the host fold of the same partial.
+
+Sums (avg, avlen) are compared within 1e-12 relative: the device reduces in a
+different order than the reference's sequential loop; everything else (counts,
+histograms, minima/maxima and the elements realising them, per-tet qualities)
+is exact.  Edge-length histogram bins may differ for lengths within an ulp of
+a bin boundary (the length is the same formula but a different operation
+order); the tests allow a couple of such edges.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import compare_volume, cube_case, split_partitions
+from oracle import oracle as O
+from parmmg_amd import _native as N
+from parmmg_amd import mesh as M
+from parmmg_amd import shard
+from parmmg_amd.transfer import Transfer, comm_unique_id
+
+pytestmark = pytest.mark.gpu
+
+GEO, REQ, NOM, CRN = 2, 4, 8, 32
+
+
+def assert_len_equal(L, Lo, hl_slack=2):
+    assert L["ned"] == Lo["ned"] and L["nullEdge"] == Lo["nullEdge"]
+    assert sum(abs(a - b) for a, b in zip(L["hl"], Lo["hl"])) <= hl_slack
+    assert abs(L["avlen"] - Lo["avlen"]) <= 1e-12 * abs(Lo["avlen"])
+    assert abs(L["lmin"] - Lo["lmin"]) <= 1e-14 * Lo["lmin"]
+    assert abs(L["lmax"] - Lo["lmax"]) <= 1e-14 * Lo["lmax"]
+    if L["lmin"] == Lo["lmin"]:
+        assert (L["amin"], L["bmin"]) == (Lo["amin"], Lo["bmin"])
+    if L["lmax"] == Lo["lmax"]:
+        assert (L["amax"], L["bmax"]) == (Lo["amax"], Lo["bmax"])
+
+
+def assert_qual_equal(h, ho):
+    for f in ("ne", "iel", "good", "med", "min", "max", "nrid"):
+        assert h[f] == ho[f], f
+    assert h["his"] == ho["his"]
+    assert abs(h["avg"] - ho["avg"]) <= 1e-12 * abs(ho["avg"])
+
+
+def ridge_tags(m, seed=3):
+    """Ridge points on the x < 0.4 slab (mixed with singular / non-manifold
+    ones that are NOT ridge points for the filter)."""
+    rng = np.random.default_rng(seed)
+    tags = np.zeros(m.np + 1, np.uint16)
+    slab = np.nonzero(m.xyz[:, 0] < 0.4)[0]
+    slab = slab[slab > 0]
+    tags[slab] = GEO
+    extra = rng.choice(slab, size=len(slab) // 6, replace=False)
+    tags[extra[: len(extra) // 3]] |= REQ
+    tags[extra[len(extra) // 3: 2 * len(extra) // 3]] |= NOM
+    tags[extra[2 * len(extra) // 3:]] |= CRN
+    return tags
+
+
+@pytest.mark.parametrize("metric", ["iso", "ani"])
+def test_ridge_filter_and_outqua(transfer, metric):
+    m, x, t, sols = cube_case(7, metric=metric, fields=False)
+    tags = ridge_tags(m)
+    transfer.upload_background(m, sols, 0)
+    transfer.upload_point_tags(tags)
+    L = transfer.prilen()
+    Lo = O.prilen(m, sols[0], tags=tags)
+    Lall = O.prilen(m, sols[0])
+    assert Lo["ned"] + Lo["nullEdge"] < Lall["ned"] + Lall["nullEdge"], "the filter must bite"
+    assert_len_equal(L, Lo)
+    qo = O.tetra_qual(m, sols[0] if metric == "ani" else None)
+    h = transfer.qualhisto(N.OUTQUA)
+    ho = O.qualhisto(m, qo, tags=tags)
+    assert ho["nrid"] > 0
+    assert_qual_equal(h, ho)
+    hin = transfer.qualhisto(N.INQUA)
+    assert hin["nrid"] == 0 and hin["ne"] == ho["ne"]
+    # tags dropped: the filter is off again
+    transfer.upload_point_tags(None)
+    assert_len_equal(transfer.prilen(), Lall)
+
+
+def test_count_nodes_matches_oracle(transfer):
+    m = M.kuhn_cube(6)
+    transfer.upload_background(m, [M.on_vertices(m, M.iso_metric)], 0)
+    rng = np.random.default_rng(11)
+    nitem = 60
+    idx_ip = rng.choice(np.arange(1, m.np + 1), size=45, replace=False).astype(np.int32)
+    idx_comm = rng.choice(nitem, size=45, replace=False).astype(np.int32)
+    iv = np.zeros(nitem, np.int32)
+    iv[rng.choice(nitem, size=20, replace=False)] = 1     # nodes another rank counts
+    iv_o = iv.copy()
+    n = transfer.count_nodes(idx_ip, idx_comm, iv, base=1)
+    no = O.count_nodes(m, idx_ip, idx_comm, iv_o)
+    assert n == no and np.array_equal(iv, iv_o)
+    assert transfer.count_nodes() == m.np               # no communicator: touched points
+    # the partial carries the count
+    d = torch.zeros(shard.QUAL_WORDS, dtype=torch.float64, device="cuda:0")
+    transfer.count_nodes(idx_ip, idx_comm, np.zeros(nitem, np.int32))
+    transfer.qualhisto_device(d.data_ptr())
+    transfer.synchronize()
+    assert shard.fold_qual(d.cpu().numpy()[None])["np"] == O.count_nodes(
+        m, idx_ip, idx_comm, np.zeros(nitem, np.int32))
+
+
+@pytest.mark.parametrize("once", [0, 1])
+def test_distributed_prilen_partitions(transfer, once):
+    """Both partitions of a split cube: each rank's partial matches the
+    oracle's PMMG_computePrilen, and the two partials add up to the whole
+    cube's edges (plus the interface edges again in the reference's semantics)."""
+    full = M.kuhn_cube(6)
+    parts, nshared = split_partitions(full)
+    tot = 0
+    for rank, (mr, glob, par) in enumerate(parts):
+        met = M.on_vertices(mr, M.shock_metric)
+        p = dict(par, myrank=rank, owner=np.zeros(len(par["a"]), np.int32), exact_once=once)
+        transfer.upload_background(mr, [met], 0)
+        L = transfer.prilen(par=p)
+        Lo = O.prilen(mr, met, par=p)
+        assert_len_equal(L, Lo)
+        tot += L["ned"] + L["nullEdge"]
+    n = 6
+    edges = 3 * n * (n + 1) ** 2 + 3 * n * n * (n + 1) + n ** 3
+    assert tot == edges + (0 if once else nshared)
+
+
+@pytest.mark.parametrize("metric", ["iso", "ani"])
+def test_new_mesh_quality_after_interpolation(transfer, metric):
+    """PMMG_tetraQual on the new mesh right after PMMG_interpMetricsAndFields:
+    the new tets, the device-resident new points and interpolated metric."""
+    m, _, _, sols = cube_case(6, metric=metric, fields=False)
+    new = M.kuhn_cube(9, seed=77)                 # the "remeshed" group: another jittered cube
+    x = new.xyz[1:].copy()
+    t = np.zeros(len(x), np.uint16)
+    tets0 = new.tet.copy() - 1                    # 0-based point indices
+    tets0[0] = -1
+    transfer.upload_background(m, sols, 0)
+    transfer.upload_points(x, t, tets0)
+    transfer.run()
+    r = transfer.download()
+    q = transfer.new_mesh_qual(tets0, N.INQUA)
+    met = np.zeros((new.np + 1, sols[0].shape[1]))
+    met[1:] = r.sols[0]
+    qo = O.tetra_qual(new, met if metric == "ani" else None)
+    assert np.array_equal(q[1:], qo[1:]), "new-mesh quality not bit-exact"
+    # the partial of the new mesh (np = the points)
+    d = torch.zeros(shard.QUAL_WORDS, dtype=torch.float64, device="cuda:0")
+    transfer.new_mesh_qual(tets0, N.INQUA, d.data_ptr())
+    transfer.synchronize()
+    h = shard.fold_qual(d.cpu().numpy()[None])
+    ho = O.qualhisto(new, qo)
+    assert_qual_equal(dict(h, nrid=0), dict(ho, nrid=0))
+    assert h["np"] == len(x)
+    # the oracle's own interpolation (carry-over walk) gives the same metric
+    # on all but documented ties, hence the same qualities on their tets
+    o = O.Oracle(m)
+    outs, elem, st, *_ = o.interp(x, t, sols, imet=0)
+    same = np.all(outs[0].view(np.int64) == r.sols[0].view(np.int64), axis=1)
+    mo = np.zeros_like(met)
+    mo[1:] = outs[0]
+    qo2 = O.tetra_qual(new, mo if metric == "ani" else None)
+    c = compare_volume(o, x, t, (r.sols, r.elem, r.status), (outs, elem, st), sols)
+    assert c["same"] + c["ties"] == len(x)
+    # the new cube's boundary points lie on background faces: many ties there
+    good = np.all(same[new.tet[1:] - 1], axis=1)
+    assert good.mean() > 0.9
+    assert np.array_equal(q[1:][good], qo2[1:][good])
+
+
+def test_new_mesh_quality_deleted_tets_and_bad_index(transfer):
+    m, _, _, sols = cube_case(5, metric="ani", fields=False)
+    new = M.kuhn_cube(4, seed=5)
+    x = new.xyz[1:].copy()
+    tets0 = new.tet.copy() - 1
+    tets0[0] = -1
+    tets0[3, 0] = -1                               # deleted (!MG_EOK)
+    transfer.upload_background(m, sols, 0)
+    transfer.upload_points(x, np.zeros(len(x), np.uint16), tets0)
+    transfer.run()
+    r = transfer.download()
+    q = transfer.new_mesh_qual(tets0)
+    assert q[3] == 0.0 and np.all(q[4:] > 0)
+    bad = tets0.copy()
+    bad[2, 1] = len(x)                             # outside the uploaded points
+    with pytest.raises(RuntimeError, match="outside"):
+        transfer.new_mesh_qual(bad)
+
+
+def test_rccl_single_rank_equals_fold(transfer):
+    """pmx_qualhisto_allreduce / pmx_prilen_allreduce over a 1-rank RCCL
+    communicator: the all-gather + fold of the group partials equals the
+    host fold of the same partials."""
+    m, x, t, sols = cube_case(6, metric="ani", fields=False)
+    transfer.upload_background(m, sols, 0)
+    comm = transfer.comm_init(1, comm_unique_id(), 0)
+    try:
+        d = torch.zeros((2, shard.QUAL_WORDS), dtype=torch.float64, device="cuda:0")
+        transfer.qualhisto_device(d[0].data_ptr())
+        transfer.qualhisto_device(d[1].data_ptr())     # a second "group"
+        dl = torch.zeros(shard.LEN_WORDS, dtype=torch.float64, device="cuda:0")
+        transfer.prilen_device(dl.data_ptr())
+        transfer.synchronize()
+        rq = transfer.qualhisto_allreduce(comm, 1, d.data_ptr(), 2)
+        rl = transfer.prilen_allreduce(comm, 1, dl.data_ptr())
+    finally:
+        transfer.comm_destroy(comm)
+    fq = shard.fold_qual(d.cpu().numpy(), np.zeros(2, np.int32))
+    fl = shard.fold_len(dl.cpu().numpy()[None])
+    assert rq == fq and rl == fl
+    assert rq["ne"] == 2 * m.ne and rq["cpu"] == 0 and rq["iel_grp"] == 0

@@ -43,8 +43,9 @@ def main():
     tr.upload_background(m, [met], 0)
     t_setup = time.perf_counter() - t0
     dev = torch.device("cuda", 0)
-    qpart = torch.zeros(12, dtype=torch.float64, device=dev)
-    lpart = torch.zeros(16, dtype=torch.float64, device=dev)
+    from parmmg_amd import shard
+    qpart = torch.zeros(shard.QUAL_WORDS, dtype=torch.float64, device=dev)
+    lpart = torch.zeros(shard.LEN_WORDS, dtype=torch.float64, device=dev)
 
     def timed(fn):
         fn()

@@ -421,7 +421,7 @@ struct LenAcc {
 // IARE and the two other local vertices of edge ia, as nibble tables (no
 // constant-memory load for a per-lane index)
 __device__ __forceinline__ int iare0(int ia) { return (0x211000 >> (4 * ia)) & 15; }
-__device__ __forceinline__ int iare1(int ia) { return (0x323321 >> (4 * ia)) & 15; }
+__device__ __forceinline__ int iare1(int ia) { return (0x332321 >> (4 * ia)) & 15; }
 __device__ __forceinline__ int oth0(int ia) { return (0x000112 >> (4 * ia)) & 15; }
 __device__ __forceinline__ int oth1(int ia) { return (0x123233 >> (4 * ia)) & 15; }
 

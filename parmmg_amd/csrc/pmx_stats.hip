@@ -291,13 +291,6 @@ __device__ __forceinline__ int pick_nb(const TetRec &t, int l) {
          (t.nb[3] & -(int)(l == 3));
 }
 
-__device__ __forceinline__ int loc_of(const TetRec &t, int p) {
-  int l = 3;
-  if (t.v[0] == p) l = 0;
-  else if (t.v[1] == p) l = 1;
-  else if (t.v[2] == p) l = 2;
-  return l;
-}
 
 // MMG5_lenEdg_iso / lenEdg33_ani (restated, unpinned; the surface lengths
 // MMG5_lenSurfEdg_iso / lenSurfEdg33_ani of the parallel edges take the same
@@ -373,9 +366,12 @@ struct LenAcc {
   __device__ void add(bool on, double len, long long key) {
     if (!on) return;
     if (len == 0.0) { atomicAdd(&cnt[9], 1u); return; }
-    int bin = 8;
+    // bin i: BD[i] <= len < BD[i+1]; 8: len >= 5, negative or NaN -- the
+    // number of bounds BD[1..8] at or below len
+    int bin = 0;
 #pragma unroll
-    for (int i = 7; i >= 0; i--) bin = (BD[i] <= len && len < BD[i + 1]) ? i : bin;
+    for (int i = 1; i < 9; i++) bin += (len >= BD[i]) ? 1 : 0;
+    if (!(len >= 0.0)) bin = 8;
     atomicAdd(&cnt[bin], 1u);
     avlen += len;
     if (len < lmin || (len == lmin && key < kmin)) { lmin = len; kmin = key; }
@@ -430,15 +426,16 @@ __device__ __forceinline__ bool rec_4ridge(const StatArgs &A, const TetRec &t) {
   return tet_4ridge(A, v);
 }
 
-// the vertex of t that is none of a, b, keep
-__device__ __forceinline__ int other_vertex(const TetRec &t, int a, int b, int keep) {
-  int nk = 0;
-#pragma unroll
-  for (int l = 0; l < 4; l++) {
-    const int w = t.v[l];
-    nk = (w != a && w != b && w != keep) ? w : nk;
-  }
-  return nk;
+// One rotation step around the edge (a, b): the shell entered tet r through
+// its face (a, b, keep); the next tet is across the face (a, b, w) of r, i.e.
+// opposite keep, and w (the sum of r's vertices minus a, b, keep, in modular
+// arithmetic) is the vertex of the face crossed next.
+__device__ __forceinline__ int rotate_step(const TetRec &r, int a, int b, int &keep) {
+  const bool e0 = r.v[0] == keep, e1 = r.v[1] == keep, e2 = r.v[2] == keep;
+  const int nb = e0 ? r.nb[0] : e1 ? r.nb[1] : e2 ? r.nb[2] : r.nb[3];
+  keep = (int)((unsigned)r.v[0] + (unsigned)r.v[1] + (unsigned)r.v[2] + (unsigned)r.v[3] -
+               (unsigned)a - (unsigned)b - (unsigned)keep);
+  return nb;
 }
 
 // True iff no admissible tet with index < k contains the edge (a, b) of tet
@@ -464,13 +461,11 @@ __device__ bool owns_edge(const StatArgs &A, int64_t k, int a, int b, int c0, in
     int n0 = 0, n1 = 0;
     if (c0) {
       if (TAGS && c0 < k && !rec_4ridge(A, r0)) return false;
-      n0 = pick_nb(r0, loc_of(r0, keep0));
-      keep0 = other_vertex(r0, a, b, keep0);
+      n0 = rotate_step(r0, a, b, keep0);
     }
     if (c1) {
       if (TAGS && c1 < k && !rec_4ridge(A, r1)) return false;
-      n1 = pick_nb(r1, loc_of(r1, keep1));
-      keep1 = other_vertex(r1, a, b, keep1);
+      n1 = rotate_step(r1, a, b, keep1);
     }
     // closed shell: the next tet of one direction is the one the other just saw
     if (c0 && c1 && (n0 == c1 || n1 == c0)) return true;
@@ -592,17 +587,18 @@ __global__ __launch_bounds__(256) void k_prilen(StatArgs A, LenPart *parts) {
       if (tid < cnt) {
         const unsigned it = q[(head + tid) & (LEN_QCAP - 1)];
         const int eb = (int)(it >> 11), slot = (int)((it >> 3) & 255u), ia = (int)(it & 7u);
-        const TetRec t = srec[eb][slot];
+        // the record's fields by LDS address (no per-lane selects)
+        const int *sv = srec[eb][slot].v, *sn = srec[eb][slot].nb;
         const int64_t kk = kbase[eb] + slot;
-        const int a = pick_v(t, iare0(ia)), b = pick_v(t, iare1(ia));
         const int o0 = oth0(ia), o1 = oth1(ia);
-        const int c0 = pick_nb(t, o0), c1 = pick_nb(t, o1);
+        const int a = sv[iare0(ia)], b = sv[iare1(ia)], keep0 = sv[o1], keep1 = sv[o0];
+        const int c0 = sn[o0], c1 = sn[o1];
         // the first rotation step's records, issued with the points' loads
         TetRec r0{}, r1{};
         if (c0) r0 = A.tets[c0];
         if (c1) r1 = A.tets[c1];
         len = edge_len_t<ANI>(A, a, b);
-        on = owns_edge<TAGS>(A, kk, a, b, c0, c1, pick_v(t, o1), pick_v(t, o0), r0, r1) &&
+        on = owns_edge<TAGS>(A, kk, a, b, c0, c1, keep0, keep1, r0, r1) &&
              !(PAR && par_excluded(A, a, b));
         key = LEN_STEP2 + 6 * kk + ia;
       }
@@ -610,6 +606,7 @@ __global__ __launch_bounds__(256) void k_prilen(StatArgs A, LenPart *parts) {
       head += cnt;
     }
     if (more) {                                  // no entry of the previous batch is left
+      __syncthreads();                           // ... once every wave is past its rounds
       int4 *srow = reinterpret_cast<int4 *>(&srec[buf ^ 1][tid]);
       srow[0] = pv;
       srow[1] = pn;

@@ -144,6 +144,9 @@ def test_c5_share_stats_counts():
     L = tr.prilen()
     assert L["ned"] + L["nullEdge"] == kuhn_edges(n)
     assert sum(L["hl"]) == L["ned"]
+    # deterministic: the same partials and the same fixed-order reduction
+    for _ in range(3):
+        assert tr.prilen() == L and tr.qualhisto() == q
     tr.close()
 
 

@@ -239,6 +239,34 @@ typedef struct {
   int64_t hl[9];
 } pmx_len_part;                /* 18 x 8 B */
 
+/* ---- device residency across ParMmg iterations -------------------------
+ * PMMG_update_oldGrps (src/libparmmg1.c:653) makes the group's current mesh
+ * -- this iteration's new mesh with its interpolated metric and fields, and
+ * the frozen points' copies (PMMG_copyMetricsAndFields_point, :792) -- the
+ * next interpolation's background.  On the device that mesh already exists:
+ * the new points, their tags and the step's results.  Replaces the
+ * background upload (pmx_upload_background) of the next iteration when the
+ * group was not renumbered in between (no load balancing of this group).
+ *
+ * pmx_upload_new_tets: the new mesh's tets (tetra_v as in pmx_mesh_view,
+ * vertex indices in the last points view's numbering, !MG_EOK entries kept
+ * as deleted) -- after pmx_upload_points, once per iteration (they also
+ * serve pmx_new_mesh_qual).
+ *
+ * pmx_promote_background: after a pmx_run on those points, the new points
+ * (view first must be 1) become the background vertices 1..np, the step's
+ * results its solutions (same list as the step), their tags its point tags.
+ * Rows the step did not write (points not located, frozen, NUL, failed
+ * interpolations) take the caller's values from sols[] (Mmg layout, entry
+ * `first` on) -- the arrays pmx_download wrote into.  m: the new mesh --
+ * np, ne (= the uploaded new tets), nt / tria_v / adjt / hausd of its
+ * boundary trias (host, Mmg numbering), adja (optional: Mmg's mesh->adja,
+ * else built on the device); point_c and tetra_v are not read.  Only the
+ * trias (and adja when given) cross PCIe.  The new points and results are
+ * consumed: upload the next iteration's points before the next pmx_run. */
+int pmx_upload_new_tets(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, int64_t ne);
+int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const pmx_sol_view *sols);
+
 /* Results (one group, or reduced over groups and ranks). */
 typedef struct {
   int64_t ne, np;
@@ -307,7 +335,8 @@ int pmx_prilen(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, pmx_len_st
 
 /* PMMG_tetraQual on the NEW mesh right after the interpolation
  * (src/libparmmg1.c:845): the new tets (1-based records through a stride,
- * vertex indices in the last points view's numbering) are uploaded; the
+ * vertex indices in the last points view's numbering) are uploaded as by
+ * pmx_upload_new_tets -- or tetra_v = NULL: the ones already uploaded; the
  * coordinates and the interpolated metric are the step's device-resident
  * points and results.  qual (ne+1 doubles, host) and/or dev_result (the
  * qualhisto partial of the new mesh, opt as above; np = the points) may be

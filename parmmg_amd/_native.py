@@ -151,6 +151,8 @@ SIGNATURES = {
     "pmx_prilen_device": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(ParEdges), C.c_void_p]),
     "pmx_prilen": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(ParEdges), C.POINTER(LenStats)]),
     "pmx_new_mesh_qual": (C.c_int, [C.c_void_p, iptr, i64, i64, C.c_int, dptr, C.c_void_p]),
+    "pmx_upload_new_tets": (C.c_int, [C.c_void_p, iptr, i64, i64]),
+    "pmx_promote_background": (C.c_int, [C.c_void_p, C.POINTER(MeshView), C.c_int, C.POINTER(SolView)]),
     "pmx_qual_fold": (C.c_int, [C.POINTER(QualPart), iptr, C.c_int, C.POINTER(QualStats)]),
     "pmx_len_fold": (C.c_int, [C.POINTER(LenPart), C.c_int, C.POINTER(LenStats)]),
     "pmx_comm_unique_id": (C.c_int, [C.c_char_p, C.c_int]),

@@ -104,6 +104,58 @@ bool pmx_ctx::check_device_errors() {
   return true;
 }
 
+// boundary triangles of a mesh view -> TriRec records, validated against np
+static bool stage_trias(pmx_ctx *ctx, const pmx_mesh_view *m, int64_t np, std::vector<TriRec> &htr) {
+  const int64_t nt = m->nt;
+  htr.assign((size_t)(nt + 1), TriRec{});
+  if (nt < 1) return true;
+  const char *rc = (const char *)m->tria_v;
+  for (int64_t k = 1; k <= nt; k++) {
+    const int *v = (const int *)(rc + k * m->tria_stride);
+    TriRec &r = htr[(size_t)k];
+    for (int l = 0; l < 3; l++) {
+      r.v[l] = v[l];
+      const int a = m->adjt[3 * (k - 1) + 1 + l];
+      r.nb[l] = a / 3;
+      if (v[l] < 1 || v[l] > np || a < 0 || a / 3 > nt) {
+        ctx->err = "tria vertex or adjacency index out of range";
+        return false;
+      }
+    }
+  }
+  return true;
+}
+
+// the volume hint grid over the background bbox [lo, hi] (about one cell per
+// 6 tets) and the surface (tria) grid
+static bool setup_grids(pmx_ctx *ctx, const double lo[3], const double hi[3], int64_t ne) {
+  double ext[3], vol = 1.0;
+  for (int a = 0; a < 3; a++) {
+    ext[a] = std::max(hi[a] - lo[a], 1e-300);
+    vol *= ext[a];
+  }
+  double target = std::max(1.0, (double)ne / 6.0);
+  double h = std::cbrt(vol / target);
+  GridDesc g;
+  int64_t cells = 1;
+  for (int a = 0; a < 3; a++) {
+    // 1e-9 slack: libm cbrt is not correctly rounded, and 255.00000000000003
+    // cells must stay 255 (r01: C3 got 256 per axis, misaligned with the
+    // mesh: 10% empty cells, 0.73 instead of 0.44 cells start distance)
+    int d = (int)std::ceil(ext[a] / h * (1.0 - 1e-9));
+    d = std::max(1, std::min(d, 4096));
+    g.dim[a] = d;
+    g.lo[a] = lo[a];
+    g.inv[a] = (double)d / ext[a];
+    cells *= d;
+  }
+  ctx->grid = g;
+  ctx->gcells = cells;
+  for (int a = 0; a < 3; a++) { ctx->bblo[a] = lo[a]; ctx->bbhi[a] = hi[a]; }
+  if (!ctx->size_tria_grid()) return false;
+  return pmx_dgrow(ctx, ctx->d_grid, (size_t)cells);
+}
+
 extern "C" {
 
 pmx_ctx *pmx_create(int device) {
@@ -314,53 +366,13 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     });
   }
   // boundary triangles
-  std::vector<TriRec> htr((size_t)(nt + 1));
-  memset(&htr[0], 0, sizeof(TriRec));
-  if (nt > 0) {
-    const char *rc = (const char *)m->tria_v;
-    for (int64_t k = 1; k <= nt; k++) {
-      const int *v = (const int *)(rc + k * m->tria_stride);
-      TriRec &r = htr[(size_t)k];
-      for (int l = 0; l < 3; l++) {
-        r.v[l] = v[l];
-        const int a = m->adjt[3 * (k - 1) + 1 + l];
-        r.nb[l] = a / 3;
-        if (v[l] < 1 || v[l] > np || a < 0 || a / 3 > nt) {
-          ctx->err = "pmx_upload_background: tria vertex or adjacency index out of range";
-          return 0;
-        }
-      }
-    }
-  }
+  std::vector<TriRec> htr;
+  if (!stage_trias(ctx, m, np, htr)) return 0;
   ctx->np = np; ctx->ne = ne; ctx->nt = nt; ctx->hausd = m->hausd;
   ctx->sd = sd;
   ctx->host_build_node_trias(htr);
 
-  // hint grid over the background bbox: about one cell per 6 tets
-  double ext[3], vol = 1.0;
-  for (int a = 0; a < 3; a++) {
-    ext[a] = std::max(hi[a] - lo[a], 1e-300);
-    vol *= ext[a];
-  }
-  double target = std::max(1.0, (double)ne / 6.0);
-  double h = std::cbrt(vol / target);
-  GridDesc g;
-  int64_t cells = 1;
-  for (int a = 0; a < 3; a++) {
-    // 1e-9 slack: libm cbrt is not correctly rounded, and 255.00000000000003
-    // cells must stay 255 (r01: C3 got 256 per axis, misaligned with the
-    // mesh: 10% empty cells, 0.73 instead of 0.44 cells start distance)
-    int d = (int)std::ceil(ext[a] / h * (1.0 - 1e-9));
-    d = std::max(1, std::min(d, 4096));
-    g.dim[a] = d;
-    g.lo[a] = lo[a];
-    g.inv[a] = (double)d / ext[a];
-    cells *= d;
-  }
-  ctx->grid = g;
-  ctx->gcells = cells;
-  for (int a = 0; a < 3; a++) { ctx->bblo[a] = lo[a]; ctx->bbhi[a] = hi[a]; }
-  if (!ctx->size_tria_grid()) return 0;
+  if (!setup_grids(ctx, lo, hi, ne)) return 0;
 
   if (!dgrow(ctx, ctx->d_xyz, (size_t)(np + 1) * 3)) return 0;
   if (!dgrow(ctx, ctx->d_tets, (size_t)(ne + 1))) return 0;
@@ -368,7 +380,6 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   if (!dgrow(ctx, ctx->d_sol, hs_n)) return 0;
   if (!dgrow(ctx, ctx->d_tris, (size_t)(nt + 1))) return 0;
   if (!dgrow(ctx, ctx->d_trn, (size_t)(nt + 1))) return 0;
-  if (!dgrow(ctx, ctx->d_grid, (size_t)cells)) return 0;
   if (!dgrow(ctx, ctx->d_xyzq, (size_t)(np + 1))) return 0;
   if (!dgrow(ctx, ctx->d_ntoff, ctx->h_ntoff.size())) return 0;
   if (!dgrow(ctx, ctx->d_ntlist, std::max<size_t>(ctx->h_ntlist.size(), 1))) return 0;
@@ -388,6 +399,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
 int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   if (!ctx) return 0;
   ctx->have_pts = ctx->ran = false;
+  ctx->have_ntet = false;                  // the new tets belong to the points
   if (!pv) { ctx->err = "pmx_upload_points: null view"; return 0; }
   hipSetDevice(ctx->device);
   const int64_t n = pv->last - pv->first + 1;
@@ -444,11 +456,17 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   // two passes over fixed chunks (threads): classify + count, then fill the
   // per-path point lists at the chunks' exclusive offsets (input order kept)
   std::vector<int64_t> cv(65, 0), cb(65, 0);
+  double qlo[64][3], qhi[64][3];   // bbox per chunk (a promoted background's hint grid)
   const int C = par_chunks(0, n, [&](int ci, int64_t j0, int64_t j1) {
     int64_t a = 0, b = 0;
+    double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
     for (int64_t j = j0; j < j1; j++) {
       const double *c = (const double *)(pc + (pv->first + j) * pv->stride);
       hq[j] = Pt4{c[0], c[1], c[2], 0.0};
+      for (int ax = 0; ax < 3; ax++) {
+        lo[ax] = std::min(lo[ax], c[ax]);
+        hi[ax] = std::max(hi[ax], c[ax]);
+      }
       unsigned tag = tg ? *(const uint16_t *)(tg + (pv->first + j) * pv->tag_stride) : 0u;
       if (tg) htg[j] = (uint16_t)tag;
       int8_t kd;
@@ -461,7 +479,16 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
     }
     cv[(size_t)ci + 1] = a;
     cb[(size_t)ci + 1] = b;
+    for (int ax = 0; ax < 3; ax++) { qlo[ci][ax] = lo[ax]; qhi[ci][ax] = hi[ax]; }
   });
+  for (int ax = 0; ax < 3; ax++) {
+    ctx->qlo[ax] = HUGE_VAL;
+    ctx->qhi[ax] = -HUGE_VAL;
+    for (int i = 0; i < C; i++) {
+      ctx->qlo[ax] = std::min(ctx->qlo[ax], qlo[i][ax]);
+      ctx->qhi[ax] = std::max(ctx->qhi[ax], qhi[i][ax]);
+    }
+  }
   for (int i = 0; i < C; i++) { cv[(size_t)i + 1] += cv[(size_t)i]; cb[(size_t)i + 1] += cb[(size_t)i]; }
   const int64_t nv = cv[(size_t)C], nb = cb[(size_t)C];
   par_chunks(0, n, [&](int ci, int64_t j0, int64_t j1) {
@@ -785,6 +812,168 @@ double pmx_kernel_ms(pmx_ctx *ctx, int which) {
   return tot / ctx->ev_used;
 }
 
+// ---- device residency across ParMmg iterations --------------------------------
+//
+// PMMG_update_oldGrps (src/libparmmg1.c:653) makes the group's current mesh --
+// the previous iteration's new mesh with its interpolated metric and fields
+// -- the next interpolation's background.  The new points, their tags and the
+// step's results are already on the device; with the new tets uploaded once
+// (pmx_upload_new_tets, also used by pmx_new_mesh_qual) the next background
+// needs only its boundary trias from the host.
+
+int pmx_upload_new_tets(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, int64_t ne) {
+  if (!ctx) return 0;
+  ctx->have_ntet = false;
+  if (!ctx->have_pts) { ctx->err = "pmx_upload_new_tets: upload the new points first"; return 0; }
+  if (!tetra_v || ne < 1 || tetra_stride < 16 || 4 * ne >= (1LL << 31)) {
+    ctx->err = "pmx_upload_new_tets: bad new tets";
+    return 0;
+  }
+  hipSetDevice(ctx->device);
+  const int64_t first = ctx->pts_first, n = ctx->nq;
+  CK(hipStreamSynchronize(ctx->stream));   // the arena may still feed an earlier copy
+  char *st = hstage(ctx, (size_t)(ne + 1) * sizeof(int4));
+  if (!st) return 0;
+  int4 *h = (int4 *)st;
+  h[0] = make_int4(0, 0, 0, 0);
+  const char *tc = (const char *)tetra_v;
+  bool bad = false;
+  // vertices renumbered from the points view (first..last) to 1..n: the
+  // numbering of a promoted background
+  par_for(1, ne + 1, [&](int64_t k0, int64_t k1) {
+    bool b = false;
+    for (int64_t k = k0; k < k1; k++) {
+      const int *v = (const int *)(tc + k * tetra_stride);
+      if (v[0] <= 0) { h[k] = make_int4(0, 0, 0, 0); continue; }   // !MG_EOK
+      int w[4];
+      for (int l = 0; l < 4; l++) {
+        const int64_t j = (int64_t)v[l] - first;
+        if (j < 0 || j >= n) b = true;
+        w[l] = (int)(j + 1);
+      }
+      h[k] = make_int4(w[0], w[1], w[2], w[3]);
+    }
+    if (b) __atomic_store_n(&bad, true, __ATOMIC_RELAXED);
+  });
+  if (bad) { ctx->err = "pmx_upload_new_tets: tet vertex outside the uploaded points"; return 0; }
+  if (!dgrow(ctx, ctx->d_ntetv, (size_t)(ne + 1))) return 0;
+  CK(hipMemcpyAsync(ctx->d_ntetv.p, h, (size_t)(ne + 1) * sizeof(int4), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  ctx->n_ntet = ne;
+  ctx->have_ntet = true;
+  return 1;
+}
+
+int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const pmx_sol_view *sols) {
+  if (!ctx) return 0;
+  if (!m) { ctx->err = "pmx_promote_background: null mesh"; return 0; }
+  if (!ctx->ran || !ctx->have_pts || ctx->out_n != ctx->nq || ctx->out_S != ctx->sd.S) {
+    ctx->err = "pmx_promote_background: no step has run on the current uploads";
+    return 0;
+  }
+  if (!ctx->have_ntet) { ctx->err = "pmx_promote_background: upload the new tets first"; return 0; }
+  if (ctx->pts_first != 1) {
+    ctx->err = "pmx_promote_background: the points view must start at 1 (Mmg numbering)";
+    return 0;
+  }
+  const int64_t n = ctx->nq, ne = ctx->n_ntet, nt = m->nt;
+  if (m->np != n || m->ne != ne || n < 1) {
+    ctx->err = "pmx_promote_background: mesh sizes differ from the uploaded points / new tets";
+    return 0;
+  }
+  if (nt < 0 || (nt > 0 && (!m->tria_v || !m->adjt || m->tria_stride < 12))) {
+    ctx->err = "pmx_promote_background: nt > 0 requires tria_v and adjt";
+    return 0;
+  }
+  const SolDesc sd = ctx->sd;
+  if (nsol != sd.nsol || (nsol > 0 && !sols)) {
+    ctx->err = "pmx_promote_background: solution list differs from the step's";
+    return 0;
+  }
+  for (int s = 0; s < nsol; s++)
+    if (sols[s].size != sd.size[s]) {
+      ctx->err = "pmx_promote_background: solution size differs from the step's";
+      return 0;
+    }
+  hipSetDevice(ctx->device);
+  hipStream_t st = ctx->stream;
+  CK(hipStreamSynchronize(st));
+  if (!ctx->check_device_errors()) return 0;
+  const int S = sd.S;
+  const int64_t first = ctx->pts_first;
+  // rows the step did not write keep the caller's values (Mmg's own, or the
+  // frozen-point copy): which ones, from the write masks
+  char *stg = hstage(ctx, (size_t)n);
+  if (!stg) return 0;
+  CK(hipMemcpyAsync(stg, ctx->d_wmask.p, (size_t)n, hipMemcpyDeviceToHost, st));
+  CK(hipStreamSynchronize(st));
+  std::vector<uint8_t> wm((const uint8_t *)stg, (const uint8_t *)stg + n);
+  std::vector<int4> ent;
+  std::vector<double> vals;
+  for (int s = 0; s < nsol; s++) {
+    const int sz = sd.size[s];
+    for (int64_t j = 0; j < n; j++) {
+      if (wm[(size_t)j] & (1u << s)) continue;
+      if (!sols[s].m) {
+        ctx->err = "pmx_promote_background: a row the step did not write needs the caller's solution";
+        return 0;
+      }
+      ent.push_back(make_int4((int)(j + 1), sd.off[s], sz, 0));
+      const double *src = sols[s].m + (first + j) * sz;
+      for (int q = 0; q < 6; q++) vals.push_back(q < sz ? src[q] : 0.0);
+    }
+  }
+  // boundary trias of the new mesh (the host's: Mmg's numbering)
+  std::vector<TriRec> htr;
+  if (!stage_trias(ctx, m, n, htr)) return 0;
+  // the background invalid until this completes
+  ctx->have_bg = ctx->have_derived = ctx->have_tetv = ctx->have_qual = ctx->have_ptag = false;
+  ctx->stat_np = -1;
+  const int64_t ns = (ne + PMX_HINT_STRIDE - 1) / PMX_HINT_STRIDE;
+  if (!dgrow(ctx, ctx->d_xyz, (size_t)(n + 1) * 3) || !dgrow(ctx, ctx->d_sol, (size_t)(n + 1) * std::max(S, 1)) ||
+      !dgrow(ctx, ctx->d_tets, (size_t)(ne + 1)) || !dgrow(ctx, ctx->d_tets_s, (size_t)std::max<int64_t>(ns, 1)) ||
+      !dgrow(ctx, ctx->d_adja, (size_t)(4 * ne + 5)) || !dgrow(ctx, ctx->d_tris, (size_t)(nt + 1)) ||
+      !dgrow(ctx, ctx->d_trn, (size_t)(nt + 1)) || !dgrow(ctx, ctx->d_xyzq, (size_t)(n + 1)))
+    return 0;
+  const bool tags = ctx->have_qtag;
+  if (tags && !dgrow(ctx, ctx->d_ptag, (size_t)(n + 1))) return 0;
+  launch_promote(ctx->d_q.p, ctx->d_out.p, tags ? ctx->d_qtag.p : nullptr, n, S, ctx->d_xyz.p, ctx->d_sol.p,
+                 tags ? ctx->d_ptag.p : nullptr, st);
+  if (!ent.empty()) {
+    if (!dgrow(ctx, ctx->d_pent, ent.size()) || !dgrow(ctx, ctx->d_pval, vals.size())) return 0;
+    CK(hipMemcpyAsync(ctx->d_pent.p, ent.data(), ent.size() * sizeof(int4), hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(ctx->d_pval.p, vals.data(), vals.size() * sizeof(double), hipMemcpyHostToDevice, st));
+    launch_patch_rows(ctx->d_pent.p, ctx->d_pval.p, (int64_t)ent.size(), S, ctx->d_sol.p, st);
+  }
+  // face adjacency: the caller's (Mmg's mesh->adja after remeshing) or built
+  // here from the device-resident new tets
+  if (m->adja) {
+    CK(hipMemcpyAsync(ctx->d_adja.p, m->adja, (size_t)(4 * ne + 5) * sizeof(int), hipMemcpyHostToDevice, st));
+  } else if (!pmx_ctx_build_adja_device(ctx, ctx->d_ntetv.p, ne, n, ctx->d_adja.p)) {
+    return 0;
+  }
+  launch_build_tetrec(ctx->d_ntetv.p, ctx->d_adja.p, ne, PMX_HINT_STRIDE, ctx->d_tets.p, ctx->d_tets_s.p, st);
+  ctx->np = n;
+  ctx->ne = ne;
+  ctx->nt = nt;
+  ctx->hausd = m->hausd;
+  ctx->host_build_node_trias(htr);
+  if (!setup_grids(ctx, ctx->qlo, ctx->qhi, ne)) return 0;
+  if (!dgrow(ctx, ctx->d_ntoff, ctx->h_ntoff.size())) return 0;
+  if (!dgrow(ctx, ctx->d_ntlist, std::max<size_t>(ctx->h_ntlist.size(), 1))) return 0;
+  CK(hipMemcpyAsync(ctx->d_tris.p, htr.data(), htr.size() * sizeof(TriRec), hipMemcpyHostToDevice, st));
+  CK(hipMemcpyAsync(ctx->d_ntoff.p, ctx->h_ntoff.data(), ctx->h_ntoff.size() * sizeof(int), hipMemcpyHostToDevice, st));
+  if (!ctx->h_ntlist.empty())
+    CK(hipMemcpyAsync(ctx->d_ntlist.p, ctx->h_ntlist.data(), ctx->h_ntlist.size() * sizeof(int), hipMemcpyHostToDevice, st));
+  CK(hipGetLastError());
+  CK(hipStreamSynchronize(st));            // host vectors die here
+  ctx->have_ptag = tags;
+  // the points and the results were consumed: the next step needs new points
+  ctx->have_pts = ctx->ran = ctx->have_ntet = false;
+  ctx->have_bg = true;
+  return 1;
+}
+
 }  // extern "C"
 
 // ---- pmx_ctx members ----------------------------------------------------------
@@ -814,12 +1003,15 @@ void pmx_ctx::free_all() {
   dfree(d_qual); dfree(d_red); dfree(d_blist); dfree(d_olist); dfree(d_ows);
   dfree(d_ptag); dfree(d_touch); dfree(d_cidx); dfree(d_intv); dfree(d_pub); dfree(d_pkey);
   dfree(d_ppt); dfree(d_pedge); dfree(d_ntetv); dfree(d_nqual); dfree(d_qtag); dfree(d_gather);
+  dfree(d_adja); dfree(d_tcnt); dfree(d_toff); dfree(d_tbad); dfree(d_trec); dfree(d_ttmp);
+  dfree(d_pent); dfree(d_pval);
   dfree(d_cmet); dfree(d_ctag); dfree(d_cperm); dfree(d_cdst); dfree(d_ccnt); dfree(d_cold);
   dfree(d_cvals);
   if (d_tgrid) hipFree(d_tgrid);
   d_tgrid = nullptr;
   d_tgrid_cap = 0;
   have_bg = have_pts = ran = have_derived = have_tetv = have_qual = have_ptag = have_qtag = false;
+  have_ntet = false;
   stat_np = -1;
 }
 

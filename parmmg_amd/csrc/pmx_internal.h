@@ -98,7 +98,17 @@ struct pmx_ctx {
   DevBuf<unsigned long long> d_pkey;    // prilen: excluded parallel edges (sorted keys)
   DevBuf<uint8_t> d_ppt;
   DevBuf<int2> d_pedge;                 // prilen: owned parallel edges (step 1)
-  DevBuf<int4> d_ntetv;                 // new-mesh quality: the new tets
+  DevBuf<int4> d_ntetv;                 // the new tets (pmx_upload_new_tets), 1-based
+  bool have_ntet = false;               //   vertex = points-view index - first + 1
+  int64_t n_ntet = 0;
+  double qlo[3]{}, qhi[3]{};            // bbox of the uploaded new points
+  // device adjacency of promoted backgrounds (pmx_topo.hip), reused buffers
+  DevBuf<int> d_adja;
+  DevBuf<unsigned> d_tcnt, d_toff, d_tbad;
+  DevBuf<int4> d_trec;
+  DevBuf<char> d_ttmp;
+  DevBuf<int4> d_pent;                  // promote: patched rows
+  DevBuf<double> d_pval;
   DevBuf<double> d_nqual;
   bool have_qtag = false;               // raw tags of the new points
   DevBuf<uint16_t> d_qtag;
@@ -138,4 +148,8 @@ template <class T> inline bool pmx_dgrow(pmx_ctx *ctx, DevBuf<T> &b, size_t n) {
 char *pmx_hstage(pmx_ctx *ctx, size_t bytes);
 
 bool pmx_ctx_build_adja_host(pmx_ctx *ctx, const pmx_mesh_view *m, std::vector<int> &adja);
+// face adjacency of device connectivity (1-based int4, slot 0 unused) into
+// dadja (Mmg layout, 4 ne + 5 ints), context-owned scratch; false on a
+// non-manifold face or a failure (ctx->err)
+bool pmx_ctx_build_adja_device(pmx_ctx *ctx, const int4 *tv, int64_t ne, int64_t np, int *dadja);
 extern "C" int pmx_timing_reset(pmx_ctx *ctx);

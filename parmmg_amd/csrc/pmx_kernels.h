@@ -76,6 +76,12 @@ void launch_const_metric(const int8_t *kind, int64_t nq, double *out, int S, int
 void launch_prologue(uint8_t *wmask, int64_t n, unsigned *counts, int *grid, int64_t gcells,
                      hipStream_t s);
 void launch_tet_conn(const TetRec *src, int64_t n, int4 *dst, hipStream_t s);
+// device residency (pmx_promote_background): new points + results -> background
+void launch_promote(const Pt4 *q, const double *out, const uint16_t *qtag, int64_t n, int S, double *xyz,
+                    double *sol, uint16_t *ptag, hipStream_t s);
+void launch_patch_rows(const int4 *ent, const double *vals, int64_t n, int S, double *sol, hipStream_t s);
+void launch_build_tetrec(const int4 *tv, const int *adja, int64_t ne, int stride, TetRec *tets, int4 *sample,
+                         hipStream_t s);
 // workgroups of k_fallback that can be co-resident with `share` other
 // launches of it on this device (0 on error)
 int fallback_coresident_blocks(int device, int share);

@@ -435,3 +435,68 @@ void launch_prologue(uint8_t *wmask, int64_t n, unsigned *counts, int *grid, int
   int64_t nb = std::min<int64_t>(std::max<int64_t>((work + 255) / 256, 1), 4096);
   hipLaunchKernelGGL(k_prologue, dim3((unsigned)nb), dim3(256), 0, s, wmask, n, counts, grid, gcells);
 }
+
+// ---- device residency across iterations (pmx_promote_background) ----------------
+
+// the last step's new points and results become the background: vertex ip
+// (1..n) = new point ip-1, its solution row = the step's output row ip-1
+__global__ __launch_bounds__(256) void k_promote(const Pt4 *__restrict__ q, const double *__restrict__ out,
+                                                 const uint16_t *__restrict__ qtag, int64_t n, int S,
+                                                 double *__restrict__ xyz, double *__restrict__ sol,
+                                                 uint16_t *__restrict__ ptag) {
+  for (int64_t ip = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ip <= n;
+       ip += (int64_t)gridDim.x * blockDim.x) {
+    if (ip == 0) {
+      xyz[0] = xyz[1] = xyz[2] = 0.0;
+      for (int j = 0; j < S; j++) sol[j] = 0.0;
+      if (ptag) ptag[0] = 0;
+      continue;
+    }
+    const Pt4 p = q[ip - 1];
+    xyz[3 * ip] = p.x;
+    xyz[3 * ip + 1] = p.y;
+    xyz[3 * ip + 2] = p.z;
+    for (int j = 0; j < S; j++) sol[ip * S + j] = out[(ip - 1) * S + j];
+    if (ptag) ptag[ip] = qtag[ip - 1];
+  }
+}
+// rows the step did not write (not located, frozen, failed): the caller's
+// values, uploaded as (row, offset, size) + 6 doubles
+__global__ __launch_bounds__(256) void k_patch_rows(const int4 *__restrict__ ent, const double *__restrict__ vals,
+                                                    int64_t n, int S, double *__restrict__ sol) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int4 e = ent[i];                       // x: vertex, y: offset, z: size
+    for (int j = 0; j < e.z; j++) sol[(int64_t)e.x * S + e.y + j] = vals[6 * i + j];
+  }
+}
+// tet records from the new tets and their Mmg face adjacency
+// (adja[4*(k-1)+1+f] = 4*k'+f'), and the packed hint sample
+__global__ __launch_bounds__(256) void k_build_tetrec(const int4 *__restrict__ tv, const int *__restrict__ adja,
+                                                      int64_t ne, int stride, TetRec *__restrict__ tets,
+                                                      int4 *__restrict__ sample) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= ne;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    TetRec r;
+    const int4 v = tv[k];
+    r.v[0] = v.x; r.v[1] = v.y; r.v[2] = v.z; r.v[3] = v.w;
+    for (int f = 0; f < 4; f++) r.nb[f] = k ? adja[4 * (k - 1) + 1 + f] / 4 : 0;
+    tets[k] = r;
+    if (k >= 1 && (k - 1) % stride == 0) sample[(k - 1) / stride] = v;
+  }
+}
+void launch_promote(const Pt4 *q, const double *out, const uint16_t *qtag, int64_t n, int S, double *xyz,
+                    double *sol, uint16_t *ptag, hipStream_t s) {
+  const int64_t nb = std::min<int64_t>(std::max<int64_t>((n + 256) / 256, 1), 16384);
+  hipLaunchKernelGGL(k_promote, dim3((unsigned)nb), dim3(256), 0, s, q, out, qtag, n, S, xyz, sol, ptag);
+}
+void launch_patch_rows(const int4 *ent, const double *vals, int64_t n, int S, double *sol, hipStream_t s) {
+  if (n < 1) return;
+  const int64_t nb = std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_patch_rows, dim3((unsigned)nb), dim3(256), 0, s, ent, vals, n, S, sol);
+}
+void launch_build_tetrec(const int4 *tv, const int *adja, int64_t ne, int stride, TetRec *tets, int4 *sample,
+                         hipStream_t s) {
+  const int64_t nb = std::min<int64_t>(std::max<int64_t>((ne + 256) / 256, 1), 16384);
+  hipLaunchKernelGGL(k_build_tetrec, dim3((unsigned)nb), dim3(256), 0, s, tv, adja, ne, stride, tets, sample);
+}

@@ -1000,36 +1000,22 @@ int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, in
     ctx->err = "pmx_new_mesh_qual: run a step on the new points first";
     return 0;
   }
-  if (!tetra_v || ne < 1 || tetra_stride < 16 || ne >= (1LL << 31)) {
-    ctx->err = "pmx_new_mesh_qual: bad new tets";
+  // the new tets: given here (uploaded, as pmx_upload_new_tets), or NULL for
+  // the ones already uploaded; vertex j+1 = new point j
+  if (tetra_v) {
+    if (!pmx_upload_new_tets(ctx, tetra_v, tetra_stride, ne)) return 0;
+  } else if (!ctx->have_ntet) {
+    ctx->err = "pmx_new_mesh_qual: no new tets uploaded";
     return 0;
   }
-  // the new tets, 1-based, vertex indices in the points view's numbering
-  const int64_t first = ctx->pts_first, n = ctx->nq;
-  char *st = pmx_hstage(ctx, (size_t)(ne + 1) * 16);
-  if (!st) return 0;
-  int4 *h = (int4 *)st;
-  h[0] = make_int4(0, 0, 0, 0);
-  for (int64_t k = 1; k <= ne; k++) {
-    const int *v = (const int *)((const char *)tetra_v + k * tetra_stride);
-    h[k] = make_int4(v[0], v[1], v[2], v[3]);
-    if (v[0] <= 0) continue;
-    for (int l = 0; l < 4; l++)
-      if (v[l] < first || v[l] >= first + n) {
-        ctx->err = "pmx_new_mesh_qual: tet vertex outside the uploaded points";
-        return 0;
-      }
-  }
+  ne = ctx->n_ntet;
+  const int64_t n = ctx->nq;
   hipStream_t s = ctx->stream;
-  if (!pmx_dgrow(ctx, ctx->d_ntetv, (size_t)(ne + 1)) || !pmx_dgrow(ctx, ctx->d_nqual, (size_t)(ne + 1))) return 0;
-  if (hipMemcpyAsync(ctx->d_ntetv.p, h, (size_t)(ne + 1) * 16, hipMemcpyHostToDevice, s) != hipSuccess) {
-    ctx->err = "pmx_new_mesh_qual: upload";
-    return 0;
-  }
+  if (!pmx_dgrow(ctx, ctx->d_nqual, (size_t)(ne + 1))) return 0;
   StatArgs A{};
   A.xyz = reinterpret_cast<const double *>(ctx->d_q.p);   // Pt4 {x, y, z, 0}
   A.xstride = 4;
-  A.vbase = (int)first;
+  A.vbase = 1;
   A.tetv = ctx->d_ntetv.p;
   A.ne = ne;
   // the interpolated metric, in the step's output rows (a constant-size

@@ -265,6 +265,38 @@ bool pmx_ctx_build_adja_host(pmx_ctx *ctx, const pmx_mesh_view *m, std::vector<i
   return true;
 }
 
+
+// face adjacency of a device connectivity stream with the context's buffers
+// (promoted backgrounds: the new tets are already on the device)
+bool pmx_ctx_build_adja_device(pmx_ctx *ctx, const int4 *tv, int64_t ne, int64_t np, int *dadja) {
+  hipStream_t s = ctx->stream;
+  size_t bytes = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const unsigned *)nullptr, (unsigned *)nullptr,
+                                   (int)(np + 2), s);
+  if (!pmx_dgrow(ctx, ctx->d_tcnt, (size_t)(np + 2)) || !pmx_dgrow(ctx, ctx->d_toff, (size_t)(np + 2)) ||
+      !pmx_dgrow(ctx, ctx->d_trec, (size_t)(4 * ne)) || !pmx_dgrow(ctx, ctx->d_tbad, 1) ||
+      !pmx_dgrow(ctx, ctx->d_ttmp, bytes))
+    return false;
+  unsigned *cnt = ctx->d_tcnt.p, *off = ctx->d_toff.p, *nbad = ctx->d_tbad.p;
+  bool okk = hipMemsetAsync(cnt, 0, sizeof(unsigned) * (size_t)(np + 2), s) == hipSuccess &&
+             hipMemsetAsync(nbad, 0, sizeof(unsigned), s) == hipSuccess &&
+             hipMemsetAsync(dadja, 0, sizeof(int) * (size_t)(4 * ne + 5), s) == hipSuccess;
+  if (!okk) return topo_fail(ctx, "device adjacency: memset");
+  hipLaunchKernelGGL(k_face_count, dim3(nblk(4 * ne)), dim3(256), 0, s, tv, ne, cnt);
+  if (hipcub::DeviceScan::ExclusiveSum(ctx->d_ttmp.p, bytes, cnt, off, (int)(np + 2), s) != hipSuccess)
+    return topo_fail(ctx, "device adjacency: scan");
+  hipMemcpyAsync(cnt, off, sizeof(unsigned) * (size_t)(np + 2), hipMemcpyDeviceToDevice, s);
+  hipLaunchKernelGGL(k_face_scatter, dim3(nblk(4 * ne)), dim3(256), 0, s, tv, ne, cnt, ctx->d_trec.p);
+  hipLaunchKernelGGL(k_face_match, dim3(nblk(4 * ne)), dim3(256), 0, s, ctx->d_trec.p, np + 1, off, dadja,
+                     nbad);
+  unsigned hb = 0;
+  if (hipMemcpyAsync(&hb, nbad, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return topo_fail(ctx, "device adjacency: launch");
+  if (hb) return topo_fail(ctx, "device adjacency: non-manifold tet faces");
+  return true;
+}
+
 extern "C" {
 
 int pmx_build_adja(pmx_ctx *ctx, int64_t ne, int64_t np, const int *tetra_v, int64_t tetra_stride,

@@ -82,6 +82,7 @@ class Transfer:
         self._keep = []
         self.sizes: list[int] = []
         self.npts = 0
+        self.n_new_tets = 0
 
     def close(self):
         if self.ctx:
@@ -354,13 +355,43 @@ class Transfer:
                   "pmx_prilen_device")
         del keep
 
-    def new_mesh_qual(self, tets: np.ndarray, opt: int = N.INQUA, dev_ptr: int = 0) -> np.ndarray:
-        """PMMG_tetraQual on the new mesh after the last step: tets (ne+1, 4)
-        with indices of the uploaded points (0-based here, v[0] < 0: deleted)."""
+    def upload_new_tets(self, tets: np.ndarray):
+        """The new mesh's tets, (ne+1, 4) with 0-based point indices (v[0] < 0:
+        deleted), for pmx_promote_background / pmx_new_mesh_qual."""
         tv = _tets_1based(tets)
-        q = np.zeros(tv.shape[0])
-        self._chk(self.lib.pmx_new_mesh_qual(self.ctx, _ip(tv), 16, tv.shape[0] - 1, opt, _dp(q),
-                                             C.c_void_p(dev_ptr or None)), "pmx_new_mesh_qual")
+        self._chk(self.lib.pmx_upload_new_tets(self.ctx, _ip(tv), 16, tv.shape[0] - 1),
+                  "pmx_upload_new_tets")
+        self.n_new_tets = tv.shape[0] - 1
+
+    def promote_background(self, new_mesh: Mesh, sols: list[np.ndarray] | None = None,
+                           adja: bool = True):
+        """The last step's new points + results become the background (device
+        resident).  new_mesh: the new mesh (its trias/adjt/hausd and, with
+        adja=True, its adjacency are read; coordinates and tets are not);
+        sols: the (n, size) result arrays of the last download (values of the
+        rows the step did not write)."""
+        mv = mesh_view(new_mesh)
+        if not adja:
+            mv.adja = None
+        arr = [np.ascontiguousarray(s, np.float64) for s in (sols or [])]
+        views = (N.SolView * max(len(arr), 1))()
+        for i, a in enumerate(arr):
+            views[i].size = a.shape[1] if a.ndim == 2 else 1
+            views[i].m = _shift(a, 8 * views[i].size, C.c_double)     # Mmg layout: entry 1 = row 0
+        self._chk(self.lib.pmx_promote_background(self.ctx, C.byref(mv), len(arr), views),
+                  "pmx_promote_background")
+        self.npts = 0
+
+    def new_mesh_qual(self, tets: np.ndarray | None, opt: int = N.INQUA, dev_ptr: int = 0) -> np.ndarray:
+        """PMMG_tetraQual on the new mesh after the last step: tets (ne+1, 4)
+        with indices of the uploaded points (0-based here, v[0] < 0: deleted);
+        None: the tets of the last upload_new_tets."""
+        tv = _tets_1based(tets) if tets is not None else None
+        q = np.zeros((tv.shape[0] if tv is not None else self.n_new_tets + 1))
+        self._chk(self.lib.pmx_new_mesh_qual(self.ctx, _ip(tv), 16, tv.shape[0] - 1 if tv is not None else 0,
+                                             opt, _dp(q), C.c_void_p(dev_ptr or None)), "pmx_new_mesh_qual")
+        if tv is not None:
+            self.n_new_tets = tv.shape[0] - 1
         return q
 
     def comm_init(self, nranks: int, uid: bytes, rank: int) -> int:

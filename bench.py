@@ -155,7 +155,9 @@ def pcie_inclusive(tr, m, x, t, sols, reps: int = 3) -> dict:
     """Wall-clock rate of the host-staged cycles of one group:
     points = upload new vertices + step + download fields/elements;
     full = also re-upload the background mesh and its solutions (SoA gather,
-    device adjacency/boundary build when the mesh carries none)."""
+    device adjacency/boundary build when the mesh carries none);
+    resident_cycle (added by the caller) = the iteration with the background
+    kept on the device."""
     # the caller's output arrays exist before the step (ParMmg: met->m,
     # field->m), so they are allocated once, outside the window
     out = tr.download()
@@ -185,6 +187,57 @@ def pcie_inclusive(tr, m, x, t, sols, reps: int = 3) -> dict:
     return {"unit": "vertices/s", "reps": reps, "timing": "best of reps, wall clock",
             "points_cycle": {"value": n / tp, "ms": tp * 1e3, "phases": pp},
             "full_cycle": {"value": n / tf, "ms": tf * 1e3, "phases": pf}}
+
+
+def resident_cycle(m, sols, cfg: dict, local: int, iters: int = 4, warmup: int = 2) -> dict:
+    """One ParMmg iteration with the background device resident (DESIGN.md §7,
+    pmx_promote_background): upload the new mesh's points (+ its tets, same
+    pass), step, download the fields into the caller's arrays, promote the new
+    mesh + results to the next background (only its boundary trias and Mmg
+    adjacency cross PCIe).  Two jittered Kuhn meshes of the config's size
+    alternate as background and new mesh; wall clock per iteration."""
+    from parmmg_amd import mesh as M
+    from parmmg_amd.transfer import Result, Transfer
+    mb = M.kuhn_cube(cfg["n"], seed=777)
+
+    def case(mm):
+        x = mm.xyz[1:]
+        onb = np.any((x == 0.0) | (x == 1.0), axis=1)
+        t = np.where(onb, M.TAG_BDY, 0).astype(np.uint16)
+        return mm, x, t, mm.tet            # Mmg layout: passed as is
+
+    cases = [case(mb), case(m)]
+    tr = Transfer(local)
+    tr.set_residency(True)
+    tr.upload_background(m, sols, 0)
+    sizes = [s.shape[1] for s in sols]
+    res = [Result([np.zeros((len(c[1]), sz)) for sz in sizes], *(np.zeros(len(c[1]), np.int32)
+                                                                   for _ in range(3))) for c in cases]
+    rows = []
+    for it in range(warmup + iters):
+        mm, x, t, tets1 = cases[it % 2]
+        out = res[it % 2]
+        tr.synchronize()
+        t0 = time.perf_counter()
+        tr.upload_points(x, t, tets_mmg=tets1)
+        t1 = time.perf_counter()
+        tr.run()
+        tr.synchronize()
+        t2 = time.perf_counter()
+        tr.download(into=out, sols_only=True)
+        t3 = time.perf_counter()
+        tr.promote_background(mm, out.sols, adja=False)
+        t4 = time.perf_counter()
+        if it >= warmup:
+            rows.append((t4 - t0, t1 - t0, t2 - t1, t3 - t2, t4 - t3, len(x)))
+    tr.close()
+    best = min(rows)
+    mean = float(np.mean([r[0] for r in rows]))
+    return {"value": best[5] / best[0], "ms": best[0] * 1e3, "mean_ms": mean * 1e3,
+            "new_vertices": best[5], "new_tets": int(mb.ne),
+            "phases": {"points_and_tets_ms": best[1] * 1e3, "step_ms": best[2] * 1e3,
+                       "download_ms": best[3] * 1e3, "promote_ms": best[4] * 1e3},
+            "timing": f"best of {iters} iterations after {warmup}, wall clock"}
 
 
 def main():
@@ -295,6 +348,7 @@ def main():
     pcie = None
     if world == 1 and not args.no_pcie:
         pcie = pcie_inclusive(tr, m, x, t, sols)
+        pcie["resident_cycle"] = resident_cycle(m, sols, cfg, local)
 
     if dist is not None:
         import torch

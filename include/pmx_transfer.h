@@ -65,7 +65,8 @@ typedef struct {
  * indices in the same numbering as ip): only the points of valid tets
  * (v[0] > 0) are located, as in the reference's vertex loop over the new tets
  * (src/interpmesh_pmmg.c:535-541); the others are left untouched (a constant
- * size metric is still written on every valid point).  NULL: every point. */
+ * size metric is still written on every valid point).  NULL: every point.
+ * The tets also stay on the device (pmx_new_mesh_qual, pmx_promote_background). */
 typedef struct {
   int64_t         first, last;
   const double   *c;    int64_t stride;
@@ -251,7 +252,8 @@ typedef struct {
  * pmx_upload_new_tets: the new mesh's tets (tetra_v as in pmx_mesh_view,
  * vertex indices in the last points view's numbering, !MG_EOK entries kept
  * as deleted) -- after pmx_upload_points, once per iteration (they also
- * serve pmx_new_mesh_qual).
+ * serve pmx_new_mesh_qual).  A points view with tetra_v uploads them too
+ * (same pass as the orphan marking): no separate call needed then.
  *
  * pmx_promote_background: after a pmx_run on those points, the new points
  * (view first must be 1) become the background vertices 1..np, the step's
@@ -265,6 +267,12 @@ typedef struct {
  * trias (and adja when given) cross PCIe.  The new points and results are
  * consumed: upload the next iteration's points before the next pmx_run. */
 int pmx_upload_new_tets(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, int64_t ne);
+/* on: every points upload with new tets also builds, on a stream of its own
+ * and while the step on those points runs, the next background's tet
+ * records (face adjacency from the device-resident new tets); the following
+ * pmx_promote_background (with m->adja = NULL) only swaps them in.  Off by
+ * default: the drop-in path does not promote. */
+int pmx_set_residency(pmx_ctx *ctx, int on);
 int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const pmx_sol_view *sols);
 
 /* Results (one group, or reduced over groups and ranks). */

@@ -10,6 +10,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -65,18 +69,90 @@ static int64_t host_threads_min() {
   }();
   return M;
 }
+// a persistent pool of host_threads()-1 workers (thread creation per pass
+// cost ~0.1 ms per pass and dominated the chunked copies); the calling thread
+// takes part.  One job at a time (a mutex serialises concurrent callers).
+namespace {
+struct HostPool {
+  std::mutex run_m;                      // one job at a time
+  std::mutex m;
+  std::condition_variable cv, done_cv;
+  std::vector<std::thread> th;
+  const std::function<void(int)> *job = nullptr;
+  int njob = 0;
+  std::atomic<int> next{0};
+  int active = 0;
+  unsigned gen = 0;
+  bool stop = false;
+  explicit HostPool(unsigned nworkers) {
+    for (unsigned i = 0; i < nworkers; i++) th.emplace_back([this] { work(); });
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> g(m);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto &t : th) t.join();
+  }
+  void drain(const std::function<void(int)> &f, int n) {
+    for (int i = next.fetch_add(1); i < n; i = next.fetch_add(1)) f(i);
+  }
+  void work() {
+    unsigned seen = 0;
+    for (;;) {
+      const std::function<void(int)> *f;
+      int n;
+      {
+        std::unique_lock<std::mutex> g(m);
+        cv.wait(g, [&] { return stop || gen != seen; });
+        if (stop) return;
+        seen = gen;
+        f = job;
+        n = njob;
+        if (!f) continue;                  // woke after that job had finished
+        active++;
+      }
+      drain(*f, n);
+      {
+        std::lock_guard<std::mutex> g(m);
+        if (--active == 0) done_cv.notify_all();
+      }
+    }
+  }
+  void run(const std::function<void(int)> &f, int n) {
+    std::lock_guard<std::mutex> r(run_m);
+    {
+      std::lock_guard<std::mutex> g(m);
+      job = &f;
+      njob = n;
+      next.store(0);
+      gen++;
+    }
+    cv.notify_all();
+    drain(f, n);
+    std::unique_lock<std::mutex> g(m);
+    done_cv.wait(g, [&] { return active == 0 && next.load() >= n; });
+    job = nullptr;
+  }
+};
+HostPool &host_pool() {
+  static HostPool *p = new HostPool(host_threads() - 1);   // never destroyed: no exit-time joins
+  return *p;
+}
+}  // namespace
+
 // f(chunk, lo, hi) over C contiguous chunks of [lo, hi); returns C
 template <class F> static int par_chunks(int64_t lo, int64_t hi, F f) {
   const int64_t n = hi - lo;
   const int C = (host_threads() <= 1 || n < host_threads_min()) ? 1 : (int)host_threads();
   if (C == 1) { f(0, lo, hi); return 1; }
-  std::vector<std::thread> th;
   const int64_t chunk = (n + C - 1) / C;
-  for (int i = 0; i < C; i++) {
+  const std::function<void(int)> job = [&](int i) {
     const int64_t a = lo + (int64_t)i * chunk, b = std::min(hi, a + chunk);
-    th.emplace_back(f, i, a, std::max(a, b));
-  }
-  for (auto &x : th) x.join();
+    f(i, a, std::max(a, b));
+  };
+  host_pool().run(job, C);
   return C;
 }
 template <class F> static void par_for(int64_t lo, int64_t hi, F f) {
@@ -172,6 +248,14 @@ pmx_ctx *pmx_create(int device) {
   }
   ctx->stream = ctx->own;
   if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->topo, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_topo, hipEventDisableTiming) != hipSuccess ||
+      hipHostMalloc((void **)&ctx->h_nbad, sizeof(unsigned), hipHostMallocDefault) != hipSuccess ||
+      [&] {
+        for (auto &e : ctx->ev_dl)
+          if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return true;
+        return false;
+      }() ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess) {
     pmx_destroy(ctx);
@@ -193,11 +277,17 @@ void pmx_destroy(pmx_ctx *ctx) {
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
   if (ctx->side) hipStreamSynchronize(ctx->side);
+  if (ctx->topo) hipStreamSynchronize(ctx->topo);
   ctx->free_all();
   for (auto &e : ctx->events) hipEventDestroy(e);
   if (ctx->ev_fork) hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) hipEventDestroy(ctx->ev_join);
   if (ctx->side) hipStreamDestroy(ctx->side);
+  if (ctx->topo) hipStreamDestroy(ctx->topo);
+  if (ctx->ev_topo) hipEventDestroy(ctx->ev_topo);
+  for (auto &e : ctx->ev_dl)
+    if (e) hipEventDestroy(e);
+  if (ctx->h_nbad) hipHostFree(ctx->h_nbad);
   if (ctx->own) hipStreamDestroy(ctx->own);
   delete ctx;
 }
@@ -400,6 +490,10 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   if (!ctx) return 0;
   ctx->have_pts = ctx->ran = false;
   ctx->have_ntet = false;                  // the new tets belong to the points
+  if (ctx->next_topo) {                     // its buffers are about to be reused
+    CK(hipStreamSynchronize(ctx->topo));
+    ctx->next_topo = false;
+  }
   if (!pv) { ctx->err = "pmx_upload_points: null view"; return 0; }
   hipSetDevice(ctx->device);
   const int64_t n = pv->last - pv->first + 1;
@@ -414,10 +508,13 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   const size_t nn = (size_t)std::max<int64_t>(n, 1);
   // staging layout (pinned): q | kind | vol list | bdy list | dense vol coords
   // | raw tags (statistics of the new mesh)
+  // | the new tets (kept on the device: new-mesh quality, residency)
+  const int64_t ntet = pv->tetra_v ? pv->ne : 0;
   const size_t o_q = 0, o_k = o_q + al256(nn * sizeof(Pt4)), o_vl = o_k + al256(nn),
                o_bl = o_vl + al256(nn * sizeof(int)), o_qv = o_bl + al256(nn * sizeof(int)),
                o_tg = o_qv + al256(nn * 3 * sizeof(double)),
-               total = o_tg + al256(pv->tag ? nn * 2 : 0);
+               o_tv = o_tg + al256(pv->tag ? nn * 2 : 0),
+               total = o_tv + al256(ntet ? (size_t)(ntet + 1) * sizeof(int4) : 0);
   CK(hipStreamSynchronize(ctx->stream));   // the arena may still feed an earlier copy
   char *st = hstage(ctx, total);
   if (!st) return 0;
@@ -429,24 +526,39 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   const char *pc = (const char *)pv->c;
   const char *tg = (const char *)pv->tag;
   // points referenced by a valid new tet (the reference visits only those,
-  // src/interpmesh_pmmg.c:535-541); marked into the kind array first
+  // src/interpmesh_pmmg.c:535-541); marked into the kind array first.  The
+  // same pass packs the tets (vertex = view index - first + 1) for the device
+  int4 *htv = (int4 *)(st + o_tv);
   if (pv->tetra_v) {
     memset(hk, 0, (size_t)n);
+    htv[0] = make_int4(0, 0, 0, 0);
+    if (!dgrow(ctx, ctx->d_ntetv, (size_t)(ntet + 1))) return 0;
     const char *tc = (const char *)pv->tetra_v;
     bool bad = false;
-    par_for(1, pv->ne + 1, [&](int64_t k0, int64_t k1) {
-      bool b = false;
-      for (int64_t k = k0; k < k1; k++) {
-        const int *v = (const int *)(tc + k * pv->tetra_stride);
-        if (v[0] <= 0) continue;                     // !MG_EOK
-        for (int l = 0; l < 4; l++) {
-          const int64_t j = (int64_t)v[l] - pv->first;
-          if (j < 0 || j >= n) { b = true; continue; }
-          __atomic_store_n(&hk[j], (int8_t)1, __ATOMIC_RELAXED);
+    // in chunks: the DMA of a packed chunk overlaps the packing of the next
+    const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(8, ntet >> 20));
+    for (int64_t c = 0; c < nch; c++) {
+      const int64_t lo = (c == 0) ? 0 : 1 + ntet * c / nch, hi = 1 + ntet * (c + 1) / nch;
+      par_for(std::max<int64_t>(lo, 1), hi, [&](int64_t k0, int64_t k1) {
+        bool b = false;
+        for (int64_t k = k0; k < k1; k++) {
+          const int *v = (const int *)(tc + k * pv->tetra_stride);
+          if (v[0] <= 0) { htv[k] = make_int4(0, 0, 0, 0); continue; }   // !MG_EOK
+          int w[4];
+          for (int l = 0; l < 4; l++) {
+            const int64_t j = (int64_t)v[l] - pv->first;
+            w[l] = (int)(j + 1);
+            if (j < 0 || j >= n) { b = true; continue; }
+            __atomic_store_n(&hk[j], (int8_t)1, __ATOMIC_RELAXED);
+          }
+          htv[k] = make_int4(w[0], w[1], w[2], w[3]);
         }
-      }
-      if (b) __atomic_store_n(&bad, true, __ATOMIC_RELAXED);
-    });
+        if (b) __atomic_store_n(&bad, true, __ATOMIC_RELAXED);
+      });
+      if (bad) break;
+      CK(hipMemcpyAsync(ctx->d_ntetv.p + lo, htv + lo, (size_t)(hi - lo) * sizeof(int4), hipMemcpyHostToDevice,
+                        ctx->stream));
+    }
     if (bad) {
       ctx->err = "pmx_upload_points: new tet vertex outside [first, last]";
       return 0;
@@ -489,6 +601,12 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
       ctx->qhi[ax] = std::max(ctx->qhi[ax], qhi[i][ax]);
     }
   }
+  // the points and their kinds go down while the lists are built
+  if (!dgrow(ctx, ctx->d_q, nn) || !dgrow(ctx, ctx->d_kind, nn)) return 0;
+  if (n) {
+    CK(hipMemcpyAsync(ctx->d_q.p, hq, (size_t)n * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
+    CK(hipMemcpyAsync(ctx->d_kind.p, hk, (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+  }
   for (int i = 0; i < C; i++) { cv[(size_t)i + 1] += cv[(size_t)i]; cb[(size_t)i + 1] += cb[(size_t)i]; }
   const int64_t nv = cv[(size_t)C], nb = cb[(size_t)C];
   par_chunks(0, n, [&](int ci, int64_t j0, int64_t j1) {
@@ -506,12 +624,14 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   ctx->nq = n;
   ctx->nq_vol = nv;
   ctx->nq_bdy = nb;
-  if (!dgrow(ctx, ctx->d_q, nn)) return 0;
-  if (!dgrow(ctx, ctx->d_kind, nn)) return 0;
   if (!dgrow(ctx, ctx->d_wmask, nn)) return 0;
   if (!dgrow(ctx, ctx->d_elem, nn)) return 0;
   if (!dgrow(ctx, ctx->d_status, nn)) return 0;
   if (!dgrow(ctx, ctx->d_steps, nn)) return 0;
+  // points a step never locates (NUL, frozen, orphans) report element 0
+  CK(hipMemsetAsync(ctx->d_elem.p, 0, nn * sizeof(int), ctx->stream));
+  CK(hipMemsetAsync(ctx->d_status.p, 0, nn * sizeof(int), ctx->stream));
+  CK(hipMemsetAsync(ctx->d_steps.p, 0, nn * sizeof(int), ctx->stream));
   if (!dgrow(ctx, ctx->d_start, nn)) return 0;
   if (!dgrow(ctx, ctx->d_edge, nn)) return 0;
   if (!dgrow(ctx, ctx->d_vertex, nn)) return 0;
@@ -527,10 +647,6 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   if (!dgrow(ctx, ctx->d_vstat, (size_t)std::max<int64_t>((nv + 255) / 256 * 4 + 4, 1))) return 0;
   if (!dgrow(ctx, ctx->d_bstat, (size_t)std::max<int64_t>((nb + 255) / 256 * 4 + 4, 1))) return 0;
   if (!dgrow(ctx, ctx->d_qv, (size_t)std::max<int64_t>(nv, 1) * 3)) return 0;
-  if (n) {   // no new vertex at all is a valid (empty) step
-    CK(hipMemcpyAsync(ctx->d_q.p, hq, (size_t)n * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
-    CK(hipMemcpyAsync(ctx->d_kind.p, hk, (size_t)n, hipMemcpyHostToDevice, ctx->stream));
-  }
   if (nv) CK(hipMemcpyAsync(ctx->d_vollist.p, vl, (size_t)nv * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
   if (nv) CK(hipMemcpyAsync(ctx->d_qv.p, hqv, (size_t)nv * 3 * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
   if (nb) CK(hipMemcpyAsync(ctx->d_bdylist.p, bl, (size_t)nb * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
@@ -543,6 +659,22 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   ctx->have_qtag = tg && n;
   ctx->pts_first = pv->first;
   ctx->have_pts = true;
+  ctx->have_ntet = ntet > 0;
+  ctx->n_ntet = ntet;
+  // residency: the next background's tet records (face adjacency built on
+  // the device) on the topo stream, while the step on these points runs
+  if (ctx->residency && ntet > 0) {
+    const int64_t ns = (ntet + PMX_HINT_STRIDE - 1) / PMX_HINT_STRIDE;
+    if (!dgrow(ctx, ctx->d_adja, (size_t)(4 * ntet + 5)) || !dgrow(ctx, ctx->d_tets_next, (size_t)(ntet + 1)) ||
+        !dgrow(ctx, ctx->d_tets_s_next, (size_t)std::max<int64_t>(ns, 1)))
+      return 0;
+    *ctx->h_nbad = 0;
+    if (!pmx_ctx_build_adja_device(ctx, ctx->d_ntetv.p, ntet, n, ctx->d_adja.p, ctx->topo, ctx->h_nbad)) return 0;
+    launch_build_tetrec(ctx->d_ntetv.p, ctx->d_adja.p, ntet, PMX_HINT_STRIDE, ctx->d_tets_next.p,
+                        ctx->d_tets_s_next.p, ctx->topo);
+    CK(hipEventRecord(ctx->ev_topo, ctx->topo));
+    ctx->next_topo = true;
+  }
   return 1;
 }
 
@@ -681,27 +813,35 @@ int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem, int *sta
   if (!st) return 0;
   const double *h = (const double *)(st + o_out);
   const uint8_t *wm = (const uint8_t *)(st + o_wm);
-  if (want_sol) {
-    CK(hipMemcpyAsync(st + o_out, ctx->d_out.p, (size_t)(n * S) * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-    CK(hipMemcpyAsync(st + o_wm, ctx->d_wmask.p, (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+  // the fields in chunks: a chunk's scatter into the caller's arrays overlaps
+  // the DMA of the next one
+  const int64_t nch = want_sol ? std::max<int64_t>(1, std::min<int64_t>(4, (n * S) >> 21)) : 0;
+  for (int64_t c = 0; c < nch; c++) {
+    const int64_t lo = n * c / nch, hi = n * (c + 1) / nch;
+    CK(hipMemcpyAsync(st + o_out + (size_t)(lo * S) * sizeof(double), ctx->d_out.p + lo * S,
+                      (size_t)((hi - lo) * S) * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    CK(hipMemcpyAsync(st + o_wm + lo, ctx->d_wmask.p + lo, (size_t)(hi - lo), hipMemcpyDeviceToHost, ctx->stream));
+    CK(hipEventRecord(ctx->ev_dl[c], ctx->stream));
   }
   if (elem) CK(hipMemcpyAsync(st + o_el, ctx->d_elem.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   if (status) CK(hipMemcpyAsync(st + o_st, ctx->d_status.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   if (steps) CK(hipMemcpyAsync(st + o_sp, ctx->d_steps.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-  CK(hipStreamSynchronize(ctx->stream));
-  if (want_sol) {
-    for (int s = 0; s < ctx->sd.nsol; s++) {
-      double *dst = new_sols[s].m;
-      const int sz = ctx->sd.size[s], off = ctx->sd.off[s];
-      if (!dst) continue;
-      par_for(0, n, [&](int64_t i0, int64_t i1) {
+  for (int64_t c = 0; c < nch; c++) {
+    const int64_t lo = n * c / nch, hi = n * (c + 1) / nch;
+    CK(hipEventSynchronize(ctx->ev_dl[c]));
+    par_for(lo, hi, [&](int64_t i0, int64_t i1) {
+      for (int s = 0; s < ctx->sd.nsol; s++) {
+        double *dst = new_sols[s].m;
+        const int sz = ctx->sd.size[s], off = ctx->sd.off[s];
+        if (!dst) continue;
         for (int64_t i = i0; i < i1; i++) {
           if (!(wm[i] & (1u << s))) continue;
           for (int j = 0; j < sz; j++) dst[i * sz + j] = h[(size_t)(i * S + off + j)];
         }
-      });
-    }
+      }
+    });
   }
+  CK(hipStreamSynchronize(ctx->stream));
   if (elem) memcpy(elem, st + o_el, (size_t)n * sizeof(int));
   if (status) memcpy(status, st + o_st, (size_t)n * sizeof(int));
   if (steps) memcpy(steps, st + o_sp, (size_t)n * sizeof(int));
@@ -821,9 +961,19 @@ double pmx_kernel_ms(pmx_ctx *ctx, int which) {
 // (pmx_upload_new_tets, also used by pmx_new_mesh_qual) the next background
 // needs only its boundary trias from the host.
 
+int pmx_set_residency(pmx_ctx *ctx, int on) {
+  if (!ctx) return 0;
+  ctx->residency = on != 0;
+  return 1;
+}
+
 int pmx_upload_new_tets(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, int64_t ne) {
   if (!ctx) return 0;
   ctx->have_ntet = false;
+  if (ctx->next_topo) {                     // built from other tets: drop it
+    CK(hipStreamSynchronize(ctx->topo));
+    ctx->next_topo = false;
+  }
   if (!ctx->have_pts) { ctx->err = "pmx_upload_new_tets: upload the new points first"; return 0; }
   if (!tetra_v || ne < 1 || tetra_stride < 16 || 4 * ne >= (1LL << 31)) {
     ctx->err = "pmx_upload_new_tets: bad new tets";
@@ -945,14 +1095,22 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
     CK(hipMemcpyAsync(ctx->d_pval.p, vals.data(), vals.size() * sizeof(double), hipMemcpyHostToDevice, st));
     launch_patch_rows(ctx->d_pent.p, ctx->d_pval.p, (int64_t)ent.size(), S, ctx->d_sol.p, st);
   }
-  // face adjacency: the caller's (Mmg's mesh->adja after remeshing) or built
-  // here from the device-resident new tets
-  if (m->adja) {
-    CK(hipMemcpyAsync(ctx->d_adja.p, m->adja, (size_t)(4 * ne + 5) * sizeof(int), hipMemcpyHostToDevice, st));
-  } else if (!pmx_ctx_build_adja_device(ctx, ctx->d_ntetv.p, ne, n, ctx->d_adja.p)) {
-    return 0;
+  // tet records: prepared while the step ran (residency on), else from the
+  // caller's Mmg adjacency (mesh->adja after remeshing) or one built here
+  if (ctx->next_topo && !m->adja) {
+    CK(hipEventSynchronize(ctx->ev_topo));
+    ctx->next_topo = false;
+    if (*ctx->h_nbad) { ctx->err = "pmx_promote_background: non-manifold tet faces"; return 0; }
+    std::swap(ctx->d_tets, ctx->d_tets_next);
+    std::swap(ctx->d_tets_s, ctx->d_tets_s_next);
+  } else {
+    if (m->adja) {
+      CK(hipMemcpyAsync(ctx->d_adja.p, m->adja, (size_t)(4 * ne + 5) * sizeof(int), hipMemcpyHostToDevice, st));
+    } else if (!pmx_ctx_build_adja_device(ctx, ctx->d_ntetv.p, ne, n, ctx->d_adja.p, st, nullptr)) {
+      return 0;
+    }
+    launch_build_tetrec(ctx->d_ntetv.p, ctx->d_adja.p, ne, PMX_HINT_STRIDE, ctx->d_tets.p, ctx->d_tets_s.p, st);
   }
-  launch_build_tetrec(ctx->d_ntetv.p, ctx->d_adja.p, ne, PMX_HINT_STRIDE, ctx->d_tets.p, ctx->d_tets_s.p, st);
   ctx->np = n;
   ctx->ne = ne;
   ctx->nt = nt;
@@ -1004,7 +1162,8 @@ void pmx_ctx::free_all() {
   dfree(d_ptag); dfree(d_touch); dfree(d_cidx); dfree(d_intv); dfree(d_pub); dfree(d_pkey);
   dfree(d_ppt); dfree(d_pedge); dfree(d_ntetv); dfree(d_nqual); dfree(d_qtag); dfree(d_gather);
   dfree(d_adja); dfree(d_tcnt); dfree(d_toff); dfree(d_tbad); dfree(d_trec); dfree(d_ttmp);
-  dfree(d_pent); dfree(d_pval);
+  dfree(d_pent); dfree(d_pval); dfree(d_tets_next); dfree(d_tets_s_next);
+  next_topo = false;
   dfree(d_cmet); dfree(d_ctag); dfree(d_cperm); dfree(d_cdst); dfree(d_ccnt); dfree(d_cold);
   dfree(d_cvals);
   if (d_tgrid) hipFree(d_tgrid);

@@ -23,6 +23,7 @@ struct pmx_ctx {
   // joined before the fallback: it overlaps the volume walk
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_dl[8] = {};             // chunked download: one per chunk
   std::string err;
   int fallback_blocks = 0;              // co-resident k_fallback workgroups
   // pinned host staging arena (hipHostMalloc, grown on demand, reused across
@@ -109,6 +110,15 @@ struct pmx_ctx {
   DevBuf<char> d_ttmp;
   DevBuf<int4> d_pent;                  // promote: patched rows
   DevBuf<double> d_pval;
+  // residency (pmx_set_residency): the next background's tet records, built
+  // from the new tets on the `topo` stream while the current step runs
+  bool residency = false;
+  hipStream_t topo = nullptr;
+  hipEvent_t ev_topo = nullptr;
+  bool next_topo = false;               // d_tets_next / d_tets_s_next are being built
+  DevBuf<TetRec> d_tets_next;
+  DevBuf<int4> d_tets_s_next;
+  unsigned *h_nbad = nullptr;           // pinned: non-manifold faces of that build
   DevBuf<double> d_nqual;
   bool have_qtag = false;               // raw tags of the new points
   DevBuf<uint16_t> d_qtag;
@@ -151,5 +161,8 @@ bool pmx_ctx_build_adja_host(pmx_ctx *ctx, const pmx_mesh_view *m, std::vector<i
 // face adjacency of device connectivity (1-based int4, slot 0 unused) into
 // dadja (Mmg layout, 4 ne + 5 ints), context-owned scratch; false on a
 // non-manifold face or a failure (ctx->err)
-bool pmx_ctx_build_adja_device(pmx_ctx *ctx, const int4 *tv, int64_t ne, int64_t np, int *dadja);
+// h_nbad != NULL: asynchronous on stream s, the non-manifold count lands in
+// *h_nbad (pinned) when the stream gets there; NULL: checked before returning
+bool pmx_ctx_build_adja_device(pmx_ctx *ctx, const int4 *tv, int64_t ne, int64_t np, int *dadja,
+                               hipStream_t s, unsigned *h_nbad);
 extern "C" int pmx_timing_reset(pmx_ctx *ctx);

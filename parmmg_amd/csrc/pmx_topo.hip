@@ -268,8 +268,8 @@ bool pmx_ctx_build_adja_host(pmx_ctx *ctx, const pmx_mesh_view *m, std::vector<i
 
 // face adjacency of a device connectivity stream with the context's buffers
 // (promoted backgrounds: the new tets are already on the device)
-bool pmx_ctx_build_adja_device(pmx_ctx *ctx, const int4 *tv, int64_t ne, int64_t np, int *dadja) {
-  hipStream_t s = ctx->stream;
+bool pmx_ctx_build_adja_device(pmx_ctx *ctx, const int4 *tv, int64_t ne, int64_t np, int *dadja,
+                               hipStream_t s, unsigned *h_nbad) {
   size_t bytes = 0;
   hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const unsigned *)nullptr, (unsigned *)nullptr,
                                    (int)(np + 2), s);
@@ -289,6 +289,11 @@ bool pmx_ctx_build_adja_device(pmx_ctx *ctx, const int4 *tv, int64_t ne, int64_t
   hipLaunchKernelGGL(k_face_scatter, dim3(nblk(4 * ne)), dim3(256), 0, s, tv, ne, cnt, ctx->d_trec.p);
   hipLaunchKernelGGL(k_face_match, dim3(nblk(4 * ne)), dim3(256), 0, s, ctx->d_trec.p, np + 1, off, dadja,
                      nbad);
+  if (h_nbad) {
+    if (hipMemcpyAsync(h_nbad, nbad, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess)
+      return topo_fail(ctx, "device adjacency: launch");
+    return true;
+  }
   unsigned hb = 0;
   if (hipMemcpyAsync(&hb, nbad, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)

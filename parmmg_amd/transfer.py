@@ -123,13 +123,18 @@ class Transfer:
                                                  imet if arr else -1), "pmx_upload_background")
         self.sizes = [v.size for v in views[: len(arr)]]
 
+    def set_residency(self, on: bool = True):
+        self._chk(self.lib.pmx_set_residency(self.ctx, int(on)), "pmx_set_residency")
+
     def upload_points(self, xyz: np.ndarray, tags: np.ndarray | None = None,
-                      tets: np.ndarray | None = None):
+                      tets: np.ndarray | None = None, tets_mmg: np.ndarray | None = None):
         """xyz: (n, 3) new points (0-based list); tags: MMG5_Point.tag values;
         tets: optional (ne+1, 4) new tets with 0-based point indices in rows
         1..ne -- only points of valid tets (v[0] >= 0 here) are located.
         The C view is Mmg's 1-based one (points 1..n, a tet valid when
-        v[0] > 0), so the pointers are shifted by one record."""
+        v[0] > 0), so the pointers are shifted by one record.  tets_mmg: the
+        same tets already in that layout (1-based, v[0] = 0 deleted; passed
+        as is, as a C caller would)."""
         xyz = np.ascontiguousarray(xyz, np.float64)
         pv = N.PointsView()
         pv.first, pv.last = 1, xyz.shape[0]
@@ -139,8 +144,8 @@ class Transfer:
             t = np.ascontiguousarray(tags, np.uint16)
             self._keep.append(t)
             pv.tag, pv.tag_stride = _shift(t, 2, C.c_uint16), 2
-        if tets is not None:
-            tv = _tets_1based(tets)
+        if tets is not None or tets_mmg is not None:
+            tv = _tets_1based(tets) if tets_mmg is None else np.ascontiguousarray(tets_mmg, np.int32)
             self._keep.append(tv)
             pv.tetra_v, pv.tetra_stride, pv.ne = _ip(tv), 16, tv.shape[0] - 1
         self._chk(self.lib.pmx_upload_points(self.ctx, C.byref(pv)), "pmx_upload_points")
@@ -158,10 +163,13 @@ class Transfer:
         o.hsiz, o.timing, o.max_walk, o.hint_stride, o.flags = hsiz, int(timing), max_walk, hint_stride, flags
         self._chk(self.lib.pmx_run(self.ctx, C.byref(o)), "pmx_run")
 
-    def download(self, init: list[np.ndarray] | None = None, into: Result | None = None) -> Result:
+    def download(self, init: list[np.ndarray] | None = None, into: Result | None = None,
+                 sols_only: bool = False) -> Result:
         """Results into new arrays (``init`` = values kept where a field is not
         written), or in place into the arrays of ``into`` -- ParMmg's case, whose
-        ``met->m`` / ``field->m`` already exist (no allocation per step)."""
+        ``met->m`` / ``field->m`` already exist (no allocation per step).
+        sols_only: the fields only (what PMMG_interpMetricsAndFields returns;
+        elem/status/steps are not copied)."""
         n = self.npts
         if into is not None:
             outs, elem, status, steps = into.sols, into.elem, into.status, into.steps
@@ -182,8 +190,11 @@ class Transfer:
         views = (N.SolView * max(len(self.sizes), 1))()
         for i, (a, sz) in enumerate(zip(outs, self.sizes)):
             views[i].size, views[i].m = sz, _dp(a)
-        self._chk(self.lib.pmx_download(self.ctx, views, _ip(elem), _ip(status), _ip(steps)),
-                  "pmx_download")
+        if sols_only:
+            self._chk(self.lib.pmx_download(self.ctx, views, None, None, None), "pmx_download")
+        else:
+            self._chk(self.lib.pmx_download(self.ctx, views, _ip(elem), _ip(status), _ip(steps)),
+                      "pmx_download")
         return Result(outs, elem, status, steps)
 
     def starts(self) -> np.ndarray:

@@ -48,8 +48,11 @@ def compare(a, b, nsol):
         assert bits_equal(a.sols[s], b.sols[s]).all(), f"sol {s} differs"
 
 
-@pytest.mark.parametrize("adja", [True, False])
-def test_promoted_background_equals_host_upload(adja):
+@pytest.mark.parametrize("adja,residency", [(True, False), (False, False), (False, True),
+                                             (True, True)])
+def test_promoted_background_equals_host_upload(adja, residency):
+    """residency: the next background's tet records are built on the device
+    while the step runs (pmx_set_residency) and swapped in by the promotion."""
     m1 = M.kuhn_cube(7, seed=101)
     sols1 = fields(m1)
     m2, x2, t2, tets2 = new_mesh(8, 202)
@@ -59,9 +62,9 @@ def test_promoted_background_equals_host_upload(adja):
     init2[0][::97] = 0.25                      # a few distinct values
 
     tr = Transfer(0)
+    tr.set_residency(residency)
     tr.upload_background(m1, sols1, 0)
     tr.upload_points(x2, t2, tets2)
-    tr.upload_new_tets(tets2)
     tr.run()
     r2 = tr.download(init=init2)
     assert (r2.status != 0).any()
@@ -78,7 +81,6 @@ def test_promoted_background_equals_host_upload(adja):
     r3ref = ref.download()
     compare(r3, r3ref, len(sols1))
     # and one more iteration on the promoted background of the promoted one
-    tr.upload_new_tets(tets3)
     tr.promote_background(m3, r3.sols, adja=adja)
     tr.upload_points(x2, t2, tets2)
     tr.run()
@@ -123,7 +125,7 @@ def test_promote_requires_step_and_tets():
     m2, x2, t2, tets2 = new_mesh(4, 2)
     tr = Transfer(0)
     tr.upload_background(m1, fields(m1)[:1], 0)
-    tr.upload_points(x2, t2, tets2)
+    tr.upload_points(x2, t2)                      # no tets with the points
     with pytest.raises(RuntimeError, match="no step"):
         tr.promote_background(m2, None)
     tr.run()

@@ -12,6 +12,7 @@
 // (visited trias, wedge/cone marks) are kept in thread-private lists.
 #include "pmx_device.h"
 #include "pmx_kernels.h"
+#include <hipcub/hipcub.hpp>
 #include "pmx_internal.h"
 #include <algorithm>
 #include <cmath>
@@ -612,6 +613,68 @@ __device__ int tria_hint(const BdyArgs &A, D3 p) {
 #define BDY_CAP 8
 #define OVF_CAP 2048
 #define OVF_THREADS (64 * 64)
+
+// node -> trias graph (the content of PMMG_precompute_nodeTrias,
+// src/locate_pmmg.c:134-195, in CSR form: ntoff[np+2], ntlist[3 nt], fan order
+// = increasing tria index as in the reference), built on the device from the
+// uploaded trias: count, scan, fill, then each (short) fan sorted.  A host
+// build over np+2 offsets cost 3.6 ms per background at 1.7M vertices.
+__global__ __launch_bounds__(256) void k_nt_count(const TriRec *__restrict__ tris, int64_t nt,
+                                                  int *__restrict__ cnt) {
+  for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= nt;
+       k += (int64_t)gridDim.x * blockDim.x)
+    for (int l = 0; l < 3; l++) atomicAdd(&cnt[tris[k].v[l] + 1], 1);
+}
+__global__ __launch_bounds__(256) void k_nt_fill(const TriRec *__restrict__ tris, int64_t nt,
+                                                 int *__restrict__ cur, int *__restrict__ list) {
+  for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= nt;
+       k += (int64_t)gridDim.x * blockDim.x)
+    for (int l = 0; l < 3; l++) list[atomicAdd(&cur[tris[k].v[l]], 1)] = (int)k;
+}
+__global__ __launch_bounds__(256) void k_nt_sort(const int *__restrict__ off, int64_t np,
+                                                 int *__restrict__ list) {
+  for (int64_t v = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v <= np;
+       v += (int64_t)gridDim.x * blockDim.x) {
+    const int lo = off[v], hi = off[v + 1];
+    for (int i = lo + 1; i < hi; i++) {
+      const int x = list[i];
+      int j = i - 1;
+      while (j >= lo && list[j] > x) { list[j + 1] = list[j]; j--; }
+      list[j + 1] = x;
+    }
+  }
+}
+
+bool pmx_ctx::build_node_trias(hipStream_t s) {
+  if (!pmx_dgrow(this, d_ntoff, (size_t)(np + 2)) || !pmx_dgrow(this, d_ntcur, (size_t)(np + 2)) ||
+      !pmx_dgrow(this, d_ntlist, (size_t)std::max<int64_t>(3 * nt, 1)))
+    return false;
+  size_t bytes = 0;
+  hipcub::DeviceScan::InclusiveSum(nullptr, bytes, (const int *)nullptr, (int *)nullptr, (int)(np + 2), s);
+  if (!pmx_dgrow(this, d_nttmp, bytes)) return false;
+  if (hipMemsetAsync(d_ntcur.p, 0, sizeof(int) * (size_t)(np + 2), s) != hipSuccess) {
+    err = "node trias: memset";
+    return false;
+  }
+  const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nt + 255) / 256, 4096));
+  if (nt > 0) hipLaunchKernelGGL(k_nt_count, dim3(nb), dim3(256), 0, s, d_tris.p, nt, d_ntcur.p);
+  if (hipcub::DeviceScan::InclusiveSum(d_nttmp.p, bytes, d_ntcur.p, d_ntoff.p, (int)(np + 2), s) != hipSuccess ||
+      hipMemcpyAsync(d_ntcur.p, d_ntoff.p, sizeof(int) * (size_t)(np + 2), hipMemcpyDeviceToDevice, s) !=
+          hipSuccess) {
+    err = "node trias: scan";
+    return false;
+  }
+  if (nt > 0) {
+    hipLaunchKernelGGL(k_nt_fill, dim3(nb), dim3(256), 0, s, d_tris.p, nt, d_ntcur.p, d_ntlist.p);
+    const unsigned nv = (unsigned)std::max<int64_t>(1, std::min<int64_t>((np + 255) / 256, 8192));
+    hipLaunchKernelGGL(k_nt_sort, dim3(nv), dim3(256), 0, s, d_ntoff.p, np, d_ntlist.p);
+  }
+  if (hipGetLastError() != hipSuccess) {
+    err = "node trias: launch";
+    return false;
+  }
+  return true;
+}
 
 // the coarser tria hint grid over the background bbox: cells of about 8
 // boundary trias.  The grid is 3-D but only its surface cells are used, so it

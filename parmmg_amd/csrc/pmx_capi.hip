@@ -11,12 +11,14 @@
 #include <cstring>
 #include <string>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
 #include <thread>
 #include <vector>
 
+#include <hipcub/hipcub.hpp>
 #include "pmx_transfer.h"
 #include "pmx_kernels.h"
 #include "pmx_internal.h"
@@ -51,7 +53,8 @@ static char *hstage(pmx_ctx *ctx, size_t bytes) { return pmx_hstage(ctx, bytes);
 static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 // host gathers/scatters of large AoS arrays split over a few threads
-// (PMX_HOST_THREADS, default min(8, hardware threads)); ranges below
+// (PMX_HOST_THREADS, default min(8, hardware threads); 16 measured slower on a
+// GPU box's 16-CPU share); ranges below
 // PMX_HOST_THREADS_MIN elements (default 2^18) stay serial
 static unsigned host_threads() {
   static const unsigned T = [] {
@@ -69,6 +72,25 @@ static int64_t host_threads_min() {
   }();
   return M;
 }
+// PMX_TRACE=1: host phase timings of the staging calls on stderr
+namespace {
+struct Trace {
+  const char *who;
+  bool on;
+  std::chrono::steady_clock::time_point t0, last;
+  explicit Trace(const char *w) : who(w), on(getenv("PMX_TRACE") != nullptr) {
+    if (on) t0 = last = std::chrono::steady_clock::now();
+  }
+  void mark(const char *what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[pmx] %s %-22s %8.3f ms\n", who, what,
+            std::chrono::duration<double, std::milli>(now - last).count());
+    last = now;
+  }
+};
+}  // namespace
+
 // a persistent pool of host_threads()-1 workers (thread creation per pass
 // cost ~0.1 ms per pass and dominated the chunked copies); the calling thread
 // takes part.  One job at a time (a mutex serialises concurrent callers).
@@ -460,7 +482,6 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   if (!stage_trias(ctx, m, np, htr)) return 0;
   ctx->np = np; ctx->ne = ne; ctx->nt = nt; ctx->hausd = m->hausd;
   ctx->sd = sd;
-  ctx->host_build_node_trias(htr);
 
   if (!setup_grids(ctx, lo, hi, ne)) return 0;
 
@@ -471,16 +492,12 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   if (!dgrow(ctx, ctx->d_tris, (size_t)(nt + 1))) return 0;
   if (!dgrow(ctx, ctx->d_trn, (size_t)(nt + 1))) return 0;
   if (!dgrow(ctx, ctx->d_xyzq, (size_t)(np + 1))) return 0;
-  if (!dgrow(ctx, ctx->d_ntoff, ctx->h_ntoff.size())) return 0;
-  if (!dgrow(ctx, ctx->d_ntlist, std::max<size_t>(ctx->h_ntlist.size(), 1))) return 0;
   CK(hipMemcpyAsync(ctx->d_xyz.p, hp, (size_t)(np + 1) * 24, hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_tets.p, ht, (size_t)(ne + 1) * sizeof(TetRec), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_tets_s.p, hh, (size_t)ns * sizeof(int4), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_sol.p, hs, hs_n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_tris.p, htr.data(), htr.size() * sizeof(TriRec), hipMemcpyHostToDevice, ctx->stream));
-  CK(hipMemcpyAsync(ctx->d_ntoff.p, ctx->h_ntoff.data(), ctx->h_ntoff.size() * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
-  if (!ctx->h_ntlist.empty())
-    CK(hipMemcpyAsync(ctx->d_ntlist.p, ctx->h_ntlist.data(), ctx->h_ntlist.size() * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+  if (!ctx->build_node_trias(ctx->stream)) return 0;
   CK(hipStreamSynchronize(ctx->stream));   // host staging vectors die here
   ctx->have_bg = true;
   return 1;
@@ -490,6 +507,7 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   if (!ctx) return 0;
   ctx->have_pts = ctx->ran = false;
   ctx->have_ntet = false;                  // the new tets belong to the points
+  Trace tr("points");
   if (ctx->next_topo) {                     // its buffers are about to be reused
     CK(hipStreamSynchronize(ctx->topo));
     ctx->next_topo = false;
@@ -506,36 +524,64 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
     return 0;
   }
   const size_t nn = (size_t)std::max<int64_t>(n, 1);
-  // staging layout (pinned): q | kind | vol list | bdy list | dense vol coords
-  // | raw tags (statistics of the new mesh)
-  // | the new tets (kept on the device: new-mesh quality, residency)
+  // The host packs and sends only what the device cannot derive -- dense
+  // coordinates (24 B), tags (2 B), the new tets (16 B) -- in a pinned
+  // staging arena, chunked so that DMA overlaps packing; the kinds, the
+  // per-path lists (order-preserving compaction) and the list-ordered volume
+  // coordinates are built on the device (r02: host classification + lists +
+  // their DMA were 3-5 ms of the 1.7M-point C2 upload).
   const int64_t ntet = pv->tetra_v ? pv->ne : 0;
-  const size_t o_q = 0, o_k = o_q + al256(nn * sizeof(Pt4)), o_vl = o_k + al256(nn),
-               o_bl = o_vl + al256(nn * sizeof(int)), o_qv = o_bl + al256(nn * sizeof(int)),
-               o_tg = o_qv + al256(nn * 3 * sizeof(double)),
+  const size_t o_x = 0, o_tg = o_x + al256(nn * 3 * sizeof(double)),
                o_tv = o_tg + al256(pv->tag ? nn * 2 : 0),
                total = o_tv + al256(ntet ? (size_t)(ntet + 1) * sizeof(int4) : 0);
   CK(hipStreamSynchronize(ctx->stream));   // the arena may still feed an earlier copy
   char *st = hstage(ctx, total);
   if (!st) return 0;
-  Pt4 *hq = (Pt4 *)(st + o_q);
-  int8_t *hk = (int8_t *)(st + o_k);
-  int *vl = (int *)(st + o_vl), *bl = (int *)(st + o_bl);
-  double *hqv = (double *)(st + o_qv);
+  double *hx = (double *)(st + o_x);
   uint16_t *htg = (uint16_t *)(st + o_tg);
+  int4 *htv = (int4 *)(st + o_tv);
   const char *pc = (const char *)pv->c;
   const char *tg = (const char *)pv->tag;
-  // points referenced by a valid new tet (the reference visits only those,
-  // src/interpmesh_pmmg.c:535-541); marked into the kind array first.  The
-  // same pass packs the tets (vertex = view index - first + 1) for the device
-  int4 *htv = (int4 *)(st + o_tv);
-  if (pv->tetra_v) {
-    memset(hk, 0, (size_t)n);
+  if (!dgrow(ctx, ctx->d_qxyz, nn * 3) || !dgrow(ctx, ctx->d_q, nn) || !dgrow(ctx, ctx->d_kind, nn) ||
+      !dgrow(ctx, ctx->d_qmark, nn) || !dgrow(ctx, ctx->d_fvol, nn) || !dgrow(ctx, ctx->d_fbdy, nn) ||
+      !dgrow(ctx, ctx->d_nsel, 2) || !dgrow(ctx, ctx->d_vollist, nn) || !dgrow(ctx, ctx->d_bdylist, nn) ||
+      !dgrow(ctx, ctx->d_qv, nn * 3) || (tg && !dgrow(ctx, ctx->d_qtag, nn)) ||
+      (ntet && !dgrow(ctx, ctx->d_ntetv, (size_t)(ntet + 1))))
+    return 0;
+  // coordinates (+ bounding box: a promoted background's hint grid) and tags
+  double qlo[64][3], qhi[64][3];
+  const int C = par_chunks(0, n, [&](int ci, int64_t j0, int64_t j1) {
+    double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+    for (int64_t j = j0; j < j1; j++) {
+      const double *c = (const double *)(pc + (pv->first + j) * pv->stride);
+      for (int ax = 0; ax < 3; ax++) {
+        hx[3 * j + ax] = c[ax];
+        lo[ax] = std::min(lo[ax], c[ax]);
+        hi[ax] = std::max(hi[ax], c[ax]);
+      }
+      if (tg) htg[j] = *(const uint16_t *)(tg + (pv->first + j) * pv->tag_stride);
+    }
+    for (int ax = 0; ax < 3; ax++) { qlo[ci][ax] = lo[ax]; qhi[ci][ax] = hi[ax]; }
+  });
+  for (int ax = 0; ax < 3; ax++) {
+    ctx->qlo[ax] = HUGE_VAL;
+    ctx->qhi[ax] = -HUGE_VAL;
+    for (int i = 0; i < C; i++) {
+      ctx->qlo[ax] = std::min(ctx->qlo[ax], qlo[i][ax]);
+      ctx->qhi[ax] = std::max(ctx->qhi[ax], qhi[i][ax]);
+    }
+  }
+  if (n) {
+    CK(hipMemcpyAsync(ctx->d_qxyz.p, hx, (size_t)n * 3 * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    if (tg) CK(hipMemcpyAsync(ctx->d_qtag.p, htg, (size_t)n * 2, hipMemcpyHostToDevice, ctx->stream));
+  }
+  tr.mark("coords");
+  // the new tets (vertex = view index - first + 1), validated, packed in
+  // chunks whose DMA overlaps the packing of the next
+  if (ntet) {
     htv[0] = make_int4(0, 0, 0, 0);
-    if (!dgrow(ctx, ctx->d_ntetv, (size_t)(ntet + 1))) return 0;
     const char *tc = (const char *)pv->tetra_v;
     bool bad = false;
-    // in chunks: the DMA of a packed chunk overlaps the packing of the next
     const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(8, ntet >> 20));
     for (int64_t c = 0; c < nch; c++) {
       const int64_t lo = (c == 0) ? 0 : 1 + ntet * c / nch, hi = 1 + ntet * (c + 1) / nch;
@@ -546,10 +592,9 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
           if (v[0] <= 0) { htv[k] = make_int4(0, 0, 0, 0); continue; }   // !MG_EOK
           int w[4];
           for (int l = 0; l < 4; l++) {
-            const int64_t j = (int64_t)v[l] - pv->first;
-            w[l] = (int)(j + 1);
-            if (j < 0 || j >= n) { b = true; continue; }
-            __atomic_store_n(&hk[j], (int8_t)1, __ATOMIC_RELAXED);
+            const int64_t jj = (int64_t)v[l] - pv->first;
+            if (jj < 0 || jj >= n) b = true;
+            w[l] = (int)(jj + 1);
           }
           htv[k] = make_int4(w[0], w[1], w[2], w[3]);
         }
@@ -564,66 +609,27 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
       return 0;
     }
   }
-  const bool use_mark = pv->tetra_v != nullptr;
-  // two passes over fixed chunks (threads): classify + count, then fill the
-  // per-path point lists at the chunks' exclusive offsets (input order kept)
-  std::vector<int64_t> cv(65, 0), cb(65, 0);
-  double qlo[64][3], qhi[64][3];   // bbox per chunk (a promoted background's hint grid)
-  const int C = par_chunks(0, n, [&](int ci, int64_t j0, int64_t j1) {
-    int64_t a = 0, b = 0;
-    double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
-    for (int64_t j = j0; j < j1; j++) {
-      const double *c = (const double *)(pc + (pv->first + j) * pv->stride);
-      hq[j] = Pt4{c[0], c[1], c[2], 0.0};
-      for (int ax = 0; ax < 3; ax++) {
-        lo[ax] = std::min(lo[ax], c[ax]);
-        hi[ax] = std::max(hi[ax], c[ax]);
-      }
-      unsigned tag = tg ? *(const uint16_t *)(tg + (pv->first + j) * pv->tag_stride) : 0u;
-      if (tg) htg[j] = (uint16_t)tag;
-      int8_t kd;
-      if (tag >= PMX_TAG_NUL) kd = KIND_NUL;                 // !MG_VOK
-      else if (use_mark && !hk[j]) kd = KIND_ORPH;           // in no valid new tet
-      else if (tag & PMX_TAG_REQ) kd = KIND_SKIP;
-      else if (tag & PMX_TAG_BDY) { kd = KIND_BDY; b++; }
-      else { kd = KIND_VOL; a++; }
-      hk[j] = kd;
-    }
-    cv[(size_t)ci + 1] = a;
-    cb[(size_t)ci + 1] = b;
-    for (int ax = 0; ax < 3; ax++) { qlo[ci][ax] = lo[ax]; qhi[ci][ax] = hi[ax]; }
-  });
-  for (int ax = 0; ax < 3; ax++) {
-    ctx->qlo[ax] = HUGE_VAL;
-    ctx->qhi[ax] = -HUGE_VAL;
-    for (int i = 0; i < C; i++) {
-      ctx->qlo[ax] = std::min(ctx->qlo[ax], qlo[i][ax]);
-      ctx->qhi[ax] = std::max(ctx->qhi[ax], qhi[i][ax]);
-    }
-  }
-  // the points and their kinds go down while the lists are built
-  if (!dgrow(ctx, ctx->d_q, nn) || !dgrow(ctx, ctx->d_kind, nn)) return 0;
-  if (n) {
-    CK(hipMemcpyAsync(ctx->d_q.p, hq, (size_t)n * sizeof(Pt4), hipMemcpyHostToDevice, ctx->stream));
-    CK(hipMemcpyAsync(ctx->d_kind.p, hk, (size_t)n, hipMemcpyHostToDevice, ctx->stream));
-  }
-  for (int i = 0; i < C; i++) { cv[(size_t)i + 1] += cv[(size_t)i]; cb[(size_t)i + 1] += cb[(size_t)i]; }
-  const int64_t nv = cv[(size_t)C], nb = cb[(size_t)C];
-  par_chunks(0, n, [&](int ci, int64_t j0, int64_t j1) {
-    int64_t a = cv[(size_t)ci], b = cb[(size_t)ci];
-    for (int64_t j = j0; j < j1; j++) {
-      if (hk[j] == KIND_BDY) bl[b++] = (int)j;
-      else if (hk[j] == KIND_VOL) {
-        // the volume points' coordinates once more, dense (24 B) and contiguous
-        // in list order: the walks read them coalesced, without a list -> q gather
-        hqv[3 * a] = hq[j].x; hqv[3 * a + 1] = hq[j].y; hqv[3 * a + 2] = hq[j].z;
-        vl[a++] = (int)j;
-      }
-    }
-  });
+  tr.mark("tets pack+dma");
+  // kinds, lists (input order kept), list-ordered volume coordinates
   ctx->nq = n;
-  ctx->nq_vol = nv;
-  ctx->nq_bdy = nb;
+  if (n) {
+    launch_classify_points(ctx->d_qxyz.p, tg ? ctx->d_qtag.p : nullptr, pv->tetra_v != nullptr,
+                           ntet ? ctx->d_ntetv.p : nullptr, ntet, ctx->d_qmark.p, n, ctx->d_q.p, ctx->d_kind.p,
+                           ctx->d_fvol.p, ctx->d_fbdy.p, ctx->stream);
+    hipcub::CountingInputIterator<int> idx(0);
+    size_t bytes = 0;
+    hipcub::DeviceSelect::Flagged(nullptr, bytes, idx, ctx->d_fvol.p, ctx->d_vollist.p, ctx->d_nsel.p, (int)n,
+                                  ctx->stream);
+    if (!dgrow(ctx, ctx->d_seltmp, bytes)) return 0;
+    CK(hipcub::DeviceSelect::Flagged(ctx->d_seltmp.p, bytes, idx, ctx->d_fvol.p, ctx->d_vollist.p, ctx->d_nsel.p,
+                                     (int)n, ctx->stream));
+    CK(hipcub::DeviceSelect::Flagged(ctx->d_seltmp.p, bytes, idx, ctx->d_fbdy.p, ctx->d_bdylist.p,
+                                     ctx->d_nsel.p + 1, (int)n, ctx->stream));
+    launch_gather_qv(ctx->d_qxyz.p, ctx->d_vollist.p, ctx->d_nsel.p, n, ctx->d_qv.p, ctx->stream);
+    CK(hipGetLastError());
+  }
+  int cnt[2] = {0, 0};
+  if (n) CK(hipMemcpyAsync(cnt, ctx->d_nsel.p, sizeof cnt, hipMemcpyDeviceToHost, ctx->stream));
   if (!dgrow(ctx, ctx->d_wmask, nn)) return 0;
   if (!dgrow(ctx, ctx->d_elem, nn)) return 0;
   if (!dgrow(ctx, ctx->d_status, nn)) return 0;
@@ -641,21 +647,14 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   if (!dgrow(ctx, ctx->d_best, nn)) return 0;
   if (!dgrow(ctx, ctx->d_ties, nn)) return 0;
   if (!dgrow(ctx, ctx->d_counts, 32)) return 0;
-  if (!dgrow(ctx, ctx->d_vollist, (size_t)std::max<int64_t>(nv, 1))) return 0;
-  if (!dgrow(ctx, ctx->d_bdylist, (size_t)std::max<int64_t>(nb, 1))) return 0;
-  // one record per wave
-  if (!dgrow(ctx, ctx->d_vstat, (size_t)std::max<int64_t>((nv + 255) / 256 * 4 + 4, 1))) return 0;
-  if (!dgrow(ctx, ctx->d_bstat, (size_t)std::max<int64_t>((nb + 255) / 256 * 4 + 4, 1))) return 0;
-  if (!dgrow(ctx, ctx->d_qv, (size_t)std::max<int64_t>(nv, 1) * 3)) return 0;
-  if (nv) CK(hipMemcpyAsync(ctx->d_vollist.p, vl, (size_t)nv * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
-  if (nv) CK(hipMemcpyAsync(ctx->d_qv.p, hqv, (size_t)nv * 3 * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-  if (nb) CK(hipMemcpyAsync(ctx->d_bdylist.p, bl, (size_t)nb * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+  // one record per wave (sized for every point on one path)
+  if (!dgrow(ctx, ctx->d_vstat, (nn + 255) / 256 * 4 + 4)) return 0;
+  if (!dgrow(ctx, ctx->d_bstat, (nn + 255) / 256 * 4 + 4)) return 0;
   ctx->have_qtag = false;
-  if (tg && n) {
-    if (!dgrow(ctx, ctx->d_qtag, nn)) return 0;
-    CK(hipMemcpyAsync(ctx->d_qtag.p, htg, (size_t)n * 2, hipMemcpyHostToDevice, ctx->stream));
-  }
   CK(hipStreamSynchronize(ctx->stream));
+  tr.mark("classify + sync");
+  ctx->nq_vol = cnt[0];
+  ctx->nq_bdy = cnt[1];
   ctx->have_qtag = tg && n;
   ctx->pts_first = pv->first;
   ctx->have_pts = true;
@@ -1046,9 +1045,11 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
       return 0;
     }
   hipSetDevice(ctx->device);
+  Trace tr("promote");
   hipStream_t st = ctx->stream;
   CK(hipStreamSynchronize(st));
   if (!ctx->check_device_errors()) return 0;
+  tr.mark("sync");
   const int S = sd.S;
   const int64_t first = ctx->pts_first;
   // rows the step did not write keep the caller's values (Mmg's own, or the
@@ -1057,25 +1058,40 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
   if (!stg) return 0;
   CK(hipMemcpyAsync(stg, ctx->d_wmask.p, (size_t)n, hipMemcpyDeviceToHost, st));
   CK(hipStreamSynchronize(st));
-  std::vector<uint8_t> wm((const uint8_t *)stg, (const uint8_t *)stg + n);
+  const uint8_t *wm = (const uint8_t *)stg;
+  const unsigned full = (1u << nsol) - 1u;
+  // per chunk, then concatenated in chunk order
+  std::vector<std::vector<int4>> cent(64);
+  std::vector<std::vector<double>> cval(64);
+  bool missing = false;
+  const int nch = par_chunks(0, n, [&](int c, int64_t j0, int64_t j1) {
+    for (int64_t j = j0; j < j1; j++) {
+      if ((wm[j] & full) == full) continue;      // every solution written (the common case)
+      for (int s = 0; s < nsol; s++) {
+        if (wm[j] & (1u << s)) continue;
+        const int sz = sd.size[s];
+        if (!sols[s].m) { __atomic_store_n(&missing, true, __ATOMIC_RELAXED); continue; }
+        cent[(size_t)c].push_back(make_int4((int)(j + 1), sd.off[s], sz, 0));
+        const double *src = sols[s].m + (first + j) * sz;
+        for (int q = 0; q < 6; q++) cval[(size_t)c].push_back(q < sz ? src[q] : 0.0);
+      }
+    }
+  });
+  if (missing) {
+    ctx->err = "pmx_promote_background: a row the step did not write needs the caller's solution";
+    return 0;
+  }
   std::vector<int4> ent;
   std::vector<double> vals;
-  for (int s = 0; s < nsol; s++) {
-    const int sz = sd.size[s];
-    for (int64_t j = 0; j < n; j++) {
-      if (wm[(size_t)j] & (1u << s)) continue;
-      if (!sols[s].m) {
-        ctx->err = "pmx_promote_background: a row the step did not write needs the caller's solution";
-        return 0;
-      }
-      ent.push_back(make_int4((int)(j + 1), sd.off[s], sz, 0));
-      const double *src = sols[s].m + (first + j) * sz;
-      for (int q = 0; q < 6; q++) vals.push_back(q < sz ? src[q] : 0.0);
-    }
+  for (int c = 0; c < nch; c++) {
+    ent.insert(ent.end(), cent[(size_t)c].begin(), cent[(size_t)c].end());
+    vals.insert(vals.end(), cval[(size_t)c].begin(), cval[(size_t)c].end());
   }
+  tr.mark("unwritten rows");
   // boundary trias of the new mesh (the host's: Mmg's numbering)
   std::vector<TriRec> htr;
   if (!stage_trias(ctx, m, n, htr)) return 0;
+  tr.mark("trias");
   // the background invalid until this completes
   ctx->have_bg = ctx->have_derived = ctx->have_tetv = ctx->have_qual = ctx->have_ptag = false;
   ctx->stat_np = -1;
@@ -1097,8 +1113,10 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
   }
   // tet records: prepared while the step ran (residency on), else from the
   // caller's Mmg adjacency (mesh->adja after remeshing) or one built here
+  tr.mark("promote launch");
   if (ctx->next_topo && !m->adja) {
     CK(hipEventSynchronize(ctx->ev_topo));
+    tr.mark("wait topo");
     ctx->next_topo = false;
     if (*ctx->h_nbad) { ctx->err = "pmx_promote_background: non-manifold tet faces"; return 0; }
     std::swap(ctx->d_tets, ctx->d_tets_next);
@@ -1115,16 +1133,14 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
   ctx->ne = ne;
   ctx->nt = nt;
   ctx->hausd = m->hausd;
-  ctx->host_build_node_trias(htr);
+  tr.mark("tet records");
   if (!setup_grids(ctx, ctx->qlo, ctx->qhi, ne)) return 0;
-  if (!dgrow(ctx, ctx->d_ntoff, ctx->h_ntoff.size())) return 0;
-  if (!dgrow(ctx, ctx->d_ntlist, std::max<size_t>(ctx->h_ntlist.size(), 1))) return 0;
+  tr.mark("grids");
   CK(hipMemcpyAsync(ctx->d_tris.p, htr.data(), htr.size() * sizeof(TriRec), hipMemcpyHostToDevice, st));
-  CK(hipMemcpyAsync(ctx->d_ntoff.p, ctx->h_ntoff.data(), ctx->h_ntoff.size() * sizeof(int), hipMemcpyHostToDevice, st));
-  if (!ctx->h_ntlist.empty())
-    CK(hipMemcpyAsync(ctx->d_ntlist.p, ctx->h_ntlist.data(), ctx->h_ntlist.size() * sizeof(int), hipMemcpyHostToDevice, st));
+  if (!ctx->build_node_trias(st)) return 0;
   CK(hipGetLastError());
   CK(hipStreamSynchronize(st));            // host vectors die here
+  tr.mark("uploads + sync");
   ctx->have_ptag = tags;
   // the points and the results were consumed: the next step needs new points
   ctx->have_pts = ctx->ran = ctx->have_ntet = false;
@@ -1153,7 +1169,7 @@ void pmx_ctx::free_all() {
   h_stage = nullptr;
   h_stage_cap = 0;
   dfree(d_xyz); dfree(d_tets); dfree(d_sol); dfree(d_tets_s); dfree(d_tris); dfree(d_ntoff);
-  dfree(d_ntlist); dfree(d_xyzq); dfree(d_trn); dfree(d_grid); dfree(d_tetv);
+  dfree(d_ntlist); dfree(d_ntcur); dfree(d_nttmp); dfree(d_xyzq); dfree(d_trn); dfree(d_grid); dfree(d_tetv);
   dfree(d_q); dfree(d_kind); dfree(d_wmask); dfree(d_out); dfree(d_elem); dfree(d_status);
   dfree(d_steps); dfree(d_start); dfree(d_edge); dfree(d_vertex); dfree(d_list); dfree(d_found);
   dfree(d_bestk); dfree(d_best); dfree(d_ties); dfree(d_counts); dfree(d_vollist); dfree(d_bdylist);
@@ -1174,16 +1190,3 @@ void pmx_ctx::free_all() {
   stat_np = -1;
 }
 
-// node -> trias graph: offsets[np+2] (0-based CSR) + list of incident trias
-// (the content of PMMG_precompute_nodeTrias, src/locate_pmmg.c:134-195, in
-// CSR form; fan order = increasing tria index, as in the reference)
-void pmx_ctx::host_build_node_trias(const std::vector<TriRec> &tr) {
-  h_ntoff.assign((size_t)(np + 2), 0);
-  for (int64_t k = 1; k <= nt; k++)
-    for (int l = 0; l < 3; l++) h_ntoff[(size_t)tr[(size_t)k].v[l] + 1]++;
-  for (int64_t i = 1; i <= np + 1; i++) h_ntoff[(size_t)i] += h_ntoff[(size_t)i - 1];
-  h_ntlist.assign((size_t)h_ntoff[(size_t)np + 1], 0);
-  std::vector<int> fill(h_ntoff.begin(), h_ntoff.end() - 1);
-  for (int64_t k = 1; k <= nt; k++)
-    for (int l = 0; l < 3; l++) h_ntlist[(size_t)fill[(size_t)tr[(size_t)k].v[l]]++] = (int)k;
-}

@@ -44,8 +44,8 @@ struct pmx_ctx {
   DevBuf<double> d_sol;
   DevBuf<int4> d_tets_s;                // host-packed hint sample: tets 1, 1+4, 1+8, ...
   DevBuf<TriRec> d_tris;
-  DevBuf<int> d_ntoff, d_ntlist;
-  std::vector<int> h_ntoff, h_ntlist;
+  DevBuf<int> d_ntoff, d_ntlist, d_ntcur;   // node -> trias CSR (built on the device)
+  DevBuf<char> d_nttmp;
   // derived from the raw uploads on the device (k_bg_derive), by the first
   // step after an upload or by every step with PMX_RUN_FRESH_BACKGROUND
   bool have_derived = false;
@@ -72,6 +72,10 @@ struct pmx_ctx {
   DevBuf<unsigned> d_counts;            // step counters, see pmx_kernels.h
   DevBuf<int> d_vollist, d_bdylist;     // compacted point lists per path
   DevBuf<double> d_qv;                  // volume points, dense xyz in list order
+  DevBuf<double> d_qxyz;                // new points as uploaded (dense xyz)
+  DevBuf<uint8_t> d_qmark, d_fvol, d_fbdy;
+  DevBuf<int> d_nsel;                   // compaction counts: volume, surface
+  DevBuf<char> d_seltmp;
   DevBuf<uint4> d_vstat, d_bstat;       // per-wave walk statistics
   DevBuf<int> d_blist, d_olist, d_ows;
   int *d_tgrid = nullptr;
@@ -132,7 +136,7 @@ struct pmx_ctx {
 
   hipEvent_t *next_event_slot();
   void free_all();
-  void host_build_node_trias(const std::vector<TriRec> &tr);
+  bool build_node_trias(hipStream_t s);   // from d_tris, np, nt (pmx_bdy.hip)
   bool launch_bdy(const VolArgs &a, hipStream_t s);
   bool size_tria_grid();
   // device error word of the last step (after a stream sync): 0 = none

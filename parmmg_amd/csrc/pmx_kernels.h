@@ -80,6 +80,12 @@ void launch_tet_conn(const TetRec *src, int64_t n, int4 *dst, hipStream_t s);
 void launch_promote(const Pt4 *q, const double *out, const uint16_t *qtag, int64_t n, int S, double *xyz,
                     double *sol, uint16_t *ptag, hipStream_t s);
 void launch_patch_rows(const int4 *ent, const double *vals, int64_t n, int S, double *sol, hipStream_t s);
+// new points on the device: orphan marks from the new tets, kinds, path flags
+void launch_classify_points(const double *xyz, const uint16_t *tag, bool use_mark, const int4 *tv, int64_t ne,
+                            uint8_t *mark, int64_t n, Pt4 *q, int8_t *kind, uint8_t *fvol, uint8_t *fbdy,
+                            hipStream_t s);
+void launch_gather_qv(const double *xyz, const int *list, const int *count, int64_t n, double *qv,
+                      hipStream_t s);
 void launch_build_tetrec(const int4 *tv, const int *adja, int64_t ne, int stride, TetRec *tets, int4 *sample,
                          hipStream_t s);
 // workgroups of k_fallback that can be co-resident with `share` other

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include "pmx_device.h"
 #include "pmx_kernels.h"
+#include "pmx_transfer.h"
 
 __device__ __forceinline__ int clampi(double t, int n) {
   if (!(t > 0.0)) return 0;                 // also catches NaN
@@ -499,4 +500,72 @@ void launch_build_tetrec(const int4 *tv, const int *adja, int64_t ne, int stride
                          hipStream_t s) {
   const int64_t nb = std::min<int64_t>(std::max<int64_t>((ne + 256) / 256, 1), 16384);
   hipLaunchKernelGGL(k_build_tetrec, dim3((unsigned)nb), dim3(256), 0, s, tv, adja, ne, stride, tets, sample);
+}
+
+// ---- new points: classification on the device (pmx_upload_points) ---------------
+
+// the points of the valid new tets (the reference's vertex loop over the new
+// tets, src/interpmesh_pmmg.c:535-541); vertex j+1 = point j
+__global__ __launch_bounds__(256) void k_mark_tets(const int4 *__restrict__ tv, int64_t ne,
+                                                   uint8_t *__restrict__ mark) {
+  for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= ne;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int4 t = tv[k];
+    if (t.x <= 0) continue;                      // !MG_EOK
+    mark[t.x - 1] = 1;
+    mark[t.y - 1] = 1;
+    mark[t.z - 1] = 1;
+    mark[t.w - 1] = 1;
+  }
+}
+// kind of every new point (PMMG_interpMetricsAndFields_mesh's dispatch,
+// :541-560) + the per-path flags for the order-preserving compaction
+__global__ __launch_bounds__(256) void k_classify(const double *__restrict__ xyz, const uint16_t *__restrict__ tag,
+                                                  const uint8_t *__restrict__ mark, int64_t n, Pt4 *__restrict__ q,
+                                                  int8_t *__restrict__ kind, uint8_t *__restrict__ fvol,
+                                                  uint8_t *__restrict__ fbdy) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    q[j] = Pt4{xyz[3 * j], xyz[3 * j + 1], xyz[3 * j + 2], 0.0};
+    const unsigned t = tag ? tag[j] : 0u;
+    int8_t kd;
+    if (t >= PMX_TAG_NUL) kd = KIND_NUL;                  // !MG_VOK
+    else if (mark && !mark[j]) kd = KIND_ORPH;            // in no valid new tet
+    else if (t & PMX_TAG_REQ) kd = KIND_SKIP;
+    else if (t & PMX_TAG_BDY) kd = KIND_BDY;
+    else kd = KIND_VOL;
+    kind[j] = kd;
+    fvol[j] = kd == KIND_VOL;
+    fbdy[j] = kd == KIND_BDY;
+  }
+}
+// the volume points' coordinates once more, dense and in list order: the
+// walks read them coalesced, without a list -> point gather
+__global__ __launch_bounds__(256) void k_gather_qv(const double *__restrict__ xyz, const int *__restrict__ list,
+                                                   const int *__restrict__ count, double *__restrict__ qv) {
+  const int64_t nv = count[0];
+  for (int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; a < nv; a += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = list[a];
+    qv[3 * a] = xyz[3 * j];
+    qv[3 * a + 1] = xyz[3 * j + 1];
+    qv[3 * a + 2] = xyz[3 * j + 2];
+  }
+}
+void launch_classify_points(const double *xyz, const uint16_t *tag, bool use_mark, const int4 *tv, int64_t ne,
+                            uint8_t *mark, int64_t n, Pt4 *q, int8_t *kind, uint8_t *fvol, uint8_t *fbdy,
+                            hipStream_t s) {
+  if (use_mark) {                                // new tets given (possibly none)
+    hipMemsetAsync(mark, 0, (size_t)n, s);
+    if (ne > 0) {
+      const int64_t nb = std::min<int64_t>((ne + 255) / 256, 16384);
+      hipLaunchKernelGGL(k_mark_tets, dim3((unsigned)nb), dim3(256), 0, s, tv, ne, mark);
+    }
+  }
+  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 16384));
+  hipLaunchKernelGGL(k_classify, dim3((unsigned)nb), dim3(256), 0, s, xyz, tag, use_mark ? mark : nullptr, n, q,
+                     kind, fvol, fbdy);
+}
+void launch_gather_qv(const double *xyz, const int *list, const int *count, int64_t n, double *qv,
+                      hipStream_t s) {
+  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 16384));
+  hipLaunchKernelGGL(k_gather_qv, dim3((unsigned)nb), dim3(256), 0, s, xyz, list, count, qv);
 }

@@ -36,34 +36,85 @@ __device__ __forceinline__ void sort3i(int &a, int &b, int &c) {
 
 // ---- tet faces -------------------------------------------------------------------
 
+// One thread per tet (its 4 faces), the faces of a workgroup aggregated per
+// bucket (smallest vertex) in an LDS hash table: one global atomic per
+// distinct bucket and workgroup instead of one per face (the neighbouring
+// tets of a workgroup share most of their vertices; per-face atomics cost
+// 3.7 ms of 4.4 at 10M tets).
+#define FACE_HT 2048
+__device__ __forceinline__ void face_key(const int4 t, int f, int &a, int &b, int &c) {
+  const int v[4] = {t.x, t.y, t.z, t.w};
+  a = v[TOPO_IDIR[f][0]];
+  b = v[TOPO_IDIR[f][1]];
+  c = v[TOPO_IDIR[f][2]];
+  sort3i(a, b, c);
+}
+// slot of key a (inserted if absent); the table holds < FACE_HT / 2 keys
+__device__ __forceinline__ int ht_slot(int *keys, int a) {
+  unsigned h = ((unsigned)a * 2654435761u) >> (32 - 11);
+  for (;;) {
+    const int old = atomicCAS(&keys[h], -1, a);
+    if (old == -1 || old == a) return (int)h;
+    h = (h + 1) & (FACE_HT - 1);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_face_count(const int4 *__restrict__ tv, int64_t ne,
                                                     unsigned *__restrict__ cnt) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // face index 4(k-1)+f
-  if (i >= 4 * ne) return;
-  const int64_t k = i / 4 + 1;
-  const int f = (int)(i & 3);
-  const int4 t = tv[k];
-  if (t.x <= 0) return;                          // !MG_EOK: no faces
-  const int v[4] = {t.x, t.y, t.z, t.w};
-  int a = v[TOPO_IDIR[f][0]], b = v[TOPO_IDIR[f][1]], c = v[TOPO_IDIR[f][2]];
-  sort3i(a, b, c);
-  atomicAdd(cnt + a, 1u);
+  __shared__ int keys[FACE_HT];
+  __shared__ unsigned cnts[FACE_HT];
+  for (int i = threadIdx.x; i < FACE_HT; i += blockDim.x) { keys[i] = -1; cnts[i] = 0u; }
+  __syncthreads();
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (k <= ne) {
+    const int4 t = tv[k];
+    if (t.x > 0) {                               // !MG_EOK: no faces
+      for (int f = 0; f < 4; f++) {
+        int a, b, c;
+        face_key(t, f, a, b, c);
+        atomicAdd(&cnts[ht_slot(keys, a)], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < FACE_HT; i += blockDim.x)
+    if (keys[i] >= 0) atomicAdd(cnt + keys[i], cnts[i]);
 }
 
 __global__ __launch_bounds__(256) void k_face_scatter(const int4 *__restrict__ tv, int64_t ne,
                                                       unsigned *__restrict__ cursor,
                                                       int4 *__restrict__ rec) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 4 * ne) return;
-  const int64_t k = i / 4 + 1;
-  const int f = (int)(i & 3);
-  const int4 t = tv[k];
-  if (t.x <= 0) return;                          // !MG_EOK: no faces
-  const int v[4] = {t.x, t.y, t.z, t.w};
-  int a = v[TOPO_IDIR[f][0]], b = v[TOPO_IDIR[f][1]], c = v[TOPO_IDIR[f][2]];
-  sort3i(a, b, c);
-  const unsigned s = atomicAdd(cursor + a, 1u);
-  rec[s] = make_int4(a, b, c, (int)(4 * k + f));
+  __shared__ int keys[FACE_HT];
+  __shared__ unsigned cnts[FACE_HT];
+  for (int i = threadIdx.x; i < FACE_HT; i += blockDim.x) { keys[i] = -1; cnts[i] = 0u; }
+  __syncthreads();
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
+  int4 t = make_int4(0, 0, 0, 0);
+  int slot[4] = {0, 0, 0, 0};
+  unsigned rank[4] = {0u, 0u, 0u, 0u};
+  if (k <= ne) {
+    t = tv[k];
+    if (t.x > 0) {
+      for (int f = 0; f < 4; f++) {
+        int a, b, c;
+        face_key(t, f, a, b, c);
+        slot[f] = ht_slot(keys, a);
+        rank[f] = atomicAdd(&cnts[slot[f]], 1u);   // place inside the workgroup's run
+      }
+    }
+  }
+  __syncthreads();
+  // one reservation per bucket: the workgroup's run starts there
+  for (int i = threadIdx.x; i < FACE_HT; i += blockDim.x)
+    if (keys[i] >= 0) cnts[i] = atomicAdd(cursor + keys[i], cnts[i]);
+  __syncthreads();
+  if (k <= ne && t.x > 0) {
+    for (int f = 0; f < 4; f++) {
+      int a, b, c;
+      face_key(t, f, a, b, c);
+      rec[cnts[slot[f]] + rank[f]] = make_int4(a, b, c, (int)(4 * k + f));
+    }
+  }
 }
 
 // one thread per record: its partner in the bucket of its smallest vertex
@@ -236,10 +287,10 @@ bool build_adja_dev(pmx_ctx *ctx, const int4 *tv, int64_t ne, int64_t np, int *d
   hipMemsetAsync(cnt, 0, sizeof(unsigned) * (size_t)(np + 2), s);
   hipMemsetAsync(nbad, 0, sizeof(unsigned), s);
   hipMemsetAsync(dadja, 0, sizeof(int) * (size_t)(4 * ne + 5), s);
-  hipLaunchKernelGGL(k_face_count, dim3(nblk(4 * ne)), dim3(256), 0, s, tv, ne, cnt);
+  hipLaunchKernelGGL(k_face_count, dim3(nblk(ne)), dim3(256), 0, s, tv, ne, cnt);
   if (!scan_counts(cnt, off, np + 1, s, sc)) return topo_fail(ctx, "pmx_build_adja: scan");
   hipMemcpyAsync(cnt, off, sizeof(unsigned) * (size_t)(np + 2), hipMemcpyDeviceToDevice, s);
-  hipLaunchKernelGGL(k_face_scatter, dim3(nblk(4 * ne)), dim3(256), 0, s, tv, ne, cnt, rec);
+  hipLaunchKernelGGL(k_face_scatter, dim3(nblk(ne)), dim3(256), 0, s, tv, ne, cnt, rec);
   hipLaunchKernelGGL(k_face_match, dim3(nblk(4 * ne)), dim3(256), 0, s, rec, np + 1, off, dadja,
                      nbad);
   if (hipMemcpyAsync(nbad_out, nbad, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -282,11 +333,11 @@ bool pmx_ctx_build_adja_device(pmx_ctx *ctx, const int4 *tv, int64_t ne, int64_t
              hipMemsetAsync(nbad, 0, sizeof(unsigned), s) == hipSuccess &&
              hipMemsetAsync(dadja, 0, sizeof(int) * (size_t)(4 * ne + 5), s) == hipSuccess;
   if (!okk) return topo_fail(ctx, "device adjacency: memset");
-  hipLaunchKernelGGL(k_face_count, dim3(nblk(4 * ne)), dim3(256), 0, s, tv, ne, cnt);
+  hipLaunchKernelGGL(k_face_count, dim3(nblk(ne)), dim3(256), 0, s, tv, ne, cnt);
   if (hipcub::DeviceScan::ExclusiveSum(ctx->d_ttmp.p, bytes, cnt, off, (int)(np + 2), s) != hipSuccess)
     return topo_fail(ctx, "device adjacency: scan");
   hipMemcpyAsync(cnt, off, sizeof(unsigned) * (size_t)(np + 2), hipMemcpyDeviceToDevice, s);
-  hipLaunchKernelGGL(k_face_scatter, dim3(nblk(4 * ne)), dim3(256), 0, s, tv, ne, cnt, ctx->d_trec.p);
+  hipLaunchKernelGGL(k_face_scatter, dim3(nblk(ne)), dim3(256), 0, s, tv, ne, cnt, ctx->d_trec.p);
   hipLaunchKernelGGL(k_face_match, dim3(nblk(4 * ne)), dim3(256), 0, s, ctx->d_trec.p, np + 1, off, dadja,
                      nbad);
   if (h_nbad) {

@@ -211,11 +211,23 @@ typedef struct {
 int PMX_interpMetricsAndFields(pmx_ctx *ctx, int ngrp, pmx_group *grps,
                                const int *permNodGlob, int inputMet);
 
-/* PMMG_copyMetricsAndFields_point (src/interpmesh_pmmg.c:432-446). Old-point
+/* PMMG_copyMetricsAndFields_point (src/interpmesh_pmmg.c:432-446) on the
+ * caller's host arrays (a host loop: nothing to do on the device). Old-point
  * tags are read through old_tag (uint16_t, stride bytes). */
 int PMX_copyMetricsAndFields_point(pmx_ctx *ctx, pmx_group *grp,
                                    const uint16_t *old_tag, int64_t old_tag_stride,
                                    const int *permNodGlob, int renum, int inputMet);
+
+/* The same copy on device-resident data (PMMG_copySol_point, :311-358),
+ * after a pmx_run: rows of the new points that the step did not write take
+ * the background's values of its MG_REQ points (old ip -> new point
+ * permNodGlob[ip], or ip; points-view numbering).  Equivalent to the
+ * reference's copy before the interpolation, which then overwrites the rows
+ * it writes.  Needs the background's point tags on the device (promoted, or
+ * pmx_upload_point_tags); copy_metric: the metric too (inputMet and no
+ * -hsiz, :378).  The copied rows count as written (pmx_download,
+ * pmx_promote_background). */
+int pmx_copy_required(pmx_ctx *ctx, const int *permNodGlob, int copy_metric);
 
 /* ---- statistics ---------------------------------------------------------- */
 /* Reference: PMMG_tetraQual / PMMG_qualhisto / PMMG_prilen (src/parmmg.h:564-566,

@@ -153,6 +153,7 @@ SIGNATURES = {
     "pmx_new_mesh_qual": (C.c_int, [C.c_void_p, iptr, i64, i64, C.c_int, dptr, C.c_void_p]),
     "pmx_upload_new_tets": (C.c_int, [C.c_void_p, iptr, i64, i64]),
     "pmx_set_residency": (C.c_int, [C.c_void_p, C.c_int]),
+    "pmx_copy_required": (C.c_int, [C.c_void_p, iptr, C.c_int]),
     "pmx_promote_background": (C.c_int, [C.c_void_p, C.POINTER(MeshView), C.c_int, C.POINTER(SolView)]),
     "pmx_qual_fold": (C.c_int, [C.POINTER(QualPart), iptr, C.c_int, C.POINTER(QualStats)]),
     "pmx_len_fold": (C.c_int, [C.POINTER(LenPart), C.c_int, C.POINTER(LenStats)]),

@@ -296,6 +296,8 @@ pmx_ctx *pmx_create(int device) {
 
 void pmx_destroy(pmx_ctx *ctx) {
   if (!ctx) return;
+  if (ctx->peer) pmx_destroy(ctx->peer);
+  ctx->peer = nullptr;
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
   if (ctx->side) hipStreamSynchronize(ctx->side);
@@ -1180,8 +1182,7 @@ void pmx_ctx::free_all() {
   dfree(d_adja); dfree(d_tcnt); dfree(d_toff); dfree(d_tbad); dfree(d_trec); dfree(d_ttmp);
   dfree(d_pent); dfree(d_pval); dfree(d_tets_next); dfree(d_tets_s_next);
   next_topo = false;
-  dfree(d_cmet); dfree(d_ctag); dfree(d_cperm); dfree(d_cdst); dfree(d_ccnt); dfree(d_cold);
-  dfree(d_cvals);
+  dfree(d_cmet); dfree(d_cperm); dfree(d_ccnt);
   if (d_tgrid) hipFree(d_tgrid);
   d_tgrid = nullptr;
   d_tgrid_cap = 0;

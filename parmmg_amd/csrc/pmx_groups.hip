@@ -42,20 +42,42 @@ static int constant_metric(pmx_ctx *ctx, const pmx_sol_view *met, int64_t first,
 
 extern "C" {
 
+// Groups alternate between the context and a second one on the same device
+// (created on first use): group g+1's host staging and upload overlap group
+// g's step on the other context's streams, and group g's download waits until
+// the context is needed again (g+2).
 int PMX_interpMetricsAndFields(pmx_ctx *ctx, int ngrp, pmx_group *grps, const int *permNodGlob,
                                int inputMet) {
   (void)permNodGlob;  // only used by the frozen-point copy, as in the reference (:477-484)
   if (!ctx || ngrp < 0 || (ngrp > 0 && !grps)) return 0;
   hipSetDevice(ctx->device);
+  if (ngrp > 1 && !ctx->peer) {
+    ctx->peer = pmx_create(ctx->device);
+    if (!ctx->peer) { ctx->err = "PMX_interpMetricsAndFields: second context"; return 0; }
+  }
   // a failing group makes the call fail but the other groups are still
   // processed (reference :715-721)
   int ier = 1;
   std::string first_err;
-  auto fail = [&]() {
+  auto fail = [&](pmx_ctx *c) {
     ier = 0;
-    if (first_err.empty()) first_err = ctx->err;
+    if (first_err.empty()) first_err = c->err;
+  };
+  struct Pending {
+    bool on = false;
+    int ns = 0;
+    pmx_sol_view news[PMX_MAX_SOLS];
+  } pend[2];
+  auto finish = [&](int c) {
+    pmx_ctx *X = c ? ctx->peer : ctx;
+    if (!pend[c].on) return;
+    pend[c].on = false;
+    if (!pmx_download(X, pend[c].news, nullptr, nullptr, nullptr)) fail(X);
   };
   for (int g = 0; g < ngrp; g++) {
+    const int c = (ngrp > 1) ? (g & 1) : 0;
+    pmx_ctx *X = c ? ctx->peer : ctx;
+    finish(c);                               // group g-2's results, same context
     pmx_group &G = grps[g];
     // reference :497-512: with -hsiz the metric is the constant one (written
     // whenever there is a metric array), otherwise it is interpolated when the
@@ -64,8 +86,8 @@ int PMX_interpMetricsAndFields(pmx_ctx *ctx, int ngrp, pmx_group *grps, const in
     const bool ismet = (inputMet == 1) && !(G.hsiz > 0.0) && G.met && G.met->m && G.old_met &&
                        G.old_met->m;
     if (G.nsols < 0 || G.nsols > PMX_MAX_SOLS || (G.nsols > 0 && (!G.fields || !G.old_fields))) {
-      ctx->err = "PMX_interpMetricsAndFields: bad field list";
-      fail();
+      X->err = "PMX_interpMetricsAndFields: bad field list";
+      fail(X);
       continue;
     }
     if (!ismet && !cst && G.nsols == 0) continue;   // nothing to do (:508-512)
@@ -76,33 +98,37 @@ int PMX_interpMetricsAndFields(pmx_ctx *ctx, int ngrp, pmx_group *grps, const in
       pv.tetra_stride = G.mesh.tetra_stride;
       pv.ne = G.mesh.ne;
     }
-    if (!pmx_upload_points(ctx, &pv)) { fail(); continue; }
-    if (cst && !constant_metric(ctx, G.met, G.points.first, G.hsiz)) { fail(); continue; }
+    if (!pmx_upload_points(X, &pv)) { fail(X); continue; }
+    if (cst && !constant_metric(X, G.met, G.points.first, G.hsiz)) { fail(X); continue; }
     if (!ismet && G.nsols == 0) continue;            // constant metric only: no locate
-    pmx_sol_view olds[PMX_MAX_SOLS], news[PMX_MAX_SOLS];
+    pmx_sol_view olds[PMX_MAX_SOLS];
+    Pending &P = pend[c];
     int ns = 0, imet = -1;
     if (ismet) {
       olds[ns] = *G.old_met;
-      news[ns] = *G.met;
+      P.news[ns] = *G.met;
       imet = ns++;
     }
     bool bad = false;
     for (int j = 0; j < G.nsols; j++) {
       if (ns >= PMX_MAX_SOLS) { bad = true; break; }
       olds[ns] = G.old_fields[j];
-      news[ns] = G.fields[j];
+      P.news[ns] = G.fields[j];
       ns++;
     }
-    if (bad) { ctx->err = "PMX_interpMetricsAndFields: too many solution fields"; fail(); continue; }
-    if (!pmx_upload_background(ctx, &G.old_mesh, ns, olds, imet)) { fail(); continue; }
+    if (bad) { X->err = "PMX_interpMetricsAndFields: too many solution fields"; fail(X); continue; }
+    if (!pmx_upload_background(X, &G.old_mesh, ns, olds, imet)) { fail(X); continue; }
     // the background upload invalidated nothing of the points; run the step
     pmx_run_opts o{};
-    if (!pmx_run(ctx, &o)) { fail(); continue; }
+    if (!pmx_run(X, &o)) { fail(X); continue; }
     // outputs in Mmg layout start at point index `first`
-    for (int s = 0; s < ns; s++)
-      if (news[s].m) news[s].m += (int64_t)news[s].size * G.points.first;
-    if (!pmx_download(ctx, news, nullptr, nullptr, nullptr)) fail();
+    for (int k = 0; k < ns; k++)
+      if (P.news[k].m) P.news[k].m += (int64_t)P.news[k].size * G.points.first;
+    P.ns = ns;
+    P.on = true;
   }
+  finish(0);
+  finish(1);
   if (!ier) ctx->err = first_err;
   return ier;
 }
@@ -110,25 +136,14 @@ int PMX_interpMetricsAndFields(pmx_ctx *ctx, int ngrp, pmx_group *grps, const in
 }  // extern "C"
 
 // copy of frozen (MG_REQ) points, optionally through the Scotch permutation
-// (PMMG_copySol_point, src/interpmesh_pmmg.c:311-358): compacted (dest, values)
-__global__ void k_copy_req(const uint16_t *tag, const int *perm, int64_t np, const double *old,
-                           int S, int *cnt, int *dst, double *vals) {
-  for (int64_t ip = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ip <= np;
-       ip += (int64_t)gridDim.x * blockDim.x) {
-    unsigned t = tag[ip];
-    if (t >= PMX_TAG_NUL) continue;          // MG_VOK
-    if (!(t & PMX_TAG_REQ)) continue;
-    int slot = atomicAdd(cnt, 1);
-    dst[slot] = perm ? perm[ip] : (int)ip;
-    for (int j = 0; j < S; j++) vals[(int64_t)slot * S + j] = old[ip * S + j];
-  }
-}
-
+// (PMMG_copySol_point, src/interpmesh_pmmg.c:311-358).  The caller's arrays
+// are host arrays, both sides: a host loop (an O(np) tag scan, REQ rows
+// copied); no device round trip.  The device-resident variant is
+// pmx_copy_required (below).
 extern "C" int PMX_copyMetricsAndFields_point(pmx_ctx *ctx, pmx_group *G, const uint16_t *old_tag,
                                               int64_t old_tag_stride, const int *permNodGlob,
                                               int renum, int inputMet) {
   if (!ctx || !G) return 0;
-  hipSetDevice(ctx->device);
   const int64_t np = G->old_mesh.np;
   std::vector<const pmx_sol_view *> olds, news;
   if (inputMet && G->hsiz <= 0.0 && G->met && G->old_met) {   // :378
@@ -141,71 +156,81 @@ extern "C" int PMX_copyMetricsAndFields_point(pmx_ctx *ctx, pmx_group *G, const 
   }
   if (olds.empty() || np < 1) return 1;
   if (!old_tag) { ctx->err = "PMX_copyMetricsAndFields_point: old point tags required"; return 0; }
-  int S = 0;
-  for (auto *s : olds) {
-    if (!s->m) { ctx->err = "PMX_copyMetricsAndFields_point: null solution"; return 0; }
-    S += s->size;
-  }
-  const bool use_perm = renum && permNodGlob;
-  // staging (pinned, reused): tags | permutation | interleaved old solutions
-  const size_t b_tag = ((size_t)(np + 1) * 2 + 255) & ~(size_t)255;
-  const size_t b_perm = use_perm ? (((size_t)(np + 1) * 4 + 255) & ~(size_t)255) : 0;
-  const size_t b_sol = (size_t)(np + 1) * S * sizeof(double);
-  char *st = pmx_hstage(ctx, b_tag + b_perm + b_sol);
-  if (!st) return 0;
-  uint16_t *ht = (uint16_t *)st;
-  int *hp = (int *)(st + b_tag);
-  double *hs = (double *)(st + b_tag + b_perm);
-  ht[0] = 0;
-  for (int64_t ip = 1; ip <= np; ip++)
-    ht[ip] = *(const uint16_t *)((const char *)old_tag + ip * old_tag_stride);
-  if (use_perm) memcpy(hp, permNodGlob, (size_t)(np + 1) * 4);
-  {
-    int off = 0;
-    for (auto *s : olds) {
-      for (int64_t ip = 1; ip <= np; ip++)
-        for (int j = 0; j < s->size; j++) hs[(size_t)ip * S + off + j] = s->m[ip * s->size + j];
-      off += s->size;
+  for (size_t k = 0; k < olds.size(); k++)
+    if (!olds[k]->m || olds[k]->size != news[k]->size) {
+      ctx->err = "PMX_copyMetricsAndFields_point: null or mismatched solution";
+      return 0;
+    }
+  const bool use_perm = renum && permNodGlob;   // :328 (!oldMesh->info.renum || !permNodGlob)
+  for (int64_t ip = 1; ip <= np; ip++) {
+    const unsigned t = *(const uint16_t *)((const char *)old_tag + ip * old_tag_stride);
+    if (t >= PMX_TAG_NUL || !(t & PMX_TAG_REQ)) continue;   // !MG_VOK / not frozen
+    const int64_t dst = use_perm ? permNodGlob[ip] : ip;
+    for (size_t k = 0; k < olds.size(); k++) {
+      if (!news[k]->m) continue;
+      const int sz = olds[k]->size;
+      memcpy(news[k]->m + dst * sz, olds[k]->m + ip * sz, sizeof(double) * (size_t)sz);
     }
   }
-  hipStream_t s = ctx->stream;
-  if (!pmx_dgrow(ctx, ctx->d_ctag, (size_t)(np + 1)) || !pmx_dgrow(ctx, ctx->d_cold, (size_t)(np + 1) * S) ||
-      !pmx_dgrow(ctx, ctx->d_ccnt, 1) || !pmx_dgrow(ctx, ctx->d_cdst, (size_t)(np + 1)) ||
-      !pmx_dgrow(ctx, ctx->d_cvals, (size_t)(np + 1) * S) ||
-      (use_perm && !pmx_dgrow(ctx, ctx->d_cperm, (size_t)(np + 1))))
+  return 1;
+}
+
+// the same copy on device-resident data, after a step: rows of the new
+// points the step did not write take the background's values of the old
+// frozen points mapped to them -- equivalent to the reference's copy before
+// the interpolation, which then overwrites the rows it writes
+__global__ __launch_bounds__(256) void k_copy_required(const uint16_t *__restrict__ ptag, const int *__restrict__ perm,
+                                                       int64_t np, int64_t first, int64_t n, const double *__restrict__ sol,
+                                                       int S, SolDesc sd, unsigned smask, double *__restrict__ out,
+                                                       uint8_t *__restrict__ wmask, unsigned *__restrict__ nbad) {
+  for (int64_t ip = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ip <= np;
+       ip += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned t = ptag[ip];
+    if (t >= PMX_TAG_NUL || !(t & PMX_TAG_REQ)) continue;
+    const int64_t j = (perm ? (int64_t)perm[ip] : ip) - first;
+    if (j < 0 || j >= n) { atomicAdd(nbad, 1u); continue; }
+    unsigned w = wmask[j];
+    for (int s = 0; s < sd.nsol; s++) {
+      const unsigned bit = 1u << s;
+      if (!(smask & bit) || (w & bit)) continue;
+      for (int c = 0; c < sd.size[s]; c++) out[j * S + sd.off[s] + c] = sol[ip * S + sd.off[s] + c];
+      w |= bit;
+    }
+    wmask[j] = (uint8_t)w;
+  }
+}
+
+extern "C" int pmx_copy_required(pmx_ctx *ctx, const int *permNodGlob, int copy_metric) {
+  if (!ctx) return 0;
+  hipSetDevice(ctx->device);
+  if (!ctx->ran || !ctx->have_pts || ctx->out_n != ctx->nq || ctx->out_S != ctx->sd.S) {
+    ctx->err = "pmx_copy_required: no step has run on the current uploads";
     return 0;
-  bool okk = hipMemcpyAsync(ctx->d_ctag.p, ht, (size_t)(np + 1) * 2, hipMemcpyHostToDevice, s) == hipSuccess &&
-             hipMemcpyAsync(ctx->d_cold.p, hs, b_sol, hipMemcpyHostToDevice, s) == hipSuccess &&
-             (!use_perm || hipMemcpyAsync(ctx->d_cperm.p, hp, (size_t)(np + 1) * 4, hipMemcpyHostToDevice, s) == hipSuccess) &&
-             hipMemsetAsync(ctx->d_ccnt.p, 0, 4, s) == hipSuccess;
-  int n = 0;
-  if (okk) {
-    const int64_t nb = std::min<int64_t>((np + 255) / 256, 4096);
-    hipLaunchKernelGGL(k_copy_req, dim3((unsigned)nb), dim3(256), 0, s, ctx->d_ctag.p,
-                       use_perm ? ctx->d_cperm.p : nullptr, np, ctx->d_cold.p, S, ctx->d_ccnt.p,
-                       ctx->d_cdst.p, ctx->d_cvals.p);
-    okk = hipMemcpyAsync(&n, ctx->d_ccnt.p, 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
-          hipStreamSynchronize(s) == hipSuccess;
   }
-  if (okk && n > 0) {
-    // the arena is free again (the uploads completed): the compacted entries
-    int *hd = (int *)st;
-    double *hv = (double *)(st + (((size_t)n * 4 + 255) & ~(size_t)255));
-    okk = hipMemcpyAsync(hd, ctx->d_cdst.p, (size_t)n * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
-          hipMemcpyAsync(hv, ctx->d_cvals.p, (size_t)n * S * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
-          hipStreamSynchronize(s) == hipSuccess;
-    if (okk) {
-      for (int q = 0; q < n; q++) {
-        int off = 0;
-        for (size_t k = 0; k < news.size(); k++) {
-          const int sz = olds[k]->size;
-          if (news[k]->m)
-            for (int j = 0; j < sz; j++) news[k]->m[(int64_t)hd[q] * sz + j] = hv[(size_t)q * S + off + j];
-          off += sz;
-        }
-      }
+  if (!ctx->have_ptag) { ctx->err = "pmx_copy_required: the background's point tags are not on the device"; return 0; }
+  const int64_t np = ctx->np;
+  hipStream_t s = ctx->stream;
+  if (permNodGlob) {
+    if (!pmx_dgrow(ctx, ctx->d_cperm, (size_t)(np + 1))) return 0;
+    if (hipMemcpyAsync(ctx->d_cperm.p, permNodGlob, (size_t)(np + 1) * sizeof(int), hipMemcpyHostToDevice, s) !=
+        hipSuccess) {
+      ctx->err = "pmx_copy_required: permutation upload";
+      return 0;
     }
   }
-  if (!okk) ctx->err = "PMX_copyMetricsAndFields_point: device copy failed";
-  return okk ? 1 : 0;
+  if (!pmx_dgrow(ctx, ctx->d_ccnt, 1) || hipMemsetAsync(ctx->d_ccnt.p, 0, sizeof(int), s) != hipSuccess) return 0;
+  unsigned smask = (1u << ctx->sd.nsol) - 1u;
+  if (!copy_metric && ctx->sd.imet >= 0) smask &= ~(1u << ctx->sd.imet);
+  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((np + 255) / 256, 4096));
+  hipLaunchKernelGGL(k_copy_required, dim3((unsigned)nb), dim3(256), 0, s, ctx->d_ptag.p,
+                     permNodGlob ? ctx->d_cperm.p : nullptr, np, ctx->pts_first, ctx->nq, ctx->d_sol.p,
+                     ctx->sd.S, ctx->sd, smask, ctx->d_out.p, ctx->d_wmask.p, (unsigned *)ctx->d_ccnt.p);
+  unsigned bad = 0;
+  if (hipMemcpyAsync(&bad, ctx->d_ccnt.p, sizeof bad, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    ctx->err = "pmx_copy_required: launch";
+    return 0;
+  }
+  if (bad) { ctx->err = "pmx_copy_required: a frozen point maps outside the new points"; return 0; }
+  return 1;
 }

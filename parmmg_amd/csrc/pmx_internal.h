@@ -26,6 +26,9 @@ struct pmx_ctx {
   hipEvent_t ev_dl[8] = {};             // chunked download: one per chunk
   std::string err;
   int fallback_blocks = 0;              // co-resident k_fallback workgroups
+  // PMX_interpMetricsAndFields: a second context on the same device, groups
+  // alternate between the two (created on first use, destroyed with this one)
+  pmx_ctx *peer = nullptr;
   // pinned host staging arena (hipHostMalloc, grown on demand, reused across
   // steps): uploads and downloads go through it as async DMA
   void *h_stage = nullptr;
@@ -86,9 +89,7 @@ struct pmx_ctx {
   // group seams (pmx_groups.hip): constant-size metric of a step without a
   // background, and the frozen-point copy (buffers reused across calls)
   DevBuf<double> d_cmet;
-  DevBuf<uint16_t> d_ctag;
-  DevBuf<int> d_cperm, d_cdst, d_ccnt;
-  DevBuf<double> d_cold, d_cvals;
+  DevBuf<int> d_cperm, d_ccnt;         // pmx_copy_required
 
   // statistics
   DevBuf<double> d_qual;

@@ -123,6 +123,13 @@ class Transfer:
                                                  imet if arr else -1), "pmx_upload_background")
         self.sizes = [v.size for v in views[: len(arr)]]
 
+    def copy_required(self, perm: np.ndarray | None = None, copy_metric: bool = True):
+        """pmx_copy_required: frozen (MG_REQ) background points' values into the
+        unwritten rows of the last step's results; perm: (np+1,) permNodGlob
+        (1-based new point of background vertex ip)."""
+        pp = None if perm is None else np.ascontiguousarray(perm, np.int32)
+        self._chk(self.lib.pmx_copy_required(self.ctx, _ip(pp), int(copy_metric)), "pmx_copy_required")
+
     def set_residency(self, on: bool = True):
         self._chk(self.lib.pmx_set_residency(self.ctx, int(on)), "pmx_set_residency")
 

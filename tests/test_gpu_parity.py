@@ -167,9 +167,11 @@ def test_constant_size_and_required_points(transfer):
 
 
 def test_dropin_interp_metrics_and_fields(transfer):
-    """PMX_interpMetricsAndFields on two groups in Mmg layout (1-based arrays)."""
+    """PMX_interpMetricsAndFields on three groups in Mmg layout (1-based
+    arrays): the groups alternate between two contexts (group 2 waits for
+    group 0's download on the first)."""
     groups, refs = [], []
-    for n, seed in ((6, 1), (7, 2)):
+    for n, seed in ((6, 1), (7, 2), (5, 3)):
         m, x, t, sols = cube_case(n, metric="iso", seed_pts=seed)
         xyz1 = np.concatenate([np.zeros((1, 3)), x])
         tag1 = np.concatenate([np.zeros(1, np.uint16), t])

@@ -140,3 +140,48 @@ def test_promote_requires_step_and_tets():
     with pytest.raises(RuntimeError, match="upload background and points"):
         tr.run()                                  # the points were consumed
     tr.close()
+
+
+@pytest.mark.parametrize("use_perm,copy_metric", [(False, True), (True, True), (True, False)])
+def test_copy_required_on_device(use_perm, copy_metric):
+    """pmx_copy_required: the frozen (MG_REQ) background points' values land
+    in the rows of their new points that the step did not write -- the
+    reference's PMMG_copySol_point (src/interpmesh_pmmg.c:311-358) before the
+    interpolation, which then overwrites the rows it writes."""
+    m1 = M.kuhn_cube(5, seed=31)
+    sols1 = fields(m1)
+    m2, x2, t2, tets2 = new_mesh(6, 32)
+    np1, np2 = m1.np, len(x2)
+    perm = np.zeros(np1 + 1, np.int32)
+    perm[1:] = (np2 - np.arange(1, np1 + 1) + 1) if use_perm else np.arange(1, np1 + 1)
+    tags1 = np.zeros(np1 + 1, np.uint16)
+    req = np.array([3, 10, 27, 50, 51, 120, 200])
+    tags1[req] = M.TAG_REQ
+    t2 = t2.copy()
+    frozen = req[req != 50]                       # old point 50's new point is not frozen
+    t2[perm[frozen] - 1] |= M.TAG_REQ
+    init = [np.full((np2, s.shape[1]), -9.0) for s in sols1]
+
+    def step(copy):
+        tr = Transfer(0)
+        tr.upload_background(m1, sols1, 0)
+        tr.upload_point_tags(tags1)
+        tr.upload_points(x2, t2, tets2)
+        tr.run()
+        if copy:
+            tr.copy_required(perm if use_perm else None, copy_metric)
+        r = tr.download(init=init)
+        tr.close()
+        return r
+
+    r0, r1 = step(False), step(True)
+    expect = [a.copy() for a in r0.sols]
+    for s in range(len(sols1)):
+        if s == 0 and not copy_metric:
+            continue
+        for ip in frozen:
+            expect[s][perm[ip] - 1] = sols1[s][ip]
+    for s in range(len(sols1)):
+        assert bits_equal(r1.sols[s], expect[s]).all(), f"sol {s}"
+    j50 = perm[50] - 1
+    assert np.all(r1.sols[1][j50] == r0.sols[1][j50]) and r0.sols[1][j50][0] != -9.0

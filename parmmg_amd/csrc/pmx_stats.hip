@@ -896,7 +896,12 @@ int pmx_qualhisto(pmx_ctx *ctx, int opt, pmx_qual_stats *st) {
 }
 
 int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, void *dev_result) {
-  (void)metRidTyp;   // classic metric storage (size 1 or 6 on every point), see the header
+  // classic metric storage only (size 1 or 6 on every point); Mmg's ridge
+  // metric storage (metRidTyp = 1) is refused, not approximated
+  if (metRidTyp != 0) {
+    if (ctx) ctx->err = "pmx_prilen: metRidTyp = 1 (ridge metric storage) is not supported";
+    return 0;
+  }
   if (!ctx || !dev_result) return 0;
   hipSetDevice(ctx->device);
   StatArgs A;

@@ -229,6 +229,34 @@ int PMX_copyMetricsAndFields_point(pmx_ctx *ctx, pmx_group *grp,
  * pmx_promote_background). */
 int pmx_copy_required(pmx_ctx *ctx, const int *permNodGlob, int copy_metric);
 
+/* ---- Medit files ---------------------------------
+ * The wire format of the path's inputs and outputs: ParMmg reads/writes them
+ * through Mmg (src/inout_pmmg.c:440-991 -> MMG3D_loadMesh / saveMesh /
+ * loadSol / saveSol).  ASCII .mesh/.sol and binary .meshb/.solb (chosen by
+ * the extension; binary versions 1-4 read, 2-4 written).  Arrays in Mmg's
+ * layout (1-based, slot 0 untouched; tensors (11,12,13,22,23,33), converted
+ * from/to Medit's (11,12,22,13,23,33)).  Keywords other than Vertices,
+ * Tetrahedra, Triangles, RequiredVertices (mesh) and SolAtVertices (solution)
+ * are skipped.  No context: errors in pmx_medit_last_error() (per thread). */
+typedef struct {
+  int64_t np, ne, nt, nreq;    /* vertices, tetrahedra, triangles, required vertices */
+  int     dim, version;
+} pmx_medit_info;
+const char *pmx_medit_last_error(void);
+int pmx_medit_mesh_info(const char *path, pmx_medit_info *info);
+/* xyz[3*(np+1)], tet[4*(ne+1)] required; vref[np+1], tetref[ne+1],
+ * tria[3*(nt+1)], triaref[nt+1], req[nreq] may be NULL */
+int pmx_medit_mesh_read(const char *path, double *xyz, int *vref, int *tet, int *tetref, int *tria,
+                        int *triaref, int *req);
+int pmx_medit_mesh_write(const char *path, int64_t np, const double *xyz, const int *vref, int64_t ne,
+                         const int *tet, const int *tetref, int64_t nt, const int *tria, const int *triaref,
+                         int64_t nreq, const int *req);
+/* solutions at vertices: types 1 scalar, 2 vector (3), 3 symmetric tensor (6) */
+int pmx_medit_sol_info(const char *path, int64_t *np, int *nsol, int *types);
+int pmx_medit_sol_read(const char *path, double **fields);   /* fields[s]: size*(np+1) */
+int pmx_medit_sol_write(const char *path, int64_t np, int nsol, const int *types,
+                        const double *const *fields);
+
 /* ---- statistics ---------------------------------------------------------- */
 /* Reference: PMMG_tetraQual / PMMG_qualhisto / PMMG_prilen (src/parmmg.h:564-566,
  * def src/quality_pmmg.c:156-733).  The per-element arithmetic is Mmg's,

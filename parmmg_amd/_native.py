@@ -117,6 +117,11 @@ class ParEdges(C.Structure):
 INQUA, OUTQUA = 0, 1
 
 
+class MeditInfo(C.Structure):
+    _fields_ = [("np", i64), ("ne", i64), ("nt", i64), ("nreq", i64), ("dim", C.c_int),
+                ("version", C.c_int)]
+
+
 # symbol -> (restype, argtypes); every function declared in include/pmx_transfer.h
 SIGNATURES = {
     "pmx_create": (C.c_void_p, [C.c_int]),
@@ -163,6 +168,14 @@ SIGNATURES = {
     "pmx_qualhisto_allreduce": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
                                           C.POINTER(QualStats)]),
     "pmx_prilen_allreduce": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.POINTER(LenStats)]),
+    "pmx_medit_last_error": (C.c_char_p, []),
+    "pmx_medit_mesh_info": (C.c_int, [C.c_char_p, C.POINTER(MeditInfo)]),
+    "pmx_medit_mesh_read": (C.c_int, [C.c_char_p, dptr, iptr, iptr, iptr, iptr, iptr, iptr]),
+    "pmx_medit_mesh_write": (C.c_int, [C.c_char_p, i64, dptr, iptr, i64, iptr, iptr, i64, iptr, iptr,
+                                       i64, iptr]),
+    "pmx_medit_sol_info": (C.c_int, [C.c_char_p, C.POINTER(i64), C.POINTER(C.c_int), iptr]),
+    "pmx_medit_sol_read": (C.c_int, [C.c_char_p, C.POINTER(dptr)]),
+    "pmx_medit_sol_write": (C.c_int, [C.c_char_p, i64, C.c_int, iptr, C.POINTER(dptr)]),
 }
 
 _lib = None

@@ -26,7 +26,7 @@ MESHGEN_SO = os.path.join(PKG, "libpmx_meshgen.so")
 ORACLE_SO = os.path.join(ORACLE, "liboracle.so")
 
 HIP_SOURCES = ["pmx_capi.hip", "pmx_kernels.hip", "pmx_walk.hip", "pmx_bdy.hip", "pmx_stats.hip",
-               "pmx_groups.hip", "pmx_topo.hip"]
+               "pmx_groups.hip", "pmx_topo.hip", "pmx_medit.hip"]
 HIPCC_FLAGS = [
     "-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-shared",
     "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",

@@ -4,6 +4,8 @@
   (parmmg_amd/csrc/meshgen.c), driven end to end by tests/c/oracle_asan.c and
   run here (CPU): leaks, out-of-bounds accesses and undefined behaviour fail
   the test;
+* the library's Medit I/O (parmmg_amd/csrc/pmx_medit.hip, host code) compiled
+  with g++ and driven by tests/c/medit_asan.cpp (CPU);
 * the C driver of the drop-in seam (tests/c/dropin_demo.c) built with the same
   flags (its host code instrumented, the HIP library as is); it runs on the
   GPU box (-m gpu), with leak checking off for the HIP runtime's allocations.
@@ -40,6 +42,21 @@ def test_oracle_and_meshgen_under_asan_ubsan():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "oracle asan ok" in r.stdout
+
+
+def test_medit_io_under_asan_ubsan(tmp_path):
+    os.makedirs(BUILD, exist_ok=True)
+    exe = os.path.join(BUILD, "medit_asan")
+    cmd = ["g++", "-std=c++17", "-Wall", "-x", "c++", *SAN, "-I", os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "parmmg_amd", "csrc", "pmx_medit.hip"),
+           os.path.join(ROOT, "tests", "c", "medit_asan.cpp"), "-o", exe]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "medit asan ok" in r.stdout
 
 
 def _demo_asan():

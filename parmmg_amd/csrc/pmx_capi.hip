@@ -385,15 +385,12 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   if (!m) { ctx->err = "pmx_upload_background: null mesh"; return 0; }
   hipSetDevice(ctx->device);
   if (!check_background(ctx, m, nsol, sols, imet)) return 0;
-  // no adjacency given (MMG3D_hashTetra not run on the host): face matching on
-  // the device (pmx_topo.hip)
-  std::vector<int> built_adja;
-  const int *adja_in = m->adja;
-  if (!adja_in) {
-    if (!pmx_ctx_build_adja_host(ctx, m, built_adja)) return 0;
-    adja_in = built_adja.data();
-  }
   const int64_t np = m->np, ne = m->ne, nt = m->nt;
+  const bool dev_adja = m->adja == nullptr;   // no MMG3D_hashTetra on the host: device face matching
+  // a residency build of the next background's records shares the adjacency
+  // scratch: let it finish (its result, in the *_next buffers, is kept)
+  if (ctx->next_topo) CK(hipStreamSynchronize(ctx->topo));
+  Trace tr("background");
   SolDesc sd{};
   sd.nsol = nsol;
   sd.imet = imet;
@@ -406,15 +403,24 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   sd.S = S;
   const int64_t ns = (ne + PMX_HINT_STRIDE - 1) / PMX_HINT_STRIDE;
   const size_t hs_n = (size_t)(np + 1) * std::max(S, 1);
-  // pinned staging: xyz | tets | packed hint sample | solutions (async DMA,
-  // one sync at the end)
+  // pinned staging: xyz | tets (TetRec, or int4 when the device builds the
+  // adjacency) | packed hint sample | solutions; each part goes down as soon
+  // as it is packed (the tets in chunks), one sync at the end
+  const size_t trec = dev_adja ? sizeof(int4) : sizeof(TetRec);
   const size_t o_p = 0, o_t = o_p + al256((size_t)(np + 1) * 24),
-               o_h = o_t + al256((size_t)(ne + 1) * sizeof(TetRec)),
+               o_h = o_t + al256((size_t)(ne + 1) * trec),
                o_s = o_h + al256((size_t)ns * sizeof(int4)),
                total = o_s + al256(hs_n * sizeof(double));
   CK(hipStreamSynchronize(ctx->stream));   // the arena may still feed an earlier copy
   char *stg = hstage(ctx, total);
   if (!stg) return 0;
+  if (!dgrow(ctx, ctx->d_xyz, (size_t)(np + 1) * 3) || !dgrow(ctx, ctx->d_tets, (size_t)(ne + 1)) ||
+      !dgrow(ctx, ctx->d_tets_s, (size_t)std::max<int64_t>(ns, 1)) || !dgrow(ctx, ctx->d_sol, hs_n) ||
+      !dgrow(ctx, ctx->d_tris, (size_t)(nt + 1)) || !dgrow(ctx, ctx->d_trn, (size_t)(nt + 1)) ||
+      !dgrow(ctx, ctx->d_xyzq, (size_t)(np + 1)) ||
+      (dev_adja && (!dgrow(ctx, ctx->d_btv, (size_t)(ne + 1)) || !dgrow(ctx, ctx->d_adja, (size_t)(4 * ne + 5)))))
+    return 0;
+  hipStream_t st = ctx->stream;
 
   // points -> dense xyz (24 B), bounding box per chunk
   double *hp = (double *)(stg + o_p);
@@ -436,71 +442,95 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
   for (int c = 0; c < nch; c++)
     for (int a = 0; a < 3; a++) { lo[a] = std::min(lo[a], blo[c][a]); hi[a] = std::max(hi[a], bhi[c][a]); }
-  // tets -> TetRec with neighbour tet index, + the packed hint sample (the
-  // connectivity of every PMX_HINT_STRIDE-th tet, contiguous: the hint build
-  // streams ne/4 * 16 B instead of touching every line of the tet records)
+  CK(hipMemcpyAsync(ctx->d_xyz.p, hp, (size_t)(np + 1) * 24, hipMemcpyHostToDevice, st));
+  tr.mark("points");
+  // tets -> TetRec with neighbour tet index (or the bare connectivity), + the
+  // packed hint sample (the connectivity of every PMX_HINT_STRIDE-th tet,
+  // contiguous: the hint build streams ne/4 * 16 B instead of touching every
+  // line of the tet records); in chunks, each DMA'd while the next is packed
   TetRec *ht = (TetRec *)(stg + o_t);
+  int4 *htv = (int4 *)(stg + o_t);
   int4 *hh = (int4 *)(stg + o_h);
-  memset(&ht[0], 0, sizeof(TetRec));
+  if (dev_adja) htv[0] = make_int4(0, 0, 0, 0);
+  else memset(&ht[0], 0, sizeof(TetRec));
   const char *tc = (const char *)m->tetra_v;
+  const int *adja_in = m->adja;
   bool bad = false;
-  par_for(1, ne + 1, [&](int64_t k0, int64_t k1) {
-    bool b = false;
-    for (int64_t k = k0; k < k1; k++) {
-      const int *v = (const int *)(tc + k * m->tetra_stride);
-      TetRec &r = ht[(size_t)k];
-      // indices the kernels will gather through: a valid tet (v[0] > 0,
-      // MG_EOK) must name vertices 1..np and neighbours 0..ne
-      const bool valid = v[0] > 0;
-      for (int l = 0; l < 4; l++) {
-        r.v[l] = v[l];
-        const int a = adja_in[4 * (k - 1) + 1 + l];
-        r.nb[l] = a / 4;
-        if (valid && (v[l] < 1 || v[l] > np || a < 0 || a / 4 > ne)) b = true;
+  const int64_t ntc = std::max<int64_t>(1, std::min<int64_t>(8, ne >> 20));
+  for (int64_t c = 0; c < ntc; c++) {
+    const int64_t klo = (c == 0) ? 0 : 1 + ne * c / ntc, khi = 1 + ne * (c + 1) / ntc;
+    par_for(std::max<int64_t>(klo, 1), khi, [&](int64_t k0, int64_t k1) {
+      bool b = false;
+      for (int64_t k = k0; k < k1; k++) {
+        const int *v = (const int *)(tc + k * m->tetra_stride);
+        // indices the kernels will gather through: a valid tet (v[0] > 0,
+        // MG_EOK) must name vertices 1..np and neighbours 0..ne
+        const bool valid = v[0] > 0;
+        if (dev_adja) {
+          if (!valid) { htv[k] = make_int4(0, 0, 0, 0); }
+          else {
+            for (int l = 0; l < 4; l++)
+              if (v[l] < 1 || v[l] > np) b = true;
+            htv[k] = make_int4(v[0], v[1], v[2], v[3]);
+          }
+        } else {
+          TetRec &r = ht[(size_t)k];
+          for (int l = 0; l < 4; l++) {
+            r.v[l] = v[l];
+            const int a = adja_in[4 * (k - 1) + 1 + l];
+            r.nb[l] = a / 4;
+            if (valid && (v[l] < 1 || v[l] > np || a < 0 || a / 4 > ne)) b = true;
+          }
+        }
+        if ((k - 1) % PMX_HINT_STRIDE == 0) hh[(k - 1) / PMX_HINT_STRIDE] = make_int4(v[0], v[1], v[2], v[3]);
       }
-      if ((k - 1) % PMX_HINT_STRIDE == 0) hh[(k - 1) / PMX_HINT_STRIDE] = make_int4(v[0], v[1], v[2], v[3]);
-    }
-    if (b) __atomic_store_n(&bad, true, __ATOMIC_RELAXED);
-  });
+      if (b) __atomic_store_n(&bad, true, __ATOMIC_RELAXED);
+    });
+    if (bad) break;
+    if (dev_adja)
+      CK(hipMemcpyAsync(ctx->d_btv.p + klo, htv + klo, (size_t)(khi - klo) * sizeof(int4), hipMemcpyHostToDevice, st));
+    else
+      CK(hipMemcpyAsync(ctx->d_tets.p + klo, ht + klo, (size_t)(khi - klo) * sizeof(TetRec), hipMemcpyHostToDevice,
+                        st));
+  }
   if (bad) {
     ctx->err = "pmx_upload_background: tet vertex or adjacency index out of range";
     return 0;
   }
+  if (!dev_adja) CK(hipMemcpyAsync(ctx->d_tets_s.p, hh, (size_t)ns * sizeof(int4), hipMemcpyHostToDevice, st));
+  tr.mark("tets");
   // solutions -> interleaved [np+1][S]
   double *hs = (double *)(stg + o_s);
   memset(hs, 0, (size_t)std::max(S, 1) * sizeof(double));   // row 0 (unused slot)
   if (S == 0) memset(hs, 0, hs_n * sizeof(double));
-  for (int s = 0; s < nsol; s++) {
-    const int sz = sols[s].size;
-    const double *src = sols[s].m;
-    const int off = sd.off[s];
-    par_for(1, np + 1, [&](int64_t i0, int64_t i1) {
+  par_chunks(1, np + 1, [&](int, int64_t i0, int64_t i1) {
+    for (int s = 0; s < nsol; s++) {
+      const int sz = sols[s].size, off = sd.off[s];
+      const double *src = sols[s].m;
       for (int64_t i = i0; i < i1; i++)
         for (int j = 0; j < sz; j++) hs[(size_t)i * S + off + j] = src[i * sz + j];
-    });
-  }
+    }
+  });
+  CK(hipMemcpyAsync(ctx->d_sol.p, hs, hs_n * sizeof(double), hipMemcpyHostToDevice, st));
+  tr.mark("solutions");
   // boundary triangles
   std::vector<TriRec> htr;
   if (!stage_trias(ctx, m, np, htr)) return 0;
   ctx->np = np; ctx->ne = ne; ctx->nt = nt; ctx->hausd = m->hausd;
   ctx->sd = sd;
-
   if (!setup_grids(ctx, lo, hi, ne)) return 0;
-
-  if (!dgrow(ctx, ctx->d_xyz, (size_t)(np + 1) * 3)) return 0;
-  if (!dgrow(ctx, ctx->d_tets, (size_t)(ne + 1))) return 0;
-  if (!dgrow(ctx, ctx->d_tets_s, (size_t)std::max<int64_t>(ns, 1))) return 0;
-  if (!dgrow(ctx, ctx->d_sol, hs_n)) return 0;
-  if (!dgrow(ctx, ctx->d_tris, (size_t)(nt + 1))) return 0;
-  if (!dgrow(ctx, ctx->d_trn, (size_t)(nt + 1))) return 0;
-  if (!dgrow(ctx, ctx->d_xyzq, (size_t)(np + 1))) return 0;
-  CK(hipMemcpyAsync(ctx->d_xyz.p, hp, (size_t)(np + 1) * 24, hipMemcpyHostToDevice, ctx->stream));
-  CK(hipMemcpyAsync(ctx->d_tets.p, ht, (size_t)(ne + 1) * sizeof(TetRec), hipMemcpyHostToDevice, ctx->stream));
-  CK(hipMemcpyAsync(ctx->d_tets_s.p, hh, (size_t)ns * sizeof(int4), hipMemcpyHostToDevice, ctx->stream));
-  CK(hipMemcpyAsync(ctx->d_sol.p, hs, hs_n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-  CK(hipMemcpyAsync(ctx->d_tris.p, htr.data(), htr.size() * sizeof(TriRec), hipMemcpyHostToDevice, ctx->stream));
-  if (!ctx->build_node_trias(ctx->stream)) return 0;
+  CK(hipMemcpyAsync(ctx->d_tris.p, htr.data(), htr.size() * sizeof(TriRec), hipMemcpyHostToDevice, st));
+  if (!ctx->build_node_trias(st)) return 0;
+  if (dev_adja) {
+    // face matching on the device (pmx_topo.hip), then the tet records and
+    // the hint sample from the device connectivity
+    if (!pmx_ctx_build_adja_device(ctx, ctx->d_btv.p, ne, np, ctx->d_adja.p, st, nullptr)) return 0;
+    launch_build_tetrec(ctx->d_btv.p, ctx->d_adja.p, ne, PMX_HINT_STRIDE, ctx->d_tets.p, ctx->d_tets_s.p, st);
+  }
+  CK(hipGetLastError());
+  tr.mark("trias + topology");
   CK(hipStreamSynchronize(ctx->stream));   // host staging vectors die here
+  tr.mark("sync");
   ctx->have_bg = true;
   return 1;
 }

@@ -110,6 +110,7 @@ struct pmx_ctx {
   double qlo[3]{}, qhi[3]{};            // bbox of the uploaded new points
   // device adjacency of promoted backgrounds (pmx_topo.hip), reused buffers
   DevBuf<int> d_adja;
+  DevBuf<int4> d_btv;                   // background connectivity when its adjacency is built here
   DevBuf<unsigned> d_tcnt, d_toff, d_tbad;
   DevBuf<int4> d_trec;
   DevBuf<char> d_ttmp;
@@ -162,7 +163,6 @@ template <class T> inline bool pmx_dgrow(pmx_ctx *ctx, DevBuf<T> &b, size_t n) {
 // the context's pinned staging arena, at least `bytes` (pmx_capi.hip)
 char *pmx_hstage(pmx_ctx *ctx, size_t bytes);
 
-bool pmx_ctx_build_adja_host(pmx_ctx *ctx, const pmx_mesh_view *m, std::vector<int> &adja);
 // face adjacency of device connectivity (1-based int4, slot 0 unused) into
 // dadja (Mmg layout, 4 ne + 5 ints), context-owned scratch; false on a
 // non-manifold face or a failure (ctx->err)

@@ -301,20 +301,6 @@ bool build_adja_dev(pmx_ctx *ctx, const int4 *tv, int64_t ne, int64_t np, int *d
 
 }  // namespace
 
-// internal: adjacency of the tets of an upload without one (pmx_upload_background)
-bool pmx_ctx_build_adja_host(pmx_ctx *ctx, const pmx_mesh_view *m, std::vector<int> &adja) {
-  Scratch sc;
-  int4 *tv = upload_tets(ctx, m->ne, m->np, m->tetra_v, m->tetra_stride, sc);
-  if (!tv) return topo_fail(ctx, "pmx_upload_background: adjacency upload");
-  int *dadja = sc.get<int>((size_t)(4 * m->ne + 5));
-  unsigned nbad = 0;
-  if (!dadja || !build_adja_dev(ctx, tv, m->ne, m->np, dadja, sc, &nbad)) return false;
-  adja.resize((size_t)(4 * m->ne + 5));
-  if (hipMemcpy(adja.data(), dadja, adja.size() * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
-    return topo_fail(ctx, "pmx_upload_background: adjacency download");
-  if (nbad) return topo_fail(ctx, "pmx_upload_background: non-manifold tet faces");
-  return true;
-}
 
 
 // face adjacency of a device connectivity stream with the context's buffers

@@ -26,6 +26,7 @@
  */
 #ifndef PMX_TRANSFER_H
 #define PMX_TRANSFER_H
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -157,6 +158,10 @@ int pmx_locate_stats_get(pmx_ctx *ctx, pmx_locate_stats *st);
 /* Device pointers of the resident result buffers (for collectives / chaining):
  * which = 0 packed solutions [npts][S], 1 elem, 2 status. */
 void *pmx_device_buffer(pmx_ctx *ctx, int which);
+/* Device memory on the context's GPU for a C caller (zeroed): e.g. the
+ * per-group partial records of the _device statistics functions. */
+void *pmx_device_alloc(pmx_ctx *ctx, size_t bytes);
+int pmx_device_free(pmx_ctx *ctx, void *p);
 /* Inspection: copy the volume hint grid of the last run to host (cap cells);
  * returns the number of cells (0 on error). */
 int64_t pmx_debug_hint_grid(pmx_ctx *ctx, int *host, int64_t cap);

@@ -138,6 +138,8 @@ SIGNATURES = {
     "pmx_download_border": (C.c_int, [C.c_void_p, iptr, iptr]),
     "pmx_locate_stats_get": (C.c_int, [C.c_void_p, C.POINTER(LocateStats)]),
     "pmx_device_buffer": (C.c_void_p, [C.c_void_p, C.c_int]),
+    "pmx_device_alloc": (C.c_void_p, [C.c_void_p, C.c_size_t]),
+    "pmx_device_free": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pmx_debug_hint_grid": (C.c_int64, [C.c_void_p, C.c_void_p, C.c_int64]),
     "pmx_build_adja": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64,
                                  C.c_void_p]),

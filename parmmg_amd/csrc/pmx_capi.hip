@@ -952,6 +952,30 @@ void *pmx_device_buffer(pmx_ctx *ctx, int which) {
   }
 }
 
+void *pmx_device_alloc(pmx_ctx *ctx, size_t bytes) {
+  if (!ctx) return nullptr;
+  hipSetDevice(ctx->device);
+  void *p = nullptr;
+  const hipError_t e = hipMalloc(&p, std::max<size_t>(bytes, 1));
+  if (e != hipSuccess) {
+    ctx->err = std::string("pmx_device_alloc: ") + hipGetErrorString(e);
+    return nullptr;
+  }
+  if (hipMemset(p, 0, std::max<size_t>(bytes, 1)) != hipSuccess) {
+    hipFree(p);
+    ctx->err = "pmx_device_alloc: memset";
+    return nullptr;
+  }
+  return p;
+}
+
+int pmx_device_free(pmx_ctx *ctx, void *p) {
+  if (!ctx) return 0;
+  hipSetDevice(ctx->device);
+  hipStreamSynchronize(ctx->stream);
+  return (p == nullptr || hipFree(p) == hipSuccess) ? 1 : 0;
+}
+
 int64_t pmx_debug_hint_grid(pmx_ctx *ctx, int *host, int64_t cap) {
   if (!ctx || !ctx->ran || !host) return 0;
   if (hipStreamSynchronize(ctx->stream) != hipSuccess) return 0;

@@ -304,8 +304,8 @@ typedef struct {
  * (view first must be 1) become the background vertices 1..np, the step's
  * results its solutions (same list as the step), their tags its point tags.
  * Rows the step did not write (points not located, frozen, NUL, failed
- * interpolations) take the caller's values from sols[] (Mmg layout, entry
- * `first` on) -- the arrays pmx_download wrote into.  m: the new mesh --
+ * interpolations) take the caller's values from sols[], in pmx_download's
+ * point-list layout (entry 0 = point 1) -- the arrays pmx_download wrote into.  m: the new mesh --
  * np, ne (= the uploaded new tets), nt / tria_v / adjt / hausd of its
  * boundary trias (host, Mmg numbering), adja (optional: Mmg's mesh->adja,
  * else built on the device); point_c and tetra_v are not read.  Only the

@@ -1107,7 +1107,6 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
   if (!ctx->check_device_errors()) return 0;
   tr.mark("sync");
   const int S = sd.S;
-  const int64_t first = ctx->pts_first;
   // rows the step did not write keep the caller's values (Mmg's own, or the
   // frozen-point copy): which ones, from the write masks
   char *stg = hstage(ctx, (size_t)n);
@@ -1128,7 +1127,7 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
         const int sz = sd.size[s];
         if (!sols[s].m) { __atomic_store_n(&missing, true, __ATOMIC_RELAXED); continue; }
         cent[(size_t)c].push_back(make_int4((int)(j + 1), sd.off[s], sz, 0));
-        const double *src = sols[s].m + (first + j) * sz;
+        const double *src = sols[s].m + j * sz;   // pmx_download's layout
         for (int q = 0; q < 6; q++) cval[(size_t)c].push_back(q < sz ? src[q] : 0.0);
       }
     }
@@ -1170,10 +1169,13 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
   // tet records: prepared while the step ran (residency on), else from the
   // caller's Mmg adjacency (mesh->adja after remeshing) or one built here
   tr.mark("promote launch");
-  if (ctx->next_topo && !m->adja) {
+  const bool prepared = ctx->next_topo;
+  if (prepared) {                          // the residency build shares d_adja: wait for it
     CK(hipEventSynchronize(ctx->ev_topo));
     tr.mark("wait topo");
     ctx->next_topo = false;
+  }
+  if (prepared && !m->adja) {
     if (*ctx->h_nbad) { ctx->err = "pmx_promote_background: non-manifold tet faces"; return 0; }
     std::swap(ctx->d_tets, ctx->d_tets_next);
     std::swap(ctx->d_tets_s, ctx->d_tets_s_next);

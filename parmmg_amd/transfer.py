@@ -395,7 +395,7 @@ class Transfer:
         views = (N.SolView * max(len(arr), 1))()
         for i, a in enumerate(arr):
             views[i].size = a.shape[1] if a.ndim == 2 else 1
-            views[i].m = _shift(a, 8 * views[i].size, C.c_double)     # Mmg layout: entry 1 = row 0
+            views[i].m = _dp(a)                 # pmx_download's layout: entry 0 = point 1
         self._chk(self.lib.pmx_promote_background(self.ctx, C.byref(mv), len(arr), views),
                   "pmx_promote_background")
         self.npts = 0

@@ -97,10 +97,15 @@ int main(void) {
   memset(&o, 0, sizeof o);
   CK(pmx_run(ctx, &o));
   double *h2 = calloc((size_t)m2.np + 1, sizeof(double)), *ls2 = calloc((size_t)m2.np + 1, sizeof(double));
-  pmx_sol_view new2[2] = {{1, h2}, {1, ls2}};
+  /* pmx_download writes in point-list order: entry 0 = point 1 (Mmg's m[1]) */
+  pmx_sol_view new2[2] = {{1, h2 + 1}, {1, ls2 + 1}};
   CK(pmx_download(ctx, new2, NULL, NULL, NULL));
   /* quality of the new mesh in the interpolated metric, reduced over the
    * (one-rank) RCCL communicator */
+  const int stats = getenv("PMX_DEMO_NO_STATS") == NULL;
+  pmx_qual_stats qs;
+  memset(&qs, 0, sizeof qs);
+  if (stats) {
   char id[256];
   int idlen = pmx_comm_unique_id(id, sizeof id);
   void *comm = NULL;
@@ -109,7 +114,6 @@ int main(void) {
   void *d = NULL;
   if (!(d = pmx_device_alloc(ctx, sizeof(pmx_qual_part)))) { fprintf(stderr, "%s\n", pmx_last_error(ctx)); return 1; }
   CK(pmx_new_mesh_qual(ctx, NULL, 0, 0, PMX_INQUA, NULL, d));
-  pmx_qual_stats qs;
   CK(pmx_qualhisto_allreduce(ctx, comm, 1, d, 1, &qs));
   if (qs.ne != m2.ne || qs.np != m2.np || qs.min <= 0.0 || qs.max > 1.0 + 1e-12) {
     fprintf(stderr, "new-mesh statistics: ne %lld np %lld min %g max %g\n", (long long)qs.ne,
@@ -118,25 +122,37 @@ int main(void) {
   }
   pmx_device_free(ctx, d);
   pmx_comm_destroy(comm);
+  }
   /* iteration 2: M2 promoted, new mesh M3 */
   CK(pmx_promote_background(ctx, &v2, 2, new2));
   CK(pmx_upload_points(ctx, &p3));
   CK(pmx_run(ctx, &o));
   double *h3 = calloc((size_t)m3.np + 1, sizeof(double)), *ls3 = calloc((size_t)m3.np + 1, sizeof(double));
-  pmx_sol_view new3[2] = {{1, h3}, {1, ls3}};
+  pmx_sol_view new3[2] = {{1, h3 + 1}, {1, ls3 + 1}};
   CK(pmx_download(ctx, new3, NULL, NULL, NULL));
   /* the same iteration 2 from a host upload of M2 and iteration 1's fields */
   pmx_ctx *ref = pmx_create(0);
   double *h3r = calloc((size_t)m3.np + 1, sizeof(double)), *ls3r = calloc((size_t)m3.np + 1, sizeof(double));
-  pmx_sol_view new3r[2] = {{1, h3r}, {1, ls3r}};
-  if (!ref || !pmx_upload_background(ref, &v2, 2, new2, 0) || !pmx_upload_points(ref, &p3) ||
+  pmx_sol_view new3r[2] = {{1, h3r + 1}, {1, ls3r + 1}};
+  if (!ref || !pmx_upload_background(ref, &v2, 2, (pmx_sol_view[2]){{1, h2}, {1, ls2}}, 0) || !pmx_upload_points(ref, &p3) ||
       !pmx_run(ref, &o) || !pmx_download(ref, new3r, NULL, NULL, NULL)) {
     fprintf(stderr, "reference context: %s\n", ref ? pmx_last_error(ref) : "create");
     return 1;
   }
-  if (memcmp(h3 + 1, h3r + 1, (size_t)m3.np * 8) || memcmp(ls3 + 1, ls3r + 1, (size_t)m3.np * 8)) {
-    fprintf(stderr, "promoted background differs from the host upload\n");
-    return 1;
+  {
+    int64_t nd = 0, nb = 0, first = -1;
+    for (int64_t i = 1; i <= m3.np; i++)
+      if (memcmp(h3 + i, h3r + i, 8) || memcmp(ls3 + i, ls3r + i, 8)) {
+        nd++;
+        nb += m3.tag[i] ? 1 : 0;
+        if (first < 0) first = i;
+      }
+    if (nd) {
+      fprintf(stderr, "promoted background differs from the host upload: %lld points (%lld surface), "
+              "first %lld: h %.17g vs %.17g, ls %.17g vs %.17g\n", (long long)nd, (long long)nb,
+              (long long)first, h3[first], h3r[first], ls3[first], ls3r[first]);
+      return 1;
+    }
   }
   pmx_destroy(ref);
   pmx_destroy(ctx);

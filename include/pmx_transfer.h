@@ -102,7 +102,10 @@ int         pmx_device_info(pmx_ctx *ctx, char *buf, int buflen);
 
 /* ---- background (old) group -------------------------------------------- */
 /* AoS -> SoA conversion on the host, then upload.  imet = index of the
- * metric in sols[] (or -1).  If adja is NULL it is rebuilt from tetra_v.
+ * metric in sols[] (or -1).  If adja is NULL it is rebuilt from tetra_v by
+ * device face matching (overlapped with the solutions' upload; half the tet
+ * bytes over PCIe -- the faster choice for a valid conforming mesh, whose
+ * face adjacency is unique; non-manifold faces fail the upload).
  * Every argument is checked before the context changes; on failure the
  * context holds no background (pmx_run refuses until a good upload). */
 int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *old_mesh,

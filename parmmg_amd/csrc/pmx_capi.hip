@@ -414,6 +414,12 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   CK(hipStreamSynchronize(ctx->stream));   // the arena may still feed an earlier copy
   char *stg = hstage(ctx, total);
   if (!stg) return 0;
+  // any return after the topology fork first waits for that stream (a later
+  // call may regrow the buffers its kernels use)
+  struct StreamGuard {
+    hipStream_t s = nullptr;
+    ~StreamGuard() { if (s) hipStreamSynchronize(s); }
+  } topo_guard;
   if (!dgrow(ctx, ctx->d_xyz, (size_t)(np + 1) * 3) || !dgrow(ctx, ctx->d_tets, (size_t)(ne + 1)) ||
       !dgrow(ctx, ctx->d_tets_s, (size_t)std::max<int64_t>(ns, 1)) || !dgrow(ctx, ctx->d_sol, hs_n) ||
       !dgrow(ctx, ctx->d_tris, (size_t)(nt + 1)) || !dgrow(ctx, ctx->d_trn, (size_t)(nt + 1)) ||
@@ -498,6 +504,20 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     return 0;
   }
   if (!dev_adja) CK(hipMemcpyAsync(ctx->d_tets_s.p, hh, (size_t)ns * sizeof(int4), hipMemcpyHostToDevice, st));
+  if (dev_adja) {
+    // face matching on the device (pmx_topo.hip), then the tet records and
+    // the hint sample from the device connectivity -- on the topology stream
+    // as soon as the connectivity is down, overlapping the solutions' and
+    // trias' packing and DMA; joined before the final sync
+    CK(hipEventRecord(ctx->ev_fork, st));
+    CK(hipStreamWaitEvent(ctx->topo, ctx->ev_fork, 0));
+    topo_guard.s = ctx->topo;
+    *ctx->h_nbad = 0;
+    if (!pmx_ctx_build_adja_device(ctx, ctx->d_btv.p, ne, np, ctx->d_adja.p, ctx->topo, ctx->h_nbad)) return 0;
+    launch_build_tetrec(ctx->d_btv.p, ctx->d_adja.p, ne, PMX_HINT_STRIDE, ctx->d_tets.p, ctx->d_tets_s.p,
+                        ctx->topo);
+    CK(hipEventRecord(ctx->ev_join, ctx->topo));
+  }
   tr.mark("tets");
   // solutions -> interleaved [np+1][S]
   double *hs = (double *)(stg + o_s);
@@ -521,16 +541,15 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   if (!setup_grids(ctx, lo, hi, ne)) return 0;
   CK(hipMemcpyAsync(ctx->d_tris.p, htr.data(), htr.size() * sizeof(TriRec), hipMemcpyHostToDevice, st));
   if (!ctx->build_node_trias(st)) return 0;
-  if (dev_adja) {
-    // face matching on the device (pmx_topo.hip), then the tet records and
-    // the hint sample from the device connectivity
-    if (!pmx_ctx_build_adja_device(ctx, ctx->d_btv.p, ne, np, ctx->d_adja.p, st, nullptr)) return 0;
-    launch_build_tetrec(ctx->d_btv.p, ctx->d_adja.p, ne, PMX_HINT_STRIDE, ctx->d_tets.p, ctx->d_tets_s.p, st);
-  }
+  if (dev_adja) CK(hipStreamWaitEvent(st, ctx->ev_join, 0));
   CK(hipGetLastError());
   tr.mark("trias + topology");
   CK(hipStreamSynchronize(ctx->stream));   // host staging vectors die here
   tr.mark("sync");
+  if (dev_adja && *ctx->h_nbad) {
+    ctx->err = "pmx_upload_background: non-manifold tet faces";
+    return 0;
+  }
   ctx->have_bg = true;
   return 1;
 }

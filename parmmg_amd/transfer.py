@@ -111,14 +111,19 @@ class Transfer:
         self._chk(self.lib.pmx_synchronize(self.ctx), "pmx_synchronize")
 
     # ---- device-resident interface ------------------------------------------
-    def upload_background(self, m: Mesh, sols: list[np.ndarray], imet: int = 0):
-        """sols: (np+1, size) arrays in Mmg layout; imet: index of the metric or -1."""
+    def upload_background(self, m: Mesh, sols: list[np.ndarray], imet: int = 0, adja: bool = True):
+        """sols: (np+1, size) arrays in Mmg layout; imet: index of the metric or -1.
+        adja=False: Mmg's adjacency is not sent; the device rebuilds it from the
+        connectivity (16 B/tet less over PCIe, face matching overlapped with
+        the rest of the upload)."""
         arr = [np.ascontiguousarray(s, np.float64) for s in sols]
         views = (N.SolView * max(len(arr), 1))()
         for i, a in enumerate(arr):
             views[i].size = a.shape[1] if a.ndim == 2 else 1
             views[i].m = _dp(a)
         mv = mesh_view(m)
+        if not adja:
+            mv.adja = None
         self._chk(self.lib.pmx_upload_background(self.ctx, C.byref(mv), len(arr), views,
                                                  imet if arr else -1), "pmx_upload_background")
         self.sizes = [v.size for v in views[: len(arr)]]

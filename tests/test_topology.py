@@ -67,6 +67,37 @@ def test_upload_without_adjacency(transfer):
     assert np.array_equal(a.sols[0].view(np.int64), b.sols[0].view(np.int64))
 
 
+def test_upload_device_adjacency_chunked_and_refused(transfer):
+    """The device face matching runs on the topology stream beside the
+    solutions' upload: at a size where the connectivity goes down in several
+    chunks (ne > 2^21) the located elements and fields equal those of the
+    host-adjacency upload bit for bit; a non-manifold mesh is refused after
+    the sync, and the context then takes a good upload again."""
+    m = M.kuhn_cube(72)
+    x, t = M.new_points(72)
+    sols = [M.on_vertices(m, M.iso_metric), M.on_vertices(m, M.velocity)]
+    res = []
+    for adja in (True, False):
+        transfer.upload_background(m, sols, 0, adja=adja)
+        transfer.upload_points(x, t)
+        transfer.run()
+        res.append(transfer.download())
+    a, b = res
+    assert np.array_equal(a.elem, b.elem) and np.array_equal(a.status, b.status)
+    for sa, sb in zip(a.sols, b.sols):
+        assert np.array_equal(sa.view(np.int64), sb.view(np.int64))
+    bad = M.Mesh(m.xyz, np.concatenate([m.tet, m.tet[1:2]]), None, m.tria, m.adjt, m.hausd)
+    with pytest.raises(RuntimeError, match="non-manifold"):
+        transfer.upload_background(bad, sols, 0, adja=False)
+    with pytest.raises(RuntimeError):
+        transfer.run()                                   # no background after a refused upload
+    transfer.upload_background(m, sols, 0, adja=False)
+    transfer.upload_points(x, t)
+    transfer.run()
+    c = transfer.download()
+    assert np.array_equal(a.elem, c.elem)
+
+
 def test_non_manifold_reported(transfer):
     m = M.kuhn_cube(3)
     tet = np.concatenate([m.tet, m.tet[1:2]])          # a duplicated tet

@@ -438,6 +438,29 @@ __device__ __forceinline__ int rotate_step(const TetRec &r, int a, int b, int &k
   return nb;
 }
 
+// A shell record: from the workgroup's LDS batches when the tet is one of
+// them (the current and the previous batch of 256 records: the in-cell and
+// x-neighbour shells of a lexicographic numbering), else from HBM.
+__device__ __forceinline__ TetRec shell_rec(const StatArgs &A, const TetRec (*srec)[256],
+                                            const long long *kbase, int c) {
+  const unsigned long long d0 = (unsigned long long)((long long)c - kbase[0]);
+  const unsigned long long d1 = (unsigned long long)((long long)c - kbase[1]);
+  // one LDS index into both batches (no select between LDS and global
+  // pointers: the loads stay in their own address spaces)
+  const int idx = d0 < 256ull ? (int)d0 : (d1 < 256ull ? 256 + (int)d1 : -1);
+  TetRec r;
+  if (idx >= 0) {
+    const int4 *l = reinterpret_cast<const int4 *>(&srec[0][0]) + 2 * idx;
+    const int4 lv = l[0], ln = l[1];
+    r = TetRec{{lv.x, lv.y, lv.z, lv.w}, {ln.x, ln.y, ln.z, ln.w}};
+  } else {
+    const int4 *g = reinterpret_cast<const int4 *>(A.tets) + 2 * (int64_t)c;
+    const int4 gv = g[0], gn = g[1];
+    r = TetRec{{gv.x, gv.y, gv.z, gv.w}, {gn.x, gn.y, gn.z, gn.w}};
+  }
+  return r;
+}
+
 // True iff no admissible tet with index < k contains the edge (a, b) of tet
 // k.  The shell is rotated from k through the two faces of k that contain the
 // edge (cursors c0, c1; keep0/keep1 = the vertex of the face just crossed),
@@ -447,8 +470,8 @@ __device__ __forceinline__ int rotate_step(const TetRec &r, int a, int b, int &k
 // round trip) and then one step ahead; without point tags an index alone
 // decides, so a record is only loaded when the rotation goes on through it.
 template <bool TAGS>
-__device__ bool owns_edge(const StatArgs &A, int64_t k, int a, int b, int c0, int c1, int keep0,
-                          int keep1, TetRec r0, TetRec r1) {
+__device__ __forceinline__ bool owns_edge(const StatArgs &A, const TetRec (*srec)[256], const long long *kbase, int64_t k,
+                          int a, int b, int c0, int c1, int keep0, int keep1, TetRec r0, TetRec r1) {
   for (int guard = 0; guard < 4096; guard++) {
     if (c0 == (int)k) c0 = 0;                    // a direction that wrapped around
     if (c1 == (int)k) c1 = 0;
@@ -476,8 +499,8 @@ __device__ bool owns_edge(const StatArgs &A, int64_t k, int a, int b, int c0, in
       if ((need0 && c0 < k) || (need1 && c1 < k)) return false;
       if (need0 && c0 == c1) return true;
     }
-    if (need0) r0 = A.tets[c0];
-    if (need1) r1 = A.tets[c1];
+    if (need0) r0 = shell_rec(A, srec, kbase, c0);
+    if (need1) r1 = shell_rec(A, srec, kbase, c1);
   }
   return true;
 }
@@ -524,7 +547,7 @@ __global__ __launch_bounds__(256) void k_prilen(StatArgs A, LenPart *parts) {
     int4 *srow = reinterpret_cast<int4 *>(&srec[0][tid]);
     srow[0] = recs[2 * kn];
     srow[1] = recs[2 * kn + 1];
-    if (tid == 0) kbase[0] = k0;
+    if (tid == 0) { kbase[0] = k0; kbase[1] = -(1LL << 40); }   // no second batch yet
     __syncthreads();
   }
 
@@ -595,10 +618,10 @@ __global__ __launch_bounds__(256) void k_prilen(StatArgs A, LenPart *parts) {
         const int c0 = sn[o0], c1 = sn[o1];
         // the first rotation step's records, issued with the points' loads
         TetRec r0{}, r1{};
-        if (c0) r0 = A.tets[c0];
-        if (c1) r1 = A.tets[c1];
+        if (c0) r0 = shell_rec(A, srec, kbase, c0);
+        if (c1) r1 = shell_rec(A, srec, kbase, c1);
         len = edge_len_t<ANI>(A, a, b);
-        on = owns_edge<TAGS>(A, kk, a, b, c0, c1, keep0, keep1, r0, r1) &&
+        on = owns_edge<TAGS>(A, srec, kbase, kk, a, b, c0, c1, keep0, keep1, r0, r1) &&
              !(PAR && par_excluded(A, a, b));
         key = LEN_STEP2 + 6 * kk + ia;
       }

@@ -272,7 +272,7 @@ pmx_ctx *pmx_create(int device) {
   if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->topo, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_topo, hipEventDisableTiming) != hipSuccess ||
-      hipHostMalloc((void **)&ctx->h_nbad, sizeof(unsigned), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void **)&ctx->h_nbad, 2 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess ||
       [&] {
         for (auto &e : ctx->ev_dl)
           if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return true;
@@ -512,8 +512,9 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     CK(hipEventRecord(ctx->ev_fork, st));
     CK(hipStreamWaitEvent(ctx->topo, ctx->ev_fork, 0));
     topo_guard.s = ctx->topo;
-    *ctx->h_nbad = 0;
-    if (!pmx_ctx_build_adja_device(ctx, ctx->d_btv.p, ne, np, ctx->d_adja.p, ctx->topo, ctx->h_nbad)) return 0;
+    ctx->h_nbad[1] = 0;                      // [0] belongs to a pending residency build
+    if (!pmx_ctx_build_adja_device(ctx, ctx->d_btv.p, ne, np, ctx->d_adja.p, ctx->topo, ctx->h_nbad + 1))
+      return 0;
     launch_build_tetrec(ctx->d_btv.p, ctx->d_adja.p, ne, PMX_HINT_STRIDE, ctx->d_tets.p, ctx->d_tets_s.p,
                         ctx->topo);
     CK(hipEventRecord(ctx->ev_join, ctx->topo));
@@ -546,7 +547,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   tr.mark("trias + topology");
   CK(hipStreamSynchronize(ctx->stream));   // host staging vectors die here
   tr.mark("sync");
-  if (dev_adja && *ctx->h_nbad) {
+  if (dev_adja && ctx->h_nbad[1]) {
     ctx->err = "pmx_upload_background: non-manifold tet faces";
     return 0;
   }

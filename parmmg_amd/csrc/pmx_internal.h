@@ -124,7 +124,7 @@ struct pmx_ctx {
   bool next_topo = false;               // d_tets_next / d_tets_s_next are being built
   DevBuf<TetRec> d_tets_next;
   DevBuf<int4> d_tets_s_next;
-  unsigned *h_nbad = nullptr;           // pinned: non-manifold faces of that build
+  unsigned *h_nbad = nullptr;           // pinned [2]: non-manifold faces of that build, [1] of a background upload's
   DevBuf<double> d_nqual;
   bool have_qtag = false;               // raw tags of the new points
   DevBuf<uint16_t> d_qtag;

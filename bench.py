@@ -51,6 +51,9 @@ def build_case(cfg: dict, rank: int):
     n = cfg["n"]
     m = M.kuhn_cube(n, seed=20250117 + rank)
     x, t = M.new_points(n, seed=12345 + rank)
+    # the new mesh's tets over those points: the step enumerates the vertices
+    # through them, as the reference's vertex loop does (orphan marks)
+    tv = M.new_point_tets(n, x, t)
     sols = []
     if cfg["metric"] == "ani":
         sols.append(M.on_vertices(m, M.shock_metric))
@@ -60,7 +63,7 @@ def build_case(cfg: dict, rank: int):
         sols.append(M.on_vertices(m, M.level_set))
     if "vel" in cfg["fields"]:
         sols.append(M.on_vertices(m, M.velocity))
-    return m, x, t, sols
+    return m, x, t, sols, tv
 
 
 def alg_bytes(N: int, ne: int, np_: int, S: int) -> int:
@@ -252,6 +255,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--no-pcie", action="store_true",
                     help="skip the host-staged (PCIe-inclusive) leg measured after the timed region")
+    ap.add_argument("--no-new-tets", action="store_true",
+                    help="ablation: upload the new points without the new mesh's tets (no vertex "
+                         "enumeration through the tets / orphan marks in the step)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 process group backend (nccl = RCCL; gloo only to rehearse "
                          "the multi-rank path, e.g. several ranks on one GPU)")
@@ -286,7 +292,7 @@ def main():
     # process touches the GPU
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        m, x, t, sols = cases[0]
+        m, x, t, sols, _ = cases[0]
         cpu = cpu_baseline_node(m, x, t, sols)
 
     from parmmg_amd import _native as N
@@ -296,12 +302,12 @@ def main():
     # steps are enqueued back to back and may overlap on the device
     trs = []
     for g in range(ngrp):
-        m, x, t, sols = cases[g]
+        m, x, t, sols, tv = cases[g]
         tr = Transfer(local)
         tr.upload_background(m, sols, 0)
-        tr.upload_points(x, t)
+        tr.upload_points(x, t, tets_mmg=None if args.no_new_tets else tv)
         trs.append(tr)
-    m, x, t, sols = cases[0]
+    m, x, t, sols, tv = cases[0]
     tr = trs[0]
     S = sum(s.shape[1] for s in sols)
 
@@ -400,8 +406,13 @@ def main():
                      # streams, each launch's duration includes the others'
                      "concurrent_launches": ngrp},
         "kernel_ms": k_ms,
-        "per_iteration": {"ms": ms, "includes": "derived background data (grid coordinates, tria "
-                          "normals), hint grid, volume walk + interpolation, surface path, fallback"},
+        "per_iteration": {"ms": ms, "includes": (
+            "every device pass of one PMMG_interpMetricsAndFields call on the raw uploaded arrays: "
+            "derived background data (grid coordinates, tria normals = PMMG_precompute_triaNormals), "
+            "node -> trias CSR (PMMG_precompute_nodeTrias), "
+            + ("" if args.no_new_tets else "vertex enumeration through the new tets (orphan marks), ")
+            + "tag dispatch + order-preserving compaction of the new points, hint grid, volume walk + "
+            "interpolation, surface path, fallback")},
         "resident_background_ms_per_step": resident_ms,
         "step_alg_GBs": B_all / (ms * 1e-3) / 1e9,
         "locate": st,

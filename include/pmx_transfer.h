@@ -93,6 +93,7 @@ typedef struct {
  * PMX_HOST_THREADS_MIN overrides that threshold. */
 pmx_ctx    *pmx_create(int device);
 void        pmx_destroy(pmx_ctx *ctx);
+/* ctx == NULL: the last error of a call made without a context (this thread) */
 const char *pmx_last_error(pmx_ctx *ctx);
 /* Run on an external HIP stream (hipStream_t passed as void*); NULL = own. */
 int         pmx_set_stream(pmx_ctx *ctx, void *hip_stream);
@@ -165,6 +166,9 @@ void *pmx_device_buffer(pmx_ctx *ctx, int which);
  * per-group partial records of the _device statistics functions. */
 void *pmx_device_alloc(pmx_ctx *ctx, size_t bytes);
 int pmx_device_free(pmx_ctx *ctx, void *p);
+/* Copy bytes of device memory (e.g. such partial records) to the host, after
+ * the context stream's earlier work; blocking. */
+int pmx_device_download(pmx_ctx *ctx, void *host, const void *dev, size_t bytes);
 /* Inspection: copy the volume hint grid of the last run to host (cap cells);
  * returns the number of cells (0 on error). */
 int64_t pmx_debug_hint_grid(pmx_ctx *ctx, int *host, int64_t cap);
@@ -221,7 +225,9 @@ int PMX_interpMetricsAndFields(pmx_ctx *ctx, int ngrp, pmx_group *grps,
 
 /* PMMG_copyMetricsAndFields_point (src/interpmesh_pmmg.c:432-446) on the
  * caller's host arrays (a host loop: nothing to do on the device). Old-point
- * tags are read through old_tag (uint16_t, stride bytes). */
+ * tags are read through old_tag (uint16_t, stride bytes).  ctx may be NULL
+ * (the reference calls it at src/libparmmg1.c:792, before the first
+ * interpolation): errors then in pmx_last_error(NULL), per host thread. */
 int PMX_copyMetricsAndFields_point(pmx_ctx *ctx, pmx_group *grp,
                                    const uint16_t *old_tag, int64_t old_tag_stride,
                                    const int *permNodGlob, int renum, int inputMet);
@@ -271,6 +277,9 @@ int pmx_medit_sol_write(const char *path, int64_t np, int nsol, const int *types
  * restated (MMG5_caltet_iso / caltet33_ani, MMG5_lenEdg*; unpinned). */
 #define PMX_INQUA  0          /* PMMG_INQUA : before the remesh                */
 #define PMX_OUTQUA 1          /* PMMG_OUTQUA: after it (counts nrid, below)    */
+#define PMX_LESQUA 2          /* mesh->info.optimLES: MMG3D_computeLESqua
+                                 (src/quality_pmmg.c:221-224) -- not restated:
+                                 the statistics calls refuse it (return 0)     */
 #define PMX_TAG_GEO    2      /* MG_GEO  */
 #define PMX_TAG_PARBDY 8192   /* MG_PARBDY */
 
@@ -347,9 +356,12 @@ typedef struct {
  * OUTQUA's nrid.  NULL: no tags.  Kept until the next background upload. */
 int pmx_upload_point_tags(pmx_ctx *ctx, const uint16_t *tag, int64_t tag_stride);
 
-/* Quality of every background tet in the uploaded metric (MMG3D_tetraQual).
+/* Quality of every background tet in the uploaded metric
+ * (MMG3D_tetraQual(mesh, met, metRidTyp), src/quality_pmmg.c:726).  metRidTyp
+ * 0 or 1: identical arithmetic for a size-1 metric (or none); with a size-6
+ * metric 1 (Mmg's ridge metric storage, needs the xPoint normals) is refused.
  * Result stays on the device; qual (ne+1 doubles) may be NULL. */
-int pmx_tetra_qual(pmx_ctx *ctx, double *qual);
+int pmx_tetra_qual(pmx_ctx *ctx, int metRidTyp, double *qual);
 
 /* PMMG_count_nodes_par (src/quality_pmmg.c:33-80) for the uploaded group:
  * the group's points in the internal node communicator (idx_ip[i] -> slot
@@ -362,7 +374,7 @@ int pmx_count_nodes(pmx_ctx *ctx, const int *idx_ip, const int *idx_comm, int64_
                     int *intvalues, int64_t nitem, int base, int64_t *np);
 
 /* The per-group part of PMMG_qualhisto (src/quality_pmmg.c:216-261) on the
- * uploaded group: opt PMX_INQUA / PMX_OUTQUA; use_stored: the qualities of the
+ * uploaded group: opt PMX_INQUA / PMX_OUTQUA (PMX_LESQUA is refused); use_stored: the qualities of the
  * last pmx_tetra_qual.  Partial written to dev_result (pmx_qual_part, device
  * memory) on the context stream. */
 int pmx_qualhisto_device(pmx_ctx *ctx, int opt, int use_stored, void *dev_result);
@@ -384,13 +396,15 @@ typedef struct {
 
 /* PMMG_prilen on the uploaded group: centralized (par == NULL, the
  * MMG3D_computePrilen branch) or distributed (PMMG_computePrilen).  Tets whose
- * 4 vertices are ridge points (pmx_upload_point_tags) are skipped.  metRidTyp:
- * classic metric storage only (size 1, or 6 on every point). */
+ * 4 vertices are ridge points (pmx_upload_point_tags) are skipped.  metRidTyp
+ * (src/quality_pmmg.c:462,527): 0 or 1 for a size-1 metric (the same
+ * lengths); a size-6 metric with 1 (ridge metric storage) is refused. */
 int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, void *dev_result);
 int pmx_prilen(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, pmx_len_stats *st);
 
-/* PMMG_tetraQual on the NEW mesh right after the interpolation
- * (src/libparmmg1.c:845): the new tets (1-based records through a stride,
+/* PMMG_tetraQual(parmesh, metRidTyp) on the NEW mesh right after the
+ * interpolation (src/libparmmg1.c:845, metRidTyp = 1; refused for a size-6
+ * metric as in pmx_tetra_qual): the new tets (1-based records through a stride,
  * vertex indices in the last points view's numbering) are uploaded as by
  * pmx_upload_new_tets -- or tetra_v = NULL: the ones already uploaded; the
  * coordinates and the interpolated metric are the step's device-resident
@@ -398,7 +412,7 @@ int pmx_prilen(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, pmx_len_st
  * qualhisto partial of the new mesh, opt as above; np = the points) may be
  * NULL.  Needs a pmx_run on those points. */
 int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, int64_t ne, int opt,
-                      double *qual, void *dev_result);
+                      int metRidTyp, double *qual, void *dev_result);
 
 /* The reduction across groups and ranks (the reference's MPI_Reduce with its
  * custom operators, src/quality_pmmg.c:82-144, :265-307, :661-676), as host

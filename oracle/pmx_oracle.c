@@ -41,7 +41,26 @@ struct orc_ctx {
   /* mutable flags */
   int    *pflag, *pflag0, *tflag, *trflag;
   int     base;
+  /* fresh (device-semantics) mode: the point flags a query wrote, restored
+   * from pflag0 before the next query (O(touched) instead of O(np)) */
+  int    *touched;
+  int64_t ntouched, captouched;
+  int     track;
 };
+
+static void set_pflag(orc_ctx *o, int i, int v) {
+  if (o->track) {
+    if (o->ntouched == o->captouched) {
+      int64_t c = o->captouched ? 2 * o->captouched : 64;
+      int *t = (int *)realloc(o->touched, sizeof(int) * (size_t)c);
+      if (!t) abort();
+      o->touched = t;
+      o->captouched = c;
+    }
+    o->touched[o->ntouched++] = i;
+  }
+  o->pflag[i] = v;
+}
 
 static const double *PT(const orc_ctx *o, int i) { return &o->xyz[3*(int64_t)i]; }
 
@@ -192,6 +211,7 @@ void orc_destroy(orc_ctx *o) {
   if (!o) return;
   free(o->fn); free(o->tvol); free(o->trn); free(o->trarea); free(o->ntria);
   free(o->ptmp); free(o->pflag); free(o->pflag0); free(o->tflag); free(o->trflag);
+  free(o->touched);
   free(o);
 }
 
@@ -418,7 +438,7 @@ static int in_cone(orc_ctx *o, int k, int iloc, const double *p) {
   const int *fan = &o->ntria[o->ptmp[ip]];
   double pv[3], dist = 0.0;
   int t, j, d;
-  o->pflag[ip] = o->base;
+  set_pflag(o, ip, o->base);
   for (d = 0; d < 3; d++) pv[d] = p[d] - c0[d];
   for (d = 0; d < 3; d++) dist += pv[d]*pv[d];
   dist = sqrt(dist);
@@ -429,7 +449,7 @@ static int in_cone(orc_ctx *o, int k, int iloc, const double *p) {
       double a[3], alpha;
       if (jp == ip) continue;
       if (o->pflag[jp] == ip) continue;
-      o->pflag[jp] = ip;
+      set_pflag(o, jp, ip);
       for (d = 0; d < 3; d++) a[d] = PT(o, jp)[d] - c0[d];
       if (dist > o->hausd) return 0;
       alpha = 0.0;
@@ -455,8 +475,8 @@ static int in_wedge(orc_ctx *o, int k, int l, const double *p, bcoord *b) {
   for (d = 0; d < 3; d++) dist += pv[d]*pv[d];
   dist = sqrt(dist);
   if (dist > o->hausd) return ORC_UNSET;
-  if (alpha < 0.0) { o->pflag[q1] = o->base; return i0; }
-  if (alpha > n2)  { o->pflag[q0] = o->base; return i1; }
+  if (alpha < 0.0) { set_pflag(o, q1, o->base); return i0; }
+  if (alpha > n2)  { set_pflag(o, q0, o->base); return i1; }
   for (d = 0; d < 3; d++) b[d].idx = d;
   b[l].val  = 0.0;
   b[i0].val = 1.0 - alpha/n2;
@@ -602,6 +622,8 @@ int orc_interp_points(orc_ctx *o, int64_t npts, const double *pxyz, const int *p
   int64_t it;
   int cur_vol = 1, cur_bdy = 1;      /* src/interpmesh_pmmg.c:529 */
   orc_reset(o);
+  o->ntouched = 0;
+  o->track = fresh != 0;
   for (it = 0; it < npts; it++) {
     int64_t ip = order ? order[it] : it;
     const double *p = &pxyz[3*ip];
@@ -613,7 +635,9 @@ int orc_interp_points(orc_ctx *o, int64_t npts, const double *pxyz, const int *p
     if (tag & TAG_REQ) continue;                  /* copied, :546-549 */
     if (fresh) {
       /* device semantics: flags as left by nodeTrias, base = ordinal+1 */
-      memcpy(o->pflag, o->pflag0, sizeof(int) * (size_t)(o->np+1));
+      int64_t q;
+      for (q = 0; q < o->ntouched; q++) o->pflag[o->touched[q]] = o->pflag0[o->touched[q]];
+      o->ntouched = 0;
       o->base = (int)ip;
     }
     if (tag & TAG_BDY) {
@@ -665,5 +689,6 @@ int orc_interp_points(orc_ctx *o, int64_t npts, const double *pxyz, const int *p
     if (edge) edge[ip] = e;
     if (vertex) vertex[ip] = vx;
   }
+  o->track = 0;
   return 1;
 }

@@ -114,7 +114,7 @@ class ParEdges(C.Structure):
     ]
 
 
-INQUA, OUTQUA = 0, 1
+INQUA, OUTQUA, LESQUA = 0, 1, 2
 
 
 class MeditInfo(C.Structure):
@@ -140,6 +140,7 @@ SIGNATURES = {
     "pmx_device_buffer": (C.c_void_p, [C.c_void_p, C.c_int]),
     "pmx_device_alloc": (C.c_void_p, [C.c_void_p, C.c_size_t]),
     "pmx_device_free": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "pmx_device_download": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
     "pmx_debug_hint_grid": (C.c_int64, [C.c_void_p, C.c_void_p, C.c_int64]),
     "pmx_build_adja": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64,
                                  C.c_void_p]),
@@ -150,14 +151,14 @@ SIGNATURES = {
     "pmx_timing_reset": (C.c_int, [C.c_void_p]),
     "PMX_interpMetricsAndFields": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(Group), iptr, C.c_int]),
     "PMX_copyMetricsAndFields_point": (C.c_int, [C.c_void_p, C.POINTER(Group), u16ptr, i64, iptr, C.c_int, C.c_int]),
-    "pmx_tetra_qual": (C.c_int, [C.c_void_p, dptr]),
+    "pmx_tetra_qual": (C.c_int, [C.c_void_p, C.c_int, dptr]),
     "pmx_upload_point_tags": (C.c_int, [C.c_void_p, u16ptr, i64]),
     "pmx_count_nodes": (C.c_int, [C.c_void_p, iptr, iptr, i64, iptr, i64, C.c_int, C.POINTER(i64)]),
     "pmx_qualhisto_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     "pmx_qualhisto": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(QualStats)]),
     "pmx_prilen_device": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(ParEdges), C.c_void_p]),
     "pmx_prilen": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(ParEdges), C.POINTER(LenStats)]),
-    "pmx_new_mesh_qual": (C.c_int, [C.c_void_p, iptr, i64, i64, C.c_int, dptr, C.c_void_p]),
+    "pmx_new_mesh_qual": (C.c_int, [C.c_void_p, iptr, i64, i64, C.c_int, C.c_int, dptr, C.c_void_p]),
     "pmx_upload_new_tets": (C.c_int, [C.c_void_p, iptr, i64, i64]),
     "pmx_set_residency": (C.c_int, [C.c_void_p, C.c_int]),
     "pmx_copy_required": (C.c_int, [C.c_void_p, iptr, C.c_int]),

@@ -25,10 +25,11 @@ struct BdyArgs {
   const double *xyz;        // old vertices, 24 B
   const TriRec *tris;
   const Pt4 *trn;
-  const int *ntoff, *ntlist;
+  const int2 *ntrange;      // fan [lo, hi) in ntlist of vertex l of tria k, at 3 k + l
+  const int *ntlist;
   const double *sol;
   SolDesc sd;
-  const Pt4 *q;
+  const double *q;          // new points, dense x y z (0-based)
   const int8_t *kind;
   int64_t nq, nt;
   double hausd;
@@ -42,7 +43,8 @@ struct BdyArgs {
   int *ovf_list;       // private-list overflow
   unsigned *ovf_count;
   const int *list;       // indices of the boundary points
-  int64_t nlist;
+  int64_t nlist;         // upper bound (launch size); the step's count is *nlist_dev
+  const int *nlist_dev;
   uint4 *wstats;         // per-wave walk statistics
 };
 
@@ -91,7 +93,9 @@ template <int C> __device__ __forceinline__ void mark_visited(RegState<C> &s, in
     if (i == s.nv) s.vis[i] = t;
   s.nv++;
 }
-template <int C> __device__ __forceinline__ int get_flag(RegState<C> &s, const BdyArgs &A, int p) {
+// flag of point p: the query's own override, else the incident-tria count
+// PMMG_precompute_nodeTrias leaves (cnt, from the caller's fan record)
+template <int C> __device__ __forceinline__ int get_flag(RegState<C> &s, int p, int cnt) {
   bool hit = false;
   int f = 0;
 #pragma unroll
@@ -100,7 +104,7 @@ template <int C> __device__ __forceinline__ int get_flag(RegState<C> &s, const B
     f = m ? s.ovf[i] : f;
     hit |= m;
   }
-  return hit ? f : A.ntoff[p + 1] - A.ntoff[p];
+  return hit ? f : cnt;
 }
 template <int C> __device__ __forceinline__ void set_flag(RegState<C> &s, int p, int f) {
   bool upd = false;
@@ -130,10 +134,10 @@ template <class St> __device__ void mark_visited(St &s, int t) {
   if (s.nv >= st_cap(s)) { s.over = true; return; }
   s.V(s.nv++) = t;
 }
-template <class St> __device__ int get_flag(St &s, const BdyArgs &A, int p) {
+template <class St> __device__ int get_flag(St &s, int p, int cnt) {
   for (int i = s.no - 1; i >= 0; i--)
     if (s.OP(i) == p) return s.OF(i);
-  return A.ntoff[p + 1] - A.ntoff[p];
+  return cnt;
 }
 template <class St> __device__ void set_flag(St &s, int p, int f) {
   for (int i = 0; i < s.no; i++)
@@ -259,13 +263,15 @@ __device__ bool in_cone(const BdyArgs &A, St &s, int k, int iloc, D3 p, int base
   double dist = 0.0;
   for (int d = 0; d < 3; d++) dist += pv[d] * pv[d];
   dist = sqrt(dist);
-  int f0 = A.ntoff[ip], f1 = A.ntoff[ip + 1];
-  for (int f = f0; f < f1; f++) {
-    TriRec t = A.tris[A.ntlist[f]];
+  const int2 fan = A.ntrange[3 * k + iloc];
+  for (int f = fan.x; f < fan.y; f++) {
+    const int g = A.ntlist[f];
+    TriRec t = A.tris[g];
     for (int j = 0; j < 3; j++) {
       int jp = t.v[j];
       if (jp == ip) continue;
-      if (get_flag(s, A, jp) == ip) continue;
+      const int2 r = A.ntrange[3 * g + j];
+      if (get_flag(s, jp, r.y - r.x) == ip) continue;
       set_flag(s, jp, ip);
       D3 cj = ld3(A.xyz, jp);
       double a[3] = {cj.x - c0.x, cj.y - c0.y, cj.z - c0.z};
@@ -424,10 +430,9 @@ template <int CAP>
 __global__ __launch_bounds__(256) void k_locate_bdy(BdyArgs A) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned s_cnt = 0, s_sum = 0, s_max = 0, s_min = 0xffffffffu;
-  if (j < A.nlist) {
+  if (j < *A.nlist_dev) {
     const int64_t i = A.list[j];
-    Pt4 qq = A.q[i];
-    D3 p{qq.x, qq.y, qq.z};
+    const D3 p = ld3(A.q, (int)i);
     int start = tria_hint(A, p);
     A.start[i] = start;
     RegState<CAP> s;
@@ -464,8 +469,7 @@ __global__ __launch_bounds__(64) void k_locate_bdy_ovf(BdyArgs A, int *ws, int c
   const unsigned tid = blockIdx.x * blockDim.x + threadIdx.x;
   for (unsigned j = tid; j < n; j += nthr) {
     int64_t i = A.ovf_list[j];
-    Pt4 qq = A.q[i];
-    D3 p{qq.x, qq.y, qq.z};
+    const D3 p = ld3(A.q, (int)i);
     GlobState s;
     s.init(ws + (size_t)tid * 3 * cap, cap);
     Bary b;
@@ -492,8 +496,7 @@ __global__ __launch_bounds__(256) void k_exh_bdy(BdyArgs A) {
   const unsigned n = *A.stuck_count;
   for (unsigned j = blockIdx.x; j < n; j += gridDim.x) {
     int64_t i = A.stuck_list[j];
-    Pt4 qq = A.q[i];
-    D3 p{qq.x, qq.y, qq.z};
+    const D3 p = ld3(A.q, (int)i);
     if (threadIdx.x == 0) s_min = 0x7fffffff;
     __syncthreads();
     RegState<1> dummy;
@@ -615,60 +618,59 @@ __device__ int tria_hint(const BdyArgs &A, D3 p) {
 #define OVF_THREADS (64 * 64)
 
 // node -> trias graph (the content of PMMG_precompute_nodeTrias,
-// src/locate_pmmg.c:134-195, in CSR form: ntoff[np+2], ntlist[3 nt], fan order
-// = increasing tria index as in the reference), built on the device from the
-// uploaded trias: count, scan, fill, then each (short) fan sorted.  A host
-// build over np+2 offsets cost 3.6 ms per background at 1.7M vertices.
-__global__ __launch_bounds__(256) void k_nt_count(const TriRec *__restrict__ tris, int64_t nt,
-                                                  int *__restrict__ cnt) {
+// src/locate_pmmg.c:134-195: each boundary vertex's fan of trias in increasing
+// tria index, and the fan sizes the point flags start from), rebuilt by every
+// step that rebuilds the background's derived data -- the reference builds it
+// inside PMMG_interpMetricsAndFields (src/interpmesh_pmmg.c:707).  Sized by
+// the surface, not the volume: the 3 nt (vertex, 3 k + l) pairs are radix
+// sorted by vertex (stable: fans in tria order), and every pair's slot 3 k + l
+// records its vertex's run [lo, hi) -- the surface kernels always reach a
+// vertex through a tria that holds it, so no per-vertex offsets over np.
+__global__ __launch_bounds__(256) void k_nt_pairs(const TriRec *__restrict__ tris, int64_t nt,
+                                                  unsigned *__restrict__ key, int *__restrict__ val) {
   for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= nt;
-       k += (int64_t)gridDim.x * blockDim.x)
-    for (int l = 0; l < 3; l++) atomicAdd(&cnt[tris[k].v[l] + 1], 1);
-}
-__global__ __launch_bounds__(256) void k_nt_fill(const TriRec *__restrict__ tris, int64_t nt,
-                                                 int *__restrict__ cur, int *__restrict__ list) {
-  for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= nt;
-       k += (int64_t)gridDim.x * blockDim.x)
-    for (int l = 0; l < 3; l++) list[atomicAdd(&cur[tris[k].v[l]], 1)] = (int)k;
-}
-__global__ __launch_bounds__(256) void k_nt_sort(const int *__restrict__ off, int64_t np,
-                                                 int *__restrict__ list) {
-  for (int64_t v = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v <= np;
-       v += (int64_t)gridDim.x * blockDim.x) {
-    const int lo = off[v], hi = off[v + 1];
-    for (int i = lo + 1; i < hi; i++) {
-      const int x = list[i];
-      int j = i - 1;
-      while (j >= lo && list[j] > x) { list[j + 1] = list[j]; j--; }
-      list[j + 1] = x;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const TriRec t = tris[k];
+    for (int l = 0; l < 3; l++) {
+      key[3 * (k - 1) + l] = (unsigned)t.v[l];
+      val[3 * (k - 1) + l] = (int)(3 * k + l);
     }
+  }
+}
+__global__ __launch_bounds__(256) void k_nt_runs(const unsigned *__restrict__ key, const int *__restrict__ val,
+                                                 int64_t m, int2 *__restrict__ range, int *__restrict__ list) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    list[i] = val[i] / 3;
+    if (i > 0 && key[i - 1] == key[i]) continue;           // not the start of a run
+    int64_t j = i + 1;
+    while (j < m && key[j] == key[i]) j++;
+    for (int64_t q = i; q < j; q++) range[val[q]] = make_int2((int)i, (int)j);
   }
 }
 
 bool pmx_ctx::build_node_trias(hipStream_t s) {
-  if (!pmx_dgrow(this, d_ntoff, (size_t)(np + 2)) || !pmx_dgrow(this, d_ntcur, (size_t)(np + 2)) ||
-      !pmx_dgrow(this, d_ntlist, (size_t)std::max<int64_t>(3 * nt, 1)))
+  const int64_t m = 3 * nt;
+  if (m < 1) return true;
+  int bits = 1;
+  while (bits < 32 && ((int64_t)1 << bits) <= np) bits++;
+  if (!pmx_dgrow(this, d_ntkey, (size_t)(2 * m)) || !pmx_dgrow(this, d_ntval, (size_t)(2 * m)) ||
+      !pmx_dgrow(this, d_ntrange, (size_t)(3 * (nt + 1))) || !pmx_dgrow(this, d_ntlist, (size_t)m))
     return false;
   size_t bytes = 0;
-  hipcub::DeviceScan::InclusiveSum(nullptr, bytes, (const int *)nullptr, (int *)nullptr, (int)(np + 2), s);
+  hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const unsigned *)nullptr, (unsigned *)nullptr,
+                                     (const int *)nullptr, (int *)nullptr, (int)m, 0, bits, s);
   if (!pmx_dgrow(this, d_nttmp, bytes)) return false;
-  if (hipMemsetAsync(d_ntcur.p, 0, sizeof(int) * (size_t)(np + 2), s) != hipSuccess) {
-    err = "node trias: memset";
-    return false;
-  }
   const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nt + 255) / 256, 4096));
-  if (nt > 0) hipLaunchKernelGGL(k_nt_count, dim3(nb), dim3(256), 0, s, d_tris.p, nt, d_ntcur.p);
-  if (hipcub::DeviceScan::InclusiveSum(d_nttmp.p, bytes, d_ntcur.p, d_ntoff.p, (int)(np + 2), s) != hipSuccess ||
-      hipMemcpyAsync(d_ntcur.p, d_ntoff.p, sizeof(int) * (size_t)(np + 2), hipMemcpyDeviceToDevice, s) !=
-          hipSuccess) {
-    err = "node trias: scan";
+  hipLaunchKernelGGL(k_nt_pairs, dim3(nb), dim3(256), 0, s, d_tris.p, nt, d_ntkey.p, d_ntval.p);
+  if (hipcub::DeviceRadixSort::SortPairs(d_nttmp.p, bytes, (const unsigned *)d_ntkey.p, d_ntkey.p + m,
+                                         (const int *)d_ntval.p, d_ntval.p + m, (int)m, 0, bits, s) !=
+      hipSuccess) {
+    err = "node trias: sort";
     return false;
   }
-  if (nt > 0) {
-    hipLaunchKernelGGL(k_nt_fill, dim3(nb), dim3(256), 0, s, d_tris.p, nt, d_ntcur.p, d_ntlist.p);
-    const unsigned nv = (unsigned)std::max<int64_t>(1, std::min<int64_t>((np + 255) / 256, 8192));
-    hipLaunchKernelGGL(k_nt_sort, dim3(nv), dim3(256), 0, s, d_ntoff.p, np, d_ntlist.p);
-  }
+  const unsigned nr = (unsigned)std::max<int64_t>(1, std::min<int64_t>((m + 255) / 256, 8192));
+  hipLaunchKernelGGL(k_nt_runs, dim3(nr), dim3(256), 0, s, (const unsigned *)d_ntkey.p + m,
+                     (const int *)d_ntval.p + m, m, d_ntrange.p, d_ntlist.p);
   if (hipGetLastError() != hipSuccess) {
     err = "node trias: launch";
     return false;
@@ -737,15 +739,15 @@ bool pmx_ctx::launch_bdy(const VolArgs &a, hipStream_t s) {
                        d_tris.p, d_xyz.p, nt, d_tgrid, tg);
   }
   BdyArgs B{};
-  B.xyz = d_xyz.p; B.tris = d_tris.p; B.trn = d_trn.p; B.ntoff = d_ntoff.p; B.ntlist = d_ntlist.p;
-  B.sol = d_sol.p; B.sd = a.sd; B.q = d_q.p; B.kind = d_kind.p; B.nq = nq; B.nt = nt;
+  B.xyz = d_xyz.p; B.tris = d_tris.p; B.trn = d_trn.p; B.ntrange = d_ntrange.p; B.ntlist = d_ntlist.p;
+  B.sol = d_sol.p; B.sd = a.sd; B.q = d_qxyz.p; B.kind = d_kind.p; B.nq = nq; B.nt = nt;
   B.hausd = hausd; B.grid = d_tgrid; B.g = tg;
   B.out = d_out.p; B.wmask = d_wmask.p; B.elem = d_elem.p; B.status = d_status.p;
   B.steps = d_steps.p; B.start = d_start.p; B.edge = d_edge.p; B.vertex = d_vertex.p;
   B.stuck_list = d_blist.p; B.stuck_count = d_counts.p + 1;
   B.ovf_list = d_olist.p; B.ovf_count = d_counts.p + 2;
-  B.list = d_bdylist.p; B.nlist = nq_bdy; B.wstats = d_bstat.p;
-  int64_t nb = (nq_bdy + 255) / 256;
+  B.list = d_bdylist.p; B.nlist = nq_bdy_ub; B.nlist_dev = d_nsel.p + 1; B.wstats = d_bstat.p;
+  int64_t nb = (nq_bdy_ub + 255) / 256;
   hipLaunchKernelGGL(k_locate_bdy<BDY_CAP>, dim3((unsigned)nb), dim3(256), 0, s, B);
   hipLaunchKernelGGL(k_locate_bdy_ovf, dim3(OVF_THREADS / 64), dim3(64), 0, s, B, d_ows.p, OVF_CAP);
   hipLaunchKernelGGL(k_exh_bdy, dim3(256), dim3(256), 0, s, B);

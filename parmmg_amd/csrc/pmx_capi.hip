@@ -24,8 +24,13 @@
 #include "pmx_internal.h"
 
 // events per recorded step: 0 start, 7 derived data built, 1 hint built,
-// 2 volume walk done, 3/5 surface path start/end (side stream), 6 joined, 4 end
+// 2 volume walk done, 3/5 surface path start (node -> trias fans) / end (side
+// stream), 6 joined, 4 end
 #define PMX_EV_PER_RUN 8
+
+// errors of the calls that work without a context (per host thread)
+static thread_local std::string noctx_err;
+void pmx_set_noctx_error(const char *msg) { noctx_err = msg; }
 
 static bool ok(pmx_ctx *c, hipError_t e, const char *what) {
   if (e == hipSuccess) return true;
@@ -279,6 +284,7 @@ pmx_ctx *pmx_create(int device) {
         return false;
       }() ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_fork2, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess) {
     pmx_destroy(ctx);
     return nullptr;
@@ -305,6 +311,7 @@ void pmx_destroy(pmx_ctx *ctx) {
   ctx->free_all();
   for (auto &e : ctx->events) hipEventDestroy(e);
   if (ctx->ev_fork) hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_fork2) hipEventDestroy(ctx->ev_fork2);
   if (ctx->ev_join) hipEventDestroy(ctx->ev_join);
   if (ctx->side) hipStreamDestroy(ctx->side);
   if (ctx->topo) hipStreamDestroy(ctx->topo);
@@ -316,7 +323,10 @@ void pmx_destroy(pmx_ctx *ctx) {
   delete ctx;
 }
 
-const char *pmx_last_error(pmx_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+const char *pmx_last_error(pmx_ctx *ctx) {
+  if (ctx) return ctx->err.c_str();
+  return noctx_err.empty() ? "null context" : noctx_err.c_str();
+}
 
 int pmx_set_stream(pmx_ctx *ctx, void *s) {
   if (!ctx) return 0;
@@ -380,7 +390,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   // upload has completed (a failed call must not leave sizes that disagree
   // with the device buffers)
   ctx->have_bg = ctx->ran = ctx->have_derived = ctx->have_tetv = ctx->have_qual = false;
-  ctx->have_ptag = false;
+  ctx->have_ptag = ctx->have_csr = false;
   ctx->stat_np = -1;
   if (!m) { ctx->err = "pmx_upload_background: null mesh"; return 0; }
   hipSetDevice(ctx->device);
@@ -541,7 +551,8 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   ctx->sd = sd;
   if (!setup_grids(ctx, lo, hi, ne)) return 0;
   CK(hipMemcpyAsync(ctx->d_tris.p, htr.data(), htr.size() * sizeof(TriRec), hipMemcpyHostToDevice, st));
-  if (!ctx->build_node_trias(st)) return 0;
+  // the node -> trias fans are the step's (pmx_run: PMMG_precompute_nodeTrias
+  // runs inside the reference's call)
   if (dev_adja) CK(hipStreamWaitEvent(st, ctx->ev_join, 0));
   CK(hipGetLastError());
   tr.mark("trias + topology");
@@ -578,32 +589,38 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   const size_t nn = (size_t)std::max<int64_t>(n, 1);
   // The host packs and sends only what the device cannot derive -- dense
   // coordinates (24 B), tags (2 B), the new tets (16 B) -- in a pinned
-  // staging arena, chunked so that DMA overlaps packing; the kinds, the
-  // per-path lists (order-preserving compaction) and the list-ordered volume
-  // coordinates are built on the device (r02: host classification + lists +
-  // their DMA were 3-5 ms of the 1.7M-point C2 upload).
+  // staging arena, chunked so that DMA overlaps packing.  The kinds, the
+  // per-path lists (order-preserving compaction), the list-ordered volume
+  // coordinates and the orphan marks are the step's work (pmx_run), as the
+  // vertex loop and its tag dispatch are inside the reference's call
+  // (src/interpmesh_pmmg.c:535-560).  The host's tag pass gives the launch
+  // sizes (upper bounds: orphans are found on the device).
   const int64_t ntet = pv->tetra_v ? pv->ne : 0;
   const size_t o_x = 0, o_tg = o_x + al256(nn * 3 * sizeof(double)),
                o_tv = o_tg + al256(pv->tag ? nn * 2 : 0),
-               total = o_tv + al256(ntet ? (size_t)(ntet + 1) * sizeof(int4) : 0);
+               o_mk = o_tv + al256(ntet ? (size_t)(ntet + 1) * sizeof(int4) : 0),
+               total = o_mk + al256(pv->tetra_v ? nn : 0);
   CK(hipStreamSynchronize(ctx->stream));   // the arena may still feed an earlier copy
   char *st = hstage(ctx, total);
   if (!st) return 0;
   double *hx = (double *)(st + o_x);
   uint16_t *htg = (uint16_t *)(st + o_tg);
   int4 *htv = (int4 *)(st + o_tv);
+  uint8_t *hmk = (uint8_t *)(st + o_mk);
   const char *pc = (const char *)pv->c;
   const char *tg = (const char *)pv->tag;
-  if (!dgrow(ctx, ctx->d_qxyz, nn * 3) || !dgrow(ctx, ctx->d_q, nn) || !dgrow(ctx, ctx->d_kind, nn) ||
-      !dgrow(ctx, ctx->d_qmark, nn) || !dgrow(ctx, ctx->d_fvol, nn) || !dgrow(ctx, ctx->d_fbdy, nn) ||
+  if (!dgrow(ctx, ctx->d_qxyz, nn * 3) || !dgrow(ctx, ctx->d_kind, nn) || !dgrow(ctx, ctx->d_qmark, nn) ||
       !dgrow(ctx, ctx->d_nsel, 2) || !dgrow(ctx, ctx->d_vollist, nn) || !dgrow(ctx, ctx->d_bdylist, nn) ||
-      !dgrow(ctx, ctx->d_qv, nn * 3) || (tg && !dgrow(ctx, ctx->d_qtag, nn)) ||
-      (ntet && !dgrow(ctx, ctx->d_ntetv, (size_t)(ntet + 1))))
+      !dgrow(ctx, ctx->d_qv, nn * 3) || !dgrow(ctx, ctx->d_ctile, (size_t)std::max<int64_t>(cls_tiles(n), 1)) ||
+      (tg && !dgrow(ctx, ctx->d_qtag, nn)) || (ntet && !dgrow(ctx, ctx->d_ntetv, (size_t)(ntet + 1))))
     return 0;
   // coordinates (+ bounding box: a promoted background's hint grid) and tags
+  // (+ the per-path upper bounds)
   double qlo[64][3], qhi[64][3];
+  int64_t cvol[64], cbdy[64];
   const int C = par_chunks(0, n, [&](int ci, int64_t j0, int64_t j1) {
     double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+    int64_t nv = 0, nb = 0;
     for (int64_t j = j0; j < j1; j++) {
       const double *c = (const double *)(pc + (pv->first + j) * pv->stride);
       for (int ax = 0; ax < 3; ax++) {
@@ -611,10 +628,23 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
         lo[ax] = std::min(lo[ax], c[ax]);
         hi[ax] = std::max(hi[ax], c[ax]);
       }
-      if (tg) htg[j] = *(const uint16_t *)(tg + (pv->first + j) * pv->tag_stride);
+      if (tg) {
+        const uint16_t t = *(const uint16_t *)(tg + (pv->first + j) * pv->tag_stride);
+        htg[j] = t;
+        const bool live = t < PMX_TAG_NUL && !(t & PMX_TAG_REQ);
+        nv += (live && !(t & PMX_TAG_BDY)) ? 1 : 0;
+        nb += (live && (t & PMX_TAG_BDY)) ? 1 : 0;
+      }
     }
     for (int ax = 0; ax < 3; ax++) { qlo[ci][ax] = lo[ax]; qhi[ci][ax] = hi[ax]; }
+    cvol[ci] = tg ? nv : j1 - j0;
+    cbdy[ci] = nb;
   });
+  ctx->nq_vol_ub = ctx->nq_bdy_ub = 0;
+  for (int i = 0; i < C; i++) {
+    ctx->nq_vol_ub += cvol[i];
+    ctx->nq_bdy_ub += cbdy[i];
+  }
   for (int ax = 0; ax < 3; ax++) {
     ctx->qlo[ax] = HUGE_VAL;
     ctx->qhi[ax] = -HUGE_VAL;
@@ -629,13 +659,22 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   }
   tr.mark("coords");
   // the new tets (vertex = view index - first + 1), validated, packed in
-  // chunks whose DMA overlaps the packing of the next
-  if (ntet) {
-    htv[0] = make_int4(0, 0, 0, 0);
+  // chunks whose DMA overlaps the packing of the next.  The same pass is the
+  // reference's vertex loop over the new tets (src/interpmesh_pmmg.c:535-541):
+  // it marks the points of valid tets, so that points in no valid tet
+  // (orphans: untouched, as the reference never visits them) are known.
+  // Every tet must be read here anyway to pack it; a device pass over the
+  // 16-B tets would re-read them all (C3: 1.6 GB, 0.5 ms) to find, normally,
+  // no orphan at all.  The step applies the marks only when there are some.
+  int64_t norph = 0;
+  if (pv->tetra_v) {
+    uint8_t *mk = hmk;
+    memset(mk, 0, (size_t)n);
     const char *tc = (const char *)pv->tetra_v;
     bool bad = false;
+    if (ntet) htv[0] = make_int4(0, 0, 0, 0);
     const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(8, ntet >> 20));
-    for (int64_t c = 0; c < nch; c++) {
+    for (int64_t c = 0; ntet && c < nch; c++) {
       const int64_t lo = (c == 0) ? 0 : 1 + ntet * c / nch, hi = 1 + ntet * (c + 1) / nch;
       par_for(std::max<int64_t>(lo, 1), hi, [&](int64_t k0, int64_t k1) {
         bool b = false;
@@ -644,9 +683,10 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
           if (v[0] <= 0) { htv[k] = make_int4(0, 0, 0, 0); continue; }   // !MG_EOK
           int w[4];
           for (int l = 0; l < 4; l++) {
-            const int64_t jj = (int64_t)v[l] - pv->first;
-            if (jj < 0 || jj >= n) b = true;
+            int64_t jj = (int64_t)v[l] - pv->first;
+            if (jj < 0 || jj >= n) { b = true; jj = 0; }
             w[l] = (int)(jj + 1);
+            __atomic_store_n(&mk[jj], (uint8_t)1, __ATOMIC_RELAXED);
           }
           htv[k] = make_int4(w[0], w[1], w[2], w[3]);
         }
@@ -660,28 +700,19 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
       ctx->err = "pmx_upload_points: new tet vertex outside [first, last]";
       return 0;
     }
+    // orphans among the points a step would locate or give a constant size
+    int64_t no[64] = {};
+    const int Co = par_chunks(0, n, [&](int ci, int64_t j0, int64_t j1) {
+      int64_t c = 0;
+      for (int64_t j = j0; j < j1; j++)
+        c += (!mk[j] && !(tg && htg[j] >= PMX_TAG_NUL)) ? 1 : 0;
+      no[ci] = c;
+    });
+    for (int i = 0; i < Co; i++) norph += no[i];
+    if (norph && n) CK(hipMemcpyAsync(ctx->d_qmark.p, mk, (size_t)n, hipMemcpyHostToDevice, ctx->stream));
   }
   tr.mark("tets pack+dma");
-  // kinds, lists (input order kept), list-ordered volume coordinates
   ctx->nq = n;
-  if (n) {
-    launch_classify_points(ctx->d_qxyz.p, tg ? ctx->d_qtag.p : nullptr, pv->tetra_v != nullptr,
-                           ntet ? ctx->d_ntetv.p : nullptr, ntet, ctx->d_qmark.p, n, ctx->d_q.p, ctx->d_kind.p,
-                           ctx->d_fvol.p, ctx->d_fbdy.p, ctx->stream);
-    hipcub::CountingInputIterator<int> idx(0);
-    size_t bytes = 0;
-    hipcub::DeviceSelect::Flagged(nullptr, bytes, idx, ctx->d_fvol.p, ctx->d_vollist.p, ctx->d_nsel.p, (int)n,
-                                  ctx->stream);
-    if (!dgrow(ctx, ctx->d_seltmp, bytes)) return 0;
-    CK(hipcub::DeviceSelect::Flagged(ctx->d_seltmp.p, bytes, idx, ctx->d_fvol.p, ctx->d_vollist.p, ctx->d_nsel.p,
-                                     (int)n, ctx->stream));
-    CK(hipcub::DeviceSelect::Flagged(ctx->d_seltmp.p, bytes, idx, ctx->d_fbdy.p, ctx->d_bdylist.p,
-                                     ctx->d_nsel.p + 1, (int)n, ctx->stream));
-    launch_gather_qv(ctx->d_qxyz.p, ctx->d_vollist.p, ctx->d_nsel.p, n, ctx->d_qv.p, ctx->stream);
-    CK(hipGetLastError());
-  }
-  int cnt[2] = {0, 0};
-  if (n) CK(hipMemcpyAsync(cnt, ctx->d_nsel.p, sizeof cnt, hipMemcpyDeviceToHost, ctx->stream));
   if (!dgrow(ctx, ctx->d_wmask, nn)) return 0;
   if (!dgrow(ctx, ctx->d_elem, nn)) return 0;
   if (!dgrow(ctx, ctx->d_status, nn)) return 0;
@@ -704,11 +735,10 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   if (!dgrow(ctx, ctx->d_bstat, (nn + 255) / 256 * 4 + 4)) return 0;
   ctx->have_qtag = false;
   CK(hipStreamSynchronize(ctx->stream));
-  tr.mark("classify + sync");
-  ctx->nq_vol = cnt[0];
-  ctx->nq_bdy = cnt[1];
+  tr.mark("sync");
   ctx->have_qtag = tg && n;
   ctx->pts_first = pv->first;
+  ctx->pts_mark = norph > 0;            // the step applies the orphan marks
   ctx->have_pts = true;
   ctx->have_ntet = ntet > 0;
   ctx->n_ntet = ntet;
@@ -733,7 +763,7 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
 
 static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &opts, VolArgs &A) {
   A.xyz = ctx->d_xyz.p; A.tets = ctx->d_tets.p; A.sol = ctx->d_sol.p; A.sd = sd;
-  A.q = ctx->d_q.p; A.kind = ctx->d_kind.p; A.nq = ctx->nq; A.ne = ctx->ne;
+  A.q = ctx->d_qxyz.p; A.kind = ctx->d_kind.p; A.nq = ctx->nq; A.ne = ctx->ne;
   A.grid = ctx->d_grid.p; A.g = ctx->grid;
   A.out = ctx->d_out.p; A.wmask = ctx->d_wmask.p;
   A.elem = ctx->d_elem.p; A.status = ctx->d_status.p; A.steps = ctx->d_steps.p;
@@ -741,7 +771,7 @@ static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &o
   A.stuck_list = ctx->d_list.p; A.stuck_count = ctx->d_counts.p;
   A.tie_list = ctx->d_ties.p; A.tie_count = ctx->d_counts.p + 3;
   A.found = ctx->d_found.p; A.bestk = ctx->d_bestk.p; A.best = ctx->d_best.p;
-  A.list = ctx->d_vollist.p; A.nlist = ctx->nq_vol; A.wstats = ctx->d_vstat.p;
+  A.list = ctx->d_vollist.p; A.nlist = ctx->nq_vol_ub; A.nlist_dev = ctx->d_nsel.p; A.wstats = ctx->d_vstat.p;
   A.max_walk = opts.max_walk > 0 ? opts.max_walk : 512;
   A.const_bit = sd.metric_const ? (1u << sd.imet) : 0u;
   A.inline_ties = (opts.flags & PMX_RUN_NO_INLINE_TIES) ? 0 : 1;
@@ -768,17 +798,41 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   if (opts.timing) ev = ctx->next_event_slot();
 
   hipStream_t st = ctx->stream;
+  // everything below is one iteration's device work on the uploaded raw
+  // arrays: the per-background derived data (with PMX_RUN_FRESH_BACKGROUND,
+  // or after an upload), the points' classification and compaction, the
+  // node -> trias CSR (surface points only), hint grids, walks, fallback
+  const bool derive = !ctx->have_derived || (opts.flags & PMX_RUN_FRESH_BACKGROUND);
+  const bool csr = ctx->nq_bdy_ub > 0 && (!ctx->have_csr || (opts.flags & PMX_RUN_FRESH_BACKGROUND));
   if (ev) CK(hipEventRecord(ev[0], st));
   // one prologue kernel zeroes the write masks, the counters and the hint grid
-  launch_prologue(ctx->d_wmask.p, n, ctx->d_counts.p, ctx->d_grid.p, ctx->gcells, st);
-  // per-background derived data: after an upload, or every step when the
-  // caller times whole iterations (PMX_RUN_FRESH_BACKGROUND)
-  if (!ctx->have_derived || (opts.flags & PMX_RUN_FRESH_BACKGROUND)) {
+  ZeroRanges z{};
+  z.add(ctx->d_wmask.p, n);
+  z.add(ctx->d_counts.p, 32 * sizeof(unsigned));
+  z.add(ctx->d_grid.p, ctx->gcells * (int64_t)sizeof(int));
+  launch_prologue(z, st);
+  // the node -> trias fans (PMMG_precompute_nodeTrias, surface points only)
+  // on the side stream from the start of the step: a small radix sort that
+  // overlaps the derived data, the classification and the hint build
+  const bool bdy = ctx->nq_bdy_ub > 0;
+  const bool serial = (opts.flags & PMX_RUN_SERIAL_SURFACE) != 0;
+  hipStream_t ss = serial ? st : ctx->side;
+  if (bdy && !serial) {
+    CK(hipEventRecord(ctx->ev_fork, st));
+    CK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+  }
+  if (ev) CK(hipEventRecord(ev[3], ss));
+  if (bdy && csr) {
+    if (!ctx->build_node_trias(ss)) return 0;
+    ctx->have_csr = true;
+  }
+  if (derive) {
     launch_bg_derive(ctx->d_xyz.p, ctx->np, ctx->grid, ctx->d_xyzq.p, ctx->d_tris.p, ctx->nt,
                      ctx->d_trn.p, st);
     ctx->have_derived = true;
   }
   if (ev) CK(hipEventRecord(ev[7], st));
+  if (!ctx->classify(st)) return 0;
   if (sd.metric_const)
     launch_const_metric(ctx->d_kind.p, n, ctx->d_out.p, S, sd.off[sd.imet], sd.size[sd.imet],
                         opts.hsiz, ctx->d_wmask.p, sd.imet, st);
@@ -786,6 +840,10 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   for (int s = 0; s < sd.nsol; s++)
     if (!(s == sd.imet && sd.metric_const)) any_interp = true;
   // reference early exit (src/interpmesh_pmmg.c:508-512): nothing to locate
+  if (!any_interp && bdy && !serial) {
+    CK(hipEventRecord(ctx->ev_join, ctx->side));
+    CK(hipStreamWaitEvent(st, ctx->ev_join, 0));
+  }
   if (any_interp) {
     VolArgs A{};
     fill_vol_args(ctx, sd, opts, A);
@@ -793,41 +851,38 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     launch_hint_build(stride == PMX_HINT_STRIDE ? ctx->d_tets_s.p : nullptr, ctx->d_tets.p, ctx->ne,
                       stride, ctx->d_grid.p, ctx->grid, ctx->d_xyzq.p, st);
     if (ev) CK(hipEventRecord(ev[1], st));
-    // surface path on the side stream, forked after the bandwidth-bound hint
-    // build (forking before it slowed that by 40 %, r01 sweep): it is
-    // latency-bound and overlaps the volume walk
-    const bool serial = (opts.flags & PMX_RUN_SERIAL_SURFACE) != 0;
-    if (ctx->nq_bdy && !serial) {
-      CK(hipEventRecord(ctx->ev_fork, st));
-      CK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-      if (ev) CK(hipEventRecord(ev[3], ctx->side));
+    // the surface path on the side stream once the points are classified and
+    // the bandwidth-bound hint build is done (forking the surface kernels
+    // before it slowed that by 40 %, r01 sweep): it is latency-bound and
+    // overlaps the volume walk
+    if (bdy && !serial) {
+      CK(hipEventRecord(ctx->ev_fork2, st));
+      CK(hipStreamWaitEvent(ctx->side, ctx->ev_fork2, 0));
       if (!ctx->launch_bdy(A, ctx->side)) return 0;
       if (ev) CK(hipEventRecord(ev[5], ctx->side));
       CK(hipEventRecord(ctx->ev_join, ctx->side));
     }
-    if (ctx->nq_vol) launch_walk(A, st);
+    if (ctx->nq_vol_ub) launch_walk(A, st);
     if (ev) CK(hipEventRecord(ev[2], st));
-    if (ctx->nq_bdy && !serial) {
+    if (bdy && !serial) {
       CK(hipStreamWaitEvent(st, ctx->ev_join, 0));     // surface path done
-    } else if (ctx->nq_bdy) {
-      if (ev) CK(hipEventRecord(ev[3], st));
+    } else if (bdy) {
       if (!ctx->launch_bdy(A, st)) return 0;
       if (ev) CK(hipEventRecord(ev[5], st));
     } else if (ev) {
-      CK(hipEventRecord(ev[3], st));
       CK(hipEventRecord(ev[5], st));
     }
     if (ev) CK(hipEventRecord(ev[6], st));
     ExhArgs E{};
-    E.xyz = ctx->d_xyz.p; E.tets = ctx->d_tets.p; E.ne = ctx->ne; E.q = ctx->d_q.p;
+    E.xyz = ctx->d_xyz.p; E.tets = ctx->d_tets.p; E.ne = ctx->ne; E.q = ctx->d_qxyz.p;
     E.list = ctx->d_list.p; E.count = ctx->d_counts.p; E.found = ctx->d_found.p;
     E.best = ctx->d_best.p; E.bestk = ctx->d_bestk.p;
     E.spin_limit = (opts.flags & PMX_RUN_DEBUG_BARRIER_TIMEOUT) ? 0L : (1L << 26);
-    if (ctx->nq_vol) launch_exhaustive(E, A, ctx->fallback_blocks, st);
+    if (ctx->nq_vol_ub) launch_exhaustive(E, A, ctx->fallback_blocks, st);
     if (ev) CK(hipEventRecord(ev[4], st));
   } else if (ev) {
     for (int k = 1; k < PMX_EV_PER_RUN; k++)
-      if (k != 7) CK(hipEventRecord(ev[k], st));
+      if (k != 7 && k != 3) CK(hipEventRecord(ev[k], st));
   }
   CK(hipGetLastError());
   ctx->out_S = S;
@@ -924,18 +979,20 @@ int pmx_locate_stats_get(pmx_ctx *ctx, pmx_locate_stats *st) {
   if (!ctx || !st) return 0;
   if (!results_ready(ctx, "pmx_locate_stats_get")) return 0;
   unsigned cnt[8];
+  int nsel[2] = {0, 0};
   CK(hipStreamSynchronize(ctx->stream));
   if (!ctx->check_device_errors()) return 0;
   CK(hipMemcpy(cnt, ctx->d_counts.p, sizeof cnt, hipMemcpyDeviceToHost));
+  if (ctx->nq) CK(hipMemcpy(nsel, ctx->d_nsel.p, sizeof nsel, hipMemcpyDeviceToHost));
   memset(st, 0, sizeof *st);
-  st->nvol = ctx->nq_vol;
-  st->nbdy = ctx->nq_bdy;
+  st->nvol = nsel[0];
+  st->nbdy = nsel[1];
   st->nexhaust = cnt[0] + cnt[1];
   // reduce the per-wave records of both walks
   unsigned long long located = 0, sum = 0;
   unsigned mx = 0, mn = 0xffffffffu;
   for (int path = 0; path < 2; path++) {
-    int64_t npath = path ? ctx->nq_bdy : ctx->nq_vol;
+    int64_t npath = path ? nsel[1] : nsel[0];
     if (!npath) continue;
     std::vector<uint4> w((size_t)((npath + 255) / 256 * 4));
     CK(hipMemcpy(w.data(), path ? ctx->d_bstat.p : ctx->d_vstat.p, w.size() * sizeof(uint4),
@@ -994,6 +1051,15 @@ int pmx_device_free(pmx_ctx *ctx, void *p) {
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
   return (p == nullptr || hipFree(p) == hipSuccess) ? 1 : 0;
+}
+
+int pmx_device_download(pmx_ctx *ctx, void *host, const void *dev, size_t bytes) {
+  if (!ctx) return 0;
+  if (!host || !dev) { ctx->err = "pmx_device_download: null pointer"; return 0; }
+  hipSetDevice(ctx->device);
+  CK(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  return 1;
 }
 
 int64_t pmx_debug_hint_grid(pmx_ctx *ctx, int *host, int64_t cap) {
@@ -1168,7 +1234,7 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
   if (!stage_trias(ctx, m, n, htr)) return 0;
   tr.mark("trias");
   // the background invalid until this completes
-  ctx->have_bg = ctx->have_derived = ctx->have_tetv = ctx->have_qual = ctx->have_ptag = false;
+  ctx->have_bg = ctx->have_derived = ctx->have_tetv = ctx->have_qual = ctx->have_ptag = ctx->have_csr = false;
   ctx->stat_np = -1;
   const int64_t ns = (ne + PMX_HINT_STRIDE - 1) / PMX_HINT_STRIDE;
   if (!dgrow(ctx, ctx->d_xyz, (size_t)(n + 1) * 3) || !dgrow(ctx, ctx->d_sol, (size_t)(n + 1) * std::max(S, 1)) ||
@@ -1178,7 +1244,7 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
     return 0;
   const bool tags = ctx->have_qtag;
   if (tags && !dgrow(ctx, ctx->d_ptag, (size_t)(n + 1))) return 0;
-  launch_promote(ctx->d_q.p, ctx->d_out.p, tags ? ctx->d_qtag.p : nullptr, n, S, ctx->d_xyz.p, ctx->d_sol.p,
+  launch_promote(ctx->d_qxyz.p, ctx->d_out.p, tags ? ctx->d_qtag.p : nullptr, n, S, ctx->d_xyz.p, ctx->d_sol.p,
                  tags ? ctx->d_ptag.p : nullptr, st);
   if (!ent.empty()) {
     if (!dgrow(ctx, ctx->d_pent, ent.size()) || !dgrow(ctx, ctx->d_pval, vals.size())) return 0;
@@ -1215,7 +1281,6 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
   if (!setup_grids(ctx, ctx->qlo, ctx->qhi, ne)) return 0;
   tr.mark("grids");
   CK(hipMemcpyAsync(ctx->d_tris.p, htr.data(), htr.size() * sizeof(TriRec), hipMemcpyHostToDevice, st));
-  if (!ctx->build_node_trias(st)) return 0;
   CK(hipGetLastError());
   CK(hipStreamSynchronize(st));            // host vectors die here
   tr.mark("uploads + sync");
@@ -1229,6 +1294,19 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
 }  // extern "C"
 
 // ---- pmx_ctx members ----------------------------------------------------------
+
+// the new points' classification and compaction on stream s (the marks, if
+// any, zeroed beforehand)
+bool pmx_ctx::classify(hipStream_t s) {
+  if (nq < 1) return true;
+  launch_classify(d_qxyz.p, have_qtag ? d_qtag.p : nullptr, pts_mark ? d_qmark.p : nullptr, nq, d_ctile.p, d_kind.p, d_vollist.p, d_bdylist.p, d_qv.p,
+                  d_nsel.p, s);
+  if (hipGetLastError() != hipSuccess) {
+    err = "classification: launch failed";
+    return false;
+  }
+  return true;
+}
 
 hipEvent_t *pmx_ctx::next_event_slot() {
   size_t need = (size_t)(ev_used + 1) * PMX_EV_PER_RUN;
@@ -1246,9 +1324,9 @@ void pmx_ctx::free_all() {
   if (h_stage) hipHostFree(h_stage);
   h_stage = nullptr;
   h_stage_cap = 0;
-  dfree(d_xyz); dfree(d_tets); dfree(d_sol); dfree(d_tets_s); dfree(d_tris); dfree(d_ntoff);
-  dfree(d_ntlist); dfree(d_ntcur); dfree(d_nttmp); dfree(d_xyzq); dfree(d_trn); dfree(d_grid); dfree(d_tetv);
-  dfree(d_q); dfree(d_kind); dfree(d_wmask); dfree(d_out); dfree(d_elem); dfree(d_status);
+  dfree(d_xyz); dfree(d_tets); dfree(d_sol); dfree(d_tets_s); dfree(d_tris);
+  dfree(d_ntlist); dfree(d_ntval); dfree(d_ntkey); dfree(d_ntrange); dfree(d_nttmp); dfree(d_xyzq); dfree(d_trn); dfree(d_grid); dfree(d_tetv);
+  dfree(d_kind); dfree(d_qmark); dfree(d_ctile); dfree(d_nsel); dfree(d_wmask); dfree(d_out); dfree(d_elem); dfree(d_status);
   dfree(d_steps); dfree(d_start); dfree(d_edge); dfree(d_vertex); dfree(d_list); dfree(d_found);
   dfree(d_bestk); dfree(d_best); dfree(d_ties); dfree(d_counts); dfree(d_vollist); dfree(d_bdylist);
   dfree(d_vstat); dfree(d_bstat); dfree(d_qv);
@@ -1262,7 +1340,7 @@ void pmx_ctx::free_all() {
   if (d_tgrid) hipFree(d_tgrid);
   d_tgrid = nullptr;
   d_tgrid_cap = 0;
-  have_bg = have_pts = ran = have_derived = have_tetv = have_qual = have_ptag = have_qtag = false;
+  have_bg = have_pts = ran = have_derived = have_tetv = have_qual = have_ptag = have_qtag = have_csr = false;
   have_ntet = false;
   stat_np = -1;
 }

@@ -22,7 +22,11 @@ static int constant_metric(pmx_ctx *ctx, const pmx_sol_view *met, int64_t first,
   if (sz != 1 && sz != 6) { ctx->err = "constant size: metric size must be 1 or 6"; return 0; }
   if (!pmx_dgrow(ctx, ctx->d_cmet, (size_t)(n * sz))) return 0;
   hipStream_t s = ctx->stream;
-  if (hipMemsetAsync(ctx->d_wmask.p, 0, (size_t)n, s) != hipSuccess) { ctx->err = "constant size: memset"; return 0; }
+  if (hipMemsetAsync(ctx->d_wmask.p, 0, (size_t)n, s) != hipSuccess) {
+    ctx->err = "constant size: memset";
+    return 0;
+  }
+  if (!ctx->classify(s)) return 0;       // kinds of the new points (NUL rows stay untouched)
   launch_const_metric(ctx->d_kind.p, n, ctx->d_cmet.p, sz, 0, sz, hsiz, ctx->d_wmask.p, 0, s);
   char *st = pmx_hstage(ctx, (size_t)n * sz * sizeof(double) + (size_t)n + 256);
   if (!st) return 0;
@@ -138,29 +142,36 @@ int PMX_interpMetricsAndFields(pmx_ctx *ctx, int ngrp, pmx_group *grps, const in
 // copy of frozen (MG_REQ) points, optionally through the Scotch permutation
 // (PMMG_copySol_point, src/interpmesh_pmmg.c:311-358).  The caller's arrays
 // are host arrays, both sides: a host loop (an O(np) tag scan, REQ rows
-// copied); no device round trip.  The device-resident variant is
-// pmx_copy_required (below).
+// copied); no device round trip, so no context is needed either -- the
+// reference calls it (src/libparmmg1.c:792) before the first interpolation
+// has created one.  ctx may be NULL: errors then go to pmx_last_error(NULL).
+// The device-resident variant is pmx_copy_required (below).
 extern "C" int PMX_copyMetricsAndFields_point(pmx_ctx *ctx, pmx_group *G, const uint16_t *old_tag,
                                               int64_t old_tag_stride, const int *permNodGlob,
                                               int renum, int inputMet) {
-  if (!ctx || !G) return 0;
+  auto fail = [&](const char *msg) {
+    if (ctx) ctx->err = msg;
+    else pmx_set_noctx_error(msg);
+    return 0;
+  };
+  if (!G) return fail("PMX_copyMetricsAndFields_point: null group");
   const int64_t np = G->old_mesh.np;
   std::vector<const pmx_sol_view *> olds, news;
   if (inputMet && G->hsiz <= 0.0 && G->met && G->old_met) {   // :378
     olds.push_back(G->old_met);
     news.push_back(G->met);
   }
+  if (G->nsols < 0 || G->nsols > PMX_MAX_SOLS || (G->nsols > 0 && (!G->fields || !G->old_fields)))
+    return fail("PMX_copyMetricsAndFields_point: bad field list");
   for (int j = 0; j < G->nsols; j++) {
     olds.push_back(&G->old_fields[j]);
     news.push_back(&G->fields[j]);
   }
   if (olds.empty() || np < 1) return 1;
-  if (!old_tag) { ctx->err = "PMX_copyMetricsAndFields_point: old point tags required"; return 0; }
+  if (!old_tag) return fail("PMX_copyMetricsAndFields_point: old point tags required");
   for (size_t k = 0; k < olds.size(); k++)
-    if (!olds[k]->m || olds[k]->size != news[k]->size) {
-      ctx->err = "PMX_copyMetricsAndFields_point: null or mismatched solution";
-      return 0;
-    }
+    if (!olds[k]->m || olds[k]->size != news[k]->size)
+      return fail("PMX_copyMetricsAndFields_point: null or mismatched solution");
   const bool use_perm = renum && permNodGlob;   // :328 (!oldMesh->info.renum || !permNodGlob)
   for (int64_t ip = 1; ip <= np; ip++) {
     const unsigned t = *(const uint16_t *)((const char *)old_tag + ip * old_tag_stride);

@@ -22,7 +22,7 @@ struct pmx_ctx {
   // the surface path runs on `side`, forked after the volume hint build and
   // joined before the fallback: it overlaps the volume walk
   hipStream_t side = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_fork2 = nullptr, ev_join = nullptr;
   hipEvent_t ev_dl[8] = {};             // chunked download: one per chunk
   std::string err;
   int fallback_blocks = 0;              // co-resident k_fallback workgroups
@@ -47,8 +47,13 @@ struct pmx_ctx {
   DevBuf<double> d_sol;
   DevBuf<int4> d_tets_s;                // host-packed hint sample: tets 1, 1+4, 1+8, ...
   DevBuf<TriRec> d_tris;
-  DevBuf<int> d_ntoff, d_ntlist, d_ntcur;   // node -> trias CSR (built on the device)
+  // node -> trias fans (built on the device, in the step): ntlist = trias
+  // sorted by (vertex, index), ntrange[3 k + l] = the run of vertex l of tria k
+  DevBuf<int> d_ntlist, d_ntval;
+  DevBuf<unsigned> d_ntkey;
+  DevBuf<int2> d_ntrange;
   DevBuf<char> d_nttmp;
+  bool have_csr = false;
   // derived from the raw uploads on the device (k_bg_derive), by the first
   // step after an upload or by every step with PMX_RUN_FRESH_BACKGROUND
   bool have_derived = false;
@@ -61,10 +66,12 @@ struct pmx_ctx {
 
   // new points and results
   bool have_pts = false, ran = false;
-  int64_t nq = 0, nq_vol = 0, nq_bdy = 0;
+  int64_t nq = 0;
+  // volume / surface point counts: upper bounds from the host's tag pass
+  // (launch sizes); the exact counts are the step's classification (d_nsel)
+  int64_t nq_vol_ub = 0, nq_bdy_ub = 0;
   int out_S = -1;                       // solution width the results were computed for
   int64_t out_n = -1;                   // point count the results were computed for
-  DevBuf<Pt4> d_q;
   DevBuf<int8_t> d_kind;
   DevBuf<uint8_t> d_wmask;
   DevBuf<double> d_out;
@@ -76,9 +83,9 @@ struct pmx_ctx {
   DevBuf<int> d_vollist, d_bdylist;     // compacted point lists per path
   DevBuf<double> d_qv;                  // volume points, dense xyz in list order
   DevBuf<double> d_qxyz;                // new points as uploaded (dense xyz)
-  DevBuf<uint8_t> d_qmark, d_fvol, d_fbdy;
+  DevBuf<uint8_t> d_qmark;              // orphan marks (points of valid new tets), uploaded when needed
   DevBuf<int> d_nsel;                   // compaction counts: volume, surface
-  DevBuf<char> d_seltmp;
+  DevBuf<int2> d_ctile;                 // classification tile counts
   DevBuf<uint4> d_vstat, d_bstat;       // per-wave walk statistics
   DevBuf<int> d_blist, d_olist, d_ows;
   int *d_tgrid = nullptr;
@@ -129,6 +136,7 @@ struct pmx_ctx {
   bool have_qtag = false;               // raw tags of the new points
   DevBuf<uint16_t> d_qtag;
   int64_t pts_first = 0;                // points view's first index
+  bool pts_mark = false;                // d_qmark holds the host's orphan marks (some point is in no valid new tet)
   DevBuf<double> d_gather;              // all-gathered partials
 
   // timing
@@ -139,6 +147,7 @@ struct pmx_ctx {
   hipEvent_t *next_event_slot();
   void free_all();
   bool build_node_trias(hipStream_t s);   // from d_tris, np, nt (pmx_bdy.hip)
+  bool classify(hipStream_t s);           // the new points: kinds, lists, marks (pmx_capi.hip)
   bool launch_bdy(const VolArgs &a, hipStream_t s);
   bool size_tria_grid();
   // device error word of the last step (after a stream sync): 0 = none
@@ -171,3 +180,5 @@ char *pmx_hstage(pmx_ctx *ctx, size_t bytes);
 bool pmx_ctx_build_adja_device(pmx_ctx *ctx, const int4 *tv, int64_t ne, int64_t np, int *dadja,
                                hipStream_t s, unsigned *h_nbad);
 extern "C" int pmx_timing_reset(pmx_ctx *ctx);
+// error of a call made without a context (pmx_last_error(NULL), per thread)
+void pmx_set_noctx_error(const char *msg);

@@ -19,7 +19,7 @@ struct VolArgs {
   const TetRec *tets;
   const double *sol;
   SolDesc sd;
-  const Pt4 *q;
+  const double *q;              // new points as uploaded, dense x y z (0-based)
   const int8_t *kind;
   int64_t nq, ne;
   const int *grid;
@@ -33,8 +33,9 @@ struct VolArgs {
   unsigned *tie_count;
   int *found, *bestk;
   unsigned long long *best;
-  const int *list;              // indices of the volume points (Morton order kept)
-  int64_t nlist;
+  const int *list;              // indices of the volume points (input order kept)
+  int64_t nlist;                // upper bound (launch size); the step's count is *nlist_dev
+  const int *nlist_dev;
   uint4 *wstats;                // per-wave {located, sum steps, max, min}
   int max_walk;
   unsigned const_bit;           // wmask bit of a constant-size metric (0 if none)
@@ -48,7 +49,7 @@ struct ExhArgs {
   const double *xyz;
   const TetRec *tets;
   int64_t ne;
-  const Pt4 *q;
+  const double *q;
   const int *list;
   const unsigned *count;
   int *found;
@@ -73,19 +74,32 @@ void launch_walk(const VolArgs &a, hipStream_t s);
 void launch_exhaustive(const ExhArgs &e, const VolArgs &v, int blocks, hipStream_t s);
 void launch_const_metric(const int8_t *kind, int64_t nq, double *out, int S, int off, int size,
                          double hsiz, uint8_t *wmask, int imet, hipStream_t s);
-void launch_prologue(uint8_t *wmask, int64_t n, unsigned *counts, int *grid, int64_t gcells,
-                     hipStream_t s);
+// the step's first launch zeroes up to PMX_ZERO_MAX device ranges
+#define PMX_ZERO_MAX 6
+struct ZeroRanges {
+  void *p[PMX_ZERO_MAX];
+  int64_t bytes[PMX_ZERO_MAX];
+  int n;
+  void add(void *ptr, int64_t b) {
+    if (ptr && b > 0) { p[n] = ptr; bytes[n] = b; n++; }
+  }
+};
+void launch_prologue(const ZeroRanges &z, hipStream_t s);
 void launch_tet_conn(const TetRec *src, int64_t n, int4 *dst, hipStream_t s);
 // device residency (pmx_promote_background): new points + results -> background
-void launch_promote(const Pt4 *q, const double *out, const uint16_t *qtag, int64_t n, int S, double *xyz,
+void launch_promote(const double *qxyz, const double *out, const uint16_t *qtag, int64_t n, int S, double *xyz,
                     double *sol, uint16_t *ptag, hipStream_t s);
 void launch_patch_rows(const int4 *ent, const double *vals, int64_t n, int S, double *sol, hipStream_t s);
-// new points on the device: orphan marks from the new tets, kinds, path flags
-void launch_classify_points(const double *xyz, const uint16_t *tag, bool use_mark, const int4 *tv, int64_t ne,
-                            uint8_t *mark, int64_t n, Pt4 *q, int8_t *kind, uint8_t *fvol, uint8_t *fbdy,
-                            hipStream_t s);
-void launch_gather_qv(const double *xyz, const int *list, const int *count, int64_t n, double *qv,
-                      hipStream_t s);
+// new points, every step (the tag dispatch of the reference's vertex loop,
+// src/interpmesh_pmmg.c:541-560): kinds (mark != NULL: the host's orphan
+// marks, 0 = in no valid new tet) and the order-preserving compaction into
+// the volume / surface lists + the volume points' coordinates in list order;
+// counts into nsel[0..1].  tcnt: scratch of cls_tiles(n) int2.
+#define CLS_TILE 4096
+inline int64_t cls_tiles(int64_t n) { return (n + CLS_TILE - 1) / CLS_TILE; }
+void launch_classify(const double *xyz, const uint16_t *tag, const uint8_t *mark, int64_t n, int2 *tcnt,
+                     int8_t *kind, int *vlist, int *blist, double *qv, int *nsel, hipStream_t s);
+
 void launch_build_tetrec(const int4 *tv, const int *adja, int64_t ne, int stride, TetRec *tets, int4 *sample,
                          hipStream_t s);
 // workgroups of k_fallback that can be co-resident with `share` other

@@ -170,8 +170,7 @@ __device__ void d_ties(const VolArgs &A, unsigned bid, unsigned nblk) {
   for (unsigned j = bid * blockDim.x + threadIdx.x; j < n; j += nblk * blockDim.x) {
     int2 e = A.tie_list[j];
     const int64_t i = e.x;
-    Pt4 qq = A.q[i];
-    D3 p{qq.x, qq.y, qq.z};
+    const D3 p = ld3(A.q, (int)i);
     int kc = canonical_tet(A.tets, A.xyz, e.y, p);
     if (kc < 0) {                                   // tie set too large: scan
       unsigned slot = atomicAdd(A.stuck_count, 1u);
@@ -205,10 +204,7 @@ __device__ void d_exh_find(const ExhArgs &A, unsigned bid, unsigned nblk) {
   for (unsigned c0 = 0; c0 < n; c0 += EXH_CHUNK) {
     unsigned m = min((unsigned)EXH_CHUNK, n - c0);
     __syncthreads();
-    for (unsigned j = threadIdx.x; j < m; j += blockDim.x) {
-      Pt4 qq = A.q[A.list[c0 + j]];
-      sp[j] = D3{qq.x, qq.y, qq.z};
-    }
+    for (unsigned j = threadIdx.x; j < m; j += blockDim.x) sp[j] = ld3(A.q, A.list[c0 + j]);
     __syncthreads();
     for (int64_t k = 1 + (int64_t)bid * blockDim.x + threadIdx.x; k <= A.ne;
          k += (int64_t)nblk * blockDim.x) {
@@ -249,8 +245,7 @@ __device__ void d_exh_closest(const ExhArgs &A, int pass, unsigned bid, unsigned
     unsigned m = min((unsigned)EXH_CHUNK, n - c0);
     __syncthreads();
     for (unsigned j = threadIdx.x; j < m; j += blockDim.x) {
-      Pt4 qq = A.q[A.list[c0 + j]];
-      sp[j] = D3{qq.x, qq.y, qq.z};
+      sp[j] = ld3(A.q, A.list[c0 + j]);
       act[j] = (A.found[c0 + j] == 0x7fffffff);
     }
     __syncthreads();
@@ -277,8 +272,7 @@ __device__ void d_exh_finish(const ExhArgs &A, const VolArgs &V, unsigned bid, u
   const unsigned n = *A.count;
   for (unsigned j = bid * blockDim.x + threadIdx.x; j < n; j += nblk * blockDim.x) {
     int64_t i = A.list[j];
-    Pt4 qq = A.q[i];
-    D3 p{qq.x, qq.y, qq.z};
+    const D3 p = ld3(A.q, (int)i);
     int k = A.found[j];
     int st = 1;
     double phi[4];
@@ -417,31 +411,31 @@ void launch_const_metric(const int8_t *kind, int64_t nq, double *out, int S, int
                      size, hsiz, wmask, imet);
 }
 
-// zero the write masks, the step's counters and the hint grid (one launch)
-__global__ __launch_bounds__(256) void k_prologue(uint8_t *wmask, int64_t n, unsigned *counts,
-                                                  int *grid, int64_t gcells) {
+// the step's first launch: zero the write masks, the step's counters, the
+// hint grid, the orphan marks, the node -> trias counts (whichever are given)
+__global__ __launch_bounds__(256) void k_prologue(ZeroRanges z) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
-  if (t < 32) counts[t] = 0;
-  const int64_t n16 = n / 16;
-  for (int64_t i = t; i < n16; i += st) reinterpret_cast<uint4 *>(wmask)[i] = make_uint4(0, 0, 0, 0);
-  for (int64_t i = n16 * 16 + t; i < n; i += st) wmask[i] = 0;
-  if (!grid) return;
-  const int64_t g4 = gcells / 4;
-  for (int64_t i = t; i < g4; i += st) reinterpret_cast<int4 *>(grid)[i] = make_int4(0, 0, 0, 0);
-  for (int64_t i = g4 * 4 + t; i < gcells; i += st) grid[i] = 0;
+  for (int r = 0; r < z.n; r++) {
+    // hipMalloc'd ranges: 256-B aligned starts
+    const int64_t n16 = z.bytes[r] / 16;
+    uint4 *q = reinterpret_cast<uint4 *>(z.p[r]);
+    for (int64_t i = t; i < n16; i += st) q[i] = make_uint4(0, 0, 0, 0);
+    char *c = reinterpret_cast<char *>(z.p[r]);
+    for (int64_t i = n16 * 16 + t; i < z.bytes[r]; i += st) c[i] = 0;
+  }
 }
-void launch_prologue(uint8_t *wmask, int64_t n, unsigned *counts, int *grid, int64_t gcells,
-                     hipStream_t s) {
-  int64_t work = std::max<int64_t>(n / 16, grid ? gcells / 4 : 0);
-  int64_t nb = std::min<int64_t>(std::max<int64_t>((work + 255) / 256, 1), 4096);
-  hipLaunchKernelGGL(k_prologue, dim3((unsigned)nb), dim3(256), 0, s, wmask, n, counts, grid, gcells);
+void launch_prologue(const ZeroRanges &z, hipStream_t s) {
+  int64_t work = 1;
+  for (int r = 0; r < z.n; r++) work = std::max<int64_t>(work, z.bytes[r] / 16);
+  const int64_t nb = std::min<int64_t>(std::max<int64_t>((work + 255) / 256, 1), 4096);
+  hipLaunchKernelGGL(k_prologue, dim3((unsigned)nb), dim3(256), 0, s, z);
 }
 
 // ---- device residency across iterations (pmx_promote_background) ----------------
 
 // the last step's new points and results become the background: vertex ip
 // (1..n) = new point ip-1, its solution row = the step's output row ip-1
-__global__ __launch_bounds__(256) void k_promote(const Pt4 *__restrict__ q, const double *__restrict__ out,
+__global__ __launch_bounds__(256) void k_promote(const double *__restrict__ q, const double *__restrict__ out,
                                                  const uint16_t *__restrict__ qtag, int64_t n, int S,
                                                  double *__restrict__ xyz, double *__restrict__ sol,
                                                  uint16_t *__restrict__ ptag) {
@@ -453,10 +447,9 @@ __global__ __launch_bounds__(256) void k_promote(const Pt4 *__restrict__ q, cons
       if (ptag) ptag[0] = 0;
       continue;
     }
-    const Pt4 p = q[ip - 1];
-    xyz[3 * ip] = p.x;
-    xyz[3 * ip + 1] = p.y;
-    xyz[3 * ip + 2] = p.z;
+    xyz[3 * ip] = q[3 * (ip - 1)];
+    xyz[3 * ip + 1] = q[3 * (ip - 1) + 1];
+    xyz[3 * ip + 2] = q[3 * (ip - 1) + 2];
     for (int j = 0; j < S; j++) sol[ip * S + j] = out[(ip - 1) * S + j];
     if (ptag) ptag[ip] = qtag[ip - 1];
   }
@@ -486,7 +479,7 @@ __global__ __launch_bounds__(256) void k_build_tetrec(const int4 *__restrict__ t
     if (k >= 1 && (k - 1) % stride == 0) sample[(k - 1) / stride] = v;
   }
 }
-void launch_promote(const Pt4 *q, const double *out, const uint16_t *qtag, int64_t n, int S, double *xyz,
+void launch_promote(const double *q, const double *out, const uint16_t *qtag, int64_t n, int S, double *xyz,
                     double *sol, uint16_t *ptag, hipStream_t s) {
   const int64_t nb = std::min<int64_t>(std::max<int64_t>((n + 256) / 256, 1), 16384);
   hipLaunchKernelGGL(k_promote, dim3((unsigned)nb), dim3(256), 0, s, q, out, qtag, n, S, xyz, sol, ptag);
@@ -504,68 +497,113 @@ void launch_build_tetrec(const int4 *tv, const int *adja, int64_t ne, int stride
 
 // ---- new points: classification on the device (pmx_upload_points) ---------------
 
-// the points of the valid new tets (the reference's vertex loop over the new
-// tets, src/interpmesh_pmmg.c:535-541); vertex j+1 = point j
-__global__ __launch_bounds__(256) void k_mark_tets(const int4 *__restrict__ tv, int64_t ne,
-                                                   uint8_t *__restrict__ mark) {
-  for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= ne;
-       k += (int64_t)gridDim.x * blockDim.x) {
-    const int4 t = tv[k];
-    if (t.x <= 0) continue;                      // !MG_EOK
-    mark[t.x - 1] = 1;
-    mark[t.y - 1] = 1;
-    mark[t.z - 1] = 1;
-    mark[t.w - 1] = 1;
-  }
+// kind of a new point (PMMG_interpMetricsAndFields_mesh's dispatch, :541-560)
+__device__ __forceinline__ int point_kind(const uint16_t *__restrict__ tag, const uint8_t *__restrict__ mark,
+                                          int64_t j) {
+  const unsigned t = tag ? tag[j] : 0u;
+  if (t >= PMX_TAG_NUL) return KIND_NUL;                  // !MG_VOK
+  if (mark && !mark[j]) return KIND_ORPH;                 // in no valid new tet
+  if (t & PMX_TAG_REQ) return KIND_SKIP;
+  if (t & PMX_TAG_BDY) return KIND_BDY;
+  return KIND_VOL;
 }
-// kind of every new point (PMMG_interpMetricsAndFields_mesh's dispatch,
-// :541-560) + the per-path flags for the order-preserving compaction
-__global__ __launch_bounds__(256) void k_classify(const double *__restrict__ xyz, const uint16_t *__restrict__ tag,
-                                                  const uint8_t *__restrict__ mark, int64_t n, Pt4 *__restrict__ q,
-                                                  int8_t *__restrict__ kind, uint8_t *__restrict__ fvol,
-                                                  uint8_t *__restrict__ fbdy) {
-  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
-    q[j] = Pt4{xyz[3 * j], xyz[3 * j + 1], xyz[3 * j + 2], 0.0};
-    const unsigned t = tag ? tag[j] : 0u;
-    int8_t kd;
-    if (t >= PMX_TAG_NUL) kd = KIND_NUL;                  // !MG_VOK
-    else if (mark && !mark[j]) kd = KIND_ORPH;            // in no valid new tet
-    else if (t & PMX_TAG_REQ) kd = KIND_SKIP;
-    else if (t & PMX_TAG_BDY) kd = KIND_BDY;
-    else kd = KIND_VOL;
-    kind[j] = kd;
-    fvol[j] = kd == KIND_VOL;
-    fbdy[j] = kd == KIND_BDY;
+
+// sum over the 256-thread block, in every thread (red: 4 LDS slots)
+__device__ __forceinline__ int2 block_sum2(int2 v, int2 *red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    v.x += __shfl_xor(v.x, o, 64);
+    v.y += __shfl_xor(v.y, o, 64);
   }
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int2 r = red[0];
+#pragma unroll
+  for (int w = 1; w < 4; w++) { r.x += red[w].x; r.y += red[w].y; }
+  return r;
 }
-// the volume points' coordinates once more, dense and in list order: the
-// walks read them coalesced, without a list -> point gather
-__global__ __launch_bounds__(256) void k_gather_qv(const double *__restrict__ xyz, const int *__restrict__ list,
-                                                   const int *__restrict__ count, double *__restrict__ qv) {
-  const int64_t nv = count[0];
-  for (int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; a < nv; a += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t j = list[a];
-    qv[3 * a] = xyz[3 * j];
-    qv[3 * a + 1] = xyz[3 * j + 1];
-    qv[3 * a + 2] = xyz[3 * j + 2];
+
+// per tile of CLS_TILE points: how many volume / surface points
+__global__ __launch_bounds__(256) void k_cls_count(const uint16_t *__restrict__ tag, const uint8_t *__restrict__ mark,
+                                                   int64_t n, int2 *__restrict__ tcnt) {
+  __shared__ int2 red[4];
+  const int64_t t0 = (int64_t)blockIdx.x * CLS_TILE;
+  int cv = 0, cb = 0;
+  for (int r = 0; r < CLS_TILE / 256; r++) {
+    const int64_t j = t0 + r * 256 + threadIdx.x;
+    if (j >= n) break;
+    const int k = point_kind(tag, mark, j);
+    cv += k == KIND_VOL;
+    cb += k == KIND_BDY;
   }
+  const int2 c = block_sum2(make_int2(cv, cb), red);
+  if (threadIdx.x == 0) tcnt[blockIdx.x] = c;
 }
-void launch_classify_points(const double *xyz, const uint16_t *tag, bool use_mark, const int4 *tv, int64_t ne,
-                            uint8_t *mark, int64_t n, Pt4 *q, int8_t *kind, uint8_t *fvol, uint8_t *fbdy,
-                            hipStream_t s) {
-  if (use_mark) {                                // new tets given (possibly none)
-    hipMemsetAsync(mark, 0, (size_t)n, s);
-    if (ne > 0) {
-      const int64_t nb = std::min<int64_t>((ne + 255) / 256, 16384);
-      hipLaunchKernelGGL(k_mark_tets, dim3((unsigned)nb), dim3(256), 0, s, tv, ne, mark);
+
+// kinds + the two lists in input order (wave ballots, tile base = sum of the
+// previous tiles' counts, summed again by every workgroup: a few KB of L2
+// reads instead of a third launch) + the volume points' coordinates in list
+// order (the walk reads them coalesced)
+__global__ __launch_bounds__(256) void k_cls_write(const double *__restrict__ xyz, const uint16_t *__restrict__ tag,
+                                                   const uint8_t *__restrict__ mark, int64_t n,
+                                                   const int2 *__restrict__ tcnt, int8_t *__restrict__ kind,
+                                                   int *__restrict__ vlist, int *__restrict__ blist,
+                                                   double *__restrict__ qv, int *__restrict__ nsel) {
+  __shared__ int2 red[4];
+  __shared__ int2 wc[4];
+  int pv = 0, pb = 0;
+  for (unsigned t = threadIdx.x; t < blockIdx.x; t += 256) {
+    const int2 c = tcnt[t];
+    pv += c.x;
+    pb += c.y;
+  }
+  int2 base = block_sum2(make_int2(pv, pb), red);
+  const int64_t t0 = (int64_t)blockIdx.x * CLS_TILE;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (int r = 0; r < CLS_TILE / 256; r++) {
+    const int64_t j = t0 + r * 256 + threadIdx.x;
+    int k = -1;
+    if (j < n) {
+      k = point_kind(tag, mark, j);
+      kind[j] = (int8_t)k;
     }
+    const unsigned long long bv = __ballot(k == KIND_VOL), bb = __ballot(k == KIND_BDY);
+    __syncthreads();                                      // wc of the last round read
+    if (lane == 0) wc[w] = make_int2(__popcll(bv), __popcll(bb));
+    __syncthreads();
+    int ov = base.x, ob = base.y;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int2 c = wc[q];
+      ov += q < w ? c.x : 0;
+      ob += q < w ? c.y : 0;
+      base.x += c.x;
+      base.y += c.y;
+    }
+    if (k == KIND_VOL) {
+      const int pos = ov + __popcll(bv & below);
+      vlist[pos] = (int)j;
+      qv[3 * (int64_t)pos] = xyz[3 * j];
+      qv[3 * (int64_t)pos + 1] = xyz[3 * j + 1];
+      qv[3 * (int64_t)pos + 2] = xyz[3 * j + 2];
+    } else if (k == KIND_BDY) {
+      blist[ob + __popcll(bb & below)] = (int)j;
+    }
+    if (t0 + (r + 1) * 256 >= n) break;                   // uniform: the tile's end
   }
-  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 16384));
-  hipLaunchKernelGGL(k_classify, dim3((unsigned)nb), dim3(256), 0, s, xyz, tag, use_mark ? mark : nullptr, n, q,
-                     kind, fvol, fbdy);
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+    nsel[0] = base.x;
+    nsel[1] = base.y;
+  }
 }
-void launch_gather_qv(const double *xyz, const int *list, const int *count, int64_t n, double *qv,
-                      hipStream_t s) {
-  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 16384));
-  hipLaunchKernelGGL(k_gather_qv, dim3((unsigned)nb), dim3(256), 0, s, xyz, list, count, qv);
+
+void launch_classify(const double *xyz, const uint16_t *tag, const uint8_t *mk, int64_t n, int2 *tcnt,
+                     int8_t *kind, int *vlist, int *blist, double *qv, int *nsel, hipStream_t s) {
+  if (n < 1) return;
+  const unsigned nt = (unsigned)cls_tiles(n);
+  hipLaunchKernelGGL(k_cls_count, dim3(nt), dim3(256), 0, s, tag, mk, n, tcnt);
+  hipLaunchKernelGGL(k_cls_write, dim3(nt), dim3(256), 0, s, xyz, tag, mk, n, (const int2 *)tcnt, kind, vlist,
+                     blist, qv, nsel);
 }

@@ -821,11 +821,30 @@ int pmx_upload_point_tags(pmx_ctx *ctx, const uint16_t *tag, int64_t stride) {
   return 1;
 }
 
-int pmx_tetra_qual(pmx_ctx *ctx, double *qual) {
+// MMG3D_tetraQual(mesh, met, metRidTyp) (src/quality_pmmg.c:726): metRidTyp
+// selects Mmg's ridge-metric storage.  For a size-1 metric (or none) both
+// values take the same isotropic arithmetic and are accepted; for a size-6
+// metric only the classic storage (0) is restated -- 1 needs the ridge points'
+// normals (xPoint), which the ABI does not carry: refused, not approximated.
+static bool check_met_rid_typ(pmx_ctx *ctx, int metRidTyp, int msize, const char *who) {
+  if (metRidTyp != 0 && metRidTyp != 1) {
+    ctx->err = std::string(who) + ": metRidTyp must be 0 or 1";
+    return false;
+  }
+  if (metRidTyp == 1 && msize == 6) {
+    ctx->err = std::string(who) + ": metRidTyp = 1 with an anisotropic metric (Mmg's ridge metric storage, "
+                                  "needs the xPoint normals) is not supported";
+    return false;
+  }
+  return true;
+}
+
+int pmx_tetra_qual(pmx_ctx *ctx, int metRidTyp, double *qual) {
   if (!ctx) return 0;
   hipSetDevice(ctx->device);
   StatArgs A;
   if (!stat_args(ctx, A)) return 0;
+  if (!check_met_rid_typ(ctx, metRidTyp, A.msize, "pmx_tetra_qual")) return 0;
   if (!pmx_dgrow(ctx, ctx->d_qual, (size_t)(ctx->ne + 1))) return 0;
   if (A.msize == 6)
     hipLaunchKernelGGL((k_qual<true, false>), dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
@@ -895,6 +914,16 @@ int pmx_count_nodes(pmx_ctx *ctx, const int *idx_ip, const int *idx_comm, int64_
 
 int pmx_qualhisto_device(pmx_ctx *ctx, int opt, int use_stored, void *dev_result) {
   if (!ctx || !dev_result) return 0;
+  if (opt == PMX_LESQUA) {
+    // MMG3D_computeLESqua (src/quality_pmmg.c:221-224, selected at run time by
+    // mesh->info.optimLES): Mmg's LES quality is not restated here
+    ctx->err = "pmx_qualhisto: the optimLES quality (MMG3D_computeLESqua) is not supported";
+    return 0;
+  }
+  if (opt != PMX_INQUA && opt != PMX_OUTQUA) {
+    ctx->err = "pmx_qualhisto: opt must be PMX_INQUA, PMX_OUTQUA or PMX_LESQUA";
+    return 0;
+  }
   hipSetDevice(ctx->device);
   StatArgs A;
   if (!stat_args(ctx, A)) return 0;
@@ -919,13 +948,14 @@ int pmx_qualhisto(pmx_ctx *ctx, int opt, pmx_qual_stats *st) {
 }
 
 int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, void *dev_result) {
-  // classic metric storage only (size 1 or 6 on every point); Mmg's ridge
-  // metric storage (metRidTyp = 1) is refused, not approximated
-  if (metRidTyp != 0) {
-    if (ctx) ctx->err = "pmx_prilen: metRidTyp = 1 (ridge metric storage) is not supported";
-    return 0;
-  }
+  // metRidTyp (src/quality_pmmg.c:462,527): 0 or 1 give the same lengths for a
+  // size-1 metric (MMG5_lenedg = lenedg_iso, MMG5_lenSurfEdg_iso); with a
+  // size-6 metric 1 selects Mmg's ridge storage: refused, not approximated
   if (!ctx || !dev_result) return 0;
+  if (ctx->have_bg && ctx->sd.imet >= 0 &&
+      !check_met_rid_typ(ctx, metRidTyp, ctx->sd.size[ctx->sd.imet], "pmx_prilen"))
+    return 0;
+  if (metRidTyp != 0 && metRidTyp != 1) { ctx->err = "pmx_prilen: metRidTyp must be 0 or 1"; return 0; }
   hipSetDevice(ctx->device);
   StatArgs A;
   if (!stat_args(ctx, A)) return 0;
@@ -1021,7 +1051,7 @@ int pmx_prilen(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, pmx_len_st
 }
 
 int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, int64_t ne, int opt,
-                      double *qual, void *dev_result) {
+                      int metRidTyp, double *qual, void *dev_result) {
   if (!ctx) return 0;
   hipSetDevice(ctx->device);
   if (!ctx->ran || !ctx->have_pts || ctx->out_n != ctx->nq) {
@@ -1041,8 +1071,8 @@ int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, in
   hipStream_t s = ctx->stream;
   if (!pmx_dgrow(ctx, ctx->d_nqual, (size_t)(ne + 1))) return 0;
   StatArgs A{};
-  A.xyz = reinterpret_cast<const double *>(ctx->d_q.p);   // Pt4 {x, y, z, 0}
-  A.xstride = 4;
+  A.xyz = ctx->d_qxyz.p;                  // the new points, dense x y z
+  A.xstride = 3;
   A.vbase = 1;
   A.tetv = ctx->d_ntetv.p;
   A.ne = ne;
@@ -1053,6 +1083,12 @@ int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, in
   A.msize = ctx->sd.imet >= 0 ? ctx->sd.size[ctx->sd.imet] : 0;
   A.moff = ctx->sd.imet >= 0 ? ctx->sd.off[ctx->sd.imet] : 0;
   A.ptag = (opt == PMX_OUTQUA && ctx->have_qtag) ? ctx->d_qtag.p : nullptr;
+  if (!check_met_rid_typ(ctx, metRidTyp, A.msize, "pmx_new_mesh_qual")) return 0;
+  if (dev_result && opt != PMX_INQUA && opt != PMX_OUTQUA) {
+    ctx->err = opt == PMX_LESQUA ? "pmx_new_mesh_qual: the optimLES quality (MMG3D_computeLESqua) is not supported"
+                                 : "pmx_new_mesh_qual: opt must be PMX_INQUA or PMX_OUTQUA";
+    return 0;
+  }
   const int nb = stat_blocks(ne);
   if (A.msize == 6)
     hipLaunchKernelGGL((k_qual<true, false>), dim3(nb), dim3(256), 0, s, A, ctx->d_nqual.p, (QualPart *)nullptr, 0);

@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void k_walk(VolArgs A) {
   const int64_t j = b * blockDim.x + threadIdx.x;
   unsigned s_cnt = 0, s_sum = 0, s_max = 0, s_min = 0xffffffffu;
 
-  if (j < A.nlist) {
+  if (j < *A.nlist_dev) {     // the step's count (the grid is sized by an upper bound)
     const int64_t i = A.list[j];
     const D3 p{A.qv[3 * j], A.qv[3 * j + 1], A.qv[3 * j + 2]};
     int cur = walk_hint(A.grid, A.g, p);
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
   const int64_t j = b * blockDim.x + threadIdx.x;
   unsigned s_cnt = 0, s_sum = 0, s_max = 0, s_min = 0xffffffffu;
 
-  if (j < A.nlist) {
+  if (j < *A.nlist_dev) {     // the step's count (the grid is sized by an upper bound)
     // list order == Morton order of the volume points: both reads coalesced
     // and independent (no list -> point dependent gather)
     const int64_t i = A.list[j];

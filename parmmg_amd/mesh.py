@@ -130,6 +130,59 @@ def new_points(n: int, seed: int = 12345, jitter: float = 0.3, surface: bool = T
     return xyz, tag.astype(np.uint16)
 
 
+def new_point_tets(n: int, xyz: np.ndarray, tag: np.ndarray) -> np.ndarray:
+    """Tets over the new points of new_points(n) in Mmg's layout ((ne+1, 4),
+    1-based point indices, row 0 unused), for the reference's vertex loop
+    over the new mesh's tets (src/interpmesh_pmmg.c:535-541): a Kuhn mesh of
+    the lattice of cell-centre points (6 (n-1)^3 tets, cells in Morton order
+    like the points: one space-filling numbering of both, as a Scotch
+    renumbering gives) plus one tet per surface point joining it to the
+    adjacent centres.
+    Every point is in a tet (no orphans); the tets only enumerate vertices,
+    they are not a conforming mesh of the surface layer."""
+    x = np.asarray(xyz)
+    ijk = np.clip(np.floor(x * n).astype(np.int64), 0, n - 1)
+    bdy = (np.asarray(tag) & TAG_BDY) != 0
+    vol = ~bdy
+    idx = np.zeros((n, n, n), np.int64)
+    vi = np.nonzero(vol)[0]
+    idx[ijk[vi, 0], ijk[vi, 1], ijk[vi, 2]] = vi + 1
+    c = np.arange(n - 1)
+    I, J, K = np.meshgrid(c, c, c, indexing="ij")
+    I, J, K = I.ravel(), J.ravel(), K.ravel()
+    code = np.zeros(len(I), np.int64)
+    for b in range(12):
+        code |= (((I >> b) & 1) << (3 * b)) | (((J >> b) & 1) << (3 * b + 1)) | (((K >> b) & 1) << (3 * b + 2))
+    o = np.argsort(code, kind="stable")
+    I, J, K = I[o], J[o], K[o]
+    e = np.eye(3, dtype=np.int64)
+    tets = []
+    for perm in ((0, 1, 2), (0, 2, 1), (1, 0, 2), (1, 2, 0), (2, 0, 1), (2, 1, 0)):
+        p = np.stack([I, J, K], 1)
+        vs = [idx[p[:, 0], p[:, 1], p[:, 2]]]
+        for a in perm:
+            p = p + e[a]
+            vs.append(idx[p[:, 0], p[:, 1], p[:, 2]])
+        tets.append(np.stack(vs, 1))
+    kt = np.stack(tets, 1).reshape(-1, 4)          # the 6 tets of a cell together
+    bi = np.nonzero(bdy)[0]
+    b = ijk[bi]
+    on = np.argmax((x[bi] == 0.0) | (x[bi] == 1.0), axis=1)   # the face's normal axis
+    tt = [bi + 1]
+    for d in range(3):
+        p = b.copy()
+        if d > 0:
+            ax = (on + d) % 3
+            r = np.arange(len(bi))
+            p[r, ax] = np.where(p[r, ax] < n - 1, p[r, ax] + 1, p[r, ax] - 1)
+        tt.append(idx[p[:, 0], p[:, 1], p[:, 2]])
+    st = np.stack(tt, 1)
+    out = np.zeros((1 + len(kt) + len(st), 4), np.int32)
+    out[1:1 + len(kt)] = kt
+    out[1 + len(kt):] = st
+    return out
+
+
 def count_inverted(m: Mesh) -> int:
     return int(_meshgen().pmg_count_inverted(m.ne, _p(m.xyz), _p(m.tet)))
 

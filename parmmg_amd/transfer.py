@@ -314,9 +314,10 @@ class Transfer:
         self._chk(self.lib.pmx_upload_point_tags(self.ctx, t.ctypes.data_as(N.u16ptr) if t is not None
                                                  else None, 2), "pmx_upload_point_tags")
 
-    def tetra_qual(self, ne: int) -> np.ndarray:
+    def tetra_qual(self, ne: int, met_rid_typ: int = 0) -> np.ndarray:
+        """MMG3D_tetraQual(mesh, met, metRidTyp) of the uploaded group."""
         q = np.zeros(ne + 1)
-        self._chk(self.lib.pmx_tetra_qual(self.ctx, _dp(q)), "pmx_tetra_qual")
+        self._chk(self.lib.pmx_tetra_qual(self.ctx, met_rid_typ, _dp(q)), "pmx_tetra_qual")
         return q
 
     def count_nodes(self, idx_ip=None, idx_comm=None, intvalues=None, base: int = 1) -> int:
@@ -405,14 +406,16 @@ class Transfer:
                   "pmx_promote_background")
         self.npts = 0
 
-    def new_mesh_qual(self, tets: np.ndarray | None, opt: int = N.INQUA, dev_ptr: int = 0) -> np.ndarray:
+    def new_mesh_qual(self, tets: np.ndarray | None, opt: int = N.INQUA, dev_ptr: int = 0,
+                      met_rid_typ: int = 0) -> np.ndarray:
         """PMMG_tetraQual on the new mesh after the last step: tets (ne+1, 4)
         with indices of the uploaded points (0-based here, v[0] < 0: deleted);
         None: the tets of the last upload_new_tets."""
         tv = _tets_1based(tets) if tets is not None else None
         q = np.zeros((tv.shape[0] if tv is not None else self.n_new_tets + 1))
         self._chk(self.lib.pmx_new_mesh_qual(self.ctx, _ip(tv), 16, tv.shape[0] - 1 if tv is not None else 0,
-                                             opt, _dp(q), C.c_void_p(dev_ptr or None)), "pmx_new_mesh_qual")
+                                             opt, met_rid_typ, _dp(q), C.c_void_p(dev_ptr or None)),
+                  "pmx_new_mesh_qual")
         if tv is not None:
             self.n_new_tets = tv.shape[0] - 1
         return q

@@ -113,7 +113,7 @@ int main(void) {
   CK(pmx_comm_init(ctx, &comm, 1, id, 0));
   void *d = NULL;
   if (!(d = pmx_device_alloc(ctx, sizeof(pmx_qual_part)))) { fprintf(stderr, "%s\n", pmx_last_error(ctx)); return 1; }
-  CK(pmx_new_mesh_qual(ctx, NULL, 0, 0, PMX_INQUA, NULL, d));
+  CK(pmx_new_mesh_qual(ctx, NULL, 0, 0, PMX_INQUA, 1, NULL, d));
   CK(pmx_qualhisto_allreduce(ctx, comm, 1, d, 1, &qs));
   if (qs.ne != m2.ne || qs.np != m2.np || qs.min <= 0.0 || qs.max > 1.0 + 1e-12) {
     fprintf(stderr, "new-mesh statistics: ne %lld np %lld min %g max %g\n", (long long)qs.ne,

@@ -1,0 +1,158 @@
+"""integration/pmmg_pmx.c -- ParMmg's own seams with their exact reference
+signatures (src/parmmg.h:472-473,564-566) over the C ABI -- compiled as C99
+against a test-local parmmg.h (tests/c/pmmg_stub/) and driven by
+tests/c/adapter_demo.c in the reference's call order of one iteration:
+copy (src/libparmmg1.c:792, before any device context exists) -> interp
+(:829) -> tetraQual(parmesh, 1) (:845) -> qualhisto OUTQUA (:910) ->
+prilen(parmesh, 1, 0) (:964), then the centralized input-side calls
+(src/libparmmg.c:175,185).  Results against the oracle."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from helpers import compare_volume
+from oracle import oracle as O
+from parmmg_amd import mesh as M
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = [os.path.join(ROOT, "integration", "pmmg_pmx.c"), os.path.join(ROOT, "tests", "c", "adapter_demo.c")]
+BIN = os.path.join(ROOT, "tests", "c", "_build", "adapter_demo")
+
+
+def build_adapter_demo(extra=()) -> str:
+    from parmmg_amd import build
+    lib = build.build_transfer()
+    os.makedirs(os.path.dirname(BIN), exist_ok=True)
+    out = BIN + "".join(extra).replace("-", "_").replace("=", "_")
+    deps = SRC + [os.path.join(ROOT, "include", "pmx_transfer.h"),
+                  os.path.join(ROOT, "tests", "c", "pmmg_stub", "parmmg.h"), lib]
+    if not os.path.exists(out) or any(os.path.getmtime(d) > os.path.getmtime(out) for d in deps):
+        subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-O1", *extra,
+                        "-I", os.path.join(ROOT, "tests", "c", "pmmg_stub"), "-I", os.path.join(ROOT, "include"),
+                        *SRC, "-L", os.path.dirname(lib), "-lpmx_transfer",
+                        f"-Wl,-rpath,{os.path.dirname(lib)}", "-o", out], check=True)
+    return out
+
+
+def test_adapter_compiles_as_c():
+    """The exact-signature adapter compiles as C99 (-Wall -Wextra -Werror) and
+    links against the library (no GPU needed)."""
+    assert os.path.exists(build_adapter_demo())
+
+
+def write_case(d, metric="iso", n=6, n2=7):
+    """A background group (Kuhn cube n) and a new mesh (Kuhn cube n2, another
+    jitter) in Mmg's layout; a few background vertices MG_REQ (frozen: the new
+    mesh keeps them, same index and position) and a few boundary ridge points."""
+    old = M.kuhn_cube(n, seed=3)
+    new = M.kuhn_cube(n2, seed=4)
+    otag = np.zeros(old.np + 1, np.uint16)
+    onb = np.any((old.xyz[1:] == 0.0) | (old.xyz[1:] == 1.0), axis=1)
+    otag[1:][onb] = M.TAG_BDY
+    req = np.arange(1, min(old.np, new.np) + 1, 13)
+    otag[req] |= M.TAG_REQ
+    ntag = np.zeros(new.np + 1, np.uint16)
+    nnb = np.any((new.xyz[1:] == 0.0) | (new.xyz[1:] == 1.0), axis=1)
+    ntag[1:][nnb] = M.TAG_BDY
+    ntag[1:][nnb & (np.sum((new.xyz[1:] == 0.0) | (new.xyz[1:] == 1.0), axis=1) >= 2)] |= 2   # MG_GEO ridges
+    ntag[req] = otag[req]
+    nxyz = new.xyz.copy()
+    nxyz[req] = old.xyz[req]
+    f = M.shock_metric if metric == "ani" else M.iso_metric
+    omet = M.on_vertices(old, f)
+    ofld = M.on_vertices(old, M.level_set)
+    files = dict(old_xyz=old.xyz, old_tet=old.tet, old_tag=otag, old_met=omet, old_fld=ofld,
+                 new_xyz=nxyz, new_tet=new.tet, new_tag=ntag)
+    for k, a in files.items():
+        np.ascontiguousarray(a).tofile(os.path.join(d, k + ".bin"))
+    with open(os.path.join(d, "sizes.txt"), "w") as fh:
+        fh.write(f"{old.np} {old.ne} {new.np} {new.ne} {omet.shape[1]} {ofld.shape[1]}\n")
+    return old, new, otag, ntag, nxyz, omet, ofld, req
+
+
+def run_demo(d, mode):
+    r = subprocess.run([build_adapter_demo(), d, mode], capture_output=True, text=True, timeout=300)
+    recs = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    return r, recs
+
+
+@pytest.mark.gpu
+def test_adapter_reference_call_order(tmp_path):
+    d = str(tmp_path)
+    old, new, otag, ntag, nxyz, omet, ofld, req = write_case(d, "iso")
+    r, recs = run_demo(d, "full")
+    assert r.returncode == 0, r.stdout + r.stderr
+    calls = {c["call"]: c["ret"] for c in recs if "call" in c}
+    assert calls == {"copy": 1, "interp": 1, "tetraqual": 1, "qualhisto_out": 1, "prilen_1_dist": 1,
+                     "qualhisto_in": 1, "prilen_0_central": 1}, calls
+    met = np.fromfile(os.path.join(d, "out_met.bin")).reshape(new.np + 1, 1)
+    fld = np.fromfile(os.path.join(d, "out_fld.bin")).reshape(new.np + 1, 1)
+    qual = np.fromfile(os.path.join(d, "out_qual.bin"))
+    # frozen points: the old values (the copy), untouched by the interpolation
+    assert np.array_equal(met[req], omet[req]) and np.array_equal(fld[req], ofld[req])
+    # the interpolation against the oracle: volume points bit-exact or ties
+    o = O.Oracle(old)
+    x, t = nxyz[1:], ntag[1:]
+    outs, elem, st, *_ = o.interp(x, t, [omet, ofld], imet=0)
+    from parmmg_amd.transfer import Transfer
+    tr = Transfer(0)
+    tr.upload_background(old, [omet, ofld], 0)
+    tr.upload_points(x, t, tets_mmg=new.tet)
+    tr.run()
+    g = tr.download()
+    tr.close()
+    live = (t & M.TAG_REQ) == 0
+    assert np.array_equal(g.sols[0][live], met[1:][live]) and np.array_equal(g.sols[1][live], fld[1:][live])
+    c = compare_volume(o, x, t, ([met[1:], fld[1:]], g.elem, g.status), (outs, elem, st), [omet, ofld])
+    assert c["same"] >= c["nvol"] - 3
+    # tetraQual(parmesh, 1) on the new mesh in its interpolated metric:
+    # iso, so metRidTyp 1 == 0 (the oracle's MMG3D_tetraQual restatement)
+    mesh_new = M.Mesh(nxyz, new.tet, new.adja, new.tria, new.adjt)
+    qo = O.tetra_qual(mesh_new, None)
+    assert np.array_equal(qual[1:], qo[1:])
+    # qualhisto (OUTQUA, nrid from the ridge tags) and prilen vs the oracle
+    qh = [c["qualhisto"] for c in recs if "qualhisto" in c]
+    pl = [c["prilen"] for c in recs if "prilen" in c]
+    assert len(qh) == 2 and len(pl) == 2
+    ref_out = O.qualhisto(mesh_new, qo, tags=ntag)
+    ref_in = O.qualhisto(mesh_new, qo)
+    for got, ref in ((qh[0], ref_out), (qh[1], ref_in)):
+        for k in ("ne", "good", "med", "his", "nrid"):
+            assert got[k] == (list(ref[k]) if k == "his" else ref[k]), (k, got[k], ref[k])
+        assert got["min"] == ref["min"] and got["max"] == ref["max"]
+        assert abs(got["avg"] - ref["avg"]) <= 1e-12 * abs(ref["avg"])
+    lo = O.prilen(mesh_new, met, tags=ntag)
+    for p in pl:
+        assert p["ned"] == lo["ned"] and p["nullEdge"] == lo["nullEdge"]
+        assert sum(abs(a - b) for a, b in zip(p["hl"], lo["hl"])) <= 2
+        assert p["lmin"] == pytest.approx(lo["lmin"], rel=1e-15) and p["lmax"] == pytest.approx(lo["lmax"], rel=1e-15)
+
+
+@pytest.mark.gpu
+def test_adapter_refuses_ani_ridge_metric(tmp_path):
+    """metRidTyp = 1 with an anisotropic metric (Mmg's ridge metric storage,
+    needs the xPoint normals): PMMG_tetraQual and PMMG_prilen fail loudly;
+    metRidTyp = 0 succeeds."""
+    d = str(tmp_path)
+    write_case(d, "ani")
+    r, recs = run_demo(d, "refuse_ani")
+    assert r.returncode == 0, r.stdout + r.stderr
+    calls = {c["call"]: c["ret"] for c in recs if "call" in c}
+    assert calls["tetraqual_ani_1"] == 0 and calls["prilen_ani_1"] == 0 and calls["tetraqual_ani_0"] == 1
+    assert "metRidTyp = 1 with an anisotropic metric" in r.stderr
+
+
+@pytest.mark.gpu
+def test_adapter_refuses_optimles(tmp_path):
+    """mesh->info.optimLES (a run-time flag, src/quality_pmmg.c:221-224):
+    MMG3D_computeLESqua is not restated, PMMG_qualhisto fails loudly."""
+    d = str(tmp_path)
+    write_case(d, "iso")
+    r, recs = run_demo(d, "refuse_les")
+    assert r.returncode == 0, r.stdout + r.stderr
+    calls = {c["call"]: c["ret"] for c in recs if "call" in c}
+    assert calls["qualhisto_les"] == 0
+    assert "optimLES" in r.stderr

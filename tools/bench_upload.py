@@ -26,7 +26,7 @@ def main():
     from parmmg_amd import mesh as M
     from parmmg_amd.transfer import Transfer
     cfg = bench.CONFIGS[args.config]
-    m, _, _, sols = bench.build_case(cfg, 0)
+    m, _, _, sols, _ = bench.build_case(cfg, 0)
     mb = M.kuhn_cube(cfg["n"], seed=777)
     x = mb.xyz[1:]
     onb = np.any((x == 0.0) | (x == 1.0), axis=1)

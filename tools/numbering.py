@@ -72,7 +72,7 @@ def main():
     cfg = dict(bench.CONFIGS[args.config])
     if args.n:
         cfg["n"] = args.n
-    m, x, t, sols = bench.build_case(cfg, 0)
+    m, x, t, sols, _ = bench.build_case(cfg, 0)
     rng = np.random.default_rng(7)
     trs, back = {}, {}
     for v in args.variants.split(","):

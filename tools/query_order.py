@@ -29,7 +29,7 @@ def main():
     build.build_transfer()
     from parmmg_amd.transfer import Transfer
     cfg = dict(bench.CONFIGS[args.config])
-    m, x, t, sols = bench.build_case(cfg, 0)
+    m, x, t, sols, _ = bench.build_case(cfg, 0)
     n = cfg["n"]
     c = np.clip((x * n).astype(np.int64), 0, n - 1)
     orders = {"morton": np.arange(len(x)),

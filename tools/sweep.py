@@ -34,7 +34,7 @@ def main():
     cfg = dict(bench.CONFIGS[args.config])
     if args.n:
         cfg["n"] = args.n
-    m, x, t, sols = bench.build_case(cfg, 0)
+    m, x, t, sols, _ = bench.build_case(cfg, 0)
     tr = Transfer(0)
     tr.upload_background(m, sols, 0)
     tr.upload_points(x, t)

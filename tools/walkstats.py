@@ -27,7 +27,7 @@ def main():
     build.build_transfer()
     from parmmg_amd.transfer import Transfer
     cfg = bench.CONFIGS[args.config]
-    m, x, t, sols = bench.build_case(cfg, 0)
+    m, x, t, sols, _ = bench.build_case(cfg, 0)
     tr = Transfer(0)
     tr.upload_background(m, sols, 0)
     tr.upload_points(x, t)

@@ -258,16 +258,21 @@ typedef struct {
 } pmx_medit_info;
 const char *pmx_medit_last_error(void);
 int pmx_medit_mesh_info(const char *path, pmx_medit_info *info);
-/* xyz[3*(np+1)], tet[4*(ne+1)] required; vref[np+1], tetref[ne+1],
+/* sized = the counts the arrays were allocated for (pmx_medit_mesh_info of
+ * the same file): the read fails, writing nothing past them, if the file's
+ * counts differ (changed file) or a keyword block appears twice.
+ * xyz[3*(np+1)], tet[4*(ne+1)] required; vref[np+1], tetref[ne+1],
  * tria[3*(nt+1)], triaref[nt+1], req[nreq] may be NULL */
-int pmx_medit_mesh_read(const char *path, double *xyz, int *vref, int *tet, int *tetref, int *tria,
-                        int *triaref, int *req);
+int pmx_medit_mesh_read(const char *path, const pmx_medit_info *sized, double *xyz, int *vref, int *tet,
+                        int *tetref, int *tria, int *triaref, int *req);
 int pmx_medit_mesh_write(const char *path, int64_t np, const double *xyz, const int *vref, int64_t ne,
                          const int *tet, const int *tetref, int64_t nt, const int *tria, const int *triaref,
                          int64_t nreq, const int *req);
 /* solutions at vertices: types 1 scalar, 2 vector (3), 3 symmetric tensor (6) */
 int pmx_medit_sol_info(const char *path, int64_t *np, int *nsol, int *types);
-int pmx_medit_sol_read(const char *path, double **fields);   /* fields[s]: size*(np+1) */
+/* fields[s]: size(types[s])*(np+1); np, nsol, types = what the fields were
+ * sized for (pmx_medit_sol_info): a different header fails the read */
+int pmx_medit_sol_read(const char *path, int64_t np, int nsol, const int *types, double **fields);
 int pmx_medit_sol_write(const char *path, int64_t np, int nsol, const int *types,
                         const double *const *fields);
 

@@ -173,11 +173,11 @@ SIGNATURES = {
     "pmx_prilen_allreduce": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.POINTER(LenStats)]),
     "pmx_medit_last_error": (C.c_char_p, []),
     "pmx_medit_mesh_info": (C.c_int, [C.c_char_p, C.POINTER(MeditInfo)]),
-    "pmx_medit_mesh_read": (C.c_int, [C.c_char_p, dptr, iptr, iptr, iptr, iptr, iptr, iptr]),
+    "pmx_medit_mesh_read": (C.c_int, [C.c_char_p, C.POINTER(MeditInfo), dptr, iptr, iptr, iptr, iptr, iptr, iptr]),
     "pmx_medit_mesh_write": (C.c_int, [C.c_char_p, i64, dptr, iptr, i64, iptr, iptr, i64, iptr, iptr,
                                        i64, iptr]),
     "pmx_medit_sol_info": (C.c_int, [C.c_char_p, C.POINTER(i64), C.POINTER(C.c_int), iptr]),
-    "pmx_medit_sol_read": (C.c_int, [C.c_char_p, C.POINTER(dptr)]),
+    "pmx_medit_sol_read": (C.c_int, [C.c_char_p, i64, C.c_int, iptr, C.POINTER(dptr)]),
     "pmx_medit_sol_write": (C.c_int, [C.c_char_p, i64, C.c_int, iptr, C.POINTER(dptr)]),
 }
 

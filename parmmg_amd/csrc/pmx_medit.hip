@@ -120,12 +120,14 @@ struct Text {
 struct Bin {
   FILE *f = nullptr;
   int ver = 0;
+  long size = 0;
   ~Bin() {
     if (f) fclose(f);
   }
   bool open(const char *path) {
     f = fopen(path, "rb");
     if (!f) return false;
+    if (fseek(f, 0, SEEK_END) != 0 || (size = ftell(f)) < 8 || fseek(f, 0, SEEK_SET) != 0) return false;
     int32_t code = 0, v = 0;
     if (fread(&code, 4, 1, f) != 1 || fread(&v, 4, 1, f) != 1) return false;
     if (code != 1) return false;                 // other endianness: not supported
@@ -163,6 +165,9 @@ struct Bin {
     }
     return fread(&x, 8, 1, f) == 1;
   }
+  // the next block's absolute position must move forward and stay in the
+  // file (a malformed position would loop or re-read blocks)
+  bool next_ok(int64_t next, long at) const { return next <= 0 || (next > at && next <= size); }
 };
 
 struct BinOut {
@@ -170,6 +175,13 @@ struct BinOut {
   int ver = 0;
   ~BinOut() {
     if (f) fclose(f);
+  }
+  // flush and close, reporting buffered data that could not be written
+  bool close() {
+    const bool good = fflush(f) == 0 && !ferror(f);
+    const bool closed = fclose(f) == 0;
+    f = nullptr;
+    return good && closed;
   }
   void i32(int32_t x) { fwrite(&x, 4, 1, f); }
   void integer(int64_t x) {
@@ -208,9 +220,29 @@ struct MeshOut {
   int *vref, *tet, *tetref, *tria, *triaref, *req;
 };
 
-int read_mesh(const char *path, pmx_medit_info *info, const MeshOut *out) {
+// a keyword block's count: each keyword at most once, and in the read pass
+// the count the caller's arrays were sized from (pmx_medit_mesh_info)
+bool block_count(const char *kw, int64_t n, int64_t *slot, bool *seen, const pmx_medit_info *expect,
+                 int64_t expected) {
+  if (*seen) return fail(std::string("duplicate ") + kw + " block");
+  *seen = true;
+  *slot = n;
+  if (expect && n != expected)
+    return fail(std::string(kw) + " count differs from the one the arrays were sized for");
+  return true;
+}
+
+int read_mesh(const char *path, pmx_medit_info *info, const MeshOut *out, const pmx_medit_info *expect) {
   pmx_medit_info I{};
   I.dim = 3;
+  bool seen[4] = {false, false, false, false};
+  auto count_of = [&](const char *name, int64_t n) -> bool {
+    const std::string k(name);
+    if (k == "Vertices") return block_count(name, n, &I.np, &seen[0], expect, expect ? expect->np : 0);
+    if (k == "Tetrahedra") return block_count(name, n, &I.ne, &seen[1], expect, expect ? expect->ne : 0);
+    if (k == "Triangles") return block_count(name, n, &I.nt, &seen[2], expect, expect ? expect->nt : 0);
+    return block_count(name, n, &I.nreq, &seen[3], expect, expect ? expect->nreq : 0);
+  };
   if (is_binary(path)) {
     Bin b;
     if (!b.open(path)) return fail(std::string("cannot open or not a native-endian .meshb: ") + path);
@@ -218,7 +250,9 @@ int read_mesh(const char *path, pmx_medit_info *info, const MeshOut *out) {
     for (;;) {
       int32_t kw;
       int64_t next;
+      const long at = ftell(b.f);
       if (!b.i32(kw) || !b.pos(next)) return fail("truncated .meshb");
+      if (!b.next_ok(next, at)) return fail("bad .meshb block position");
       if (kw == KW_END) break;
       if (kw == KW_DIM) {
         int32_t d;
@@ -228,10 +262,9 @@ int read_mesh(const char *path, pmx_medit_info *info, const MeshOut *out) {
       } else if (kw == KW_VERT || kw == KW_TET || kw == KW_TRI || kw == KW_REQV) {
         int64_t n;
         if (!b.count(n) || n < 0) return fail("bad .meshb count");
-        if (kw == KW_VERT) I.np = n;
-        if (kw == KW_TET) I.ne = n;
-        if (kw == KW_TRI) I.nt = n;
-        if (kw == KW_REQV) I.nreq = n;
+        if (!count_of(kw == KW_VERT ? "Vertices" : kw == KW_TET ? "Tetrahedra" : kw == KW_TRI ? "Triangles"
+                                                                                   : "RequiredVertices", n))
+          return 0;
         if (out) {
           for (int64_t k = 1; k <= n; k++) {
             int64_t x, ref = 0;
@@ -282,10 +315,7 @@ int read_mesh(const char *path, pmx_medit_info *info, const MeshOut *out) {
       } else if (kw == "Vertices" || kw == "Tetrahedra" || kw == "Triangles" || kw == "RequiredVertices") {
         if (!t.integer(n) || n < 0) return fail("bad count after " + kw);
         const int nv = kw == "Vertices" ? 0 : kw == "Tetrahedra" ? 4 : kw == "Triangles" ? 3 : 1;
-        if (kw == "Vertices") I.np = n;
-        if (kw == "Tetrahedra") I.ne = n;
-        if (kw == "Triangles") I.nt = n;
-        if (kw == "RequiredVertices") I.nreq = n;
+        if (!count_of(kw.c_str(), n)) return 0;
         for (int64_t k = 1; k <= n; k++) {
           int64_t x, ref = 0;
           if (nv == 0) {
@@ -315,6 +345,9 @@ int read_mesh(const char *path, pmx_medit_info *info, const MeshOut *out) {
       }
     }
   }
+  // a block the arrays were sized for that the file no longer holds
+  if (expect && (I.np != expect->np || I.ne != expect->ne || I.nt != expect->nt || I.nreq != expect->nreq))
+    return fail("mesh counts differ from the ones the arrays were sized for");
   if (info) *info = I;
   return 1;
 }
@@ -324,7 +357,15 @@ struct SolIn {
   int nsol = 0, types[PMX_MAX_SOLS] = {0}, version = 0;
 };
 
-int read_sol(const char *path, SolIn &S, double **fields) {
+// the read pass: the header must be the one the fields were sized for
+bool sol_header_ok(const SolIn &S, const SolIn *expect) {
+  if (!expect) return true;
+  bool same = S.np == expect->np && S.nsol == expect->nsol;
+  for (int s = 0; same && s < S.nsol; s++) same = S.types[s] == expect->types[s];
+  return same ? true : fail("SolAtVertices header differs from the one the fields were sized for");
+}
+
+int read_sol(const char *path, SolIn &S, double **fields, const SolIn *expect) {
   auto store = [&](int64_t k, int s, int j, double v) {
     const int sz = type_size(S.types[s]);
     const int jj = sz == 6 ? tensor_perm(j) : j;
@@ -338,12 +379,15 @@ int read_sol(const char *path, SolIn &S, double **fields) {
     for (;;) {
       int32_t kw;
       int64_t next;
+      const long at = ftell(b.f);
       if (!b.i32(kw) || !b.pos(next)) return fail("truncated .solb");
+      if (!b.next_ok(next, at)) return fail("bad .solb block position");
       if (kw == KW_END) break;
       if (kw == KW_DIM) {
         int32_t d;
         if (!b.i32(d) || d != 3) return fail("only 3-D solutions");
       } else if (kw == KW_SOLV) {
+        if (found) return fail("duplicate SolAtVertices block");
         int64_t n;
         int32_t nt;
         if (!b.count(n) || !b.i32(nt) || nt < 1 || nt > PMX_MAX_SOLS) return fail("bad SolAtVertices header");
@@ -355,6 +399,7 @@ int read_sol(const char *path, SolIn &S, double **fields) {
           S.types[s] = ty;
         }
         found = true;
+        if (!sol_header_ok(S, expect)) return 0;
         if (fields) {
           for (int64_t k = 1; k <= n; k++)
             for (int s = 0; s < nt; s++)
@@ -392,6 +437,7 @@ int read_sol(const char *path, SolIn &S, double **fields) {
         if (!t.integer(ty) || !type_size((int)ty)) return fail("unsupported solution type");
         S.types[s] = (int)ty;
       }
+      if (!sol_header_ok(S, expect)) return 0;
       if (!fields) return 1;
       for (int64_t k = 1; k <= n; k++)
         for (int s = 0; s < S.nsol; s++)
@@ -416,14 +462,14 @@ const char *pmx_medit_last_error(void) { return g_err.c_str(); }
 
 int pmx_medit_mesh_info(const char *path, pmx_medit_info *info) {
   if (!path || !info) return fail("pmx_medit_mesh_info: null argument");
-  return read_mesh(path, info, nullptr);
+  return read_mesh(path, info, nullptr, nullptr);
 }
 
-int pmx_medit_mesh_read(const char *path, double *xyz, int *vref, int *tet, int *tetref, int *tria,
-                        int *triaref, int *req) {
-  if (!path || !xyz || !tet) return fail("pmx_medit_mesh_read: null argument");
+int pmx_medit_mesh_read(const char *path, const pmx_medit_info *sized, double *xyz, int *vref, int *tet,
+                        int *tetref, int *tria, int *triaref, int *req) {
+  if (!path || !sized || !xyz || !tet) return fail("pmx_medit_mesh_read: null argument");
   MeshOut o{xyz, vref, tet, tetref, tria, triaref, req};
-  return read_mesh(path, nullptr, &o);
+  return read_mesh(path, nullptr, &o, sized);
 }
 
 int pmx_medit_mesh_write(const char *path, int64_t np, const double *xyz, const int *vref, int64_t ne,
@@ -472,7 +518,7 @@ int pmx_medit_mesh_write(const char *path, int64_t np, const double *xyz, const 
     }
     at = b.begin(KW_END, false, 0);
     (void)at;                                    // End: next position 0
-    if (ferror(b.f)) return fail(std::string("write error: ") + path);
+    if (!b.close()) return fail(std::string("write error: ") + path);
     return 1;
   }
   FILE *f = fopen(path, "w");
@@ -494,15 +540,15 @@ int pmx_medit_mesh_write(const char *path, int64_t np, const double *xyz, const 
     for (int64_t k = 0; k < nreq; k++) fprintf(f, "%d\n", req[k]);
   }
   fprintf(f, "\nEnd\n");
-  const bool bad = ferror(f) != 0;
-  fclose(f);
+  bool bad = fflush(f) != 0 || ferror(f) != 0;
+  bad = fclose(f) != 0 || bad;
   return bad ? fail(std::string("write error: ") + path) : 1;
 }
 
 int pmx_medit_sol_info(const char *path, int64_t *np, int *nsol, int *types) {
   if (!path || !np || !nsol) return fail("pmx_medit_sol_info: null argument");
   SolIn S;
-  if (!read_sol(path, S, nullptr)) return 0;
+  if (!read_sol(path, S, nullptr, nullptr)) return 0;
   *np = S.np;
   *nsol = S.nsol;
   if (types)
@@ -510,10 +556,14 @@ int pmx_medit_sol_info(const char *path, int64_t *np, int *nsol, int *types) {
   return 1;
 }
 
-int pmx_medit_sol_read(const char *path, double **fields) {
-  if (!path || !fields) return fail("pmx_medit_sol_read: null argument");
-  SolIn S;
-  return read_sol(path, S, fields);
+int pmx_medit_sol_read(const char *path, int64_t np, int nsol, const int *types, double **fields) {
+  if (!path || !fields || !types || nsol < 1 || nsol > PMX_MAX_SOLS || np < 0)
+    return fail("pmx_medit_sol_read: bad arguments");
+  SolIn E, S;
+  E.np = np;
+  E.nsol = nsol;
+  for (int s = 0; s < nsol; s++) E.types[s] = types[s];
+  return read_sol(path, S, fields, &E);
 }
 
 int pmx_medit_sol_write(const char *path, int64_t np, int nsol, const int *types, const double *const *fields) {
@@ -544,7 +594,7 @@ int pmx_medit_sol_write(const char *path, int64_t np, int nsol, const int *types
       }
     b.end(at);
     b.begin(KW_END, false, 0);
-    if (ferror(b.f)) return fail(std::string("write error: ") + path);
+    if (!b.close()) return fail(std::string("write error: ") + path);
     return 1;
   }
   FILE *f = fopen(path, "w");
@@ -564,8 +614,8 @@ int pmx_medit_sol_write(const char *path, int64_t np, int nsol, const int *types
     fprintf(f, "\n");
   }
   fprintf(f, "\nEnd\n");
-  const bool bad = ferror(f) != 0;
-  fclose(f);
+  bool bad = fflush(f) != 0 || ferror(f) != 0;
+  bad = fclose(f) != 0 || bad;
   return bad ? fail(std::string("write error: ") + path) : 1;
 }
 

@@ -51,8 +51,8 @@ def read_mesh(path: str) -> MeditMesh:
     tria = np.zeros((info.nt + 1, 3), np.int32)
     triaref = np.zeros(info.nt + 1, np.int32)
     req = np.zeros(max(info.nreq, 1), np.int32)
-    if not lib.pmx_medit_mesh_read(path.encode(), xyz.ctypes.data_as(N.dptr), _ip(vref), _ip(tet), _ip(tetref),
-                                   _ip(tria), _ip(triaref), _ip(req)):
+    if not lib.pmx_medit_mesh_read(path.encode(), C.byref(info), xyz.ctypes.data_as(N.dptr), _ip(vref), _ip(tet),
+                                   _ip(tetref), _ip(tria), _ip(triaref), _ip(req)):
         _err("pmx_medit_mesh_read")
     return MeditMesh(xyz, vref, tet, tetref, tria, triaref, req[: info.nreq], info.version)
 
@@ -81,7 +81,7 @@ def read_sol(path: str) -> list[np.ndarray]:
         _err("pmx_medit_sol_info")
     out = [np.zeros((n.value + 1, _SIZE[types[s]])) for s in range(nsol.value)]
     ptrs = (N.dptr * len(out))(*[a.ctypes.data_as(N.dptr) for a in out])
-    if not lib.pmx_medit_sol_read(path.encode(), ptrs):
+    if not lib.pmx_medit_sol_read(path.encode(), n, nsol, types, ptrs):
         _err("pmx_medit_sol_read")
     return out
 

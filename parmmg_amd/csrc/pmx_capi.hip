@@ -30,6 +30,12 @@
 
 // errors of the calls that work without a context (per host thread)
 static thread_local std::string noctx_err;
+
+// live contexts per device in this process (the fallback grids share the GPU)
+static std::atomic<int> &live_contexts(int device) {
+  static std::atomic<int> n[64];
+  return n[device & 63];
+}
 void pmx_set_noctx_error(const char *msg) { noctx_err = msg; }
 
 static bool ok(pmx_ctx *c, hipError_t e, const char *what) {
@@ -248,6 +254,9 @@ static bool setup_grids(pmx_ctx *ctx, const double lo[3], const double hi[3], in
     int d = (int)std::ceil(ext[a] / h * (1.0 - 1e-9));
     d = std::max(1, std::min(d, 4096));
     g.dim[a] = d;
+    int bits = 0;
+    while ((1 << bits) < d) bits++;
+    g.qf[a] = 21 - bits;
     g.lo[a] = lo[a];
     g.inv[a] = (double)d / ext[a];
     cells *= d;
@@ -290,9 +299,14 @@ pmx_ctx *pmx_create(int device) {
     return nullptr;
   }
   // the fallback's grid barrier needs every workgroup resident at once: size
-  // its grid from the occupancy query, leaving room for a second context's
-  // fallback on the same GPU (ParMmg groups of one rank, C4: 2 per GPU)
-  ctx->fallback_blocks = fallback_coresident_blocks(device, 2);
+  // its grid from the occupancy query, sharing the GPU with every live
+  // context of this process (at least two: ParMmg groups of one rank, C4: 2
+  // per GPU, PMX_interpMetricsAndFields' peer); re-sized in pmx_run when
+  // contexts come and go.  Contexts of other processes on the same GPU are
+  // not counted: one rank per GPU is the supported deployment.
+  live_contexts(device)++;
+  ctx->fallback_share = std::max(2, live_contexts(device).load());
+  ctx->fallback_blocks = fallback_coresident_blocks(device, ctx->fallback_share);
   if (ctx->fallback_blocks < 1) {
     pmx_destroy(ctx);
     return nullptr;
@@ -302,6 +316,7 @@ pmx_ctx *pmx_create(int device) {
 
 void pmx_destroy(pmx_ctx *ctx) {
   if (!ctx) return;
+  if (ctx->fallback_share > 0) live_contexts(ctx->device)--;
   if (ctx->peer) pmx_destroy(ctx->peer);
   ctx->peer = nullptr;
   hipSetDevice(ctx->device);
@@ -778,6 +793,9 @@ static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &o
   A.qv = ctx->d_qv.p;
   A.ref_walk = (opts.flags & PMX_RUN_REFERENCE_WALK) ? 1 : 0;
   A.rec_start = (opts.flags & PMX_RUN_RECORD_STARTS) ? 1 : 0;
+  A.xyzq = ctx->d_xyzq.p;
+  A.exp = (opts.flags >> PMX_RUN_EXP_SHIFT) & 0xff;
+  A.qguard = 5.e-3f;
 }
 
 int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
@@ -878,6 +896,13 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     E.list = ctx->d_list.p; E.count = ctx->d_counts.p; E.found = ctx->d_found.p;
     E.best = ctx->d_best.p; E.bestk = ctx->d_bestk.p;
     E.spin_limit = (opts.flags & PMX_RUN_DEBUG_BARRIER_TIMEOUT) ? 0L : (1L << 26);
+    const int share = std::max(2, live_contexts(ctx->device).load());
+    if (share != ctx->fallback_share) {
+      const int fb = fallback_coresident_blocks(ctx->device, share);
+      if (fb < 1) { ctx->err = "pmx_run: occupancy query failed"; return 0; }
+      ctx->fallback_blocks = fb;
+      ctx->fallback_share = share;
+    }
     if (ctx->nq_vol_ub) launch_exhaustive(E, A, ctx->fallback_blocks, st);
     if (ev) CK(hipEventRecord(ev[4], st));
   } else if (ev) {
@@ -1186,6 +1211,23 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
       ctx->err = "pmx_promote_background: solution size differs from the step's";
       return 0;
     }
+  if (m->adja) {
+    // the walks gather through these: every neighbour of a valid tet must
+    // name a face of 1..ne (as pmx_upload_background checks)
+    bool badj = false;
+    par_chunks(1, ne + 1, [&](int, int64_t k0, int64_t k1) {
+      bool b = false;
+      for (int64_t k = k0; k < k1 && !b; k++) {
+        if (m->tetra_v && *(const int *)((const char *)m->tetra_v + k * m->tetra_stride) <= 0) continue;
+        for (int f = 0; f < 4; f++) {
+          const int a = m->adja[4 * (k - 1) + 1 + f];
+          if (a < 0 || a / 4 > ne) b = true;
+        }
+      }
+      if (b) __atomic_store_n(&badj, true, __ATOMIC_RELAXED);
+    });
+    if (badj) { ctx->err = "pmx_promote_background: adjacency entry out of range"; return 0; }
+  }
   hipSetDevice(ctx->device);
   Trace tr("promote");
   hipStream_t st = ctx->stream;

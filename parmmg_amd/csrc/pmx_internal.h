@@ -15,6 +15,8 @@ template <class T> struct DevBuf {
 // hint grid from every 4th tet: 1/4 of the stores and of the tet bytes of a
 // full build, at ~0.5 extra walk step (r01 measurements)
 #define PMX_HINT_STRIDE 4
+// pmx_run_opts.flags bits 16-23: walk experiment selector (tools/sweep.py only)
+#define PMX_RUN_EXP_SHIFT 16
 
 struct pmx_ctx {
   int device = 0;
@@ -26,6 +28,7 @@ struct pmx_ctx {
   hipEvent_t ev_dl[8] = {};             // chunked download: one per chunk
   std::string err;
   int fallback_blocks = 0;              // co-resident k_fallback workgroups
+  int fallback_share = 0;               // live contexts on the device they were sized for
   // PMX_interpMetricsAndFields: a second context on the same device, groups
   // alternate between the two (created on first use, destroyed with this one)
   pmx_ctx *peer = nullptr;

@@ -6,6 +6,8 @@ struct GridDesc {
   int dim[3];
   double lo[3];
   double inv[3];
+  int qf[3];        // fraction bits of the fixed-point grid coordinates:
+                    // dim << qf fits 21 bits (qf = 21 - ceil(log2 dim))
 };
 
 // counters of one step (d_counts, zeroed by the prologue):
@@ -43,6 +45,9 @@ struct VolArgs {
   const double *qv;             // coordinates of the volume points in list order (xyz, 24 B)
   int ref_walk;                 // 1: k_walk (reference-order walk) instead of k_walks
   int rec_start;                // write the start tet of every point (diagnostics)
+  const unsigned long long *xyzq; // fixed-point grid coordinates of the old vertices
+  int exp;                      // experiment selector (tools/sweep.py), 0 = production
+  float qguard;                 // fixed-point walk: candidate when lambda_min > -qguard
 };
 
 struct ExhArgs {
@@ -58,8 +63,6 @@ struct ExhArgs {
   long spin_limit;              // grid-barrier poll budget (debug: 0 forces a timeout)
 };
 
-// fraction bits of the fixed-point grid coordinates (dim <= 4096: 12 + 9 = 21 bits)
-#define HINT_QF 9
 // volume hint grid from every stride-th tet: `packed` = the host-packed
 // connectivity of tets 1, 1+stride, ... (stride == PMX_HINT_STRIDE), else the
 // tet records are read strided
@@ -123,4 +126,6 @@ struct StatArgs {
   const unsigned long long *par_key;
   int64_t npar;
   const uint8_t *par_pt;
+  int order;                    // k_qual tet order (experiment): 0 contiguous per block,
+                                // 1 chip-wide sliding window of 256-tet chunks, 2 per-XCD window
 };

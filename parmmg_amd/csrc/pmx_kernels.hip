@@ -26,9 +26,10 @@ __device__ __forceinline__ int clampi(double t, int n) {
 
 // ---- per-background derived data -----------------------------------------------
 
-// grid coordinates of the vertices in fixed point for k_hint_build:
-// q = (x - lo) * inv * 2^HINT_QF, clamped to [0, dim * 2^HINT_QF - 1], packed
-// x | y << 21 | z << 42; and the tria normals + areas
+// grid coordinates of the vertices in fixed point (k_hint_build's centroids,
+// the fixed-point walk of k_walkq): q = (x - lo) * inv * 2^qf, clamped to
+// [0, dim * 2^qf - 1] (21 bits per axis), packed x | y << 21 | z << 42; and
+// the tria normals + areas
 __global__ __launch_bounds__(256) void k_bg_derive(const double *__restrict__ xyz, int64_t np, GridDesc g,
                                                    unsigned long long *__restrict__ q,
                                                    const TriRec *__restrict__ tris, int64_t nt,
@@ -39,8 +40,8 @@ __global__ __launch_bounds__(256) void k_bg_derive(const double *__restrict__ xy
     unsigned long long r = 0;
 #pragma unroll
     for (int a = 0; a < 3; a++) {
-      const double t = (c[a] - g.lo[a]) * g.inv[a] * (double)(1 << HINT_QF);
-      const long long hi = ((long long)g.dim[a] << HINT_QF) - 1;
+      const double t = (c[a] - g.lo[a]) * g.inv[a] * (double)(1 << g.qf[a]);
+      const long long hi = ((long long)g.dim[a] << g.qf[a]) - 1;
       const long long u = !(t > 0.0) ? 0 : (t >= (double)hi ? hi : (long long)t);
       r |= (unsigned long long)u << (21 * a);
     }
@@ -91,7 +92,7 @@ __global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ pac
     const int sh = 21 * ax;
     const unsigned s4 = (unsigned)((a >> sh) & M) + (unsigned)((b >> sh) & M) +
                         (unsigned)((c >> sh) & M) + (unsigned)((d >> sh) & M);
-    cq[ax] = min((int)(s4 >> (HINT_QF + 2)), g.dim[ax] - 1);
+    cq[ax] = min((int)(s4 >> (g.qf[ax] + 2)), g.dim[ax] - 1);
   }
   grid[(int64_t)cq[0] + (int64_t)g.dim[0] * ((int64_t)cq[1] + (int64_t)g.dim[1] * cq[2])] = (int)k;
 }

@@ -158,12 +158,16 @@ __device__ __forceinline__ void qual_init(QualPart &p) {
 // ANI: the metric is a 6-component tensor (compiled apart: the iso variant
 // does not carry the tensor path's registers).  OUT: MMG3D_computeOutqua's
 // count of tets with 4 ridge vertices.
+// Each workgroup takes a contiguous tet range, 256 tets per iteration, the
+// next iteration's connectivity loaded before this one's vertex gathers (two
+// dependent levels in flight).  Counts are wave-uniform (ballot + popcount,
+// scalar registers); sum and extrema per lane, reduced by a fixed shuffle
+// tree and the 4 waves in order (deterministic), so the workgroup needs no
+// 256-entry LDS reduction buffer (occupancy no longer LDS-bound).
 template <bool ANI, bool OUT>
 __global__ __launch_bounds__(256) void k_qual(StatArgs A, double *qual, QualPart *parts,
                                               int use_stored) {
-  __shared__ QualPart sh[256];
-  // thread-local accumulators with 32-bit counts (a thread sees < 2^32 tets):
-  // half the registers of QualPart's 64-bit fields
+  __shared__ QualPart sh[4];
   double avg = 0.0, qmax = 0.0, qmin = 2.0;
   long long iel = 0x7fffffffffffffffLL;
   unsigned cne = 0, cgood = 0, cmed = 0, cnrid = 0, chis[5] = {0, 0, 0, 0, 0};
@@ -171,45 +175,72 @@ __global__ __launch_bounds__(256) void k_qual(StatArgs A, double *qual, QualPart
   // the next z-layer's points (another chunk) are in its own L2
   const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
   const int64_t per = (A.ne + gridDim.x - 1) / gridDim.x;
-  const int64_t k0 = 1 + lb * per, k1 = min(A.ne, k0 + per - 1);
-  for (int64_t k = k0 + threadIdx.x; k <= k1; k += blockDim.x) {
-    // 16-B connectivity stream: the neighbours are not needed here
-    const int4 cv = A.tetv[k];
+  int64_t k0 = 1 + lb * per, k1 = min(A.ne, k0 + per - 1), kstep = blockDim.x;
+  if (A.order == 1) {            // chunk blockIdx.x, + gridDim.x, ...: the chip sweeps one window
+    k0 = 1 + (int64_t)blockIdx.x * blockDim.x;
+    k1 = A.ne;
+    kstep = (int64_t)gridDim.x * blockDim.x;
+  } else if (A.order == 2) {     // each XCD sweeps its contiguous eighth with its own window
+    const int64_t x = blockIdx.x & 7, r = blockIdx.x >> 3, R = gridDim.x >> 3;
+    const int64_t eighth = (A.ne + 7) / 8;
+    k0 = 1 + x * eighth + r * blockDim.x;
+    k1 = min(A.ne, x * eighth + eighth);
+    kstep = R * blockDim.x;
+  }
+  // 16-B connectivity stream: the neighbours are not needed here
+  int4 cv = (k0 + (int64_t)threadIdx.x <= k1) ? A.tetv[k0 + threadIdx.x] : make_int4(0, 0, 0, 0);
+  for (int64_t kb = k0; kb <= k1; kb += kstep) {   // uniform over the block
+    const int64_t k = kb + threadIdx.x;
+    const bool in = k <= k1;
     const int v[4] = {cv.x, cv.y, cv.z, cv.w};
-    if (v[0] <= 0) {                      // !MG_EOK: no quality (0, not a stale value)
-      if (!use_stored && qual) qual[k] = 0.0;
-      continue;
+    const int64_t kn = k + kstep;
+    if (kn <= k1) cv = A.tetv[kn];
+    const bool valid = in && v[0] > 0;
+    // !MG_EOK: no quality (0, not a stale value)
+    if (in && !valid && !use_stored && qual) qual[k] = 0.0;
+    double rap = 0.0;
+    if (valid) {
+      const double q = use_stored ? qual[k] : tet_quality<ANI>(A, v);
+      if (!use_stored && qual) qual[k] = q;
+      rap = ALPHAD * q;
+      if (rap < qmin || (rap == qmin && k < iel)) { qmin = rap; iel = k; }
+      avg += rap;
+      qmax = fmax(qmax, rap);
     }
-    double q = use_stored ? qual[k] : tet_quality<ANI>(A, v);
-    if (!use_stored && qual) qual[k] = q;
     if (!parts) continue;
-    double rap = ALPHAD * q;
-    cne++;
-    if (OUT && tet_4ridge(A, v)) cnrid++;
-    if (rap < qmin || (rap == qmin && k < iel)) { qmin = rap; iel = k; }
-    if (rap > 0.5) cmed++;
-    if (rap > 0.12) cgood++;
-    avg += rap;
-    qmax = fmax(qmax, rap);
+    cne += (unsigned)__popcll(__ballot(valid));
+    cgood += (unsigned)__popcll(__ballot(valid && rap > 0.12));
+    cmed += (unsigned)__popcll(__ballot(valid && rap > 0.5));
+    if (OUT) cnrid += (unsigned)__popcll(__ballot(valid && tet_4ridge(A, v)));
     int ir = (int)(5.0 * rap);
     ir = ir < 4 ? ir : 4;
-    // predicated, static indices: the histogram stays in VGPRs (no scratch)
 #pragma unroll
-    for (int i = 0; i < 5; i++) chis[i] += (i == ir) ? 1u : 0u;
+    for (int i = 0; i < 5; i++) chis[i] += (unsigned)__popcll(__ballot(valid && ir == i));
   }
   if (!parts) return;
-  QualPart p;
-  p.avg = avg; p.max = qmax; p.min = qmin; p.iel = iel;
-  p.ne = cne; p.good = cgood; p.med = cmed; p.nrid = cnrid;
+  // the same tree on every lane (the lower lane's value first)
 #pragma unroll
-  for (int i = 0; i < 5; i++) p.his[i] = chis[i];
-  sh[threadIdx.x] = p;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) qual_merge(sh[threadIdx.x], sh[threadIdx.x + o]);
-    __syncthreads();
+  for (int o = 1; o < 64; o <<= 1) {
+    const double ya = __shfl_xor(avg, o, 64), ymx = __shfl_xor(qmax, o, 64), ymn = __shfl_xor(qmin, o, 64);
+    const long long yi = __shfl_xor(iel, o, 64);
+    avg = (threadIdx.x & o) == 0 ? avg + ya : ya + avg;
+    qmax = fmax(qmax, ymx);
+    if (ymn < qmin || (ymn == qmin && yi < iel)) { qmin = ymn; iel = yi; }
   }
-  if (threadIdx.x == 0) parts[lb] = sh[0];
+  if ((threadIdx.x & 63) == 0) {
+    QualPart p;
+    p.avg = avg; p.max = qmax; p.min = qmin; p.iel = iel;
+    p.ne = cne; p.good = cgood; p.med = cmed; p.nrid = cnrid;
+#pragma unroll
+    for (int i = 0; i < 5; i++) p.his[i] = chis[i];
+    sh[threadIdx.x >> 6] = p;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    QualPart r = sh[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); w++) qual_merge(r, sh[w]);
+    parts[lb] = r;
+  }
 }
 
 // fixed-order reduction of n partials (launched twice: FINAL_GRID blocks, then
@@ -618,11 +649,13 @@ __global__ __launch_bounds__(256) void k_prilen(StatArgs A, LenPart *parts) {
         const int c0 = sn[o0], c1 = sn[o1];
         // the first rotation step's records, issued with the points' loads
         TetRec r0{}, r1{};
-        if (c0) r0 = shell_rec(A, srec, kbase, c0);
-        if (c1) r1 = shell_rec(A, srec, kbase, c1);
-        len = edge_len_t<ANI>(A, a, b);
-        on = owns_edge<TAGS>(A, srec, kbase, kk, a, b, c0, c1, keep0, keep1, r0, r1) &&
-             !(PAR && par_excluded(A, a, b));
+        if (A.order != 1) {
+          if (c0) r0 = shell_rec(A, srec, kbase, c0);
+          if (c1) r1 = shell_rec(A, srec, kbase, c1);
+        }
+        len = A.order == 2 ? 1.0 : edge_len_t<ANI>(A, a, b);       // experiment 2: no point loads
+        on = (A.order == 1 || owns_edge<TAGS>(A, srec, kbase, kk, a, b, c0, c1, keep0, keep1, r0, r1)) &&
+             !(PAR && par_excluded(A, a, b));                       // experiment 1: no rotation
         key = LEN_STEP2 + 6 * kk + ia;
       }
       acc.add(on, len, key);
@@ -763,17 +796,23 @@ static bool ensure_red(pmx_ctx *ctx, size_t bytes) {
 // qualhisto partial of the mesh described by A (background or new mesh)
 static int qual_partial(pmx_ctx *ctx, const StatArgs &A, int opt, double *qual_dev, int use_stored,
                         pmx_qual_part *pub, long long np) {
-  const int nb = stat_blocks(A.ne);
+  int nb = stat_blocks(A.ne);
+  if (const char *e = getenv("PMX_EXP_QUAL_ORDER"))                    // experiment: resident grid
+    if (atoi(e) && getenv("PMX_EXP_QUAL_BLOCKS")) nb = atoi(getenv("PMX_EXP_QUAL_BLOCKS"));
   if (!ensure_red(ctx, sizeof(QualPart) * (nb + FINAL_GRID + 1))) return 0;
   QualPart *parts = (QualPart *)ctx->d_red.p;
   hipStream_t s = ctx->stream;
   const bool ani = A.msize == 6, out = opt == PMX_OUTQUA && A.ptag;
+  StatArgs B = A;
+  if (const char *e = getenv("PMX_EXP_QUAL_ORDER")) B.order = atoi(e);   // experiment
+  #define A B
   double *q = use_stored ? qual_dev : nullptr;
   if (ani && out) hipLaunchKernelGGL((k_qual<true, true>), dim3(nb), dim3(256), 0, s, A, q, parts, use_stored);
   else if (ani) hipLaunchKernelGGL((k_qual<true, false>), dim3(nb), dim3(256), 0, s, A, q, parts, use_stored);
   else if (out) hipLaunchKernelGGL((k_qual<false, true>), dim3(nb), dim3(256), 0, s, A, q, parts, use_stored);
   else hipLaunchKernelGGL((k_qual<false, false>), dim3(nb), dim3(256), 0, s, A, q, parts, use_stored);
   QualPart *mid = parts + nb;
+  #undef A
   hipLaunchKernelGGL(k_qual_final, dim3(FINAL_GRID), dim3(256), 0, s, parts, nb, mid,
                      (pmx_qual_part *)nullptr, 0LL);
   hipLaunchKernelGGL(k_qual_final, dim3(1), dim3(256), 0, s, mid, FINAL_GRID, (QualPart *)nullptr, pub, np);
@@ -1010,6 +1049,7 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
     A.par_key = ctx->d_pkey.p;
     A.par_pt = ctx->d_ppt.p;
   }
+  if (const char *e = getenv("PMX_EXP_PRILEN")) A.order = atoi(e);   // experiment
   // partials: [0] step 1 (owned parallel edges), [1..nb] step 2 (tet edges)
   if (!own.empty())
     hipLaunchKernelGGL(k_prilen_par, dim3(1), dim3(256), 0, s, A, ctx->d_pedge.p, (int64_t)own.size(), parts);

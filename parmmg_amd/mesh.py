@@ -194,6 +194,16 @@ def iso_metric(x: np.ndarray) -> np.ndarray:
     return (0.05 + 0.1 * x[:, 0])[:, None]
 
 
+def graded_iso_metric(n: int):
+    """h(x) = (1.2 / n) exp(1.6 (x0 + x1 + x2 - 1.5)) on a Kuhn cube of n
+    cells per axis: metric edge lengths l / h from about 0.04 to 20, so every
+    bin of PMMG_prilen's histogram (bounds 0.3 ... 5) is populated -- a
+    statistics workload that is not one bin (shape (n, 1))."""
+    def f(x: np.ndarray) -> np.ndarray:
+        return ((1.2 / n) * np.exp(1.6 * (x.sum(axis=1) - 1.5)))[:, None]
+    return f
+
+
 def shock_metric(x: np.ndarray) -> np.ndarray:
     """Anisotropic shock metric across the plane n.x = 0.5, n = (1,1,1)/sqrt(3);
     stored (m11, m12, m13, m22, m23, m33), shape (n, 6)."""

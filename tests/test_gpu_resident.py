@@ -136,6 +136,13 @@ def test_promote_requires_step_and_tets():
     bad = M.kuhn_cube(5, seed=2)
     with pytest.raises(RuntimeError, match="sizes"):
         tr.promote_background(bad, r.sols)
+    # an adjacency entry past the last face is refused before anything moves
+    # (the walks would gather through it), and the step stays promotable
+    saved = m2.adja.copy()
+    m2.adja[4 * 3 + 2] = 4 * m2.ne + 4
+    with pytest.raises(RuntimeError, match="adjacency entry out of range"):
+        tr.promote_background(m2, r.sols)
+    m2.adja[:] = saved
     tr.promote_background(m2, r.sols)
     with pytest.raises(RuntimeError, match="upload background and points"):
         tr.run()                                  # the points were consumed

@@ -25,7 +25,8 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=275, help="Kuhn cube cells per axis (ne = 6 n^3)")
-    ap.add_argument("--metric", default="iso", choices=["iso", "ani"])
+    ap.add_argument("--metric", default="iso", choices=["iso", "graded", "ani"],
+                    help="iso: h = 0.05 + 0.1 x (every edge in bin 0); graded: lengths over all 9 bins")
     ap.add_argument("--reps", type=int, default=10)
     args = ap.parse_args()
     import numpy as np
@@ -38,7 +39,8 @@ def main():
 
     t0 = time.perf_counter()
     m = M.kuhn_cube(args.n)
-    met = M.on_vertices(m, M.iso_metric if args.metric == "iso" else M.shock_metric)
+    met = M.on_vertices(m, {"iso": M.iso_metric, "graded": M.graded_iso_metric(args.n),
+                            "ani": M.shock_metric}[args.metric])
     tr = Transfer(0)
     tr.upload_background(m, [met], 0)
     t_setup = time.perf_counter() - t0

@@ -8,6 +8,7 @@ lex    = the generator's numbering (cell-lexicographic tets, lexicographic
          vertices);
 morton = tets by the Morton key of their centroid, vertices by their own key
          (what a device renumbering at upload would produce);
+vmorton / tmorton = only the vertices / only the tets in Morton order;
 random = both permuted at random (a numbering without spatial locality).
 Prints per-variant median/min kernel times and checks that every variant
 locates the same points (elements mapped back through the permutation).
@@ -82,6 +83,12 @@ def main():
             if v == "morton":
                 tp = np.argsort(morton_keys(m.centroids()), kind="stable")
                 vp = np.argsort(morton_keys(m.xyz[1:]), kind="stable")
+            elif v == "vmorton":                      # vertices only (tets keep their order)
+                tp = np.arange(m.ne)
+                vp = np.argsort(morton_keys(m.xyz[1:]), kind="stable")
+            elif v == "tmorton":                      # tets only
+                tp = np.argsort(morton_keys(m.centroids()), kind="stable")
+                vp = np.arange(m.np)
             elif v == "random":
                 tp, vp = rng.permutation(m.ne), rng.permutation(m.np)
             else:

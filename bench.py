@@ -99,6 +99,17 @@ def _cpu_rank(r: int):
     return res["value"], res["sample"]
 
 
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline_node(m, x, t, sols, budget_s: float = 20.0) -> dict:
     """K concurrent single-core oracle processes on the same workload, the
     ParMmg model of one MPI rank per core: each measures its
@@ -117,7 +128,7 @@ def cpu_baseline_node(m, x, t, sols, budget_s: float = 20.0) -> dict:
         res = pool.map(_cpu_rank, range(K))
     rates = [r[0] for r in res]
     return {"value": float(sum(rates)), "unit": "vertices/s", "cores": K, "kind": "port",
-            "per_core": float(np.mean(rates)),
+            "per_core": float(np.mean(rates)), "cpu_model": _cpu_model(),
             "sample": f"{K} concurrent processes, each: {res[0][1]}; node rate = sum of the "
                       f"{K} per-process rates (min {min(rates):.3g}, max {max(rates):.3g})"}
 
@@ -149,7 +160,7 @@ def cpu_baseline(m, x, t, sols, budget_s: float = 20.0) -> dict:
         dt = time.perf_counter() - t1
     t_step = t_pre + dt * n / S
     return {"value": n / t_step, "unit": "vertices/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/pmx_oracle.c (reference algorithm, -O2, 1 thread): "
+            "sample": f"oracle/pmx_oracle.c (reference algorithm, gcc -O3, 1 thread): "
                       f"precompute over all {m.ne} tets {t_pre:.2f}s + {S}/{n} new vertices "
                       f"{dt:.2f}s, extrapolated to the full step"}
 

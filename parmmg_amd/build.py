@@ -107,9 +107,10 @@ def build_oracle(force: bool = False) -> str:
         with _locked("oracle"):
             if force or _stale(ORACLE_SO, deps):
                 tmp = ORACLE_SO + f".{os.getpid()}.tmp"
-                # x86-64 baseline (SSE2, no FMA), no contraction: the reference's
-                # Release arithmetic (CMakeLists.txt:100-116) without -ffast-math
-                _run(["gcc", "-O2", "-std=c99", "-fPIC", "-shared", "-ffp-contract=off",
+                # x86-64 baseline (SSE2, no FMA), no contraction, -O3 as the
+                # reference's Release build (CMakeLists.txt:100-116) without
+                # -ffast-math: the CPU baseline is timed at the reference's level
+                _run(["gcc", "-O3", "-std=c99", "-fPIC", "-shared", "-ffp-contract=off",
                       "-fno-fast-math", *srcs, "-o", tmp, "-lm"])
                 os.replace(tmp, ORACLE_SO)
     return ORACLE_SO

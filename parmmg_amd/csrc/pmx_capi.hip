@@ -626,7 +626,7 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   const char *tg = (const char *)pv->tag;
   if (!dgrow(ctx, ctx->d_qxyz, nn * 3) || !dgrow(ctx, ctx->d_kind, nn) || !dgrow(ctx, ctx->d_qmark, nn) ||
       !dgrow(ctx, ctx->d_nsel, 2) || !dgrow(ctx, ctx->d_vollist, nn) || !dgrow(ctx, ctx->d_bdylist, nn) ||
-      !dgrow(ctx, ctx->d_qv, nn * 3) || !dgrow(ctx, ctx->d_ctile, (size_t)std::max<int64_t>(cls_tiles(n), 1)) ||
+      !dgrow(ctx, ctx->d_ctile, (size_t)std::max<int64_t>(cls_tiles(n), 1)) ||
       (tg && !dgrow(ctx, ctx->d_qtag, nn)) || (ntet && !dgrow(ctx, ctx->d_ntetv, (size_t)(ntet + 1))))
     return 0;
   // coordinates (+ bounding box: a promoted background's hint grid) and tags
@@ -790,12 +790,9 @@ static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &o
   A.max_walk = opts.max_walk > 0 ? opts.max_walk : 512;
   A.const_bit = sd.metric_const ? (1u << sd.imet) : 0u;
   A.inline_ties = (opts.flags & PMX_RUN_NO_INLINE_TIES) ? 0 : 1;
-  A.qv = ctx->d_qv.p;
   A.ref_walk = (opts.flags & PMX_RUN_REFERENCE_WALK) ? 1 : 0;
   A.rec_start = (opts.flags & PMX_RUN_RECORD_STARTS) ? 1 : 0;
-  A.xyzq = ctx->d_xyzq.p;
   A.exp = (opts.flags >> PMX_RUN_EXP_SHIFT) & 0xff;
-  A.qguard = 5.e-3f;
 }
 
 int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
@@ -1341,7 +1338,7 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
 // any, zeroed beforehand)
 bool pmx_ctx::classify(hipStream_t s) {
   if (nq < 1) return true;
-  launch_classify(d_qxyz.p, have_qtag ? d_qtag.p : nullptr, pts_mark ? d_qmark.p : nullptr, nq, d_ctile.p, d_kind.p, d_vollist.p, d_bdylist.p, d_qv.p,
+  launch_classify(have_qtag ? d_qtag.p : nullptr, pts_mark ? d_qmark.p : nullptr, nq, d_ctile.p, d_kind.p, d_vollist.p, d_bdylist.p,
                   d_nsel.p, s);
   if (hipGetLastError() != hipSuccess) {
     err = "classification: launch failed";
@@ -1371,7 +1368,7 @@ void pmx_ctx::free_all() {
   dfree(d_kind); dfree(d_qmark); dfree(d_ctile); dfree(d_nsel); dfree(d_wmask); dfree(d_out); dfree(d_elem); dfree(d_status);
   dfree(d_steps); dfree(d_start); dfree(d_edge); dfree(d_vertex); dfree(d_list); dfree(d_found);
   dfree(d_bestk); dfree(d_best); dfree(d_ties); dfree(d_counts); dfree(d_vollist); dfree(d_bdylist);
-  dfree(d_vstat); dfree(d_bstat); dfree(d_qv);
+  dfree(d_vstat); dfree(d_bstat);
   dfree(d_qual); dfree(d_red); dfree(d_blist); dfree(d_olist); dfree(d_ows);
   dfree(d_ptag); dfree(d_touch); dfree(d_cidx); dfree(d_intv); dfree(d_pub); dfree(d_pkey);
   dfree(d_ppt); dfree(d_pedge); dfree(d_ntetv); dfree(d_nqual); dfree(d_qtag); dfree(d_gather);

@@ -15,7 +15,7 @@ template <class T> struct DevBuf {
 // hint grid from every 4th tet: 1/4 of the stores and of the tet bytes of a
 // full build, at ~0.5 extra walk step (r01 measurements)
 #define PMX_HINT_STRIDE 4
-// pmx_run_opts.flags bits 16-23: walk experiment selector (tools/sweep.py only)
+// pmx_run_opts.flags bits 16-23: the walk's measurement switch (VolArgs.exp; tools/walk_pmc.sh)
 #define PMX_RUN_EXP_SHIFT 16
 
 struct pmx_ctx {
@@ -84,7 +84,6 @@ struct pmx_ctx {
   DevBuf<unsigned long long> d_best;
   DevBuf<unsigned> d_counts;            // step counters, see pmx_kernels.h
   DevBuf<int> d_vollist, d_bdylist;     // compacted point lists per path
-  DevBuf<double> d_qv;                  // volume points, dense xyz in list order
   DevBuf<double> d_qxyz;                // new points as uploaded (dense xyz)
   DevBuf<uint8_t> d_qmark;              // orphan marks (points of valid new tets), uploaded when needed
   DevBuf<int> d_nsel;                   // compaction counts: volume, surface

@@ -42,12 +42,10 @@ struct VolArgs {
   int max_walk;
   unsigned const_bit;           // wmask bit of a constant-size metric (0 if none)
   int inline_ties;              // resolve face ties in place
-  const double *qv;             // coordinates of the volume points in list order (xyz, 24 B)
   int ref_walk;                 // 1: k_walk (reference-order walk) instead of k_walks
   int rec_start;                // write the start tet of every point (diagnostics)
-  const unsigned long long *xyzq; // fixed-point grid coordinates of the old vertices
-  int exp;                      // experiment selector (tools/sweep.py), 0 = production
-  float qguard;                 // fixed-point walk: candidate when lambda_min > -qguard
+  int exp;                      // measurement switch (tools/walk_pmc.sh): 0 production,
+                                // 4 no interpolation, 5 hint + hint record only
 };
 
 struct ExhArgs {
@@ -96,12 +94,11 @@ void launch_patch_rows(const int4 *ent, const double *vals, int64_t n, int S, do
 // new points, every step (the tag dispatch of the reference's vertex loop,
 // src/interpmesh_pmmg.c:541-560): kinds (mark != NULL: the host's orphan
 // marks, 0 = in no valid new tet) and the order-preserving compaction into
-// the volume / surface lists + the volume points' coordinates in list order;
-// counts into nsel[0..1].  tcnt: scratch of cls_tiles(n) int2.
+// the volume / surface lists; counts into nsel[0..1].  tcnt: scratch of cls_tiles(n) int2.
 #define CLS_TILE 4096
 inline int64_t cls_tiles(int64_t n) { return (n + CLS_TILE - 1) / CLS_TILE; }
-void launch_classify(const double *xyz, const uint16_t *tag, const uint8_t *mark, int64_t n, int2 *tcnt,
-                     int8_t *kind, int *vlist, int *blist, double *qv, int *nsel, hipStream_t s);
+void launch_classify(const uint16_t *tag, const uint8_t *mk, int64_t n, int2 *tcnt, int8_t *kind, int *vlist,
+                     int *blist, int *nsel, hipStream_t s);
 
 void launch_build_tetrec(const int4 *tv, const int *adja, int64_t ne, int stride, TetRec *tets, int4 *sample,
                          hipStream_t s);
@@ -126,6 +123,4 @@ struct StatArgs {
   const unsigned long long *par_key;
   int64_t npar;
   const uint8_t *par_pt;
-  int order;                    // k_qual tet order (experiment): 0 contiguous per block,
-                                // 1 chip-wide sliding window of 256-tet chunks, 2 per-XCD window
 };

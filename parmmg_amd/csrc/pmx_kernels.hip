@@ -544,13 +544,12 @@ __global__ __launch_bounds__(256) void k_cls_count(const uint16_t *__restrict__ 
 
 // kinds + the two lists in input order (wave ballots, tile base = sum of the
 // previous tiles' counts, summed again by every workgroup: a few KB of L2
-// reads instead of a third launch) + the volume points' coordinates in list
-// order (the walk reads them coalesced)
-__global__ __launch_bounds__(256) void k_cls_write(const double *__restrict__ xyz, const uint16_t *__restrict__ tag,
+// reads instead of a third launch)
+__global__ __launch_bounds__(256) void k_cls_write(const uint16_t *__restrict__ tag,
                                                    const uint8_t *__restrict__ mark, int64_t n,
                                                    const int2 *__restrict__ tcnt, int8_t *__restrict__ kind,
                                                    int *__restrict__ vlist, int *__restrict__ blist,
-                                                   double *__restrict__ qv, int *__restrict__ nsel) {
+                                                   int *__restrict__ nsel) {
   __shared__ int2 red[4];
   __shared__ int2 wc[4];
   int pv = 0, pb = 0;
@@ -584,11 +583,7 @@ __global__ __launch_bounds__(256) void k_cls_write(const double *__restrict__ xy
       base.y += c.y;
     }
     if (k == KIND_VOL) {
-      const int pos = ov + __popcll(bv & below);
-      vlist[pos] = (int)j;
-      qv[3 * (int64_t)pos] = xyz[3 * j];
-      qv[3 * (int64_t)pos + 1] = xyz[3 * j + 1];
-      qv[3 * (int64_t)pos + 2] = xyz[3 * j + 2];
+      vlist[ov + __popcll(bv & below)] = (int)j;
     } else if (k == KIND_BDY) {
       blist[ob + __popcll(bb & below)] = (int)j;
     }
@@ -600,11 +595,11 @@ __global__ __launch_bounds__(256) void k_cls_write(const double *__restrict__ xy
   }
 }
 
-void launch_classify(const double *xyz, const uint16_t *tag, const uint8_t *mk, int64_t n, int2 *tcnt,
-                     int8_t *kind, int *vlist, int *blist, double *qv, int *nsel, hipStream_t s) {
+void launch_classify(const uint16_t *tag, const uint8_t *mk, int64_t n, int2 *tcnt, int8_t *kind, int *vlist,
+                     int *blist, int *nsel, hipStream_t s) {
   if (n < 1) return;
   const unsigned nt = (unsigned)cls_tiles(n);
   hipLaunchKernelGGL(k_cls_count, dim3(nt), dim3(256), 0, s, tag, mk, n, tcnt);
-  hipLaunchKernelGGL(k_cls_write, dim3(nt), dim3(256), 0, s, xyz, tag, mk, n, (const int2 *)tcnt, kind, vlist,
-                     blist, qv, nsel);
+  hipLaunchKernelGGL(k_cls_write, dim3(nt), dim3(256), 0, s, tag, mk, n, (const int2 *)tcnt, kind, vlist,
+                     blist, nsel);
 }

@@ -175,18 +175,7 @@ __global__ __launch_bounds__(256) void k_qual(StatArgs A, double *qual, QualPart
   // the next z-layer's points (another chunk) are in its own L2
   const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
   const int64_t per = (A.ne + gridDim.x - 1) / gridDim.x;
-  int64_t k0 = 1 + lb * per, k1 = min(A.ne, k0 + per - 1), kstep = blockDim.x;
-  if (A.order == 1) {            // chunk blockIdx.x, + gridDim.x, ...: the chip sweeps one window
-    k0 = 1 + (int64_t)blockIdx.x * blockDim.x;
-    k1 = A.ne;
-    kstep = (int64_t)gridDim.x * blockDim.x;
-  } else if (A.order == 2) {     // each XCD sweeps its contiguous eighth with its own window
-    const int64_t x = blockIdx.x & 7, r = blockIdx.x >> 3, R = gridDim.x >> 3;
-    const int64_t eighth = (A.ne + 7) / 8;
-    k0 = 1 + x * eighth + r * blockDim.x;
-    k1 = min(A.ne, x * eighth + eighth);
-    kstep = R * blockDim.x;
-  }
+  const int64_t k0 = 1 + lb * per, k1 = min(A.ne, k0 + per - 1), kstep = blockDim.x;
   // 16-B connectivity stream: the neighbours are not needed here
   int4 cv = (k0 + (int64_t)threadIdx.x <= k1) ? A.tetv[k0 + threadIdx.x] : make_int4(0, 0, 0, 0);
   for (int64_t kb = k0; kb <= k1; kb += kstep) {   // uniform over the block
@@ -649,13 +638,11 @@ __global__ __launch_bounds__(256) void k_prilen(StatArgs A, LenPart *parts) {
         const int c0 = sn[o0], c1 = sn[o1];
         // the first rotation step's records, issued with the points' loads
         TetRec r0{}, r1{};
-        if (A.order != 1) {
-          if (c0) r0 = shell_rec(A, srec, kbase, c0);
-          if (c1) r1 = shell_rec(A, srec, kbase, c1);
-        }
-        len = A.order == 2 ? 1.0 : edge_len_t<ANI>(A, a, b);       // experiment 2: no point loads
-        on = (A.order == 1 || owns_edge<TAGS>(A, srec, kbase, kk, a, b, c0, c1, keep0, keep1, r0, r1)) &&
-             !(PAR && par_excluded(A, a, b));                       // experiment 1: no rotation
+        if (c0) r0 = shell_rec(A, srec, kbase, c0);
+        if (c1) r1 = shell_rec(A, srec, kbase, c1);
+        len = edge_len_t<ANI>(A, a, b);
+        on = owns_edge<TAGS>(A, srec, kbase, kk, a, b, c0, c1, keep0, keep1, r0, r1) &&
+             !(PAR && par_excluded(A, a, b));
         key = LEN_STEP2 + 6 * kk + ia;
       }
       acc.add(on, len, key);
@@ -796,23 +783,17 @@ static bool ensure_red(pmx_ctx *ctx, size_t bytes) {
 // qualhisto partial of the mesh described by A (background or new mesh)
 static int qual_partial(pmx_ctx *ctx, const StatArgs &A, int opt, double *qual_dev, int use_stored,
                         pmx_qual_part *pub, long long np) {
-  int nb = stat_blocks(A.ne);
-  if (const char *e = getenv("PMX_EXP_QUAL_ORDER"))                    // experiment: resident grid
-    if (atoi(e) && getenv("PMX_EXP_QUAL_BLOCKS")) nb = atoi(getenv("PMX_EXP_QUAL_BLOCKS"));
+  const int nb = stat_blocks(A.ne);
   if (!ensure_red(ctx, sizeof(QualPart) * (nb + FINAL_GRID + 1))) return 0;
   QualPart *parts = (QualPart *)ctx->d_red.p;
   hipStream_t s = ctx->stream;
   const bool ani = A.msize == 6, out = opt == PMX_OUTQUA && A.ptag;
-  StatArgs B = A;
-  if (const char *e = getenv("PMX_EXP_QUAL_ORDER")) B.order = atoi(e);   // experiment
-  #define A B
   double *q = use_stored ? qual_dev : nullptr;
   if (ani && out) hipLaunchKernelGGL((k_qual<true, true>), dim3(nb), dim3(256), 0, s, A, q, parts, use_stored);
   else if (ani) hipLaunchKernelGGL((k_qual<true, false>), dim3(nb), dim3(256), 0, s, A, q, parts, use_stored);
   else if (out) hipLaunchKernelGGL((k_qual<false, true>), dim3(nb), dim3(256), 0, s, A, q, parts, use_stored);
   else hipLaunchKernelGGL((k_qual<false, false>), dim3(nb), dim3(256), 0, s, A, q, parts, use_stored);
   QualPart *mid = parts + nb;
-  #undef A
   hipLaunchKernelGGL(k_qual_final, dim3(FINAL_GRID), dim3(256), 0, s, parts, nb, mid,
                      (pmx_qual_part *)nullptr, 0LL);
   hipLaunchKernelGGL(k_qual_final, dim3(1), dim3(256), 0, s, mid, FINAL_GRID, (QualPart *)nullptr, pub, np);
@@ -1049,7 +1030,6 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
     A.par_key = ctx->d_pkey.p;
     A.par_pt = ctx->d_ppt.p;
   }
-  if (const char *e = getenv("PMX_EXP_PRILEN")) A.order = atoi(e);   // experiment
   // partials: [0] step 1 (owned parallel edges), [1..nb] step 2 (tet edges)
   if (!own.empty())
     hipLaunchKernelGGL(k_prilen_par, dim3(1), dim3(256), 0, s, A, ctx->d_pedge.p, (int64_t)own.size(), parts);

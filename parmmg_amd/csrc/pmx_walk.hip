@@ -231,14 +231,6 @@ __device__ __forceinline__ bool face_tie(const VolArgs &A, D3 p, int &cur, TetRe
   return false;
 }
 
-// experiment: touch the candidate's 4 solution rows (one dword each) before
-// the exact test, so the interpolation's row loads find them in L2
-__device__ __forceinline__ unsigned touch_rows(const VolArgs &A, const TetRec &t) {
-  const unsigned *s = reinterpret_cast<const unsigned *>(A.sol);
-  const int64_t w = 2 * (int64_t)A.sd.S;
-  return s[w * t.v[0]] ^ s[w * t.v[1]] ^ s[w * t.v[2]] ^ s[w * t.v[3]];
-}
-
 // the end of a lane: interpolate, or hand the point to k_fallback
 template <int LAYOUT, int S, bool TIES>
 __device__ __forceinline__ void walk_finish(const VolArgs &A, int64_t i, D3 p, bool found, int step,
@@ -257,7 +249,7 @@ __device__ __forceinline__ void walk_finish(const VolArgs &A, int64_t i, D3 p, b
     A.status[i] = 1;
     A.steps[i] = step;
     const int v[4] = {t.v[0], t.v[1], t.v[2], t.v[3]};
-    if (A.exp == 4) return;                      // experiment: no interpolation
+    if (A.exp == 4) return;                      // measurement: no interpolation
     unsigned wm = interp_layout<LAYOUT, S>(A.sol, A.sd, v, lam, A.out + i * A.sd.S);
     A.wmask[i] = (uint8_t)(wm | A.const_bit);
     s_cnt = 1; s_sum = step; s_max = step; s_min = step;
@@ -280,7 +272,7 @@ __global__ __launch_bounds__(256) void k_walk(VolArgs A) {
 
   if (j < *A.nlist_dev) {     // the step's count (the grid is sized by an upper bound)
     const int64_t i = A.list[j];
-    const D3 p{A.qv[3 * j], A.qv[3 * j + 1], A.qv[3 * j + 2]};
+    const D3 p{A.q[3 * i], A.q[3 * i + 1], A.q[3 * i + 2]};
     int cur = walk_hint(A.grid, A.g, p);
     if (A.rec_start) A.start[i] = cur;
     int ring[WALK_RING];
@@ -420,11 +412,12 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
   unsigned s_cnt = 0, s_sum = 0, s_max = 0, s_min = 0xffffffffu;
 
   if (j < *A.nlist_dev) {     // the step's count (the grid is sized by an upper bound)
-    // list order == Morton order of the volume points: both reads coalesced
-    // and independent (no list -> point dependent gather)
+    // the list keeps the input order (order-preserving compaction): the
+    // point reads through it are as coalesced as the list itself (r03: a
+    // list-ordered copy of the coordinates saved the walk 1 % and cost the
+    // classification 0.15 ms of copying)
     const int64_t i = A.list[j];
-    const double *pq = A.exp == 9 ? A.q + 3 * i : A.qv + 3 * j;    // experiment 9: through the list
-    const D3 p{pq[0], pq[1], pq[2]};
+    const D3 p{A.q[3 * i], A.q[3 * i + 1], A.q[3 * i + 2]};
     int cur = walk_hint(A.grid, A.g, p);
     if (A.rec_start) A.start[i] = cur;
     int ring[WALK_RING];
@@ -432,10 +425,9 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
     for (int r = 0; r < WALK_RING; r++) ring[r] = 0;
     int step = 0;
     bool found = false;
-    unsigned touch = 0;
     TetRec t = A.tets[cur];
     double lam[4];
-    if (A.exp == 5) {                                 // experiment: hint + its record only
+    if (A.exp == 5) {                                 // measurement: hint + its record only
       A.elem[i] = t.v[0] + t.nb[0];
       return;
     }
@@ -516,7 +508,6 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
         neg = !neg;
       }
       if (cand) {
-        if (A.exp == 6) touch = touch_rows(A, t);
         // coordinates in tet order, then the reference's quotients; a
         // rejected candidate continues in the reference's order (rare)
         D3 P[4];
@@ -544,191 +535,12 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
       }
     }
     walk_finish<LAYOUT, S, TIES>(A, i, p, found, step, cur, t, lam, s_cnt, s_sum, s_max, s_min);
-    if (touch == 0x9e3779b9u && A.exp > 99) A.steps[i] = 0;       // sink of the touch loads
-  }
-  wave_stats_w(A.wstats + (b * blockDim.x + threadIdx.x) / 64, s_cnt, s_sum, s_max, s_min);
-}
-
-// ---- k_walkq: the slot walk on fixed-point coordinates -----------------------
-//
-// The walk's direction is taken on the 8-B fixed-point grid coordinates the
-// step already derives (xyzq: 21 bits per axis, 2^qf units per grid cell):
-// 16 vertices per 128-B line instead of 5.3, one 8-B gather per step instead
-// of 24 B, and the sub-volumes in f32 on exact integer differences
-// (barycentrics are affine invariants, so the per-axis scaling changes
-// nothing but the rounding).  The approximation only steers: a lane becomes a
-// candidate when its approximate lambda_min > -qguard (quantisation error ~
-// dim / 2^21, far below qguard on a uniform grid), or when the fixed-point
-// tet is too small to steer by (graded meshes), has no admissible neighbour,
-// or the walk is long; the candidate's exact coordinates are then gathered
-// and the reference's quotients decide, exactly as in k_walks (a rejected
-// candidate continues with the reference-order walk).  Results are k_walk's.
-#define QWALK_CAP 64
-#define QVOL_MIN 2097152.f        // fixed-point 6*volume below which the lane walks exactly
-
-__device__ __forceinline__ void unpack_q(unsigned long long q, int &x, int &y, int &z) {
-  x = (int)(q & 0x1fffffull);
-  y = (int)((q >> 21) & 0x1fffffull);
-  z = (int)(q >> 42);
-}
-
-struct F3 { float x, y, z; };
-__device__ __forceinline__ F3 fcross(F3 a, F3 b) {
-  return F3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
-}
-__device__ __forceinline__ float fdot(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-
-__device__ __forceinline__ int quant_axis(double c, double lo, double inv, int qf, int dim) {
-  const double t = (c - lo) * inv * (double)(1 << qf);
-  const int hi = (dim << qf) - 1;
-  return !(t > 0.0) ? 0 : (t >= (double)hi ? hi : (int)t);
-}
-
-template <int LAYOUT, int S, bool TIES>
-__global__ __launch_bounds__(256) void k_walkq(VolArgs A) {
-  const int64_t b = walk_xcd_remap(blockIdx.x, gridDim.x);
-  const int64_t j = b * blockDim.x + threadIdx.x;
-  unsigned s_cnt = 0, s_sum = 0, s_max = 0, s_min = 0xffffffffu;
-
-  if (j < *A.nlist_dev) {
-    const int64_t i = A.list[j];
-    const D3 p{A.qv[3 * j], A.qv[3 * j + 1], A.qv[3 * j + 2]};
-    int cur = walk_hint(A.grid, A.g, p);
-    if (A.rec_start) A.start[i] = cur;
-    int ring[WALK_RING];
-#pragma unroll
-    for (int r = 0; r < WALK_RING; r++) ring[r] = 0;
-    int step = 0;
-    bool found = false;
-    unsigned touch = 0;
-    TetRec t = A.tets[cur];
-    double lam[4];
-    if (t.v[0] <= 0) step = 1;                        // !MG_EOK start: let the scan decide
-    else {
-      const int px = quant_axis(p.x, A.g.lo[0], A.g.inv[0], A.g.qf[0], A.g.dim[0]);
-      const int py = quant_axis(p.y, A.g.lo[1], A.g.inv[1], A.g.qf[1], A.g.dim[1]);
-      const int pz = quant_axis(p.z, A.g.lo[2], A.g.inv[2], A.g.qf[2], A.g.dim[2]);
-      F3 d[4];
-      int I[4] = {t.v[0], t.v[1], t.v[2], t.v[3]};
-      int NB[4] = {t.nb[0], t.nb[1], t.nb[2], t.nb[3]};
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        int x, y, z;
-        unpack_q(A.xyzq[I[k]], x, y, z);
-        d[k] = F3{(float)(x - px), (float)(y - py), (float)(z - pz)};
-      }
-      const float qg = A.qguard;
-      const int qcap = min(QWALK_CAP, A.max_walk);
-      bool neg = false, cand = false;
-      for (;;) {
-        step++;
-        const F3 c23 = fcross(d[2], d[3]), c01 = fcross(d[0], d[1]);
-        float w[4] = {fdot(d[1], c23), -fdot(d[0], c23), fdot(d[3], c01), -fdot(d[2], c01)};
-        if (neg) {
-#pragma unroll
-          for (int k = 0; k < 4; k++) w[k] = -w[k];
-        }
-        const float vol = (w[0] + w[1]) + (w[2] + w[3]);
-        const float wmin = fminf(fminf(w[0], w[1]), fminf(w[2], w[3]));
-        // inside up to the guard, too small to steer by, or a long walk: the
-        // exact coordinates decide
-        if (!(vol > QVOL_MIN) || wmin > -qg * vol || step >= qcap) { cand = true; break; }
-#pragma unroll
-        for (int r = WALK_RING - 1; r > 0; r--) ring[r] = ring[r - 1];
-        ring[0] = cur;
-        int sb = -1;
-        float wb = 0.f;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const int nb = NB[k];
-          bool seen = false;
-#pragma unroll
-          for (int q = 0; q < WALK_RING; q++) seen |= (ring[q] == nb);
-          const bool take = nb && !seen && (sb < 0 || w[k] < wb);
-          sb = take ? k : sb;
-          wb = take ? w[k] : wb;
-        }
-        if (sb < 0) { cand = true; break; }               // boundary: the exact walk decides
-        const int next = pick4(NB, sb);
-        const TetRec u = A.tets[next];
-        cur = next;
-        t = u;
-        if (u.v[0] <= 0) break;                            // !MG_EOK: let the scan decide
-        int nnew = 0, lnew = 0;
-#pragma unroll
-        for (int l = 0; l < 4; l++) {
-          const bool any = (u.v[l] == I[0]) | (u.v[l] == I[1]) | (u.v[l] == I[2]) | (u.v[l] == I[3]);
-          nnew += any ? 0 : 1;
-          lnew = any ? lnew : l;
-        }
-        if (nnew != 1) {                                   // inconsistent adjacency: reload
-#pragma unroll
-          for (int k = 0; k < 4; k++) {
-            int x, y, z;
-            unpack_q(A.xyzq[u.v[k]], x, y, z);
-            d[k] = F3{(float)(x - px), (float)(y - py), (float)(z - pz)};
-            I[k] = u.v[k];
-            NB[k] = u.nb[k];
-          }
-          neg = false;
-          continue;
-        }
-        const int vn = pick4(u.v, lnew);
-        int x, y, z;
-        unpack_q(A.xyzq[vn], x, y, z);
-        const F3 dn{(float)(x - px), (float)(y - py), (float)(z - pz)};
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          d[k] = F3{k == sb ? dn.x : d[k].x, k == sb ? dn.y : d[k].y, k == sb ? dn.z : d[k].z};
-          I[k] = (k == sb) ? vn : I[k];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-          NB[k] = (u.nb[0] & -(int)(u.v[0] == I[k])) | (u.nb[1] & -(int)(u.v[1] == I[k])) |
-                  (u.nb[2] & -(int)(u.v[2] == I[k])) | (u.nb[3] & -(int)(u.v[3] == I[k]));
-        neg = !neg;
-      }
-      if (cand) {
-        if (A.exp == 7) touch = touch_rows(A, t);
-        // the candidate's exact coordinates in tet order, the reference's
-        // quotients; a rejected candidate continues in the reference's order
-        D3 P[4];
-#pragma unroll
-        for (int l = 0; l < 4; l++) P[l] = ld3(A.xyz, t.v[l]);
-        for (;;) {
-          double num[4], vol;
-          face_nums(P, p, num, &vol);
-#pragma unroll
-          for (int f = 0; f < 4; f++) lam[f] = -num[f] / vol;
-          const double lmin = fmin(fmin(lam[0], lam[1]), fmin(lam[2], lam[3]));
-          if (lmin > -PMX_EPS) { found = true; break; }    // src/barycoord_pmmg.c:102-107
-          if (step >= A.max_walk) break;
-          const int next = exact_next(t, lam, ring, cur);
-          if (!next) break;
-          t = A.tets[next];
-          cur = next;
-          if (t.v[0] <= 0) break;
-          step++;
-#pragma unroll
-          for (int l = 0; l < 4; l++) P[l] = ld3(A.xyz, t.v[l]);
-        }
-      }
-    }
-    walk_finish<LAYOUT, S, TIES>(A, i, p, found, step, cur, t, lam, s_cnt, s_sum, s_max, s_min);
-    if (touch == 0x9e3779b9u && A.exp > 99) A.steps[i] = 0;       // sink of the touch loads
   }
   wave_stats_w(A.wstats + (b * blockDim.x + threadIdx.x) / 64, s_cnt, s_sum, s_max, s_min);
 }
 
 template <int LAYOUT, int S>
 static void launch_walk_t(const VolArgs &a, int64_t nb, hipStream_t s) {
-  if (((a.exp >= 1 && a.exp <= 3) || a.exp == 7) && !a.ref_walk) {
-    VolArgs b = a;
-    b.qguard = a.exp == 1 ? 5.e-3f : a.exp == 2 ? 2.e-2f : 1.e-3f;
-    if (a.inline_ties) hipLaunchKernelGGL((k_walkq<LAYOUT, S, true>), dim3((unsigned)nb), dim3(256), 0, s, b);
-    else hipLaunchKernelGGL((k_walkq<LAYOUT, S, false>), dim3((unsigned)nb), dim3(256), 0, s, b);
-    return;
-  }
   if (a.ref_walk) {
     if (a.inline_ties) hipLaunchKernelGGL((k_walk<LAYOUT, S, true>), dim3((unsigned)nb), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_walk<LAYOUT, S, false>), dim3((unsigned)nb), dim3(256), 0, s, a);

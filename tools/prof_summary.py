@@ -8,9 +8,11 @@ per-dispatch PMC averages, HBM traffic per launch) and copies the rocprofv3
 kernel stats CSV next to it as <out>_kernel_stats.csv.
 
 HBM traffic per launch follows MI355X_MICROARCH.md section HBM: FETCH_SIZE and
-WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reads 1/2 of the bytes of wide
-(16 B/lane) reads, so the read side is doubled ("traffic" = 2*FETCH + WRITE);
-the raw sum is kept beside it ("traffic_raw").  Counts from separate --pmc
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts 64 B per 128-B line fetched
+-- for wide streaming reads (the guide) and, calibrated by
+tools/fetch_calib.hip (profiles/r03_fetch_calib.json), for 8/16/24/32/64/128-B
+per-lane gathers alike -- so the read side is doubled ("traffic" = 2*FETCH +
+WRITE); the raw sum is kept beside it ("traffic_raw").  Counts from separate --pmc
 passes of the same command, averaged over that kernel's dispatches.
 """
 import collections

@@ -626,6 +626,62 @@ __device__ int tria_hint(const BdyArgs &A, D3 p) {
 // sorted by vertex (stable: fans in tria order), and every pair's slot 3 k + l
 // records its vertex's run [lo, hi) -- the surface kernels always reach a
 // vertex through a tria that holds it, so no per-vertex offsets over np.
+// PMMG_precompute_nodeTrias (src/locate_pmmg.c:134-195): per boundary
+// vertex, its incident boundary trias in ascending tria order, i.e. what a
+// stable sort of the (vertex, 3 k + l) pairs gives.  Two builds with the same
+// output, chosen by size (r03, C2 / C3 steps):
+//  * a counting sort over the vertex ids -- count -> exclusive scan over np ->
+//    fill at the vertex's offset (slot by atomic, order arbitrary) -> the
+//    slot-0 writer sorts its fan (a few entries): its arrays are np-sized;
+//  * a 25-bit radix sort of the 3 nt pairs (hipCUB): latency-bound passes
+//    whose cost does not grow with np.
+// With np > 5 * 3 nt (C3: 16.8 M vertices, 2.3 M pairs) the counting sort's
+// memset and scan over np competed with the main stream's derived-data pass
+// (step 2.11 -> 2.20 ms); at C2 (1.7 M vertices, 0.5 M pairs) the radix
+// sort's passes were the surface stream's critical path (step 0.44 -> 0.36
+// ms with the counting sort).  A compacted-id counting sort (bitmap of the
+// boundary vertices) lost both: 2.3 M atomicOr on 525 K words serialise.
+__global__ __launch_bounds__(256) void k_nt_count(const TriRec *__restrict__ tris, int64_t nt,
+                                                  unsigned *__restrict__ cnt) {
+  for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= nt;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const TriRec t = tris[k];
+    if (t.v[0] <= 0) continue;
+    for (int l = 0; l < 3; l++) atomicAdd(&cnt[t.v[l]], 1u);
+  }
+}
+__global__ __launch_bounds__(256) void k_nt_fill(const TriRec *__restrict__ tris, int64_t nt,
+                                                 const unsigned *__restrict__ off, unsigned *__restrict__ cnt,
+                                                 int *__restrict__ list, int2 *__restrict__ range,
+                                                 uint8_t *__restrict__ own) {
+  for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= nt;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const TriRec t = tris[k];
+    for (int l = 0; l < 3; l++) {
+      if (t.v[0] <= 0) { range[3 * k + l] = make_int2(0, 0); own[3 * k + l] = 0; continue; }
+      const int v = t.v[l];
+      const unsigned lo = off[v], hi = off[v + 1];
+      const unsigned left = atomicSub(&cnt[v], 1u);          // hi - lo, ..., 1
+      list[lo + left - 1] = (int)k;
+      range[3 * k + l] = make_int2((int)lo, (int)hi);
+      own[3 * k + l] = left == 1u ? 1 : 0;                   // exactly one writer per fan
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_nt_sort(int64_t nt, const int2 *__restrict__ range,
+                                                 const uint8_t *__restrict__ own, int *__restrict__ list) {
+  for (int64_t i = 3 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 3 * (nt + 1);
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (!own[i]) continue;
+    const int2 r = range[i];
+    for (int a = r.x + 1; a < r.y; a++) {                 // insertion sort of the fan
+      const int x = list[a];
+      int b = a - 1;
+      while (b >= r.x && list[b] > x) { list[b + 1] = list[b]; b--; }
+      list[b + 1] = x;
+    }
+  }
+}
 __global__ __launch_bounds__(256) void k_nt_pairs(const TriRec *__restrict__ tris, int64_t nt,
                                                   unsigned *__restrict__ key, int *__restrict__ val) {
   for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= nt;
@@ -648,9 +704,47 @@ __global__ __launch_bounds__(256) void k_nt_runs(const unsigned *__restrict__ ke
   }
 }
 
+
+// the counting sort over the vertex ids
+static bool node_trias_counting(pmx_ctx *c, hipStream_t s) {
+  const int64_t m = 3 * c->nt, np = c->np, nt = c->nt;
+  if (!pmx_dgrow(c, c->d_ntkey, (size_t)(2 * (np + 2))) || !pmx_dgrow(c, c->d_ntval, (size_t)(3 * (nt + 1))) ||
+      !pmx_dgrow(c, c->d_ntrange, (size_t)(3 * (nt + 1))) || !pmx_dgrow(c, c->d_ntlist, (size_t)m))
+    return false;
+  unsigned *cnt = c->d_ntkey.p, *off = c->d_ntkey.p + (np + 2);
+  uint8_t *own = reinterpret_cast<uint8_t *>(c->d_ntval.p);
+  size_t bytes = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, cnt, off, (int)(np + 2), s);
+  if (!pmx_dgrow(c, c->d_nttmp, bytes)) return false;
+  if (hipMemsetAsync(cnt, 0, (size_t)(np + 2) * sizeof(unsigned), s) != hipSuccess) {
+    c->err = "node trias: memset";
+    return false;
+  }
+  const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nt + 255) / 256, 4096));
+  hipLaunchKernelGGL(k_nt_count, dim3(nb), dim3(256), 0, s, c->d_tris.p, nt, cnt);
+  if (hipcub::DeviceScan::ExclusiveSum(c->d_nttmp.p, bytes, cnt, off, (int)(np + 2), s) != hipSuccess) {
+    c->err = "node trias: scan";
+    return false;
+  }
+  hipLaunchKernelGGL(k_nt_fill, dim3(nb), dim3(256), 0, s, c->d_tris.p, nt, (const unsigned *)off, cnt,
+                     c->d_ntlist.p, c->d_ntrange.p, own);
+  const unsigned ns = (unsigned)std::max<int64_t>(1, std::min<int64_t>((m + 255) / 256, 4096));
+  hipLaunchKernelGGL(k_nt_sort, dim3(ns), dim3(256), 0, s, nt, (const int2 *)c->d_ntrange.p,
+                     (const uint8_t *)own, c->d_ntlist.p);
+  return true;
+}
+
 bool pmx_ctx::build_node_trias(hipStream_t s) {
   const int64_t m = 3 * nt;
   if (m < 1) return true;
+  if (np <= 5 * m) {
+    if (!node_trias_counting(this, s)) return false;
+    if (hipGetLastError() != hipSuccess) {
+      err = "node trias: launch";
+      return false;
+    }
+    return true;
+  }
   int bits = 1;
   while (bits < 32 && ((int64_t)1 << bits) <= np) bits++;
   if (!pmx_dgrow(this, d_ntkey, (size_t)(2 * m)) || !pmx_dgrow(this, d_ntval, (size_t)(2 * m)) ||

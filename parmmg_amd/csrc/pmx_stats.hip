@@ -542,8 +542,8 @@ __device__ __forceinline__ bool owns_edge(const StatArgs &A, const TetRec (*srec
 // 125M tets; a fused version with one round trip per dependent load and
 // partial rounds after every batch: 7.2 ms.)
 #define LEN_QCAP 2048                 // > 255 left over + 6 * 256 queued
-template <bool ANI, bool TAGS, bool PAR>
-__global__ __launch_bounds__(256) void k_prilen(StatArgs A, LenPart *parts) {
+template <bool ANI, bool TAGS, bool PAR, int W = 1>
+__global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
   __shared__ TetRec srec[2][256];
   __shared__ unsigned short q[LEN_QCAP];
   __shared__ unsigned wcnt[4];
@@ -1039,10 +1039,13 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
     // variants: metric kind x point tags x parallel edges (each drops the
     // other paths' registers and branches)
     using KFn = void (*)(StatArgs, LenPart *);
-    static const KFn kfn[8] = {k_prilen<false, false, false>, k_prilen<false, false, true>,
-                               k_prilen<false, true, false>,  k_prilen<false, true, true>,
-                               k_prilen<true, false, false>,  k_prilen<true, false, true>,
-                               k_prilen<true, true, false>,   k_prilen<true, true, true>};
+    // the isotropic variants held to 5 waves per SIMD (96 VGPRs, a few
+    // spills): 2 % faster at the C5 share; the anisotropic ones spill too
+    // much there (4.46 instead of 3.63 ms) and keep the compiler's choice
+    static const KFn kfn[8] = {k_prilen<false, false, false, 5>, k_prilen<false, false, true, 5>,
+                               k_prilen<false, true, false, 5>,  k_prilen<false, true, true, 5>,
+                               k_prilen<true, false, false>,     k_prilen<true, false, true>,
+                               k_prilen<true, true, false>,      k_prilen<true, true, true>};
     const int sel = (A.msize == 6 ? 4 : 0) | (A.ptag ? 2 : 0) | (A.npar ? 1 : 0);
     hipLaunchKernelGGL(kfn[sel], dim3(nb), dim3(256), 0, s, A, parts + 1);
   }

@@ -446,6 +446,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     ~StreamGuard() { if (s) hipStreamSynchronize(s); }
   } topo_guard;
   if (!dgrow(ctx, ctx->d_xyz, (size_t)(np + 1) * 3) || !dgrow(ctx, ctx->d_tets, (size_t)(ne + 1)) ||
+      !dgrow(ctx, ctx->d_wrec, (size_t)(ne + 1)) ||
       !dgrow(ctx, ctx->d_tets_s, (size_t)std::max<int64_t>(ns, 1)) || !dgrow(ctx, ctx->d_sol, hs_n) ||
       !dgrow(ctx, ctx->d_tris, (size_t)(nt + 1)) || !dgrow(ctx, ctx->d_trn, (size_t)(nt + 1)) ||
       !dgrow(ctx, ctx->d_xyzq, (size_t)(np + 1)) ||
@@ -528,7 +529,10 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     ctx->err = "pmx_upload_background: tet vertex or adjacency index out of range";
     return 0;
   }
-  if (!dev_adja) CK(hipMemcpyAsync(ctx->d_tets_s.p, hh, (size_t)ns * sizeof(int4), hipMemcpyHostToDevice, st));
+  if (!dev_adja) {
+    CK(hipMemcpyAsync(ctx->d_tets_s.p, hh, (size_t)ns * sizeof(int4), hipMemcpyHostToDevice, st));
+    launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, st);
+  }
   if (dev_adja) {
     // face matching on the device (pmx_topo.hip), then the tet records and
     // the hint sample from the device connectivity -- on the topology stream
@@ -542,6 +546,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
       return 0;
     launch_build_tetrec(ctx->d_btv.p, ctx->d_adja.p, ne, PMX_HINT_STRIDE, ctx->d_tets.p, ctx->d_tets_s.p,
                         ctx->topo);
+    launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, ctx->topo);
     CK(hipEventRecord(ctx->ev_join, ctx->topo));
   }
   tr.mark("tets");
@@ -762,12 +767,14 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   if (ctx->residency && ntet > 0) {
     const int64_t ns = (ntet + PMX_HINT_STRIDE - 1) / PMX_HINT_STRIDE;
     if (!dgrow(ctx, ctx->d_adja, (size_t)(4 * ntet + 5)) || !dgrow(ctx, ctx->d_tets_next, (size_t)(ntet + 1)) ||
+        !dgrow(ctx, ctx->d_wrec_next, (size_t)(ntet + 1)) ||
         !dgrow(ctx, ctx->d_tets_s_next, (size_t)std::max<int64_t>(ns, 1)))
       return 0;
     *ctx->h_nbad = 0;
     if (!pmx_ctx_build_adja_device(ctx, ctx->d_ntetv.p, ntet, n, ctx->d_adja.p, ctx->topo, ctx->h_nbad)) return 0;
     launch_build_tetrec(ctx->d_ntetv.p, ctx->d_adja.p, ntet, PMX_HINT_STRIDE, ctx->d_tets_next.p,
                         ctx->d_tets_s_next.p, ctx->topo);
+    launch_build_wrec(ctx->d_tets_next.p, ntet, ctx->d_wrec_next.p, ctx->topo);
     CK(hipEventRecord(ctx->ev_topo, ctx->topo));
     ctx->next_topo = true;
   }
@@ -777,7 +784,7 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
 // ---- the step ---------------------------------------------------------------
 
 static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &opts, VolArgs &A) {
-  A.xyz = ctx->d_xyz.p; A.tets = ctx->d_tets.p; A.sol = ctx->d_sol.p; A.sd = sd;
+  A.xyz = ctx->d_xyz.p; A.tets = ctx->d_tets.p; A.wrec = ctx->d_wrec.p; A.sol = ctx->d_sol.p; A.sd = sd;
   A.q = ctx->d_qxyz.p; A.kind = ctx->d_kind.p; A.nq = ctx->nq; A.ne = ctx->ne;
   A.grid = ctx->d_grid.p; A.g = ctx->grid;
   A.out = ctx->d_out.p; A.wmask = ctx->d_wmask.p;
@@ -1303,6 +1310,7 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
   if (prepared && !m->adja) {
     if (*ctx->h_nbad) { ctx->err = "pmx_promote_background: non-manifold tet faces"; return 0; }
     std::swap(ctx->d_tets, ctx->d_tets_next);
+    std::swap(ctx->d_wrec, ctx->d_wrec_next);
     std::swap(ctx->d_tets_s, ctx->d_tets_s_next);
   } else {
     if (m->adja) {
@@ -1310,7 +1318,9 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
     } else if (!pmx_ctx_build_adja_device(ctx, ctx->d_ntetv.p, ne, n, ctx->d_adja.p, st, nullptr)) {
       return 0;
     }
+    if (!dgrow(ctx, ctx->d_wrec, (size_t)(ne + 1))) return 0;
     launch_build_tetrec(ctx->d_ntetv.p, ctx->d_adja.p, ne, PMX_HINT_STRIDE, ctx->d_tets.p, ctx->d_tets_s.p, st);
+    launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, st);
   }
   ctx->np = n;
   ctx->ne = ne;
@@ -1363,7 +1373,7 @@ void pmx_ctx::free_all() {
   if (h_stage) hipHostFree(h_stage);
   h_stage = nullptr;
   h_stage_cap = 0;
-  dfree(d_xyz); dfree(d_tets); dfree(d_sol); dfree(d_tets_s); dfree(d_tris);
+  dfree(d_xyz); dfree(d_tets); dfree(d_wrec); dfree(d_wrec_next); dfree(d_sol); dfree(d_tets_s); dfree(d_tris);
   dfree(d_ntlist); dfree(d_ntval); dfree(d_ntkey); dfree(d_ntrange); dfree(d_nttmp); dfree(d_xyzq); dfree(d_trn); dfree(d_grid); dfree(d_tetv);
   dfree(d_kind); dfree(d_qmark); dfree(d_ctile); dfree(d_nsel); dfree(d_wmask); dfree(d_out); dfree(d_elem); dfree(d_status);
   dfree(d_steps); dfree(d_start); dfree(d_edge); dfree(d_vertex); dfree(d_list); dfree(d_found);

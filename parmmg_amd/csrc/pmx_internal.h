@@ -47,6 +47,7 @@ struct pmx_ctx {
   double bblo[3]{}, bbhi[3]{};
   DevBuf<double> d_xyz;                 // old vertices, x y z (24 B), slot 0 unused
   DevBuf<TetRec> d_tets;
+  DevBuf<WRec> d_wrec;                  // the walk's compact copy of d_tets (built with it)
   DevBuf<double> d_sol;
   DevBuf<int4> d_tets_s;                // host-packed hint sample: tets 1, 1+4, 1+8, ...
   DevBuf<TriRec> d_tris;
@@ -132,6 +133,7 @@ struct pmx_ctx {
   hipEvent_t ev_topo = nullptr;
   bool next_topo = false;               // d_tets_next / d_tets_s_next are being built
   DevBuf<TetRec> d_tets_next;
+  DevBuf<WRec> d_wrec_next;
   DevBuf<int4> d_tets_s_next;
   unsigned *h_nbad = nullptr;           // pinned [2]: non-manifold faces of that build, [1] of a background upload's
   DevBuf<double> d_nqual;

@@ -19,6 +19,7 @@ struct GridDesc {
 struct VolArgs {
   const double *xyz;            // old vertices, 24 B (x, y, z), 1-based
   const TetRec *tets;
+  const WRec *wrec;             // the walk's compact copy of tets (null: walk on tets)
   const double *sol;
   SolDesc sd;
   const double *q;              // new points as uploaded, dense x y z (0-based)
@@ -95,13 +96,15 @@ void launch_patch_rows(const int4 *ent, const double *vals, int64_t n, int S, do
 // src/interpmesh_pmmg.c:541-560): kinds (mark != NULL: the host's orphan
 // marks, 0 = in no valid new tet) and the order-preserving compaction into
 // the volume / surface lists; counts into nsel[0..1].  tcnt: scratch of cls_tiles(n) int2.
-#define CLS_TILE 4096
+#define CLS_TILE 16384               // 4 rounds of 256 threads x 16 points
 inline int64_t cls_tiles(int64_t n) { return (n + CLS_TILE - 1) / CLS_TILE; }
 void launch_classify(const uint16_t *tag, const uint8_t *mk, int64_t n, int2 *tcnt, int8_t *kind, int *vlist,
                      int *blist, int *nsel, hipStream_t s);
 
 void launch_build_tetrec(const int4 *tv, const int *adja, int64_t ne, int stride, TetRec *tets, int4 *sample,
                          hipStream_t s);
+// the walk's compact records from the tet records (slots 0..ne)
+void launch_build_wrec(const TetRec *tets, int64_t ne, WRec *wr, hipStream_t s);
 // workgroups of k_fallback that can be co-resident with `share` other
 // launches of it on this device (0 on error)
 int fallback_coresident_blocks(int device, int share);

@@ -35,8 +35,7 @@ __global__ __launch_bounds__(256) void k_bg_derive(const double *__restrict__ xy
                                                    const TriRec *__restrict__ tris, int64_t nt,
                                                    Pt4 *__restrict__ trn) {
   const int64_t st = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= np; i += st) {
-    const double c[3] = {xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]};
+  auto quant = [&](const double *c) {
     unsigned long long r = 0;
 #pragma unroll
     for (int a = 0; a < 3; a++) {
@@ -45,7 +44,20 @@ __global__ __launch_bounds__(256) void k_bg_derive(const double *__restrict__ xy
       const long long u = !(t > 0.0) ? 0 : (t >= (double)hi ? hi : (long long)t);
       r |= (unsigned long long)u << (21 * a);
     }
-    q[i] = r;
+    return r;
+  };
+  // two vertices per thread: three 16-B loads, one 16-B store (rows 2m, 2m+1)
+  const int64_t npair = (np + 2) / 2;           // vertices 0 .. np
+  for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < npair; m += st) {
+    if (2 * m + 1 <= np) {
+      const double2 *p = reinterpret_cast<const double2 *>(xyz + 6 * m);
+      const double2 a = p[0], b = p[1], c = p[2];
+      const double c0[3] = {a.x, a.y, b.x}, c1[3] = {b.y, c.x, c.y};
+      reinterpret_cast<ulonglong2 *>(q)[m] = make_ulonglong2(quant(c0), quant(c1));
+    } else {
+      const double c0[3] = {xyz[6 * m], xyz[6 * m + 1], xyz[6 * m + 2]};
+      q[2 * m] = quant(c0);
+    }
   }
   for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= nt; k += st) {
     const TriRec t = tris[k];
@@ -106,6 +118,23 @@ void launch_hint_build(const int4 *packed, const TetRec *tets, int64_t ne, int s
   else
     hipLaunchKernelGGL(k_hint_build<false>, dim3((unsigned)nb), dim3(256), 0, s, packed, tets, ne, stride,
                        grid, g, xyzq);
+}
+
+// the walk's compact records (WRec, pmx_device.h) from the tet records, built
+// with them at every upload / promotion (a re-layout of the connectivity, like
+// the records themselves)
+__global__ __launch_bounds__(256) void k_build_wrec(const TetRec *__restrict__ tets, int64_t ne,
+                                                    WRec *__restrict__ wr) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= ne;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    WRec r;
+    wrec_encode(tets[k], k, r);
+    wr[k] = r;
+  }
+}
+void launch_build_wrec(const TetRec *tets, int64_t ne, WRec *wr, hipStream_t s) {
+  const int64_t nb = std::min<int64_t>(std::max<int64_t>((ne + 256) / 256, 1), 16384);
+  hipLaunchKernelGGL(k_build_wrec, dim3((unsigned)nb), dim3(256), 0, s, tets, ne, wr);
 }
 
 // connectivity stream out of the tet records (statistics pass, built on demand)
@@ -498,17 +527,6 @@ void launch_build_tetrec(const int4 *tv, const int *adja, int64_t ne, int stride
 
 // ---- new points: classification on the device (pmx_upload_points) ---------------
 
-// kind of a new point (PMMG_interpMetricsAndFields_mesh's dispatch, :541-560)
-__device__ __forceinline__ int point_kind(const uint16_t *__restrict__ tag, const uint8_t *__restrict__ mark,
-                                          int64_t j) {
-  const unsigned t = tag ? tag[j] : 0u;
-  if (t >= PMX_TAG_NUL) return KIND_NUL;                  // !MG_VOK
-  if (mark && !mark[j]) return KIND_ORPH;                 // in no valid new tet
-  if (t & PMX_TAG_REQ) return KIND_SKIP;
-  if (t & PMX_TAG_BDY) return KIND_BDY;
-  return KIND_VOL;
-}
-
 // sum over the 256-thread block, in every thread (red: 4 LDS slots)
 __device__ __forceinline__ int2 block_sum2(int2 v, int2 *red) {
 #pragma unroll
@@ -525,26 +543,80 @@ __device__ __forceinline__ int2 block_sum2(int2 v, int2 *red) {
   return r;
 }
 
+// The kinds of the 16 points j0 .. j0+15 of one thread (j0 % 16 == 0): two
+// 16-B tag loads and one 16-B mark load instead of 16 narrow loads per lane
+// (r03: the one-point-per-lane rounds were latency-bound, 0.12 ms at C3 for
+// 17 M points); points at or past n get 0xff.  kw: the kinds, 4 per word.
+__device__ __forceinline__ void kinds16(const uint16_t *__restrict__ tag, const uint8_t *__restrict__ mark,
+                                        int64_t j0, int64_t n, unsigned kw[4], int &cv, int &cb) {
+  unsigned tw[8], mw[4];
+  if (j0 + 16 <= n) {
+    if (tag) {
+      const uint4 a = reinterpret_cast<const uint4 *>(tag + j0)[0];
+      const uint4 b = reinterpret_cast<const uint4 *>(tag + j0)[1];
+      tw[0] = a.x; tw[1] = a.y; tw[2] = a.z; tw[3] = a.w;
+      tw[4] = b.x; tw[5] = b.y; tw[6] = b.z; tw[7] = b.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; i++) tw[i] = 0u;
+    }
+    if (mark) {
+      const uint4 c = *reinterpret_cast<const uint4 *>(mark + j0);
+      mw[0] = c.x; mw[1] = c.y; mw[2] = c.z; mw[3] = c.w;
+    }
+  } else {                                    // the last, partial chunk
+#pragma unroll
+    for (int i = 0; i < 8; i++) tw[i] = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; i++) mw[i] = 0u;
+    for (int i = 0; i < 16 && j0 + i < n; i++) {
+      if (tag) tw[i >> 1] |= (unsigned)tag[j0 + i] << (16 * (i & 1));
+      if (mark) mw[i >> 2] |= (unsigned)mark[j0 + i] << (8 * (i & 3));
+    }
+  }
+#pragma unroll
+  for (int w = 0; w < 4; w++) kw[w] = 0u;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const unsigned t = (tw[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+    const bool in = j0 + i < n;
+    // kind of a new point: PMMG_interpMetricsAndFields_mesh's dispatch
+    // (src/interpmesh_pmmg.c:541-560): !MG_VOK, in no valid new tet, MG_REQ,
+    // MG_BDY, volume
+    unsigned k = (t >= PMX_TAG_NUL) ? KIND_NUL
+                 : (mark && !((mw[i >> 2] >> (8 * (i & 3))) & 0xffu)) ? KIND_ORPH
+                 : (t & PMX_TAG_REQ) ? KIND_SKIP
+                 : (t & PMX_TAG_BDY) ? KIND_BDY : KIND_VOL;
+    k = in ? k : 0xffu;
+    cv += k == KIND_VOL;
+    cb += k == KIND_BDY;
+    kw[i >> 2] |= k << (8 * (i & 3));
+  }
+}
+
 // per tile of CLS_TILE points: how many volume / surface points
 __global__ __launch_bounds__(256) void k_cls_count(const uint16_t *__restrict__ tag, const uint8_t *__restrict__ mark,
                                                    int64_t n, int2 *__restrict__ tcnt) {
   __shared__ int2 red[4];
   const int64_t t0 = (int64_t)blockIdx.x * CLS_TILE;
   int cv = 0, cb = 0;
-  for (int r = 0; r < CLS_TILE / 256; r++) {
-    const int64_t j = t0 + r * 256 + threadIdx.x;
-    if (j >= n) break;
-    const int k = point_kind(tag, mark, j);
-    cv += k == KIND_VOL;
-    cb += k == KIND_BDY;
+#pragma unroll
+  for (int r = 0; r < CLS_TILE / 4096; r++) {
+    const int64_t j0 = t0 + r * 4096 + 16 * (int64_t)threadIdx.x;
+    unsigned kw[4];
+    if (j0 < n) kinds16(tag, mark, j0, n, kw, cv, cb);
   }
   const int2 c = block_sum2(make_int2(cv, cb), red);
   if (threadIdx.x == 0) tcnt[blockIdx.x] = c;
 }
 
-// kinds + the two lists in input order (wave ballots, tile base = sum of the
-// previous tiles' counts, summed again by every workgroup: a few KB of L2
-// reads instead of a third launch)
+// kinds + the two lists in input order.  Per round of 4096 points: every
+// thread classifies 16 consecutive points (vector loads, one 16-B kind
+// store) into LDS; wave w owns points 1024 w .. 1024 w + 1023 of the round
+// (its own threads' chunks), so the wave totals give each wave its base, and
+// the wave then writes its list entries in 16 coalesced ballot sub-rounds.
+// Tile base = sum of the previous tiles' counts, summed again by every
+// workgroup (a few KB of L2 reads instead of a third launch).
 __global__ __launch_bounds__(256) void k_cls_write(const uint16_t *__restrict__ tag,
                                                    const uint8_t *__restrict__ mark, int64_t n,
                                                    const int2 *__restrict__ tcnt, int8_t *__restrict__ kind,
@@ -552,6 +624,7 @@ __global__ __launch_bounds__(256) void k_cls_write(const uint16_t *__restrict__ 
                                                    int *__restrict__ nsel) {
   __shared__ int2 red[4];
   __shared__ int2 wc[4];
+  __shared__ uint4 lk[256];                   // the round's 4096 kinds
   int pv = 0, pb = 0;
   for (unsigned t = threadIdx.x; t < blockIdx.x; t += 256) {
     const int2 c = tcnt[t];
@@ -562,16 +635,26 @@ __global__ __launch_bounds__(256) void k_cls_write(const uint16_t *__restrict__ 
   const int64_t t0 = (int64_t)blockIdx.x * CLS_TILE;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const unsigned long long below = (1ull << lane) - 1ull;
-  for (int r = 0; r < CLS_TILE / 256; r++) {
-    const int64_t j = t0 + r * 256 + threadIdx.x;
-    int k = -1;
-    if (j < n) {
-      k = point_kind(tag, mark, j);
-      kind[j] = (int8_t)k;
+  const uint8_t *lkb = reinterpret_cast<const uint8_t *>(lk);
+  for (int r = 0; r < CLS_TILE / 4096; r++) {
+    const int64_t r0 = t0 + r * 4096;
+    if (r0 >= n) break;                                   // uniform: the tile's end
+    const int64_t j0 = r0 + 16 * (int64_t)threadIdx.x;
+    unsigned kw[4] = {~0u, ~0u, ~0u, ~0u};
+    int cv = 0, cb = 0;
+    if (j0 < n) {
+      kinds16(tag, mark, j0, n, kw, cv, cb);
+      if (j0 + 16 <= n) *reinterpret_cast<uint4 *>(kind + j0) = make_uint4(kw[0], kw[1], kw[2], kw[3]);
+      else
+        for (int i = 0; j0 + i < n; i++) kind[j0 + i] = (int8_t)((kw[i >> 2] >> (8 * (i & 3))) & 0xffu);
     }
-    const unsigned long long bv = __ballot(k == KIND_VOL), bb = __ballot(k == KIND_BDY);
-    __syncthreads();                                      // wc of the last round read
-    if (lane == 0) wc[w] = make_int2(__popcll(bv), __popcll(bb));
+    lk[threadIdx.x] = make_uint4(kw[0], kw[1], kw[2], kw[3]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      cv += __shfl_xor(cv, o, 64);
+      cb += __shfl_xor(cb, o, 64);
+    }
+    if (lane == 0) wc[w] = make_int2(cv, cb);
     __syncthreads();
     int ov = base.x, ob = base.y;
 #pragma unroll
@@ -582,12 +665,18 @@ __global__ __launch_bounds__(256) void k_cls_write(const uint16_t *__restrict__ 
       base.x += c.x;
       base.y += c.y;
     }
-    if (k == KIND_VOL) {
-      vlist[ov + __popcll(bv & below)] = (int)j;
-    } else if (k == KIND_BDY) {
-      blist[ob + __popcll(bb & below)] = (int)j;
+    // the wave's 1024 points in input order, 64 per sub-round
+#pragma unroll 4
+    for (int s = 0; s < 16; s++) {
+      const int p = 1024 * w + 64 * s + lane;
+      const int k = lkb[p];
+      const unsigned long long bv = __ballot(k == KIND_VOL), bb = __ballot(k == KIND_BDY);
+      if (k == KIND_VOL) vlist[ov + __popcll(bv & below)] = (int)(r0 + p);
+      else if (k == KIND_BDY) blist[ob + __popcll(bb & below)] = (int)(r0 + p);
+      ov += __popcll(bv);
+      ob += __popcll(bb);
     }
-    if (t0 + (r + 1) * 256 >= n) break;                   // uniform: the tile's end
+    __syncthreads();                                      // lk and wc rewritten next round
   }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
     nsel[0] = base.x;

@@ -405,7 +405,14 @@ __device__ __forceinline__ int exact_next(const TetRec &t, const double lam[4], 
   return next;
 }
 
-template <int LAYOUT, int S, bool TIES>
+// the walk's tet record: through the compact copy (CW) or the full record
+template <bool CW>
+__device__ __forceinline__ TetRec walk_rec(const VolArgs &A, int k) {
+  if constexpr (CW) return wrec_load(A.wrec, A.tets, k);
+  else return A.tets[k];
+}
+
+template <int LAYOUT, int S, bool TIES, bool CW>
 __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
   const int64_t b = walk_xcd_remap(blockIdx.x, gridDim.x);
   const int64_t j = b * blockDim.x + threadIdx.x;
@@ -425,7 +432,7 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
     for (int r = 0; r < WALK_RING; r++) ring[r] = 0;
     int step = 0;
     bool found = false;
-    TetRec t = A.tets[cur];
+    TetRec t = walk_rec<CW>(A, cur);
     double lam[4];
     if (A.exp == 5) {                                 // measurement: hint + its record only
       A.elem[i] = t.v[0] + t.nb[0];
@@ -472,7 +479,7 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
         }
         if (sb < 0) break;
         const int next = pick4(NB, sb);
-        const TetRec u = A.tets[next];
+        const TetRec u = walk_rec<CW>(A, next);
         cur = next;
         t = u;
         if (u.v[0] <= 0) break;                            // !MG_EOK: let the scan decide
@@ -544,9 +551,12 @@ static void launch_walk_t(const VolArgs &a, int64_t nb, hipStream_t s) {
   if (a.ref_walk) {
     if (a.inline_ties) hipLaunchKernelGGL((k_walk<LAYOUT, S, true>), dim3((unsigned)nb), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_walk<LAYOUT, S, false>), dim3((unsigned)nb), dim3(256), 0, s, a);
+  } else if (a.wrec && a.exp != 6) {           // exp 6: walk on the 32-B records (A/B)
+    if (a.inline_ties) hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true>), dim3((unsigned)nb), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_walks<LAYOUT, S, false, true>), dim3((unsigned)nb), dim3(256), 0, s, a);
   } else {
-    if (a.inline_ties) hipLaunchKernelGGL((k_walks<LAYOUT, S, true>), dim3((unsigned)nb), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_walks<LAYOUT, S, false>), dim3((unsigned)nb), dim3(256), 0, s, a);
+    if (a.inline_ties) hipLaunchKernelGGL((k_walks<LAYOUT, S, true, false>), dim3((unsigned)nb), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_walks<LAYOUT, S, false, false>), dim3((unsigned)nb), dim3(256), 0, s, a);
   }
 }
 

@@ -1,0 +1,72 @@
+"""GPU: the walk's compact 24-B records (WRec, parmmg_amd/csrc/pmx_device.h).
+
+k_walks reads the tet records through a 24-B copy (vertex ids as deltas from
+v[0], neighbours as deltas from the tet index); a tet whose deltas do not fit
+is flagged and read from the 32-B records.  Both walks must locate and
+interpolate bit for bit alike, with and without escaped records (the 32-B walk
+is the one the oracle parity tests pin; run flag exp 6 selects it).
+"""
+import numpy as np
+import pytest
+
+from helpers import cube_case, lin_field
+from parmmg_amd import _native as N
+from parmmg_amd import mesh as M
+
+pytestmark = pytest.mark.gpu
+
+FULL_RECORDS = 6 << 16            # PMX_RUN_EXP_SHIFT: exp 6 = walk on the 32-B records
+
+
+def _both(tr, m, x, t, sols):
+    tr.upload_background(m, sols, 0)
+    tr.upload_points(x, t)
+    out = []
+    for flags in (0, FULL_RECORDS):
+        tr.run(flags=flags)
+        r = tr.download()
+        out.append((r.elem.copy(), r.status.copy(), [s.copy() for s in r.sols]))
+    return out
+
+
+def _assert_same(a, b):
+    assert np.array_equal(a[0], b[0])
+    assert np.array_equal(a[1], b[1])
+    for u, v in zip(a[2], b[2]):
+        assert np.array_equal(u.view(np.uint64), v.view(np.uint64))
+
+
+def test_compact_records_equal_full_records(transfer):
+    m, x, t, sols = cube_case(24, metric="ani")
+    a, b = _both(transfer, m, x, t, sols)
+    _assert_same(a, b)
+    assert np.count_nonzero(a[0]) > 0.9 * len(x)
+
+
+def test_escaped_records(transfer):
+    """Vertex ids scattered over > 2^19 (np = 83^3): most vertex deltas do not
+    fit 20 bits, so most records take the escape path; the outer layer of
+    vertices keeps its numbering so that escaped and packed records mix."""
+    n = 82
+    m0 = M.kuhn_cube(n)
+    npts = m0.np
+    assert npts > (1 << 19)
+    rng = np.random.default_rng(7)
+    perm = np.arange(npts + 1)
+    inner = np.nonzero(np.all((m0.xyz[1:] > 0.1) & (m0.xyz[1:] < 0.9), axis=1))[0] + 1
+    perm[inner] = rng.permutation(inner)          # old id -> new id
+    xyz = np.empty_like(m0.xyz)
+    xyz[perm] = m0.xyz
+    m = M.Mesh(xyz, perm[m0.tet].astype(np.int32), m0.adja, perm[m0.tria].astype(np.int32), m0.adjt,
+               m0.hausd)
+    x, t = M.new_points(n, seed=5, surface=True)
+    x, t = x[::4].copy(), t[::4].copy()
+    sols = [M.on_vertices(m, M.iso_metric), M.on_vertices(m, lin_field)]
+    a, b = _both(transfer, m, x, t, sols)
+    _assert_same(a, b)
+    vol = (t == 0) & (a[1] == 1)
+    assert vol.sum() > 0.5 * (t == 0).sum()
+    # located volume points reproduce the linear field (the interpolation
+    # went through the right vertices of the escaped records)
+    ref = lin_field(x[vol])[:, 0]
+    assert np.max(np.abs(a[2][1][vol, 0] - ref)) < 1e-12

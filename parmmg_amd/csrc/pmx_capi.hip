@@ -838,10 +838,13 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   // overlaps the derived data, the classification and the hint build
   const bool bdy = ctx->nq_bdy_ub > 0;
   const bool serial = (opts.flags & PMX_RUN_SERIAL_SURFACE) != 0;
-  hipStream_t ss = serial ? st : ctx->side;
+  // (r03: the surface stream at the highest priority measured the same,
+  // C3 2.093 vs 2.095 ms, profiles/r03_c3_sweep_surface_priority.log)
+  hipStream_t side = ctx->side;
+  hipStream_t ss = serial ? st : side;
   if (bdy && !serial) {
     CK(hipEventRecord(ctx->ev_fork, st));
-    CK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    CK(hipStreamWaitEvent(side, ctx->ev_fork, 0));
   }
   if (ev) CK(hipEventRecord(ev[3], ss));
   if (bdy && csr) {
@@ -863,27 +866,32 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     if (!(s == sd.imet && sd.metric_const)) any_interp = true;
   // reference early exit (src/interpmesh_pmmg.c:508-512): nothing to locate
   if (!any_interp && bdy && !serial) {
-    CK(hipEventRecord(ctx->ev_join, ctx->side));
+    CK(hipEventRecord(ctx->ev_join, side));
     CK(hipStreamWaitEvent(st, ctx->ev_join, 0));
   }
   if (any_interp) {
     VolArgs A{};
     fill_vol_args(ctx, sd, opts, A);
+    // the surface path on the side stream once the points are classified:
+    // after the bandwidth-bound hint build (forking the surface kernels before
+    // it slowed that by 40 %, r01 sweep), latency-bound beside the volume
+    // walk; exp 9: forked before the hint build (A/B)
+    auto fork_surface = [&]() -> bool {
+      if (!bdy || serial) return true;
+      CK(hipEventRecord(ctx->ev_fork2, st));
+      CK(hipStreamWaitEvent(side, ctx->ev_fork2, 0));
+      if (!ctx->launch_bdy(A, side)) return false;
+      if (ev) CK(hipEventRecord(ev[5], side));
+      CK(hipEventRecord(ctx->ev_join, side));
+      return true;
+    };
+    const bool early = A.exp == 9;
+    if (early && !fork_surface()) return 0;
     const int stride = opts.hint_stride > 0 ? opts.hint_stride : PMX_HINT_STRIDE;
     launch_hint_build(stride == PMX_HINT_STRIDE ? ctx->d_tets_s.p : nullptr, ctx->d_tets.p, ctx->ne,
-                      stride, ctx->d_grid.p, ctx->grid, ctx->d_xyzq.p, st);
+                      stride, ctx->d_grid.p, A.g, ctx->d_xyzq.p, st);
     if (ev) CK(hipEventRecord(ev[1], st));
-    // the surface path on the side stream once the points are classified and
-    // the bandwidth-bound hint build is done (forking the surface kernels
-    // before it slowed that by 40 %, r01 sweep): it is latency-bound and
-    // overlaps the volume walk
-    if (bdy && !serial) {
-      CK(hipEventRecord(ctx->ev_fork2, st));
-      CK(hipStreamWaitEvent(ctx->side, ctx->ev_fork2, 0));
-      if (!ctx->launch_bdy(A, ctx->side)) return 0;
-      if (ev) CK(hipEventRecord(ev[5], ctx->side));
-      CK(hipEventRecord(ctx->ev_join, ctx->side));
-    }
+    if (!early && !fork_surface()) return 0;
     if (ctx->nq_vol_ub) launch_walk(A, st);
     if (ev) CK(hipEventRecord(ev[2], st));
     if (bdy && !serial) {

@@ -10,6 +10,14 @@ struct GridDesc {
                     // dim << qf fits 21 bits (qf = 21 - ceil(log2 dim))
 };
 
+// cell (x, y, z) of the volume hint grid, row-major.  (r03: 4x4x4 blocks of
+// 64 cells, so that a wave of Morton-ordered points reads its hint cells from
+// a few lines, left the walk within 0.5 % and made the surface path overlap it
+// worse: C3 step 2.09 -> 2.19 ms, profiles/r03_c3_sweep_grid_priority.log.)
+__host__ __device__ inline int64_t gcell(const GridDesc &g, int x, int y, int z) {
+  return (int64_t)x + (int64_t)g.dim[0] * ((int64_t)y + (int64_t)g.dim[1] * z);
+}
+
 // counters of one step (d_counts, zeroed by the prologue):
 //   [0] volume stuck, [1] surface stuck, [2] surface overflow, [3] volume ties,
 //   [4] k_fallback grid-barrier arrivals, [7] device error flags (PMX_DERR_*)

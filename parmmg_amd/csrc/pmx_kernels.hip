@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ pac
                         (unsigned)((c >> sh) & M) + (unsigned)((d >> sh) & M);
     cq[ax] = min((int)(s4 >> (g.qf[ax] + 2)), g.dim[ax] - 1);
   }
-  grid[(int64_t)cq[0] + (int64_t)g.dim[0] * ((int64_t)cq[1] + (int64_t)g.dim[1] * cq[2])] = (int)k;
+  grid[gcell(g, cq[0], cq[1], cq[2])] = (int)k;
 }
 void launch_hint_build(const int4 *packed, const TetRec *tets, int64_t ne, int stride, int *grid,
                        GridDesc g, const unsigned long long *xyzq, hipStream_t s) {

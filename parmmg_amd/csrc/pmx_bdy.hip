@@ -611,9 +611,12 @@ __device__ int tria_hint(const BdyArgs &A, D3 p) {
   return 1;
 }
 
-// surface walks are short (1.5 steps on C2): 8 private slots, the rare longer
-// walk is redone by k_locate_bdy_ovf with a global workspace
-#define BDY_CAP 8
+// surface walks are short (1.5 steps on C2): 16 private slots, the rare longer
+// walk is redone by k_locate_bdy_ovf with a global workspace (r03: with 8
+// slots the overflow pass, one long serial walk per thread, was the C2 surface
+// path's tail: surface path 0.287 -> 0.217 ms, step 0.336 -> 0.328 ms with 16;
+// C3 within 0.1 %; profiles/r03_c{2,3}_sweep_bdy_cap.log)
+#define BDY_CAP 16
 #define OVF_CAP 2048
 #define OVF_THREADS (64 * 64)
 
@@ -842,7 +845,10 @@ bool pmx_ctx::launch_bdy(const VolArgs &a, hipStream_t s) {
   B.ovf_list = d_olist.p; B.ovf_count = d_counts.p + 2;
   B.list = d_bdylist.p; B.nlist = nq_bdy_ub; B.nlist_dev = d_nsel.p + 1; B.wstats = d_bstat.p;
   int64_t nb = (nq_bdy_ub + 255) / 256;
-  hipLaunchKernelGGL(k_locate_bdy<BDY_CAP>, dim3((unsigned)nb), dim3(256), 0, s, B);
+  if (a.exp == 10)                         // A/B: the r01-r03 8-entry private lists
+    hipLaunchKernelGGL(k_locate_bdy<BDY_CAP / 2>, dim3((unsigned)nb), dim3(256), 0, s, B);
+  else
+    hipLaunchKernelGGL(k_locate_bdy<BDY_CAP>, dim3((unsigned)nb), dim3(256), 0, s, B);
   hipLaunchKernelGGL(k_locate_bdy_ovf, dim3(OVF_THREADS / 64), dim3(64), 0, s, B, d_ows.p, OVF_CAP);
   hipLaunchKernelGGL(k_exh_bdy, dim3(256), dim3(256), 0, s, B);
   return hipGetLastError() == hipSuccess;

@@ -872,10 +872,11 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   if (any_interp) {
     VolArgs A{};
     fill_vol_args(ctx, sd, opts, A);
-    // the surface path on the side stream once the points are classified:
-    // after the bandwidth-bound hint build (forking the surface kernels before
-    // it slowed that by 40 %, r01 sweep), latency-bound beside the volume
-    // walk; exp 9: forked before the hint build (A/B)
+    // the surface path on the side stream as soon as the points are
+    // classified, latency-bound beside the hint build and the volume walk
+    // (r03 A/B, profiles/r03_c{2,3,4}_sweep_surface_fork.log: C2 step 0.346 ->
+    // 0.338 ms, C3 / C4 within 0.1 %); exp 9: forked after the hint build
+    // (r01-r03 order: the r01 sweep had the hint build 40 % slower beside it)
     auto fork_surface = [&]() -> bool {
       if (!bdy || serial) return true;
       CK(hipEventRecord(ctx->ev_fork2, st));
@@ -885,7 +886,7 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
       CK(hipEventRecord(ctx->ev_join, side));
       return true;
     };
-    const bool early = A.exp == 9;
+    const bool early = A.exp != 9;
     if (early && !fork_surface()) return 0;
     const int stride = opts.hint_stride > 0 ? opts.hint_stride : PMX_HINT_STRIDE;
     launch_hint_build(stride == PMX_HINT_STRIDE ? ctx->d_tets_s.p : nullptr, ctx->d_tets.p, ctx->ne,

@@ -6,7 +6,8 @@
 //                    (PMMG_precompute_triaNormals, src/locate_pmmg.c:68-90)
 // k_hint_build       uniform grid over the background bbox, cell -> a sampled
 //                    tet whose centroid falls in it (the walk start)
-// k_fallback         ties, LDS-staged exhaustive scan (smallest containing tet
+// k_ties             near-face ties: canonical (smallest-index) containing tet
+// k_fallback         LDS-staged exhaustive scan (smallest containing tet
 //                    index == the reference's first hit in index order,
 //                    src/locate_pmmg.c:737-770), closest tet (argmin of
 //                    |lambda_min|*vol, src/barycoord_pmmg.c:371-404) and the
@@ -344,8 +345,8 @@ __device__ void d_exh_finish(const ExhArgs &A, const VolArgs &V, unsigned bid, u
 
 // ---- fused fallback -------------------------------------------------------------
 //
-// Ties, exhaustive scan (find, closest value, closest index) and the final
-// interpolation of the scanned points in ONE launch (five launches that almost
+// Exhaustive scan (find, closest value, closest index) and the final
+// interpolation of the scanned points in ONE launch (four launches that almost
 // always found nothing to do cost ~4.5 us each).  The launch reads the
 // counters and leaves, or runs the phases separated by a grid barrier
 // (MI355X_MICROARCH.md "barrier-counter": release fence + waitcnt before the
@@ -383,20 +384,27 @@ __device__ bool grid_barrier(unsigned *bar, unsigned target, unsigned *err, long
   return s_ok != 0;
 }
 
+// The ties (canonical tet BFS, independent per point) are a launch of their
+// own: a step with ties but no stuck point (the common case: 71 ties at C3)
+// then needs no grid barrier, so its fallback never waits for co-residency
+// behind another context's walk (C4: two groups per GPU).  The tie launch may
+// append points to the stuck list; the kernel boundary orders that.
+__global__ __launch_bounds__(256) void k_ties(VolArgs V) {
+  if (ld_agent(V.tie_count) == 0) return;
+  d_ties(V, blockIdx.x, gridDim.x);
+}
+
 __global__ __launch_bounds__(256) void k_fallback(ExhArgs E, VolArgs V) {
   const unsigned nb = gridDim.x, b = blockIdx.x;
   unsigned *bar = V.stuck_count + 4;           // counts[4], zeroed by the prologue
   unsigned *err = V.stuck_count + PMX_CNT_ERR;
-  if (ld_agent(V.tie_count) == 0 && ld_agent(V.stuck_count) == 0) return;
-  d_ties(V, b, nb);
-  if (!grid_barrier(bar, nb, err, E.spin_limit)) return;
   if (ld_agent(V.stuck_count) == 0) return;
   d_exh_find(E, b, nb);
-  if (!grid_barrier(bar, 2 * nb, err, E.spin_limit)) return;
+  if (!grid_barrier(bar, nb, err, E.spin_limit)) return;
   d_exh_closest(E, 0, b, nb);
-  if (!grid_barrier(bar, 3 * nb, err, E.spin_limit)) return;
+  if (!grid_barrier(bar, 2 * nb, err, E.spin_limit)) return;
   d_exh_closest(E, 1, b, nb);
-  if (!grid_barrier(bar, 4 * nb, err, E.spin_limit)) return;
+  if (!grid_barrier(bar, 3 * nb, err, E.spin_limit)) return;
   d_exh_finish(E, V, b, nb);
 }
 
@@ -411,6 +419,7 @@ int fallback_coresident_blocks(int device, int share) {
 }
 
 void launch_exhaustive(const ExhArgs &e, const VolArgs &v, int blocks, hipStream_t s) {
+  hipLaunchKernelGGL(k_ties, dim3(64), dim3(256), 0, s, v);
   hipLaunchKernelGGL(k_fallback, dim3((unsigned)std::max(1, blocks)), dim3(256), 0, s, e, v);
 }
 

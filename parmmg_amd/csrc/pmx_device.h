@@ -68,10 +68,12 @@ __device__ __forceinline__ int wrec_nb(unsigned w, int k) {
   return d == WREC_NONE ? 0 : k + d;
 }
 
-// tets[k] from its compact record r (escapes read the full record)
-__device__ __forceinline__ TetRec wrec_decode(const WRec &r, const TetRec *__restrict__ tets, int k) {
-  // decoded before the escape test, so that a caller's record load is not
-  // split (a test first would turn the flag word into a load of its own)
+// tets[k] through its compact record (escapes read the full record)
+__device__ __forceinline__ TetRec wrec_load(const WRec *__restrict__ wr, const TetRec *__restrict__ tets,
+                                            int k) {
+  const WRec r = wr[k];
+  // decoded before the escape test, so the whole record is one load (a test
+  // first would split off the flag word into a dependent load of its own)
   const int v0 = (int)r.w[0];
   const unsigned u1 = (r.w[1] >> 24) | ((r.w[2] >> 24) << 8) | (((r.w[3] >> 24) & 0xfu) << 16);
   const unsigned u2 = (r.w[4] >> 24) | ((r.w[5] & 0xfffu) << 8);
@@ -86,13 +88,6 @@ __device__ __forceinline__ TetRec wrec_decode(const WRec &r, const TetRec *__res
   t.nb[3] = wrec_nb(r.w[4], k);
   if ((r.w[3] >> 28) & WREC_ESC) t = tets[k];
   return t;
-}
-
-// tets[k] through its compact record
-__device__ __forceinline__ TetRec wrec_load(const WRec *__restrict__ wr, const TetRec *__restrict__ tets,
-                                            int k) {
-  const WRec r = wr[k];
-  return wrec_decode(r, tets, k);
 }
 
 // KIND_SKIP: MG_REQ (copied by PMMG_copyMetricsAndFields_point); KIND_NUL:

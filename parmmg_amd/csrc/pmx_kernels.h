@@ -124,7 +124,6 @@ struct StatArgs {
   const double *xyz;
   int xstride, vbase;
   const TetRec *tets;           // records with neighbours (background only)
-  const WRec *wrec;             // their compact copy (prilen's record stream), or null
   const int4 *tetv;             // connectivity stream (v only)
   int64_t ne;
   const double *sol;

@@ -461,7 +461,6 @@ __device__ __forceinline__ int rotate_step(const TetRec &r, int a, int b, int &k
 // A shell record: from the workgroup's LDS batches when the tet is one of
 // them (the current and the previous batch of 256 records: the in-cell and
 // x-neighbour shells of a lexicographic numbering), else from HBM.
-template <bool CW>
 __device__ __forceinline__ TetRec shell_rec(const StatArgs &A, const TetRec (*srec)[256],
                                             const long long *kbase, int c) {
   const unsigned long long d0 = (unsigned long long)((long long)c - kbase[0]);
@@ -474,8 +473,6 @@ __device__ __forceinline__ TetRec shell_rec(const StatArgs &A, const TetRec (*sr
     const int4 *l = reinterpret_cast<const int4 *>(&srec[0][0]) + 2 * idx;
     const int4 lv = l[0], ln = l[1];
     r = TetRec{{lv.x, lv.y, lv.z, lv.w}, {ln.x, ln.y, ln.z, ln.w}};
-  } else if constexpr (CW) {
-    r = wrec_load(A.wrec, A.tets, c);
   } else {
     const int4 *g = reinterpret_cast<const int4 *>(A.tets) + 2 * (int64_t)c;
     const int4 gv = g[0], gn = g[1];
@@ -492,7 +489,7 @@ __device__ __forceinline__ TetRec shell_rec(const StatArgs &A, const TetRec (*sr
 // records of c0/c1, loaded by the caller (with the edge's points, in one
 // round trip) and then one step ahead; without point tags an index alone
 // decides, so a record is only loaded when the rotation goes on through it.
-template <bool TAGS, bool CW>
+template <bool TAGS>
 __device__ __forceinline__ bool owns_edge(const StatArgs &A, const TetRec (*srec)[256], const long long *kbase, int64_t k,
                           int a, int b, int c0, int c1, int keep0, int keep1, TetRec r0, TetRec r1) {
   for (int guard = 0; guard < 4096; guard++) {
@@ -522,8 +519,8 @@ __device__ __forceinline__ bool owns_edge(const StatArgs &A, const TetRec (*srec
       if ((need0 && c0 < k) || (need1 && c1 < k)) return false;
       if (need0 && c0 == c1) return true;
     }
-    if (need0) r0 = shell_rec<CW>(A, srec, kbase, c0);
-    if (need1) r1 = shell_rec<CW>(A, srec, kbase, c1);
+    if (need0) r0 = shell_rec(A, srec, kbase, c0);
+    if (need1) r1 = shell_rec(A, srec, kbase, c1);
   }
   return true;
 }
@@ -545,7 +542,7 @@ __device__ __forceinline__ bool owns_edge(const StatArgs &A, const TetRec (*srec
 // 125M tets; a fused version with one round trip per dependent load and
 // partial rounds after every batch: 7.2 ms.)
 #define LEN_QCAP 2048                 // > 255 left over + 6 * 256 queued
-template <bool ANI, bool TAGS, bool PAR, int W = 1, bool CW = false>
+template <bool ANI, bool TAGS, bool PAR, int W = 1>
 __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
   __shared__ TetRec srec[2][256];
   __shared__ unsigned short q[LEN_QCAP];
@@ -567,13 +564,9 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
   const int4 *recs = reinterpret_cast<const int4 *>(A.tets);
   {
     const int64_t kn = min(k0 + (int64_t)tid, A.ne);
-    if constexpr (CW) {
-      srec[0][tid] = wrec_load(A.wrec, A.tets, (int)kn);
-    } else {
-      int4 *srow = reinterpret_cast<int4 *>(&srec[0][tid]);
-      srow[0] = recs[2 * kn];
-      srow[1] = recs[2 * kn + 1];
-    }
+    int4 *srow = reinterpret_cast<int4 *>(&srec[0][tid]);
+    srow[0] = recs[2 * kn];
+    srow[1] = recs[2 * kn + 1];
     if (tid == 0) { kbase[0] = k0; kbase[1] = -(1LL << 40); }   // no second batch yet
     __syncthreads();
   }
@@ -584,11 +577,7 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
     if (!more && head == tail) break;
     const unsigned prev_end = tail;              // entries before it: the previous batch
     const int64_t kn = min(kb + 256 + (int64_t)tid, A.ne);
-    // the next batch's record, raw (decoded when it is written to LDS)
-    int4 pv, pn;
-    WRec pw;
-    if constexpr (CW) pw = A.wrec[kn];
-    else { pv = recs[2 * kn]; pn = recs[2 * kn + 1]; }
+    const int4 pv = recs[2 * kn], pn = recs[2 * kn + 1];
     if (more) {
       const int64_t k = kb + tid;
       const TetRec t = srec[buf][tid];
@@ -649,10 +638,10 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
         const int c0 = sn[o0], c1 = sn[o1];
         // the first rotation step's records, issued with the points' loads
         TetRec r0{}, r1{};
-        if (c0) r0 = shell_rec<CW>(A, srec, kbase, c0);
-        if (c1) r1 = shell_rec<CW>(A, srec, kbase, c1);
+        if (c0) r0 = shell_rec(A, srec, kbase, c0);
+        if (c1) r1 = shell_rec(A, srec, kbase, c1);
         len = edge_len_t<ANI>(A, a, b);
-        on = owns_edge<TAGS, CW>(A, srec, kbase, kk, a, b, c0, c1, keep0, keep1, r0, r1) &&
+        on = owns_edge<TAGS>(A, srec, kbase, kk, a, b, c0, c1, keep0, keep1, r0, r1) &&
              !(PAR && par_excluded(A, a, b));
         key = LEN_STEP2 + 6 * kk + ia;
       }
@@ -661,13 +650,9 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
     }
     if (more) {                                  // no entry of the previous batch is left
       __syncthreads();                           // ... once every wave is past its rounds
-      if constexpr (CW) {
-        srec[buf ^ 1][tid] = wrec_decode(pw, A.tets, (int)kn);
-      } else {
-        int4 *srow = reinterpret_cast<int4 *>(&srec[buf ^ 1][tid]);
-        srow[0] = pv;
-        srow[1] = pn;
-      }
+      int4 *srow = reinterpret_cast<int4 *>(&srec[buf ^ 1][tid]);
+      srow[0] = pv;
+      srow[1] = pn;
       if (tid == 0) kbase[buf ^ 1] = kb + 256;
     }
     __syncthreads();                             // srec, wcnt, kbase rewritten next
@@ -781,10 +766,6 @@ static bool stat_args(pmx_ctx *ctx, StatArgs &A) {
   A.xstride = 3;
   A.vbase = 0;
   A.tets = ctx->d_tets.p;
-  // prilen streams the 24-B compact records (PMX_STATS_TETREC=1: the 32-B
-  // records, for the A/B)
-  static const bool full = getenv("PMX_STATS_TETREC") != nullptr;
-  A.wrec = full ? nullptr : ctx->d_wrec.p;
   A.tetv = ctx->d_tetv.p;
   A.ne = ctx->ne;
   A.sol = ctx->d_sol.p;
@@ -1061,18 +1042,11 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
     // the isotropic variants held to 5 waves per SIMD (96 VGPRs, a few
     // spills): 2 % faster at the C5 share; the anisotropic ones spill too
     // much there (4.46 instead of 3.63 ms) and keep the compiler's choice
-    static const KFn kfn[16] = {
-        k_prilen<false, false, false, 5>,       k_prilen<false, false, true, 5>,
-        k_prilen<false, true, false, 5>,        k_prilen<false, true, true, 5>,
-        k_prilen<true, false, false>,           k_prilen<true, false, true>,
-        k_prilen<true, true, false>,            k_prilen<true, true, true>,
-        k_prilen<false, false, false, 5, true>, k_prilen<false, false, true, 5, true>,
-        k_prilen<false, true, false, 5, true>,  k_prilen<false, true, true, 5, true>,
-        k_prilen<true, false, false, 1, true>,  k_prilen<true, false, true, 1, true>,
-        k_prilen<true, true, false, 1, true>,   k_prilen<true, true, true, 1, true>};
-    // + compact 24-B records (the walk's wrec) for the record stream and the
-    // shell reads outside the LDS batches
-    const int sel = (A.wrec ? 8 : 0) | (A.msize == 6 ? 4 : 0) | (A.ptag ? 2 : 0) | (A.npar ? 1 : 0);
+    static const KFn kfn[8] = {k_prilen<false, false, false, 5>, k_prilen<false, false, true, 5>,
+                               k_prilen<false, true, false, 5>,  k_prilen<false, true, true, 5>,
+                               k_prilen<true, false, false>,     k_prilen<true, false, true>,
+                               k_prilen<true, true, false>,      k_prilen<true, true, true>};
+    const int sel = (A.msize == 6 ? 4 : 0) | (A.ptag ? 2 : 0) | (A.npar ? 1 : 0);
     hipLaunchKernelGGL(kfn[sel], dim3(nb), dim3(256), 0, s, A, parts + 1);
   }
   LenPart *mid = parts + 1 + nb;

@@ -33,6 +33,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <unordered_set>
+#include <type_traits>
 #include <vector>
 #include "pmx_internal.h"
 
@@ -461,13 +462,23 @@ __device__ __forceinline__ int rotate_step(const TetRec &r, int a, int b, int &k
 // A shell record: from the workgroup's LDS batches when the tet is one of
 // them (the current and the previous batch of 256 records: the in-cell and
 // x-neighbour shells of a lexicographic numbering), else from HBM.
-__device__ __forceinline__ TetRec shell_rec(const StatArgs &A, const TetRec (*srec)[256],
-                                            const long long *kbase, int c) {
-  const unsigned long long d0 = (unsigned long long)((long long)c - kbase[0]);
-  const unsigned long long d1 = (unsigned long long)((long long)c - kbase[1]);
+// L (lean): the batch bases and the tet index in 32-bit arithmetic (tet
+// indices < 2^31; the no-batch sentinel is 2^31 modulo 2^32): prilen is
+// VALU-bound, and these are on every shell step.
+template <bool L>
+__device__ __forceinline__ TetRec shell_rec(const StatArgs &A, const TetRec (*srec)[256], long long kb0,
+                                            long long kb1, int c) {
+  int idx;
+  if constexpr (L) {
+    const unsigned d0 = (unsigned)c - (unsigned)kb0, d1 = (unsigned)c - (unsigned)kb1;
+    idx = d0 < 256u ? (int)d0 : (d1 < 256u ? 256 + (int)d1 : -1);
+  } else {
+    const unsigned long long d0 = (unsigned long long)((long long)c - kb0);
+    const unsigned long long d1 = (unsigned long long)((long long)c - kb1);
+    idx = d0 < 256ull ? (int)d0 : (d1 < 256ull ? 256 + (int)d1 : -1);
+  }
   // one LDS index into both batches (no select between LDS and global
   // pointers: the loads stay in their own address spaces)
-  const int idx = d0 < 256ull ? (int)d0 : (d1 < 256ull ? 256 + (int)d1 : -1);
   TetRec r;
   if (idx >= 0) {
     const int4 *l = reinterpret_cast<const int4 *>(&srec[0][0]) + 2 * idx;
@@ -489,9 +500,12 @@ __device__ __forceinline__ TetRec shell_rec(const StatArgs &A, const TetRec (*sr
 // records of c0/c1, loaded by the caller (with the edge's points, in one
 // round trip) and then one step ahead; without point tags an index alone
 // decides, so a record is only loaded when the rotation goes on through it.
-template <bool TAGS>
-__device__ __forceinline__ bool owns_edge(const StatArgs &A, const TetRec (*srec)[256], const long long *kbase, int64_t k,
-                          int a, int b, int c0, int c1, int keep0, int keep1, TetRec r0, TetRec r1) {
+template <bool TAGS, bool L>
+__device__ __forceinline__ bool owns_edge(const StatArgs &A, const TetRec (*srec)[256], long long kb0, long long kb1,
+                                          int64_t k64, int a, int b, int c0, int c1, int keep0, int keep1,
+                                          TetRec r0, TetRec r1) {
+  using KT = typename std::conditional<L, int, int64_t>::type;
+  const KT k = (KT)k64;
   for (int guard = 0; guard < 4096; guard++) {
     if (c0 == (int)k) c0 = 0;                    // a direction that wrapped around
     if (c1 == (int)k) c1 = 0;
@@ -519,8 +533,8 @@ __device__ __forceinline__ bool owns_edge(const StatArgs &A, const TetRec (*srec
       if ((need0 && c0 < k) || (need1 && c1 < k)) return false;
       if (need0 && c0 == c1) return true;
     }
-    if (need0) r0 = shell_rec(A, srec, kbase, c0);
-    if (need1) r1 = shell_rec(A, srec, kbase, c1);
+    if (need0) r0 = shell_rec<L>(A, srec, kb0, kb1, c0);
+    if (need1) r1 = shell_rec<L>(A, srec, kb0, kb1, c1);
   }
   return true;
 }
@@ -542,7 +556,7 @@ __device__ __forceinline__ bool owns_edge(const StatArgs &A, const TetRec (*srec
 // 125M tets; a fused version with one round trip per dependent load and
 // partial rounds after every batch: 7.2 ms.)
 #define LEN_QCAP 2048                 // > 255 left over + 6 * 256 queued
-template <bool ANI, bool TAGS, bool PAR, int W = 1>
+template <bool ANI, bool TAGS, bool PAR, int W = 1, bool L = false>
 __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
   __shared__ TetRec srec[2][256];
   __shared__ unsigned short q[LEN_QCAP];
@@ -567,7 +581,8 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
     int4 *srow = reinterpret_cast<int4 *>(&srec[0][tid]);
     srow[0] = recs[2 * kn];
     srow[1] = recs[2 * kn + 1];
-    if (tid == 0) { kbase[0] = k0; kbase[1] = -(1LL << 40); }   // no second batch yet
+    // no second batch yet: a base no index reaches, in 64 and in 32 bits
+    if (tid == 0) { kbase[0] = k0; kbase[1] = -(1LL << 40) + (1LL << 31); }
     __syncthreads();
   }
 
@@ -622,6 +637,7 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
     unsigned nr = avail >> 8;
     if (!more) nr = (avail + 255u) >> 8;
     else if (head + (nr << 8) < prev_end) nr++;
+    const long long kb0 = kbase[0], kb1 = kbase[1];   // fixed during the rounds
     for (unsigned r = 0; r < nr; r++) {
       const unsigned cnt = min(256u, tail - head);
       bool on = false;
@@ -632,18 +648,19 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
         const int eb = (int)(it >> 11), slot = (int)((it >> 3) & 255u), ia = (int)(it & 7u);
         // the record's fields by LDS address (no per-lane selects)
         const int *sv = srec[eb][slot].v, *sn = srec[eb][slot].nb;
-        const int64_t kk = kbase[eb] + slot;
+        const int64_t kk = (eb ? kb1 : kb0) + slot;
         const int o0 = oth0(ia), o1 = oth1(ia);
         const int a = sv[iare0(ia)], b = sv[iare1(ia)], keep0 = sv[o1], keep1 = sv[o0];
         const int c0 = sn[o0], c1 = sn[o1];
         // the first rotation step's records, issued with the points' loads
         TetRec r0{}, r1{};
-        if (c0) r0 = shell_rec(A, srec, kbase, c0);
-        if (c1) r1 = shell_rec(A, srec, kbase, c1);
+        if (c0) r0 = shell_rec<L>(A, srec, kb0, kb1, c0);
+        if (c1) r1 = shell_rec<L>(A, srec, kb0, kb1, c1);
         len = edge_len_t<ANI>(A, a, b);
-        on = owns_edge<TAGS>(A, srec, kbase, kk, a, b, c0, c1, keep0, keep1, r0, r1) &&
+        on = owns_edge<TAGS, L>(A, srec, kb0, kb1, kk, a, b, c0, c1, keep0, keep1, r0, r1) &&
              !(PAR && par_excluded(A, a, b));
-        key = LEN_STEP2 + 6 * kk + ia;
+        if constexpr (L) key = LEN_STEP2 + (long long)(6u * (unsigned)kk + (unsigned)ia);   // 6 ne < 2^32
+        else key = LEN_STEP2 + 6 * kk + ia;
       }
       acc.add(on, len, key);
       head += cnt;
@@ -1042,11 +1059,20 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
     // the isotropic variants held to 5 waves per SIMD (96 VGPRs, a few
     // spills): 2 % faster at the C5 share; the anisotropic ones spill too
     // much there (4.46 instead of 3.63 ms) and keep the compiler's choice
-    static const KFn kfn[8] = {k_prilen<false, false, false, 5>, k_prilen<false, false, true, 5>,
-                               k_prilen<false, true, false, 5>,  k_prilen<false, true, true, 5>,
-                               k_prilen<true, false, false>,     k_prilen<true, false, true>,
-                               k_prilen<true, true, false>,      k_prilen<true, true, true>};
-    const int sel = (A.msize == 6 ? 4 : 0) | (A.ptag ? 2 : 0) | (A.npar ? 1 : 0);
+    static const KFn kfn[16] = {
+        k_prilen<false, false, false, 5>,        k_prilen<false, false, true, 5>,
+        k_prilen<false, true, false, 5>,         k_prilen<false, true, true, 5>,
+        k_prilen<true, false, false>,            k_prilen<true, false, true>,
+        k_prilen<true, true, false>,             k_prilen<true, true, true>,
+        k_prilen<false, false, false, 5, true>,  k_prilen<false, false, true, 5, true>,
+        k_prilen<false, true, false, 5, true>,   k_prilen<false, true, true, 5, true>,
+        k_prilen<true, false, false, 1, true>,   k_prilen<true, false, true, 1, true>,
+        k_prilen<true, true, false, 1, true>,    k_prilen<true, true, true, 1, true>};
+    // lean 32-bit index arithmetic while 6 ne + 5 fits 32 bits (PMX_PRILEN_WIDE=1:
+    // the 64-bit variant, for the A/B)
+    static const bool wide = getenv("PMX_PRILEN_WIDE") != nullptr;
+    const bool lean = !wide && A.ne < 700000000LL;
+    const int sel = (lean ? 8 : 0) | (A.msize == 6 ? 4 : 0) | (A.ptag ? 2 : 0) | (A.npar ? 1 : 0);
     hipLaunchKernelGGL(kfn[sel], dim3(nb), dim3(256), 0, s, A, parts + 1);
   }
   LenPart *mid = parts + 1 + nb;

@@ -398,6 +398,22 @@ struct LenAcc {
     if (len < lmin || (len == lmin && key < kmin)) { lmin = len; kmin = key; }
     if (len > lmax || (len == lmax && key < kmax)) { lmax = len; kmax = key; }
   }
+  // add() for a lane whose keys strictly increase from call to call (k_prilen:
+  // lane t takes ring entry head + t of every round, and the ring is in key
+  // order): an equal length never has the smaller key, so the extrema need no
+  // key tie-break (the cross-lane tie-breaks stay in store())
+  __device__ void add_ordered(bool on, double len, long long key) {
+    if (!on) return;
+    if (len == 0.0) { atomicAdd(&cnt[9], 1u); return; }
+    int bin = 0;
+#pragma unroll
+    for (int i = 1; i < 9; i++) bin += (len >= BD[i]) ? 1 : 0;
+    if (!(len >= 0.0)) bin = 8;
+    atomicAdd(&cnt[bin], 1u);
+    avlen += len;
+    if (len < lmin) { lmin = len; kmin = key; }
+    if (len > lmax) { lmax = len; kmax = key; }
+  }
   // one LenPart per workgroup: wave shuffles of the per-lane fields, the 4
   // wave results in order, the LDS counters
   __device__ void store(LenPart *out) const {
@@ -662,7 +678,8 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
         if constexpr (L) key = LEN_STEP2 + (long long)(6u * (unsigned)kk + (unsigned)ia);   // 6 ne < 2^32
         else key = LEN_STEP2 + 6 * kk + ia;
       }
-      acc.add(on, len, key);
+      if constexpr (L) acc.add_ordered(on, len, key);
+      else acc.add(on, len, key);
       head += cnt;
     }
     if (more) {                                  // no entry of the previous batch is left

@@ -550,8 +550,11 @@ static void launch_walk_t(const VolArgs &a, int64_t nb, hipStream_t s) {
     if (a.inline_ties) hipLaunchKernelGGL((k_walk<LAYOUT, S, true>), dim3((unsigned)nb), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_walk<LAYOUT, S, false>), dim3((unsigned)nb), dim3(256), 0, s, a);
   } else if (a.wrec && a.exp != 6) {           // exp 6: walk on the 32-B records (A/B)
-    if (a.inline_ties) hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true>), dim3((unsigned)nb), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_walks<LAYOUT, S, false, true>), dim3((unsigned)nb), dim3(256), 0, s, a);
+    // exp 11 / 12: 128- / 64-thread workgroups (A/B of the dispatch granularity)
+    const unsigned bs = a.exp == 11 ? 128u : a.exp == 12 ? 64u : 256u;
+    const unsigned nbb = (unsigned)((a.nlist + bs - 1) / bs);
+    if (a.inline_ties) hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true>), dim3(nbb), dim3(bs), 0, s, a);
+    else hipLaunchKernelGGL((k_walks<LAYOUT, S, false, true>), dim3(nbb), dim3(bs), 0, s, a);
   } else {
     if (a.inline_ties) hipLaunchKernelGGL((k_walks<LAYOUT, S, true, false>), dim3((unsigned)nb), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_walks<LAYOUT, S, false, false>), dim3((unsigned)nb), dim3(256), 0, s, a);

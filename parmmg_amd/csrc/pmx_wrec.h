@@ -1,0 +1,77 @@
+// pmx_wrec.h -- the tet record and the volume walk's compact copy of it.
+// Plain C++ apart from the host/device qualifiers, so that host-only tests
+// (tests/c/wrec_roundtrip.cpp, built with g++) share the encoding with the
+// kernels.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define PMX_HD __host__ __device__ __forceinline__
+#else
+#define PMX_HD inline
+#endif
+
+struct alignas(32) TetRec { int v[4]; int nb[4]; };
+
+// Compact walk record: the volume walk's copy of tets[k] in 24 B (5.33 records
+// per 128-B line instead of 4; the walk is bound by the tet lines it touches).
+// v[0] as is (<= 0: !MG_EOK), v[1..3] as 20-bit deltas from v[0], nb[f] as
+// 24-bit deltas from k (WREC_NONE: boundary face).  Six words:
+//   w0 = v0            w1 = dn0 | dv1[0:8)<<24   w2 = dn1 | dv1[8:16)<<24
+//   w3 = dn2 | dv1[16:20)<<24 | flags<<28       w4 = dn3 | dv2[0:8)<<24
+//   w5 = dv2[8:20) | dv3<<12
+// A tet whose deltas do not fit gets WREC_ESC and is read from tets[] (a
+// Mmg mesh after its Scotch renumbering, like the generator's, has none).
+struct alignas(8) WRec { unsigned w[6]; };
+#define WREC_NONE (-(1 << 23))
+#define WREC_ESC 1u
+
+PMX_HD void wrec_encode(const TetRec &t, int64_t k, WRec &r) {
+  for (int i = 0; i < 6; i++) r.w[i] = 0u;
+  r.w[0] = (unsigned)t.v[0];
+  if (t.v[0] <= 0) return;                        // never walked through
+  bool esc = false;
+  int dv[4] = {0, 0, 0, 0}, dn[4];
+  for (int i = 1; i < 4; i++) {
+    const int64_t d = (int64_t)t.v[i] - t.v[0];
+    esc = esc || d < -(1 << 19) || d >= (1 << 19);
+    dv[i] = (int)d;
+  }
+  for (int f = 0; f < 4; f++) {
+    const int64_t d = (int64_t)t.nb[f] - k;
+    esc = esc || (t.nb[f] != 0 && (d <= WREC_NONE || d >= (1 << 23)));
+    dn[f] = t.nb[f] ? (int)d : WREC_NONE;
+  }
+  if (esc) { r.w[3] = WREC_ESC << 28; return; }
+  const unsigned m24 = 0xffffffu;
+  r.w[1] = ((unsigned)dn[0] & m24) | (((unsigned)dv[1] & 0xffu) << 24);
+  r.w[2] = ((unsigned)dn[1] & m24) | ((((unsigned)dv[1] >> 8) & 0xffu) << 24);
+  r.w[3] = ((unsigned)dn[2] & m24) | ((((unsigned)dv[1] >> 16) & 0xfu) << 24);
+  r.w[4] = ((unsigned)dn[3] & m24) | (((unsigned)dv[2] & 0xffu) << 24);
+  r.w[5] = (((unsigned)dv[2] >> 8) & 0xfffu) | ((unsigned)dv[3] << 12);
+}
+
+PMX_HD int wrec_nb(unsigned w, int k) {
+  const int d = (int)(w << 8) >> 8;               // sign-extended 24 bits
+  return d == WREC_NONE ? 0 : k + d;
+}
+
+// tets[k] from its compact record r (escapes read the full record).  Decoded
+// before the escape test, so that a caller's record load is one load (a test
+// first would split off the flag word into a dependent load of its own).
+PMX_HD TetRec wrec_decode(const WRec &r, const TetRec *__restrict__ tets, int k) {
+  const int v0 = (int)r.w[0];
+  const unsigned u1 = (r.w[1] >> 24) | ((r.w[2] >> 24) << 8) | (((r.w[3] >> 24) & 0xfu) << 16);
+  const unsigned u2 = (r.w[4] >> 24) | ((r.w[5] & 0xfffu) << 8);
+  TetRec t;
+  t.v[0] = v0;
+  t.v[1] = v0 + ((int)(u1 << 12) >> 12);
+  t.v[2] = v0 + ((int)(u2 << 12) >> 12);
+  t.v[3] = v0 + ((int)r.w[5] >> 12);
+  t.nb[0] = wrec_nb(r.w[1], k);
+  t.nb[1] = wrec_nb(r.w[2], k);
+  t.nb[2] = wrec_nb(r.w[3], k);
+  t.nb[3] = wrec_nb(r.w[4], k);
+  if ((r.w[3] >> 28) & WREC_ESC) t = tets[k];
+  return t;
+}

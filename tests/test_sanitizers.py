@@ -78,3 +78,19 @@ def test_dropin_demo_runs_under_asan_ubsan():
     r = subprocess.run([_demo_asan()], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "dropin ok" in r.stdout
+
+
+def test_compact_walk_records_roundtrip_under_asan_ubsan():
+    """The walk's 24-B records (parmmg_amd/csrc/pmx_wrec.h, shared with the
+    kernels) decode to the full tet record for every valid tet: packed deltas
+    at and past their 20/24-bit limits, boundary faces, escapes, deleted tets."""
+    os.makedirs(BUILD, exist_ok=True)
+    exe = os.path.join(BUILD, "wrec_roundtrip")
+    cmd = ["g++", "-std=c++17", "-Wall", *SAN, "-I", os.path.join(ROOT, "parmmg_amd", "csrc"),
+           os.path.join(ROOT, "tests", "c", "wrec_roundtrip.cpp"), "-o", exe]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    env = dict(os.environ, UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "wrec roundtrip ok" in r.stdout

@@ -41,15 +41,18 @@ __device__ __forceinline__ int wclamp(double t, int n) {
 
 // empty hint cell: nearest non-empty cell in growing shells (rare; kept out of
 // line so that its loops do not inflate the walk's register allocation)
-__device__ __noinline__ int hint_search(const int *grid, GridDesc g, int cx, int cy, int cz) {
+// (the grid's dims as scalars: a GridDesc argument of this out-of-line call
+// would be passed through scratch, 16 -> 112 B per lane in k_walks)
+__device__ __noinline__ int hint_search(const int *grid, int gx, int gy, int gz, int cx, int cy,
+                                        int cz) {
   for (int r = 1; r <= 3; r++) {
     for (int dz = -r; dz <= r; dz++)
       for (int dy = -r; dy <= r; dy++)
         for (int dx = -r; dx <= r; dx++) {
           if (max(abs(dx), max(abs(dy), abs(dz))) != r) continue;
           int x = cx + dx, y = cy + dy, z = cz + dz;
-          if (x < 0 || y < 0 || z < 0 || x >= g.dim[0] || y >= g.dim[1] || z >= g.dim[2]) continue;
-          int kk = grid[gcell(g, x, y, z)];
+          if (x < 0 || y < 0 || z < 0 || x >= gx || y >= gy || z >= gz) continue;
+          int kk = grid[(int64_t)x + (int64_t)gx * ((int64_t)y + (int64_t)gy * z)];
           if (kk) return kk;
         }
   }
@@ -61,7 +64,7 @@ __device__ __forceinline__ int walk_hint(const int *grid, const GridDesc &g, D3 
   int cy = wclamp((p.y - g.lo[1]) * g.inv[1], g.dim[1]);
   int cz = wclamp((p.z - g.lo[2]) * g.inv[2], g.dim[2]);
   int k = grid[gcell(g, cx, cy, cz)];
-  return k ? k : hint_search(grid, g, cx, cy, cz);
+  return k ? k : hint_search(grid, g.dim[0], g.dim[1], g.dim[2], cx, cy, cz);
 }
 
 // numerators of the barycentrics: lambda_f = -num_f / vol, with exactly the

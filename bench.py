@@ -354,6 +354,7 @@ def main():
     k_ms = {name: tr.kernel_ms(i) for i, name in enumerate(["hint", "vol", "bdy", "exhaustive", "total",
                                                             "derive"])}
     st = tr.locate_stats()
+    st["volume_waves"] = tr.wave_stats(0)
     # the same step on a background already prepared by an earlier step (what
     # repeated steps on one background cost; reported, never `value`)
     sync()

@@ -158,6 +158,16 @@ int pmx_download_starts(pmx_ctx *ctx, int *start);
 /* Per-point reference-style extras for boundary points: edge/vertex (-1 unset). */
 int pmx_download_border(pmx_ctx *ctx, int *edge, int *vertex);
 int pmx_locate_stats_get(pmx_ctx *ctx, pmx_locate_stats *st);
+/* Lane utilisation of the last step's walks (path 0 volume, 1 surface): a
+ * wave iterates until its longest walk ends, so step_sum / lane_steps is the
+ * fraction of lane-steps that did work.  Over the walk's per-wave records:
+ * located points, their summed steps, 64 x the longest walk of each wave,
+ * and the waves by their longest walk (entry 15: 15 steps or more). */
+typedef struct {
+  int64_t waves, located, step_sum, lane_steps;
+  int64_t wave_max_hist[16];
+} pmx_wave_stats;
+int pmx_locate_wave_stats(pmx_ctx *ctx, int path, pmx_wave_stats *st);
 
 /* Device pointers of the resident result buffers (for collectives / chaining):
  * which = 0 packed solutions [npts][S], 1 elem, 2 status. */

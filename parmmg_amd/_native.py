@@ -48,6 +48,11 @@ class LocateStats(C.Structure):
     ]
 
 
+class WaveStats(C.Structure):
+    _fields_ = [("waves", i64), ("located", i64), ("step_sum", i64), ("lane_steps", i64),
+                ("wave_max_hist", i64 * 16)]
+
+
 class RunOpts(C.Structure):
     _fields_ = [
         ("hint_stride", C.c_int), ("max_walk", C.c_int),
@@ -137,6 +142,7 @@ SIGNATURES = {
     "pmx_download_starts": (C.c_int, [C.c_void_p, iptr]),
     "pmx_download_border": (C.c_int, [C.c_void_p, iptr, iptr]),
     "pmx_locate_stats_get": (C.c_int, [C.c_void_p, C.POINTER(LocateStats)]),
+    "pmx_locate_wave_stats": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(WaveStats)]),
     "pmx_device_buffer": (C.c_void_p, [C.c_void_p, C.c_int]),
     "pmx_device_alloc": (C.c_void_p, [C.c_void_p, C.c_size_t]),
     "pmx_device_free": (C.c_int, [C.c_void_p, C.c_void_p]),

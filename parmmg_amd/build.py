@@ -75,15 +75,43 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError("build failed: " + " ".join(cmd))
 
 
+def _jobs() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(8, n))
+
+
 def build_transfer(force: bool = False) -> str:
+    """One object per source file, compiled in parallel (the kernels and their
+    launch functions share a file, so no relocatable device code is needed),
+    then one link."""
+    from concurrent.futures import ThreadPoolExecutor
     srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES]
-    deps = srcs + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
-    deps.append(os.path.join(INC, "pmx_transfer.h"))
+    hdrs = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
+    hdrs.append(os.path.join(INC, "pmx_transfer.h"))
+    deps = srcs + hdrs
     if force or _stale(TRANSFER_SO, deps):
         with _locked("transfer"):
             if force or _stale(TRANSFER_SO, deps):
+                odir = os.path.join(PKG, "build", "obj")
+                os.makedirs(odir, exist_ok=True)
+                cflags = [f for f in HIPCC_FLAGS if f not in ("-shared",) and not f.startswith(("-l", "-L", "-Wl"))]
+                lflags = [f for f in HIPCC_FLAGS if f == "-shared" or f.startswith(("-l", "-L", "-Wl"))]
+
+                def obj(src: str) -> str:
+                    o = os.path.join(odir, os.path.basename(src) + ".o")
+                    if force or _stale(o, [src] + hdrs):
+                        tmp = o + f".{os.getpid()}.tmp"
+                        _run([_hipcc(), *cflags, "-c", "-I", INC, "-I", CSRC, src, "-o", tmp])
+                        os.replace(tmp, o)
+                    return o
+
+                with ThreadPoolExecutor(_jobs()) as ex:
+                    objs = list(ex.map(obj, srcs))
                 tmp = TRANSFER_SO + f".{os.getpid()}.tmp"
-                _run([_hipcc(), *HIPCC_FLAGS, "-I", INC, "-I", CSRC, *srcs, "-o", tmp])
+                _run([_hipcc(), "--offload-arch=gfx950", *objs, *lflags, "-o", tmp])
                 os.replace(tmp, TRANSFER_SO)
     return TRANSFER_SO
 

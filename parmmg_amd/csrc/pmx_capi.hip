@@ -802,6 +802,35 @@ static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &o
   A.exp = (opts.flags >> PMX_RUN_EXP_SHIFT) & 0xff;
 }
 
+// pmx_run_opts.flags: the public PMX_RUN_* bits, plus the experiment switch
+// in bits 16-23 (VolArgs.exp).  Switches that keep the results bit for bit
+// (A/Bs of layouts, launch shapes and stream order) are always accepted; the
+// measurement switches that skip work (4: no interpolation, 5: hint only)
+// only when PMX_EXPERIMENTS=1 is set in the environment; anything else is
+// refused, so that a stray bit never changes results silently.
+static bool run_flags_valid(int flags, std::string *err) {
+  const int pub = PMX_RUN_REFERENCE_WALK | PMX_RUN_NO_INLINE_TIES | PMX_RUN_RECORD_STARTS |
+                  PMX_RUN_SERIAL_SURFACE | PMX_RUN_FRESH_BACKGROUND | PMX_RUN_DEBUG_BARRIER_TIMEOUT;
+  if (flags & ~(pub | (0xff << PMX_RUN_EXP_SHIFT))) {
+    *err = "pmx_run: unknown flag bits";
+    return false;
+  }
+  const int e = (flags >> PMX_RUN_EXP_SHIFT) & 0xff;
+  switch (e) {
+    case 0: case 6: case 9: case 10: case 11: case 12: case 13: case 14: case 15:
+      return true;
+    case 4: case 5: {
+      const char *v = getenv("PMX_EXPERIMENTS");
+      if (v && v[0] == '1') return true;
+      *err = "pmx_run: measurement switch needs PMX_EXPERIMENTS=1";
+      return false;
+    }
+    default:
+      *err = "pmx_run: unknown experiment switch";
+      return false;
+  }
+}
+
 int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   if (!ctx) return 0;
   ctx->ran = false;
@@ -810,6 +839,7 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   pmx_run_opts opts{};
   if (o) opts = *o;
   if (opts.hint_stride < 0 || opts.max_walk < 0) { ctx->err = "pmx_run: bad options"; return 0; }
+  if (!run_flags_valid(opts.flags, &ctx->err)) return 0;
   const int64_t n = ctx->nq;
   const int S = ctx->sd.S;
   if (!dgrow(ctx, ctx->d_out, (size_t)std::max<int64_t>(n * S, 1))) return 0;
@@ -846,7 +876,9 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     CK(hipEventRecord(ctx->ev_fork, st));
     CK(hipStreamWaitEvent(side, ctx->ev_fork, 0));
   }
-  if (ev) CK(hipEventRecord(ev[3], ss));
+  // (on the side stream only once it has been forked from the main one: an
+  // unforked side stream's event could precede ev[0])
+  if (ev) CK(hipEventRecord(ev[3], bdy ? ss : st));
   if (bdy && csr) {
     if (!ctx->build_node_trias(ss)) return 0;
     ctx->have_csr = true;
@@ -1054,6 +1086,33 @@ int pmx_locate_stats_get(pmx_ctx *ctx, pmx_locate_stats *st) {
   for (int64_t i = 0; i < ctx->nq; i++)
     if ((kind[(size_t)i] == KIND_VOL || kind[(size_t)i] == KIND_BDY) && status[(size_t)i] == 0) nc++;
   st->nclosest = nc;
+  return 1;
+}
+
+int pmx_locate_wave_stats(pmx_ctx *ctx, int path, pmx_wave_stats *st) {
+  if (!ctx || !st || (path != 0 && path != 1)) {
+    if (ctx) ctx->err = "pmx_locate_wave_stats: bad arguments";
+    return 0;
+  }
+  if (!results_ready(ctx, "pmx_locate_wave_stats")) return 0;
+  int nsel[2] = {0, 0};
+  CK(hipStreamSynchronize(ctx->stream));
+  if (!ctx->check_device_errors()) return 0;
+  if (ctx->nq) CK(hipMemcpy(nsel, ctx->d_nsel.p, sizeof nsel, hipMemcpyDeviceToHost));
+  memset(st, 0, sizeof *st);
+  const int64_t npath = nsel[path];
+  if (!npath) return 1;
+  std::vector<uint4> w((size_t)((npath + 255) / 256 * 4));
+  CK(hipMemcpy(w.data(), path ? ctx->d_bstat.p : ctx->d_vstat.p, w.size() * sizeof(uint4),
+               hipMemcpyDeviceToHost));
+  for (const uint4 &r : w) {
+    if (!r.x) continue;
+    st->waves++;
+    st->located += r.x;
+    st->step_sum += r.y;
+    st->lane_steps += 64 * (int64_t)r.z;
+    st->wave_max_hist[std::min<unsigned>(r.z, 15u)]++;
+  }
   return 1;
 }
 

@@ -85,7 +85,7 @@ void launch_exhaustive(const ExhArgs &e, const VolArgs &v, int blocks, hipStream
 void launch_const_metric(const int8_t *kind, int64_t nq, double *out, int S, int off, int size,
                          double hsiz, uint8_t *wmask, int imet, hipStream_t s);
 // the step's first launch zeroes up to PMX_ZERO_MAX device ranges
-#define PMX_ZERO_MAX 6
+#define PMX_ZERO_MAX 3
 struct ZeroRanges {
   void *p[PMX_ZERO_MAX];
   int64_t bytes[PMX_ZERO_MAX];

@@ -450,8 +450,9 @@ void launch_const_metric(const int8_t *kind, int64_t nq, double *out, int S, int
                      size, hsiz, wmask, imet);
 }
 
-// the step's first launch: zero the write masks, the step's counters, the
-// hint grid, the orphan marks, the node -> trias counts (whichever are given)
+// the step's first launch: zero the ranges pmx_run adds -- the write masks,
+// the step's counters and the volume hint grid (the orphan marks come from
+// the host, the node -> trias counts are zeroed by their own builder)
 __global__ __launch_bounds__(256) void k_prologue(ZeroRanges z) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
   for (int r = 0; r < z.n; r++) {

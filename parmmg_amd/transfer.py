@@ -225,6 +225,18 @@ class Transfer:
         self._chk(self.lib.pmx_locate_stats_get(self.ctx, C.byref(st)), "pmx_locate_stats_get")
         return {f: getattr(st, f) for f, _ in N.LocateStats._fields_}
 
+    def wave_stats(self, path: int = 0) -> dict:
+        """Lane utilisation of the last step's walks (path 0 volume, 1 surface):
+        step_sum / lane_steps, lane_steps = sum over waves of 64 x the wave's
+        longest walk; wave_max_hist = waves by their longest walk."""
+        st = N.WaveStats()
+        self._chk(self.lib.pmx_locate_wave_stats(self.ctx, path, C.byref(st)), "pmx_locate_wave_stats")
+        d = {f: getattr(st, f) for f, _ in N.WaveStats._fields_}
+        d["wave_max_hist"] = list(st.wave_max_hist)
+        d["lane_utilization"] = st.step_sum / st.lane_steps if st.lane_steps else None
+        d["mean_wave_max"] = st.lane_steps / 64 / st.waves if st.waves else None
+        return d
+
     def kernel_ms(self, which: int) -> float:
         return self.lib.pmx_kernel_ms(self.ctx, which)
 

@@ -65,6 +65,21 @@ def split_partitions(m, cut: float = 0.5):
     return out, len(shared)
 
 
+def first_visit_order(tets_mmg: np.ndarray, npts: int) -> np.ndarray:
+    """The order in which the reference's vertex loop reaches the new points
+    (src/interpmesh_pmmg.c:535-544): new tets ie = 1..ne, valid ones only
+    (MG_EOK: v[0] > 0), their vertices iloc = 0..3, each point at its first
+    visit.  tets_mmg: (ne+1, 4), Mmg layout (1-based, row 0 unused); returns
+    0-based point indices (points in no valid tet are not visited).  The
+    oracle given this order runs the reference's sequential loop: the start
+    tet / tria and the surface point flags carry over along it."""
+    t = np.asarray(tets_mmg)[1:]
+    flat = t[t[:, 0] > 0].ravel().astype(np.int64) - 1
+    flat = flat[(flat >= 0) & (flat < npts)]
+    _, first = np.unique(flat, return_index=True)
+    return flat[np.sort(first)]
+
+
 def bits_equal(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     """Row-wise bitwise equality of float64 arrays (NaN == NaN)."""
     a = np.ascontiguousarray(a, np.float64).view(np.int64)

@@ -10,7 +10,7 @@ interpolated as usual while the metric stays constant.
 import numpy as np
 import pytest
 
-from helpers import bits_equal, compare_volume
+from helpers import bits_equal, compare_exact, compare_volume
 from oracle import oracle as O
 from parmmg_amd import mesh as M
 
@@ -81,18 +81,25 @@ def test_c1_constant_size_with_level_set(transfer, metric):
     # give them; the seam's field must be that step's bit for bit
     transfer.upload_background(m, [ls], -1)
     transfer.upload_points(x, t)
-    transfer.run()
+    transfer.run(record_starts=True)
     r = transfer.download(init=[np.full((len(x), 1), SENT)])
+    starts = transfer.starts()
+    edge, vert = transfer.border()
     assert bits_equal(f, r.sols[0]).all()
     o = O.Oracle(m)
     outs, elem, st, *_ = o.interp(x, t, [ls], imet=-1, init=[np.full((len(x), 1), SENT)])
     c = compare_volume(o, x, t, ([f], r.elem, r.status), (outs, elem, st), [ls])
     assert c["nvol"] == int((t == 0).sum())
     assert c["same"] >= c["nvol"] - max(3, c["nvol"] // 1000)
-    # surface points: a field value within the range of the background's
-    # (3-point interpolation of a linear-ish level set on the cube faces)
-    bdy = ((t & M.TAG_BDY) != 0) & ~(nul | req)
-    assert np.all(np.isfinite(f[bdy]))
+    # surface points (frozen and invalid ones aside): bit-exact against the
+    # oracle in device semantics -- each query from the device's start tria,
+    # the point flags as PMMG_precompute_nodeTrias leaves them -- elements,
+    # edge / vertex classification, status and the interpolated level set
+    bdy = np.nonzero(((t & M.TAG_BDY) != 0) & ~(nul | req))[0]
+    assert len(bdy) > 0
+    so, se, ss, _, sed, sve = o.interp(x, t, [ls], imet=-1, order=bdy, fresh=True, start_vol=starts,
+                                       start_bdy=starts, init=[np.full((len(x), 1), SENT)])
+    compare_exact(([f], r.elem, r.status, edge, vert), (so, se, ss, sed, sve), bdy, 1)
 
 
 def test_c1_constant_size_step_ani(transfer):

@@ -1,13 +1,15 @@
 """The BASELINE.json configurations on one GPU, against the oracle.
 
 * C2 / C3 at their full benchmark sizes (the meshes bench.py builds): every
-  volume point bit-exact vs the carry-over oracle or a documented tie; a
+  volume point bit-exact vs the oracle's sequential run in the reference's
+  own vertex order (first visit through the new tets) or a documented tie; a
   sample of the surface points bit-exact vs the oracle in device semantics;
   every surface point that differs from the reference's SEQUENTIAL run falls
   in a documented class (a containing tria, or a shadow wedge/cone acceptance
   within hausd of the returned edge/vertex).
-* C4 per-GPU share: two ParMmg groups in two contexts whose steps -- and
-  whose fallback grid barriers -- run concurrently on the GPU.
+* C4 per-GPU share: the bench's two 25M-tet groups in two contexts, steps
+  overlapping on the device, each checked like C2 / C3; and two small
+  non-convex groups whose fallback grid barriers run concurrently.
 * C5 per-GPU share (n = 275, 124.8M tets): the statistics counts against the
   analytic Kuhn-cube counts, and the device partials of two groups reduced
   across two ranks (gloo) against the oracle on the union.
@@ -19,7 +21,7 @@ import numpy as np
 import pytest
 
 import bench
-from helpers import bits_equal, compare_exact, compare_volume, lin_field
+from helpers import bits_equal, compare_exact, compare_volume, first_visit_order, lin_field
 from oracle import oracle as O
 from parmmg_amd import mesh as M
 from parmmg_amd.transfer import Transfer
@@ -44,76 +46,87 @@ def _tria_dist_classes(m, x, idx, elem, edge, vert):
 
 
 @pytest.mark.timeout(1100)
-@pytest.mark.parametrize("cfg", ["C2", "C3"])
+@pytest.mark.parametrize("cfg", ["C2", "C3", "C4"])
 def test_full_size_parity(cfg):
     """Bench-size parity (the bench's own inputs, its new tets included, so the
-    step's vertex enumeration and orphan marks run at full size).
+    step's vertex enumeration and orphan marks run at full size).  C4 is the
+    per-GPU share of the 8-GPU configuration: the bench's two 25M-tet groups
+    in two contexts, their steps enqueued back to back so that they overlap on
+    the device, each group checked on its own.
 
-    Volume: every point bit-exact against the reference's sequential walk or a
-    verified tie.  Surface (src/locate_pmmg.c:209-334,587-723, path
-    dependent): bit-exact in device semantics on >= 5 % of the points; against
-    the reference's sequential run, every point where the two differ is
-    checked on BOTH sides -- each answer is a containing tria or a wedge/cone
-    acceptance within hausd of its edge/vertex -- and where both contain the
-    point a linear field is reproduced to 1e-12 by both."""
-    m, x, t, sols, tv = bench.build_case(bench.CONFIGS[cfg], 0)
-    lin = (1.0 + 2.0 * m.xyz[:, 0] - 3.0 * m.xyz[:, 1] + 0.5 * m.xyz[:, 2])[:, None]
-    tr = Transfer(0)
-    tr.upload_background(m, sols, 0)
-    tr.upload_points(x, t, tets_mmg=tv)
-    tr.run(record_starts=True)
-    r = tr.download()
-    starts = tr.starts()
-    st = tr.locate_stats()
-    # the surface pass with a linear field beside the bench's solutions
-    sols2 = sols + [lin]
-    tr.upload_background(m, sols2, 0)
-    tr.upload_points(x, t, tets_mmg=tv)
-    tr.run()
-    r2 = tr.download()
-    edge, vert = tr.border()
-    tr.close()
-    o = O.Oracle(m)
-    vol = np.nonzero(t == 0)[0]
-    bdy = np.nonzero(t == M.TAG_BDY)[0]
-    assert st["nvol"] == len(vol) and st["nbdy"] == len(bdy)
-    # volume: the reference's carry-over walk over the Morton-ordered points
-    outs, elem, sto, *_ = o.interp(x, t, sols, imet=0, order=vol)
-    c = compare_volume(o, x, t, (r.sols, r.elem, r.status), (outs, elem, sto), sols)
-    print(f"\n{cfg}: {c['nvol']} volume points, {c['same']} identical elements, {c['ties']} ties")
-    assert c["same"] >= c["nvol"] - max(3, c["nvol"] // 1000)
-    assert np.all(r.status[vol] == 1)
-    # surface, device semantics (each query from the device's start tria, the
-    # point flags as PMMG_precompute_nodeTrias leaves them): 5 % sample
-    rng = np.random.default_rng(1)
-    sample = np.sort(rng.choice(bdy, max(len(bdy) // 20, min(len(bdy), 600)), replace=False))
-    so, se, ss, _, sed, sve = o.interp(x, t, sols2, imet=0, order=sample, fresh=True,
-                                       start_vol=starts, start_bdy=starts)
-    compare_exact((r2.sols, r2.elem, r2.status, edge, vert), (so, se, ss, sed, sve), sample, len(sols2))
-    assert np.array_equal(r.elem[bdy], r2.elem[bdy])
-    # surface, the reference's sequential run: where the answers differ, both
-    # must be acceptable answers of PMMG_locatePointBdy
-    qo, qe, qs, _, qed, qve = o.interp(x, t, sols2, imet=0, order=bdy)
-    diff = bdy[(r2.elem[bdy] != qe[bdy]) | (edge[bdy] != qed[bdy]) | (vert[bdy] != qve[bdy])]
+    The reference's sequential run is the oracle over the points in the order
+    the reference's vertex loop reaches them -- first visit through the new
+    tets (src/interpmesh_pmmg.c:535-544), the start tet / tria and the surface
+    point flags carried along that order.
 
-    def contains(el, ed, vx, stt):
-        return np.array([ed[i] < 0 and vx[i] < 0 and stt[i] == 1 and o.tria_contains(int(el[i]), x[i])
-                         for i in diff], bool)
+    Volume: every point bit-exact against that run or a verified tie.
+    Surface (src/locate_pmmg.c:209-334,587-723, path dependent): bit-exact in
+    device semantics on >= 5 % of the points; against the sequential run,
+    every point where the two differ is checked on BOTH sides -- each answer
+    is a containing tria or a wedge/cone acceptance within hausd of its
+    edge/vertex -- and where both contain the point a linear field is
+    reproduced to 1e-12 by both."""
+    conf = bench.CONFIGS[cfg]
+    cases = [bench.build_case(conf, g) for g in range(conf.get("groups", 1))]
+    trs, sols2 = [], []
+    for m, x, t, sols, tv in cases:
+        lin = (1.0 + 2.0 * m.xyz[:, 0] - 3.0 * m.xyz[:, 1] + 0.5 * m.xyz[:, 2])[:, None]
+        sols2.append(sols + [lin])
+        tr = Transfer(0)
+        tr.upload_background(m, sols2[-1], 0)
+        tr.upload_points(x, t, tets_mmg=tv)
+        trs.append(tr)
+    for tr in trs:                          # every group's step enqueued before any sync
+        tr.run(record_starts=True)
+    got = []
+    for tr in trs:
+        got.append((tr.download(), tr.starts(), tr.border(), tr.locate_stats()))
+        tr.close()
+    for g, ((m, x, t, sols, tv), s2, (r, starts, (edge, vert), st)) in enumerate(zip(cases, sols2, got)):
+        o = O.Oracle(m)
+        vol = np.nonzero(t == 0)[0]
+        bdy = np.nonzero(t == M.TAG_BDY)[0]
+        assert st["nvol"] == len(vol) and st["nbdy"] == len(bdy)
+        fv = first_visit_order(tv, len(x))
+        assert len(fv) == len(x)            # the bench's new mesh has no orphan point
+        # the reference's sequential run, in its own order
+        qo, qe, qs, _, qed, qve = o.interp(x, t, s2, imet=0, order=fv)
+        c = compare_volume(o, x, t, (r.sols, r.elem, r.status), (qo, qe, qs), s2)
+        print(f"\n{cfg} group {g}: {c['nvol']} volume points, {c['same']} identical elements, "
+              f"{c['ties']} ties")
+        assert c["same"] >= c["nvol"] - max(3, c["nvol"] // 1000)
+        assert np.all(r.status[vol] == 1)
+        # surface, device semantics (each query from the device's start tria, the
+        # point flags as PMMG_precompute_nodeTrias leaves them): 5 % sample
+        rng = np.random.default_rng(1)
+        sample = np.sort(rng.choice(bdy, max(len(bdy) // 20, min(len(bdy), 600)), replace=False))
+        so, se, ss, _, sed, sve = o.interp(x, t, s2, imet=0, order=sample, fresh=True,
+                                           start_vol=starts, start_bdy=starts)
+        compare_exact((r.sols, r.elem, r.status, edge, vert), (so, se, ss, sed, sve), sample, len(s2))
+        # surface, the reference's sequential run: where the answers differ, both
+        # must be acceptable answers of PMMG_locatePointBdy
+        diff = bdy[(r.elem[bdy] != qe[bdy]) | (edge[bdy] != qed[bdy]) | (vert[bdy] != qve[bdy])]
 
-    in_dev, in_ref = contains(r2.elem, edge, vert, r2.status), contains(qe, qed, qve, qs)
-    sh_dev = _tria_dist_classes(m, x, diff, r2.elem, edge, vert) <= m.hausd * (1 + 1e-12)
-    sh_ref = _tria_dist_classes(m, x, diff, qe, qed, qve) <= m.hausd * (1 + 1e-12)
-    print(f"{cfg}: {len(bdy)} surface points, {len(sample)} bit-exact in device semantics, "
-          f"{len(diff)} differ from the sequential run (device: {int(in_dev.sum())} containing tria, "
-          f"{int(sh_dev.sum())} wedge/cone within hausd; reference: {int(in_ref.sum())} / {int(sh_ref.sum())})")
-    assert np.all(in_dev | sh_dev), diff[~(in_dev | sh_dev)][:10]
-    assert np.all(in_ref | sh_ref), diff[~(in_ref | sh_ref)][:10]
-    assert len(diff) <= 0.05 * len(bdy)
-    both = diff[in_dev & in_ref]
-    exact = 1.0 + 2.0 * x[both, 0] - 3.0 * x[both, 1] + 0.5 * x[both, 2]
-    li = len(sols2) - 1
-    assert np.abs(r2.sols[li][both, 0] - exact).max(initial=0.0) < 1e-12
-    assert np.abs(qo[li][both, 0] - exact).max(initial=0.0) < 1e-12
+        def contains(el, ed, vx, stt):
+            return np.array([ed[i] < 0 and vx[i] < 0 and stt[i] == 1 and o.tria_contains(int(el[i]), x[i])
+                             for i in diff], bool)
+
+        in_dev, in_ref = contains(r.elem, edge, vert, r.status), contains(qe, qed, qve, qs)
+        sh_dev = _tria_dist_classes(m, x, diff, r.elem, edge, vert) <= m.hausd * (1 + 1e-12)
+        sh_ref = _tria_dist_classes(m, x, diff, qe, qed, qve) <= m.hausd * (1 + 1e-12)
+        print(f"{cfg} group {g}: {len(bdy)} surface points, {len(sample)} bit-exact in device semantics, "
+              f"{len(diff)} differ from the sequential run (device: {int(in_dev.sum())} containing tria, "
+              f"{int(sh_dev.sum())} wedge/cone within hausd; reference: {int(in_ref.sum())} / "
+              f"{int(sh_ref.sum())})")
+        assert np.all(in_dev | sh_dev), diff[~(in_dev | sh_dev)][:10]
+        assert np.all(in_ref | sh_ref), diff[~(in_ref | sh_ref)][:10]
+        assert len(diff) <= 0.05 * len(bdy)
+        both = diff[in_dev & in_ref]
+        exact = 1.0 + 2.0 * x[both, 0] - 3.0 * x[both, 1] + 0.5 * x[both, 2]
+        li = len(s2) - 1
+        assert np.abs(r.sols[li][both, 0] - exact).max(initial=0.0) < 1e-12
+        assert np.abs(qo[li][both, 0] - exact).max(initial=0.0) < 1e-12
+        del o
 
 
 def l_shaped(n, cut=(0.5, 0.5, 0.5)):

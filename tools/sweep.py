@@ -12,6 +12,8 @@ import sys
 
 import numpy as np
 
+# the measurement switches (run flag exp 4 / 5) are refused without it
+os.environ.setdefault("PMX_EXPERIMENTS", "1")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 

@@ -179,6 +179,8 @@ int pmx_device_free(pmx_ctx *ctx, void *p);
 /* Copy bytes of device memory (e.g. such partial records) to the host, after
  * the context stream's earlier work; blocking. */
 int pmx_device_download(pmx_ctx *ctx, void *host, const void *dev, size_t bytes);
+/* and the other way (e.g. an empty partial record of a rank without a group) */
+int pmx_device_upload(pmx_ctx *ctx, void *dev, const void *host, size_t bytes);
 /* Inspection: copy the volume hint grid of the last run to host (cap cells);
  * returns the number of cells (0 on error). */
 int64_t pmx_debug_hint_grid(pmx_ctx *ctx, int *host, int64_t cap);
@@ -232,6 +234,15 @@ typedef struct {
  * groups; inputMet = parmesh->info.inputMet.  Returns 1 ok / 0 fail. */
 int PMX_interpMetricsAndFields(pmx_ctx *ctx, int ngrp, pmx_group *grps,
                                const int *permNodGlob, int inputMet);
+
+/* The same with one context per group: group g on ctxs[g] (caller-owned, all
+ * on one device, e.g. kept across ParMmg iterations).  Every group's step is
+ * enqueued before the first download, and each context keeps its group's new
+ * points, new tets and results until its next upload -- so that
+ * PMMG_tetraQual (src/libparmmg1.c:845) can run on them without a re-upload
+ * (pmx_new_mesh_qual_synced).  Errors in pmx_last_error(ctxs[0]). */
+int PMX_interpMetricsAndFields_groups(pmx_ctx *const *ctxs, int ngrp, pmx_group *grps,
+                                      const int *permNodGlob, int inputMet);
 
 /* PMMG_copyMetricsAndFields_point (src/interpmesh_pmmg.c:432-446) on the
  * caller's host arrays (a host loop: nothing to do on the device). Old-point
@@ -428,6 +439,18 @@ int pmx_prilen(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, pmx_len_st
  * NULL.  Needs a pmx_run on those points. */
 int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, int64_t ne, int opt,
                       int metRidTyp, double *qual, void *dev_result);
+
+/* PMMG_tetraQual(parmesh, metRidTyp) on the new mesh of the last step
+ * (src/libparmmg1.c:845, right after PMMG_interpMetricsAndFields) in the
+ * caller's metric array met (Mmg layout, the points view's numbering; NULL
+ * or met->m NULL: no metric): the device already holds the new points, the
+ * new tets (the points view must have carried them) and the interpolated
+ * metric; only the rows the step did not write -- frozen points the caller
+ * filled (PMMG_copyMetricsAndFields_point), failed tensor inversions -- are
+ * sent, or the whole array when the step interpolated no metric (-hsiz, Mmg's
+ * own metric).  qual / dev_result as in pmx_new_mesh_qual. */
+int pmx_new_mesh_qual_synced(pmx_ctx *ctx, const pmx_sol_view *met, int opt, int metRidTyp, double *qual,
+                             void *dev_result);
 
 /* The reduction across groups and ranks (the reference's MPI_Reduce with its
  * custom operators, src/quality_pmmg.c:82-144, :265-307, :661-676), as host

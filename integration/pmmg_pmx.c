@@ -16,14 +16,29 @@
  * Compiled by tests/c/adapter_demo.c against a test-local parmmg.h
  * (tests/c/pmmg_stub/) that declares the few fields read here.
  */
+#include <float.h>
 #include "parmmg.h"
 #include "pmx_transfer.h"
 
-/* one device context per MPI rank (rank -> device rank % ndev), created by
- * the first seam that needs the device */
+/* one device context per MPI rank for the statistics (rank -> device
+ * rank % ndev), created by the first seam that needs the device */
 static pmx_ctx *PMMG_pmx = NULL;
 /* RCCL communicator of the statistics' reduction (nprocs > 1) */
 static void *PMMG_pmx_comm = NULL;
+
+/* one context per group for the interpolation, kept across iterations: each
+ * group's new points, new tets and interpolated metric stay on the device
+ * from PMMG_interpMetricsAndFields (:829) to PMMG_tetraQual (:845), which
+ * then sends only the rows the step did not write.  The bookkeeping (a few
+ * words per group) is plain heap memory, outside ParMmg's accounting like the
+ * device memory itself. */
+typedef struct {
+  const void *mesh, *point, *tetra;    /* the new mesh the step ran on */
+  int         np, ne, valid;
+} pmx_grp_state;
+static pmx_ctx      **PMMG_pmx_grp = NULL;
+static pmx_grp_state *PMMG_pmx_state = NULL;
+static int            PMMG_pmx_ngrp = 0;
 
 static pmx_ctx *pmx(PMMG_pParMesh parmesh) {
   if (!PMMG_pmx) PMMG_pmx = pmx_create(parmesh->myrank);
@@ -31,15 +46,48 @@ static pmx_ctx *pmx(PMMG_pParMesh parmesh) {
   return PMMG_pmx;
 }
 
-/* the RCCL communicator, created once: the id from rank 0, broadcast over the
- * rank's MPI communicator */
+/* the group contexts 0..ngrp-1 (created on demand, on the rank's device) */
+static pmx_ctx **pmx_groups(PMMG_pParMesh parmesh, int ngrp) {
+  int i;
+  if (ngrp > PMMG_pmx_ngrp) {
+    pmx_ctx **c = (pmx_ctx **)realloc(PMMG_pmx_grp, (size_t)ngrp * sizeof *c);
+    pmx_grp_state *st;
+    if (!c) return NULL;
+    PMMG_pmx_grp = c;
+    st = (pmx_grp_state *)realloc(PMMG_pmx_state, (size_t)ngrp * sizeof *st);
+    if (!st) return NULL;
+    PMMG_pmx_state = st;
+    for (i = PMMG_pmx_ngrp; i < ngrp; i++) {
+      PMMG_pmx_grp[i] = NULL;
+      memset(&PMMG_pmx_state[i], 0, sizeof PMMG_pmx_state[i]);
+    }
+    PMMG_pmx_ngrp = ngrp;
+  }
+  for (i = 0; i < ngrp; i++) {
+    if (!PMMG_pmx_grp[i]) PMMG_pmx_grp[i] = pmx_create(parmesh->myrank);
+    if (!PMMG_pmx_grp[i]) {
+      fprintf(stderr, "  ## Error: no HIP device for the transfer path.\n");
+      return NULL;
+    }
+  }
+  return PMMG_pmx_grp;
+}
+
+/* the RCCL communicator, created once by every rank of parmesh->comm: rank
+ * 0's id and its success broadcast together, and every rank's readiness
+ * agreed, so that either all ranks enter RCCL's collective initialisation or
+ * none does */
 static void *pmx_comm(PMMG_pParMesh parmesh, pmx_ctx *ctx) {
-  char id[256];
+  char id[257];
+  int ok;
   if (PMMG_pmx_comm) return PMMG_pmx_comm;
   memset(id, 0, sizeof id);
-  if (parmesh->myrank == 0 && !pmx_comm_unique_id(id, (int)sizeof id)) return NULL;
+  if (parmesh->myrank == 0) id[0] = (char)(pmx_comm_unique_id(id + 1, 256) > 0);
   MPI_Bcast(id, (int)sizeof id, MPI_BYTE, 0, parmesh->comm);
-  if (!pmx_comm_init(ctx, &PMMG_pmx_comm, parmesh->nprocs, id, parmesh->myrank)) return NULL;
+  ok = id[0] && ctx != NULL;
+  MPI_Allreduce(MPI_IN_PLACE, &ok, 1, MPI_INT, MPI_MIN, parmesh->comm);
+  if (!ok) return NULL;
+  if (!pmx_comm_init(ctx, &PMMG_pmx_comm, parmesh->nprocs, id + 1, parmesh->myrank)) return NULL;
   return PMMG_pmx_comm;
 }
 
@@ -92,15 +140,16 @@ int PMMG_copyMetricsAndFields_point(MMG5_pMesh mesh, MMG5_pMesh oldMesh, MMG5_pS
   return 1;
 }
 
-/* src/interpmesh_pmmg.c:663-741: every group in one call -- the library
- * alternates them over two device contexts, so group g+1's upload overlaps
- * group g's step */
+/* src/interpmesh_pmmg.c:663-741: every group in one call, each on its own
+ * context (group g+1's upload overlaps group g's step); the contexts keep the
+ * groups' new meshes and results for PMMG_tetraQual */
 int PMMG_interpMetricsAndFields(PMMG_pParMesh parmesh, int *permNodGlob) {
   int ngrp = parmesh->ngrp, igrp, j, ier;
   pmx_group *g;
   pmx_sol_view *sv;
-  pmx_ctx *ctx = pmx(parmesh);
-  if (!ctx) return 0;
+  pmx_ctx **ctxs = pmx_groups(parmesh, ngrp > 0 ? ngrp : 1);
+  if (!ctxs) return 0;
+  for (igrp = 0; igrp < PMMG_pmx_ngrp; igrp++) PMMG_pmx_state[igrp].valid = 0;
   PMMG_CALLOC(parmesh, g, ngrp, pmx_group, "pmx groups", return 0);
   PMMG_CALLOC(parmesh, sv, ngrp * 2 * (PMX_MAX_SOLS + 1), pmx_sol_view, "pmx sols",
               PMMG_DEL_MEM(parmesh, g, pmx_group, "pmx groups"); return 0);
@@ -128,8 +177,14 @@ int PMMG_interpMetricsAndFields(PMMG_pParMesh parmesh, int *permNodGlob) {
     g[igrp].hsiz = mesh->info.hsiz;
     view_mesh(O->mesh, &g[igrp].old_mesh);
   }
-  ier = PMX_interpMetricsAndFields(ctx, ngrp, g, permNodGlob, parmesh->info.inputMet);
-  if (!ier) pmx_fail(ctx, __func__);
+  ier = PMX_interpMetricsAndFields_groups(ctxs, ngrp, g, permNodGlob, parmesh->info.inputMet);
+  if (!ier) pmx_fail(ctxs[0], __func__);
+  for (igrp = 0; ier && igrp < ngrp; igrp++) {
+    MMG5_pMesh mesh = parmesh->listgrp[igrp].mesh;
+    pmx_grp_state *st = &PMMG_pmx_state[igrp];
+    st->mesh = mesh; st->point = mesh->point; st->tetra = mesh->tetra;
+    st->np = mesh->np; st->ne = mesh->ne; st->valid = 1;
+  }
   PMMG_DEL_MEM(parmesh, sv, pmx_sol_view, "pmx sols");
   PMMG_DEL_MEM(parmesh, g, pmx_group, "pmx groups");
   return ier;
@@ -151,19 +206,42 @@ static int upload_stats_group(pmx_ctx *ctx, MMG5_pMesh mesh, MMG5_pSol met) {
   return pmx_upload_point_tags(ctx, &mesh->point[0].tag, sizeof(MMG5_Point));
 }
 
-/* src/quality_pmmg.c:720-733: MMG3D_tetraQual on every group, pt->qual set */
+/* the group's new mesh of the last interpolation is still the one the
+ * group holds: ParMmg calls PMMG_tetraQual right after the interpolation
+ * (src/libparmmg1.c:829 -> :845), nothing changes the mesh in between */
+static int pmx_resident(int igrp, MMG5_pMesh mesh) {
+  const pmx_grp_state *st;
+  if (igrp >= PMMG_pmx_ngrp) return 0;
+  st = &PMMG_pmx_state[igrp];
+  return st->valid && st->mesh == (const void *)mesh && st->point == (const void *)mesh->point &&
+         st->tetra == (const void *)mesh->tetra && st->np == mesh->np && st->ne == mesh->ne;
+}
+
+/* src/quality_pmmg.c:720-733: MMG3D_tetraQual on every group, pt->qual set.
+ * After the interpolation the new mesh is on the device already: only the
+ * metric rows the step did not write cross PCIe (pmx_new_mesh_qual_synced);
+ * any other mesh is uploaded. */
 int PMMG_tetraQual(PMMG_pParMesh parmesh, int8_t metRidTyp) {
-  int igrp, k;
+  int igrp, k, ok;
   double *q;
-  pmx_ctx *ctx = pmx(parmesh);
-  if (!ctx) return 0;
   for (igrp = 0; igrp < parmesh->ngrp; igrp++) {
     PMMG_pGrp grp = &parmesh->listgrp[igrp];
     MMG5_pMesh mesh = grp->mesh;
+    pmx_ctx *ctx;
     PMMG_MALLOC(parmesh, q, mesh->ne + 1, double, "qual", return 0);
-    if (!upload_stats_group(ctx, mesh, grp->met) || !pmx_tetra_qual(ctx, metRidTyp, q)) {
+    if (pmx_resident(igrp, mesh)) {
+      pmx_sol_view mv;
+      ctx = PMMG_pmx_grp[igrp];
+      PMMG_pmx_state[igrp].valid = 0;            /* one use per interpolation */
+      if (grp->met && grp->met->m) view_sol(grp->met, &mv);
+      ok = pmx_new_mesh_qual_synced(ctx, grp->met && grp->met->m ? &mv : NULL, PMX_INQUA, metRidTyp, q, NULL);
+    } else {
+      ctx = pmx(parmesh);
+      ok = ctx && upload_stats_group(ctx, mesh, grp->met) && pmx_tetra_qual(ctx, metRidTyp, q);
+    }
+    if (!ok) {
       PMMG_DEL_MEM(parmesh, q, double, "qual");
-      pmx_fail(ctx, __func__);
+      if (ctx) pmx_fail(ctx, __func__);
       fprintf(stderr, "\n  ## Quality computation problem.\n");
       return 0;
     }
@@ -179,30 +257,35 @@ int PMMG_tetraQual(PMMG_pParMesh parmesh, int8_t metRidTyp) {
  * count of PMMG_count_nodes_par (:33-80); then the groups folded as the
  * reference's loop and the ranks reduced with its operators (one RCCL
  * all-gather + a rank-ordered fold instead of 12 MPI_Reduce), printed by
- * rank 0 through Mmg's display as the reference does. */
+ * rank 0 through Mmg's display as the reference does.  Distributed: every
+ * rank reaches the agreement on its local result (MPI_Allreduce MIN) whatever
+ * failed before it, and all ranks enter the RCCL calls or none does. */
 int PMMG_qualhisto(PMMG_pParMesh parmesh, int opt, int isCentral) {
   PMMG_pInt_comm int_node_comm = parmesh->int_node_comm;
   PMMG_pExt_comm ext_node_comm;
   pmx_qual_part *parts = NULL;
   pmx_qual_stats st;
-  void *d_parts;
+  void *d_parts = NULL;
   int *intvalues = NULL, his[PMMG_QUAL_HISSIZE];
   int i, k, igrp, ier = 1, optimLES;
+  const int dist = !isCentral && parmesh->nprocs > 1;
   pmx_ctx *ctx = pmx(parmesh);
-  if (!ctx) return 0;
+  if (!ctx) ier = 0;
   optimLES = (parmesh->ngrp && parmesh->listgrp[0].mesh) ? parmesh->listgrp[0].mesh->info.optimLES : 0;
   /* nodes shared with a higher rank are counted there (:196-209) */
-  if (int_node_comm) {
-    PMMG_CALLOC(parmesh, int_node_comm->intvalues, int_node_comm->nitem, int, "intvalues", return 0);
+  if (ier && int_node_comm) {
+    PMMG_CALLOC(parmesh, int_node_comm->intvalues, int_node_comm->nitem, int, "intvalues", ier = 0);
     intvalues = int_node_comm->intvalues;
-    for (k = 0; k < parmesh->next_node_comm; k++) {
+    for (k = 0; ier && k < parmesh->next_node_comm; k++) {
       ext_node_comm = &parmesh->ext_node_comm[k];
       if (parmesh->myrank > ext_node_comm->color_out) continue;
       for (i = 0; i < ext_node_comm->nitem; i++) intvalues[ext_node_comm->int_comm_index[i]] = 1;
     }
   }
-  d_parts = pmx_device_alloc(ctx, (size_t)(parmesh->ngrp > 0 ? parmesh->ngrp : 1) * sizeof(pmx_qual_part));
-  if (!d_parts) ier = 0;
+  if (ier) {
+    d_parts = pmx_device_alloc(ctx, (size_t)(parmesh->ngrp > 0 ? parmesh->ngrp : 1) * sizeof(pmx_qual_part));
+    if (!d_parts) ier = 0;
+  }
   for (igrp = 0; ier && igrp < parmesh->ngrp; igrp++) {
     PMMG_pGrp grp = &parmesh->listgrp[igrp];
     MMG5_pMesh mesh = grp->mesh;
@@ -219,8 +302,10 @@ int PMMG_qualhisto(PMMG_pParMesh parmesh, int opt, int isCentral) {
     }
     if (!pmx_qualhisto_device(ctx, dopt, 0, (pmx_qual_part *)d_parts + igrp)) { ier = 0; break; }
   }
-  if (ier && parmesh->info.imprim0 > PMMG_VERB_VERSION) {
-    if (isCentral || parmesh->nprocs == 1) {
+  if (!ier && ctx) pmx_fail(ctx, __func__);
+  if (parmesh->info.imprim0 > PMMG_VERB_VERSION) {
+    if (dist) MPI_Allreduce(MPI_IN_PLACE, &ier, 1, MPI_INT, MPI_MIN, parmesh->comm);
+    if (ier && !dist) {
       /* this rank's groups, folded as the reference's group loop */
       PMMG_MALLOC(parmesh, parts, parmesh->ngrp > 0 ? parmesh->ngrp : 1, pmx_qual_part, "parts", ier = 0);
       if (ier && parmesh->ngrp > 0) {
@@ -236,7 +321,7 @@ int PMMG_qualhisto(PMMG_pParMesh parmesh, int opt, int isCentral) {
         }
       }
       st.cpu = parmesh->myrank;
-    } else {
+    } else if (ier) {
       void *comm = pmx_comm(parmesh, ctx);
       ier = comm && pmx_qualhisto_allreduce(ctx, comm, parmesh->nprocs, d_parts, parmesh->ngrp, &st);
     }
@@ -256,89 +341,110 @@ int PMMG_qualhisto(PMMG_pParMesh parmesh, int opt, int isCentral) {
                                             (int)st.med, his, (int)st.nrid, optimLES,
                                             parmesh->info.imprim);
     }
+    if (!ier && ctx) pmx_fail(ctx, __func__);
   }
-  if (!ier) pmx_fail(ctx, __func__);
   if (parts) PMMG_DEL_MEM(parmesh, parts, pmx_qual_part, "parts");
   if (d_parts) pmx_device_free(ctx, d_parts);
-  if (int_node_comm) PMMG_DEL_MEM(parmesh, int_node_comm->intvalues, int, "intvalues");
+  if (int_node_comm && int_node_comm->intvalues) PMMG_DEL_MEM(parmesh, int_node_comm->intvalues, int, "intvalues");
   return ier;
 }
 
 /* src/quality_pmmg.c:370-709 (one group per rank, as the reference requires):
  * centralized = MMG3D_computePrilen, distributed = PMMG_computePrilen with
  * the parallel edges owned by the lowest rank measured first (:398-502); the
- * ranks reduced with PMMG_compute_lenStats' operator (:106-144) */
+ * ranks reduced with PMMG_compute_lenStats' operator (:106-144).  As in the
+ * reference, a rank with more than one group fails the call and a rank with no
+ * group or no metric takes part with an empty partial (:620-675); the local
+ * results are agreed by every rank before the RCCL calls (the reference
+ * reduces ier first, :664), so all ranks enter them or none does. */
 int PMMG_prilen(PMMG_pParMesh parmesh, int8_t metRidTyp, int isCentral) {
   static double bd[9] = {0.0, 0.3, 0.6, 0.7071, 0.9, 1.3, 1.4142, 2.0, 5.0};
   pmx_len_stats st;
   pmx_par_edges par;
   MMG5_HGeom hpar;
-  MMG5_pMesh mesh;
-  MMG5_pSol met;
+  MMG5_pMesh mesh = NULL;
+  MMG5_pSol met = NULL;
   void *d_part = NULL;
   int *pa = NULL, *pb = NULL, *po = NULL, *intvalues, hl[9];
-  int i, k, ier = 1, dist = 0;
+  int i, k, ier = 1, dist = 0, have = 0;
+  const int reduce = !isCentral && parmesh->nprocs > 1;
   pmx_ctx *ctx;
   if (parmesh->ngrp > 1) {
     printf("  ## Warning:%s: this function must be called with at most 1"
            "group per processor. Exit function.\n", __func__);
-    return 0;
+    ier = 0;
   }
-  if (parmesh->ngrp != 1) return 1;
-  mesh = parmesh->listgrp[0].mesh;
-  met = parmesh->listgrp[0].met;
-  if (!met || !met->m) return 1;
+  if (ier && parmesh->ngrp == 1) {
+    mesh = parmesh->listgrp[0].mesh;
+    met = parmesh->listgrp[0].met;
+    have = met && met->m;
+  }
+  if (!reduce && !have) return ier;      /* nothing measured, nothing to reduce */
   ctx = pmx(parmesh);
-  if (!ctx) return 0;
+  if (!ctx) ier = 0;
   memset(&par, 0, sizeof par);
-  if (!isCentral) {
+  if (ier && have && !isCentral) {
     /* the parallel edges and their owner (lowest rank holding them, :398-419) */
     PMMG_pInt_comm int_edge_comm;
     PMMG_pGrp grp = &parmesh->listgrp[0];
     memset(&hpar, 0, sizeof hpar);
-    if (PMMG_hashPar(mesh, &hpar) != PMMG_SUCCESS) return 0;
-    if (!PMMG_build_edgeComm(parmesh, mesh, &hpar)) return 0;
-    dist = 1;
-    int_edge_comm = parmesh->int_edge_comm;
-    PMMG_MALLOC(parmesh, int_edge_comm->intvalues, int_edge_comm->nitem, int, "intvalues", ier = 0);
-    intvalues = ier ? int_edge_comm->intvalues : NULL;
+    if (PMMG_hashPar(mesh, &hpar) != PMMG_SUCCESS) ier = 0;
+    if (ier && !PMMG_build_edgeComm(parmesh, mesh, &hpar)) ier = 0;
     if (ier) {
-      for (i = 0; i < int_edge_comm->nitem; i++) intvalues[i] = parmesh->myrank;
-      for (k = 0; k < parmesh->next_edge_comm; k++) {
-        PMMG_pExt_comm ext = &parmesh->ext_edge_comm[k];
-        for (i = 0; i < ext->nitem; i++)
-          if (ext->color_out < intvalues[ext->int_comm_index[i]]) intvalues[ext->int_comm_index[i]] = ext->color_out;
+      dist = 1;
+      int_edge_comm = parmesh->int_edge_comm;
+      PMMG_MALLOC(parmesh, int_edge_comm->intvalues, int_edge_comm->nitem, int, "intvalues", ier = 0);
+      intvalues = ier ? int_edge_comm->intvalues : NULL;
+      if (ier) {
+        for (i = 0; i < int_edge_comm->nitem; i++) intvalues[i] = parmesh->myrank;
+        for (k = 0; k < parmesh->next_edge_comm; k++) {
+          PMMG_pExt_comm ext = &parmesh->ext_edge_comm[k];
+          for (i = 0; i < ext->nitem; i++)
+            if (ext->color_out < intvalues[ext->int_comm_index[i]]) intvalues[ext->int_comm_index[i]] = ext->color_out;
+        }
+        PMMG_MALLOC(parmesh, pa, grp->nitem_int_edge_comm, int, "par a", ier = 0);
+        PMMG_MALLOC(parmesh, pb, grp->nitem_int_edge_comm, int, "par b", ier = 0);
+        PMMG_MALLOC(parmesh, po, grp->nitem_int_edge_comm, int, "par owner", ier = 0);
       }
-      PMMG_MALLOC(parmesh, pa, grp->nitem_int_edge_comm, int, "par a", ier = 0);
-      PMMG_MALLOC(parmesh, pb, grp->nitem_int_edge_comm, int, "par b", ier = 0);
-      PMMG_MALLOC(parmesh, po, grp->nitem_int_edge_comm, int, "par owner", ier = 0);
-    }
-    if (ier) {
-      for (i = 0; i < grp->nitem_int_edge_comm; i++) {
-        const int ia = grp->edge2int_edge_comm_index1[i];
-        pa[i] = mesh->edge[ia].a;
-        pb[i] = mesh->edge[ia].b;
-        po[i] = intvalues[grp->edge2int_edge_comm_index2[i]];
+      if (ier) {
+        for (i = 0; i < grp->nitem_int_edge_comm; i++) {
+          const int ia = grp->edge2int_edge_comm_index1[i];
+          pa[i] = mesh->edge[ia].a;
+          pb[i] = mesh->edge[ia].b;
+          po[i] = intvalues[grp->edge2int_edge_comm_index2[i]];
+        }
+        par.n = grp->nitem_int_edge_comm;
+        par.a = pa; par.b = pb; par.owner = po;
+        par.myrank = parmesh->myrank;
+        par.exact_once = 0;                         /* the reference's counts (:585-586) */
       }
-      par.n = grp->nitem_int_edge_comm;
-      par.a = pa; par.b = pb; par.owner = po;
-      par.myrank = parmesh->myrank;
-      par.exact_once = 0;                         /* the reference's counts (:585-586) */
     }
   }
-  if (ier) ier = upload_stats_group(ctx, mesh, met);
-  if (ier) {
-    if (parmesh->nprocs == 1 || isCentral) {
-      ier = pmx_prilen(ctx, metRidTyp, dist ? &par : NULL, &st);
-      st.cpu_min = st.cpu_max = parmesh->myrank;
-    } else {
-      void *comm = pmx_comm(parmesh, ctx);
+  if (ier && have) ier = upload_stats_group(ctx, mesh, met);
+  if (!reduce) {
+    if (ier) ier = pmx_prilen(ctx, metRidTyp, dist ? &par : NULL, &st);
+    st.cpu_min = st.cpu_max = parmesh->myrank;
+  } else {
+    if (ier) {
       d_part = pmx_device_alloc(ctx, sizeof(pmx_len_part));
-      ier = comm && d_part && pmx_prilen_device(ctx, metRidTyp, &par, d_part) &&
-            pmx_prilen_allreduce(ctx, comm, parmesh->nprocs, d_part, &st);
+      if (!d_part) ier = 0;
+    }
+    if (ier && have) ier = pmx_prilen_device(ctx, metRidTyp, &par, d_part);
+    if (ier && !have) {
+      /* the empty partial of a rank without a metric (:633-640) */
+      pmx_len_part e;
+      memset(&e, 0, sizeof e);
+      e.lmin = DBL_MAX;
+      ier = pmx_device_upload(ctx, d_part, &e, sizeof e);
+    }
+    if (!ier && ctx) pmx_fail(ctx, __func__);
+    MPI_Allreduce(MPI_IN_PLACE, &ier, 1, MPI_INT, MPI_MIN, parmesh->comm);
+    if (ier) {
+      void *comm = pmx_comm(parmesh, ctx);
+      ier = comm && pmx_prilen_allreduce(ctx, comm, parmesh->nprocs, d_part, &st);
     }
   }
-  if (!ier) pmx_fail(ctx, __func__);
+  if (!ier && ctx) pmx_fail(ctx, __func__);
   if (d_part) pmx_device_free(ctx, d_part);
   if (pa) PMMG_DEL_MEM(parmesh, pa, int, "par a");
   if (pb) PMMG_DEL_MEM(parmesh, pb, int, "par b");

@@ -147,6 +147,7 @@ SIGNATURES = {
     "pmx_device_alloc": (C.c_void_p, [C.c_void_p, C.c_size_t]),
     "pmx_device_free": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pmx_device_download": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
+    "pmx_device_upload": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
     "pmx_debug_hint_grid": (C.c_int64, [C.c_void_p, C.c_void_p, C.c_int64]),
     "pmx_build_adja": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64,
                                  C.c_void_p]),
@@ -156,6 +157,8 @@ SIGNATURES = {
     "pmx_kernel_ms": (C.c_double, [C.c_void_p, C.c_int]),
     "pmx_timing_reset": (C.c_int, [C.c_void_p]),
     "PMX_interpMetricsAndFields": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(Group), iptr, C.c_int]),
+    "PMX_interpMetricsAndFields_groups": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.POINTER(Group), iptr,
+                                                    C.c_int]),
     "PMX_copyMetricsAndFields_point": (C.c_int, [C.c_void_p, C.POINTER(Group), u16ptr, i64, iptr, C.c_int, C.c_int]),
     "pmx_tetra_qual": (C.c_int, [C.c_void_p, C.c_int, dptr]),
     "pmx_upload_point_tags": (C.c_int, [C.c_void_p, u16ptr, i64]),
@@ -165,6 +168,7 @@ SIGNATURES = {
     "pmx_prilen_device": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(ParEdges), C.c_void_p]),
     "pmx_prilen": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(ParEdges), C.POINTER(LenStats)]),
     "pmx_new_mesh_qual": (C.c_int, [C.c_void_p, iptr, i64, i64, C.c_int, C.c_int, dptr, C.c_void_p]),
+    "pmx_new_mesh_qual_synced": (C.c_int, [C.c_void_p, C.POINTER(SolView), C.c_int, C.c_int, dptr, C.c_void_p]),
     "pmx_upload_new_tets": (C.c_int, [C.c_void_p, iptr, i64, i64]),
     "pmx_set_residency": (C.c_int, [C.c_void_p, C.c_int]),
     "pmx_copy_required": (C.c_int, [C.c_void_p, iptr, C.c_int]),

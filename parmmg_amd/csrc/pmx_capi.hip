@@ -817,7 +817,7 @@ static bool run_flags_valid(int flags, std::string *err) {
   }
   const int e = (flags >> PMX_RUN_EXP_SHIFT) & 0xff;
   switch (e) {
-    case 0: case 6: case 9: case 10: case 11: case 12: case 13: case 14: case 15:
+    case 0: case 6: case 9: case 10: case 11: case 12:
       return true;
     case 4: case 5: {
       const char *v = getenv("PMX_EXPERIMENTS");
@@ -1155,6 +1155,15 @@ int pmx_device_download(pmx_ctx *ctx, void *host, const void *dev, size_t bytes)
   if (!host || !dev) { ctx->err = "pmx_device_download: null pointer"; return 0; }
   hipSetDevice(ctx->device);
   CK(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  return 1;
+}
+
+int pmx_device_upload(pmx_ctx *ctx, void *dev, const void *host, size_t bytes) {
+  if (!ctx) return 0;
+  if (!host || !dev) { ctx->err = "pmx_device_upload: null pointer"; return 0; }
+  hipSetDevice(ctx->device);
+  CK(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
   return 1;
 }

@@ -44,23 +44,13 @@ static int constant_metric(pmx_ctx *ctx, const pmx_sol_view *met, int64_t first,
   return 1;
 }
 
-extern "C" {
-
-// Groups alternate between the context and a second one on the same device
-// (created on first use): group g+1's host staging and upload overlap group
-// g's step on the other context's streams, and group g's download waits until
-// the context is needed again (g+2).
-int PMX_interpMetricsAndFields(pmx_ctx *ctx, int ngrp, pmx_group *grps, const int *permNodGlob,
-                               int inputMet) {
-  (void)permNodGlob;  // only used by the frozen-point copy, as in the reference (:477-484)
-  if (!ctx || ngrp < 0 || (ngrp > 0 && !grps)) return 0;
-  hipSetDevice(ctx->device);
-  if (ngrp > 1 && !ctx->peer) {
-    ctx->peer = pmx_create(ctx->device);
-    if (!ctx->peer) { ctx->err = "PMX_interpMetricsAndFields: second context"; return 0; }
-  }
-  // a failing group makes the call fail but the other groups are still
-  // processed (reference :715-721)
+// The group loop of PMMG_interpMetricsAndFields (src/interpmesh_pmmg.c:690-730)
+// over contexts: group g on ctxs[g]; a context's pending download is done
+// before the context takes its next group, the rest after every step is
+// enqueued, so a group's host staging and upload overlap the steps of the
+// groups before it.  A failing group makes the call fail but the other groups
+// are still processed (reference :715-721); errors go to `ectx`.
+static int interp_groups(pmx_ctx *ectx, pmx_ctx *const *ctxs, int ngrp, pmx_group *grps, int inputMet) {
   int ier = 1;
   std::string first_err;
   auto fail = [&](pmx_ctx *c) {
@@ -71,17 +61,17 @@ int PMX_interpMetricsAndFields(pmx_ctx *ctx, int ngrp, pmx_group *grps, const in
     bool on = false;
     int ns = 0;
     pmx_sol_view news[PMX_MAX_SOLS];
-  } pend[2];
-  auto finish = [&](int c) {
-    pmx_ctx *X = c ? ctx->peer : ctx;
-    if (!pend[c].on) return;
-    pend[c].on = false;
-    if (!pmx_download(X, pend[c].news, nullptr, nullptr, nullptr)) fail(X);
+  };
+  std::vector<Pending> pend((size_t)std::max(ngrp, 1));
+  auto finish = [&](int g) {
+    if (!pend[g].on) return;
+    pend[g].on = false;
+    if (!pmx_download(ctxs[g], pend[g].news, nullptr, nullptr, nullptr)) fail(ctxs[g]);
   };
   for (int g = 0; g < ngrp; g++) {
-    const int c = (ngrp > 1) ? (g & 1) : 0;
-    pmx_ctx *X = c ? ctx->peer : ctx;
-    finish(c);                               // group g-2's results, same context
+    pmx_ctx *X = ctxs[g];
+    for (int h = 0; h < g; h++)             // the context's previous group, if any
+      if (ctxs[h] == X) finish(h);
     pmx_group &G = grps[g];
     // reference :497-512: with -hsiz the metric is the constant one (written
     // whenever there is a metric array), otherwise it is interpolated when the
@@ -94,6 +84,7 @@ int PMX_interpMetricsAndFields(pmx_ctx *ctx, int ngrp, pmx_group *grps, const in
       fail(X);
       continue;
     }
+    X->ran = false;                          // no step of this call yet on this context
     if (!ismet && !cst && G.nsols == 0) continue;   // nothing to do (:508-512)
     // the points of the new mesh's valid tets only (:535-541)
     pmx_points_view pv = G.points;
@@ -106,7 +97,7 @@ int PMX_interpMetricsAndFields(pmx_ctx *ctx, int ngrp, pmx_group *grps, const in
     if (cst && !constant_metric(X, G.met, G.points.first, G.hsiz)) { fail(X); continue; }
     if (!ismet && G.nsols == 0) continue;            // constant metric only: no locate
     pmx_sol_view olds[PMX_MAX_SOLS];
-    Pending &P = pend[c];
+    Pending &P = pend[g];
     int ns = 0, imet = -1;
     if (ismet) {
       olds[ns] = *G.old_met;
@@ -131,10 +122,43 @@ int PMX_interpMetricsAndFields(pmx_ctx *ctx, int ngrp, pmx_group *grps, const in
     P.ns = ns;
     P.on = true;
   }
-  finish(0);
-  finish(1);
-  if (!ier) ctx->err = first_err;
+  for (int g = 0; g < ngrp; g++) finish(g);
+  if (!ier) ectx->err = first_err;
   return ier;
+}
+
+extern "C" {
+
+// Groups alternate between the context and a second one on the same device
+// (created on first use): group g+1's host staging and upload overlap group
+// g's step on the other context's streams, and group g's download waits until
+// the context is needed again (g+2).
+int PMX_interpMetricsAndFields(pmx_ctx *ctx, int ngrp, pmx_group *grps, const int *permNodGlob,
+                               int inputMet) {
+  (void)permNodGlob;  // only used by the frozen-point copy, as in the reference (:477-484)
+  if (!ctx || ngrp < 0 || (ngrp > 0 && !grps)) return 0;
+  hipSetDevice(ctx->device);
+  if (ngrp > 1 && !ctx->peer) {
+    ctx->peer = pmx_create(ctx->device);
+    if (!ctx->peer) { ctx->err = "PMX_interpMetricsAndFields: second context"; return 0; }
+  }
+  std::vector<pmx_ctx *> cs((size_t)std::max(ngrp, 1));
+  for (int g = 0; g < ngrp; g++) cs[(size_t)g] = (ngrp > 1 && (g & 1)) ? ctx->peer : ctx;
+  return interp_groups(ctx, cs.data(), ngrp, grps, inputMet);
+}
+
+// One context per group (the caller's, e.g. kept across ParMmg iterations):
+// every group's new points, new tets and results stay on its context for
+// pmx_new_mesh_qual_synced until that context's next upload.
+int PMX_interpMetricsAndFields_groups(pmx_ctx *const *ctxs, int ngrp, pmx_group *grps,
+                                      const int *permNodGlob, int inputMet) {
+  (void)permNodGlob;
+  if (ngrp < 0 || (ngrp > 0 && (!ctxs || !grps))) return 0;
+  for (int g = 0; g < ngrp; g++)
+    if (!ctxs[g]) return 0;
+  if (ngrp == 0) return 1;
+  hipSetDevice(ctxs[0]->device);
+  return interp_groups(ctxs[0], ctxs, ngrp, grps, inputMet);
 }
 
 }  // extern "C"

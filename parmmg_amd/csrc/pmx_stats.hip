@@ -1116,6 +1116,49 @@ int pmx_prilen(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, pmx_len_st
   return 1;
 }
 
+// the quality pass over the device-resident new mesh (the step's points and
+// the uploaded new tets), in the metric at sol[S * j + moff] (msize 0: none)
+static int new_mesh_qual_core(pmx_ctx *ctx, const char *who, int opt, int metRidTyp, double *qual,
+                              void *dev_result, const double *sol, int S, int msize, int moff) {
+  const int64_t ne = ctx->n_ntet;
+  const int64_t n = ctx->nq;
+  hipStream_t s = ctx->stream;
+  if (!pmx_dgrow(ctx, ctx->d_nqual, (size_t)(ne + 1))) return 0;
+  StatArgs A{};
+  A.xyz = ctx->d_qxyz.p;                  // the new points, dense x y z
+  A.xstride = 3;
+  A.vbase = 1;
+  A.tetv = ctx->d_ntetv.p;
+  A.ne = ne;
+  A.sol = sol;
+  A.S = S;
+  A.msize = msize;
+  A.moff = moff;
+  A.ptag = (opt == PMX_OUTQUA && ctx->have_qtag) ? ctx->d_qtag.p : nullptr;
+  if (!check_met_rid_typ(ctx, metRidTyp, A.msize, who)) return 0;
+  if (dev_result && opt != PMX_INQUA && opt != PMX_OUTQUA) {
+    ctx->err = std::string(who) + (opt == PMX_LESQUA ? ": the optimLES quality (MMG3D_computeLESqua) is not supported"
+                                                      : ": opt must be PMX_INQUA or PMX_OUTQUA");
+    return 0;
+  }
+  const int nb = stat_blocks(ne);
+  if (A.msize == 6)
+    hipLaunchKernelGGL((k_qual<true, false>), dim3(nb), dim3(256), 0, s, A, ctx->d_nqual.p, (QualPart *)nullptr, 0);
+  else
+    hipLaunchKernelGGL((k_qual<false, false>), dim3(nb), dim3(256), 0, s, A, ctx->d_nqual.p, (QualPart *)nullptr, 0);
+  if (dev_result && !qual_partial(ctx, A, opt, ctx->d_nqual.p, 1, (pmx_qual_part *)dev_result, n)) return 0;
+  if (hipGetLastError() != hipSuccess) { ctx->err = std::string(who) + ": launch"; return 0; }
+  if (qual) {
+    if (hipMemcpyAsync(qual, ctx->d_nqual.p, (size_t)(ne + 1) * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      ctx->err = std::string(who) + ": download";
+      return 0;
+    }
+    qual[0] = 0.0;
+  }
+  return 1;
+}
+
 int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, int64_t ne, int opt,
                       int metRidTyp, double *qual, void *dev_result) {
   if (!ctx) return 0;
@@ -1132,45 +1175,84 @@ int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, in
     ctx->err = "pmx_new_mesh_qual: no new tets uploaded";
     return 0;
   }
-  ne = ctx->n_ntet;
-  const int64_t n = ctx->nq;
-  hipStream_t s = ctx->stream;
-  if (!pmx_dgrow(ctx, ctx->d_nqual, (size_t)(ne + 1))) return 0;
-  StatArgs A{};
-  A.xyz = ctx->d_qxyz.p;                  // the new points, dense x y z
-  A.xstride = 3;
-  A.vbase = 1;
-  A.tetv = ctx->d_ntetv.p;
-  A.ne = ne;
   // the interpolated metric, in the step's output rows (a constant-size
   // metric of the step is there too)
-  A.sol = ctx->d_out.p;
-  A.S = ctx->sd.S;
-  A.msize = ctx->sd.imet >= 0 ? ctx->sd.size[ctx->sd.imet] : 0;
-  A.moff = ctx->sd.imet >= 0 ? ctx->sd.off[ctx->sd.imet] : 0;
-  A.ptag = (opt == PMX_OUTQUA && ctx->have_qtag) ? ctx->d_qtag.p : nullptr;
-  if (!check_met_rid_typ(ctx, metRidTyp, A.msize, "pmx_new_mesh_qual")) return 0;
-  if (dev_result && opt != PMX_INQUA && opt != PMX_OUTQUA) {
-    ctx->err = opt == PMX_LESQUA ? "pmx_new_mesh_qual: the optimLES quality (MMG3D_computeLESqua) is not supported"
-                                 : "pmx_new_mesh_qual: opt must be PMX_INQUA or PMX_OUTQUA";
+  const int msize = ctx->sd.imet >= 0 ? ctx->sd.size[ctx->sd.imet] : 0;
+  const int moff = ctx->sd.imet >= 0 ? ctx->sd.off[ctx->sd.imet] : 0;
+  return new_mesh_qual_core(ctx, "pmx_new_mesh_qual", opt, metRidTyp, qual, dev_result, ctx->d_out.p, ctx->sd.S,
+                            msize, moff);
+}
+
+// PMMG_tetraQual after PMMG_interpMetricsAndFields on the caller's metric
+// array: the step's own rows where it wrote the metric, and only the rows it
+// did not write (frozen points that PMMG_copyMetricsAndFields_point filled on
+// the host, failed tensor inversions) sent to the device; a metric the step
+// did not interpolate (-hsiz constant size, or Mmg's own) is sent whole.
+int pmx_new_mesh_qual_synced(pmx_ctx *ctx, const pmx_sol_view *met, int opt, int metRidTyp, double *qual,
+                             void *dev_result) {
+  if (!ctx) return 0;
+  hipSetDevice(ctx->device);
+  const char *who = "pmx_new_mesh_qual_synced";
+  if (!ctx->ran || !ctx->have_pts || ctx->out_n != ctx->nq) {
+    ctx->err = std::string(who) + ": run a step on the new points first";
     return 0;
   }
-  const int nb = stat_blocks(ne);
-  if (A.msize == 6)
-    hipLaunchKernelGGL((k_qual<true, false>), dim3(nb), dim3(256), 0, s, A, ctx->d_nqual.p, (QualPart *)nullptr, 0);
-  else
-    hipLaunchKernelGGL((k_qual<false, false>), dim3(nb), dim3(256), 0, s, A, ctx->d_nqual.p, (QualPart *)nullptr, 0);
-  if (dev_result && !qual_partial(ctx, A, opt, ctx->d_nqual.p, 1, (pmx_qual_part *)dev_result, n)) return 0;
-  if (hipGetLastError() != hipSuccess) { ctx->err = "pmx_new_mesh_qual: launch"; return 0; }
-  if (qual) {
-    if (hipMemcpyAsync(qual, ctx->d_nqual.p, (size_t)(ne + 1) * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess) {
-      ctx->err = "pmx_new_mesh_qual: download";
+  if (!ctx->have_ntet) { ctx->err = std::string(who) + ": the step's points view had no new tets"; return 0; }
+  const int64_t n = ctx->nq, first = ctx->pts_first;
+  hipStream_t s = ctx->stream;
+  if (!met || !met->m) return new_mesh_qual_core(ctx, who, opt, metRidTyp, qual, dev_result, nullptr, 0, 0, 0);
+  const int sz = met->size;
+  if (sz != 1 && sz != 6) { ctx->err = std::string(who) + ": metric size must be 1 or 6"; return 0; }
+  const double *hm = met->m + first * sz;      // Mmg layout: entry of point `first`
+  const int im = ctx->sd.imet;
+  if (im >= 0 && ctx->sd.size[im] == sz) {
+    // the step's metric: patch the rows it did not write from the caller's array
+    std::vector<uint8_t> wm((size_t)std::max<int64_t>(n, 1));
+    if (n && (hipMemcpyAsync(wm.data(), ctx->d_wmask.p, (size_t)n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+              hipStreamSynchronize(s) != hipSuccess)) {
+      ctx->err = std::string(who) + ": write masks";
       return 0;
     }
-    qual[0] = 0.0;
+    std::vector<int4> ent;
+    std::vector<double> val;
+    for (int64_t j = 0; j < n; j++) {
+      if (wm[(size_t)j] & (1u << im)) continue;
+      ent.push_back(make_int4((int)j, ctx->sd.off[im], sz, 0));
+      for (int c = 0; c < 6; c++) val.push_back(c < sz ? hm[j * sz + c] : 0.0);
+    }
+    const int64_t ne_ = (int64_t)ent.size();
+    if (ne_) {
+      if (!pmx_dgrow(ctx, ctx->d_pent, (size_t)ne_) || !pmx_dgrow(ctx, ctx->d_pval, (size_t)ne_ * 6)) return 0;
+      if (hipMemcpyAsync(ctx->d_pent.p, ent.data(), (size_t)ne_ * sizeof(int4), hipMemcpyHostToDevice, s) !=
+              hipSuccess ||
+          hipMemcpyAsync(ctx->d_pval.p, val.data(), (size_t)ne_ * 6 * sizeof(double), hipMemcpyHostToDevice, s) !=
+              hipSuccess) {
+        ctx->err = std::string(who) + ": patch upload";
+        return 0;
+      }
+      launch_patch_rows(ctx->d_pent.p, ctx->d_pval.p, ne_, ctx->sd.S, ctx->d_out.p, s);
+      // the rows are the caller's now (pmx_download / pmx_promote_background
+      // then give the same values)
+      const uint8_t bit = (uint8_t)(1u << im);
+      for (int64_t e = 0; e < ne_; e++) wm[(size_t)ent[(size_t)e].x] |= bit;
+      if (hipMemcpyAsync(ctx->d_wmask.p, wm.data(), (size_t)n, hipMemcpyHostToDevice, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess) {
+        ctx->err = std::string(who) + ": write masks";
+        return 0;
+      }
+    }
+    return new_mesh_qual_core(ctx, who, opt, metRidTyp, qual, dev_result, ctx->d_out.p, ctx->sd.S, sz,
+                              ctx->sd.off[im]);
   }
-  return 1;
+  // no metric in the step: the caller's whole array
+  if (!pmx_dgrow(ctx, ctx->d_cmet, (size_t)std::max<int64_t>(n * sz, 1))) return 0;
+  if (n && (hipMemcpyAsync(ctx->d_cmet.p, hm, (size_t)(n * sz) * sizeof(double), hipMemcpyHostToDevice, s) !=
+                hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)) {
+    ctx->err = std::string(who) + ": metric upload";
+    return 0;
+  }
+  return new_mesh_qual_core(ctx, who, opt, metRidTyp, qual, dev_result, ctx->d_cmet.p, sz, sz, 0);
 }
 
 // ---- the reduction across ranks (host folds + RCCL) --------------------------------

@@ -253,7 +253,6 @@ __device__ __forceinline__ void walk_finish(const VolArgs &A, int64_t i, D3 p, b
     if (A.exp == 4) return;                      // measurement: no interpolation
     unsigned wm = interp_layout<LAYOUT, S>(A.sol, A.sd, v, lam, A.out + i * A.sd.S);
     A.wmask[i] = (uint8_t)(wm | A.const_bit);
-    // accumulated: a lane of k_walkc may finish two points
     s_cnt += 1; s_sum += step;
     s_max = max(s_max, (unsigned)step); s_min = min(s_min, (unsigned)step);
   } else {
@@ -548,253 +547,11 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
   wave_stats_w(A.wstats + (b * blockDim.x + threadIdx.x) / 64, s_cnt, s_sum, s_max, s_min);
 }
 
-// ---- k_walkc: the slot walk with one workgroup-level compaction -----------------
-//
-// A wave iterates until its longest walk ends; its other lanes idle meanwhile
-// (pmx_locate_wave_stats: lane utilisation).  k_walkc runs every lane's walk
-// for at most K steps, lets the lanes that are done interpolate, then moves
-// the walks still going (their slot state without the coordinates: 60 B per
-// lane) through LDS into the first waves of the workgroup; those continue
-// with full lanes and the others end, freeing their slots for new workgroups
-// (the LDS block, 15 KB, does not limit the workgroups per CU).  Same walk,
-// same results as k_walks.
-struct SlotWalk {
-  D3 C[4];
-  int I[4], NB[4], ring[WALK_RING];
-  int cur, step;
-  bool neg;
-  TetRec t;
-};
-
-enum { SW_CAND = 0, SW_END = 1, SW_PAUSE = 2 };
-
-// k_walks' loop on a SlotWalk: stops at a candidate, at the end (stuck, step
-// cap, invalid tet), or after a move once `limit` steps are done (pause)
-template <bool CW>
-__device__ __forceinline__ int slot_walk(const VolArgs &A, D3 p, SlotWalk &w, int limit) {
-  for (;;) {
-    w.step++;
-    D3 d[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) d[k] = D3{w.C[k].x - p.x, w.C[k].y - p.y, w.C[k].z - p.z};
-    const D3 c23 = dcross(d[2], d[3]), c01 = dcross(d[0], d[1]);
-    double ww[4] = {ddot(d[1], c23), -ddot(d[0], c23), ddot(d[3], c01), -ddot(d[2], c01)};
-    if (w.neg) {
-#pragma unroll
-      for (int k = 0; k < 4; k++) ww[k] = -ww[k];
-    }
-    const double vol = (ww[0] + ww[1]) + (ww[2] + ww[3]);
-    const double wmin = fmin(fmin(ww[0], ww[1]), fmin(ww[2], ww[3]));
-    if (!(vol > 0.0) || wmin > -(PMX_EPS + SLOT_GUARD) * vol) return SW_CAND;
-    if (w.step >= A.max_walk) return SW_END;
-#pragma unroll
-    for (int r = WALK_RING - 1; r > 0; r--) w.ring[r] = w.ring[r - 1];
-    w.ring[0] = w.cur;
-    int sb = -1;
-    double wb = 0.0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int nb = w.NB[k];
-      bool seen = false;
-#pragma unroll
-      for (int q = 0; q < WALK_RING; q++) seen |= (w.ring[q] == nb);
-      const bool take = nb && !seen && (sb < 0 || ww[k] < wb);
-      sb = take ? k : sb;
-      wb = take ? ww[k] : wb;
-    }
-    if (sb < 0) return SW_END;
-    const int next = pick4(w.NB, sb);
-    const TetRec u = walk_rec<CW>(A, next);
-    w.cur = next;
-    w.t = u;
-    if (u.v[0] <= 0) return SW_END;
-    int nnew = 0, lnew = 0;
-#pragma unroll
-    for (int l = 0; l < 4; l++) {
-      const bool any = (u.v[l] == w.I[0]) | (u.v[l] == w.I[1]) | (u.v[l] == w.I[2]) | (u.v[l] == w.I[3]);
-      nnew += any ? 0 : 1;
-      lnew = any ? lnew : l;
-    }
-    if (nnew != 1) {                                     // inconsistent adjacency: reload
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        w.C[k] = ld3(A.xyz, u.v[k]);
-        w.I[k] = u.v[k];
-        w.NB[k] = u.nb[k];
-      }
-      w.neg = false;
-      continue;
-    }
-    const int vn = pick4(u.v, lnew);
-    const D3 pn = ld3(A.xyz, vn);
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      w.C[k] = dsel(k == sb, pn, w.C[k]);
-      w.I[k] = (k == sb) ? vn : w.I[k];
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-      w.NB[k] = (u.nb[0] & -(int)(u.v[0] == w.I[k])) | (u.nb[1] & -(int)(u.v[1] == w.I[k])) |
-                (u.nb[2] & -(int)(u.v[2] == w.I[k])) | (u.nb[3] & -(int)(u.v[3] == w.I[k]));
-    w.neg = !w.neg;
-    if (w.step >= limit) return SW_PAUSE;
-  }
-}
-
-// k_walks' end of a lane: the reference's quotients on a candidate (a
-// rejected one continues in the reference's order), then walk_finish
-template <int LAYOUT, int S, bool TIES>
-__device__ __forceinline__ void slot_finish(const VolArgs &A, int64_t i, D3 p, SlotWalk &w, bool cand,
-                                            unsigned &s_cnt, unsigned &s_sum, unsigned &s_max,
-                                            unsigned &s_min) {
-  bool found = false;
-  double lam[4];
-  if (cand) {
-    D3 P[4];
-#pragma unroll
-    for (int l = 0; l < 4; l++)
-      P[l] = dsel(w.t.v[l] == w.I[0], w.C[0],
-                  dsel(w.t.v[l] == w.I[1], w.C[1], dsel(w.t.v[l] == w.I[2], w.C[2], w.C[3])));
-    for (;;) {
-      double num[4], vol;
-      face_nums(P, p, num, &vol);
-#pragma unroll
-      for (int f = 0; f < 4; f++) lam[f] = -num[f] / vol;
-      const double lmin = fmin(fmin(lam[0], lam[1]), fmin(lam[2], lam[3]));
-      if (lmin > -PMX_EPS) { found = true; break; }      // src/barycoord_pmmg.c:102-107
-      if (w.step >= A.max_walk) break;
-      const int next = exact_next(w.t, lam, w.ring, w.cur);
-      if (!next) break;
-      w.t = A.tets[next];
-      w.cur = next;
-      if (w.t.v[0] <= 0) break;
-      w.step++;
-#pragma unroll
-      for (int l = 0; l < 4; l++) P[l] = ld3(A.xyz, w.t.v[l]);
-    }
-  }
-  walk_finish<LAYOUT, S, TIES>(A, i, p, found, w.step, w.cur, w.t, lam, s_cnt, s_sum, s_max, s_min);
-}
-
-// the paused walks of one workgroup, structure of arrays (conflict-free lane
-// access); the slot coordinates are not kept: the resumed walk gathers them
-// again (4 vertex rows this workgroup has just read, L2-resident)
-struct WCShared {
-  int I[4][256], NB[4][256], ring[WALK_RING][256];
-  int idx[256], cur[256], misc[256];
-  int wcnt[4];
-};
-
-template <int LAYOUT, int S, bool TIES, bool CW, int K>
-__global__ __launch_bounds__(256) void k_walkc(VolArgs A) {
-  __shared__ WCShared sh;
-  const int64_t b = walk_xcd_remap(blockIdx.x, gridDim.x);
-  const int64_t j = b * blockDim.x + threadIdx.x;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  unsigned s_cnt = 0, s_sum = 0, s_max = 0, s_min = 0xffffffffu;
-  SlotWalk w;
-  int64_t i = 0;
-  bool paused = false;
-  if (j < *A.nlist_dev) {
-    i = A.list[j];
-    const D3 p{A.q[3 * i], A.q[3 * i + 1], A.q[3 * i + 2]};
-    w.cur = walk_hint(A.grid, A.g, p);
-    if (A.rec_start) A.start[i] = w.cur;
-#pragma unroll
-    for (int r = 0; r < WALK_RING; r++) w.ring[r] = 0;
-    w.step = 0;
-    w.neg = false;
-    w.t = walk_rec<CW>(A, w.cur);
-    int r = SW_END;
-    if (w.t.v[0] <= 0) w.step = 1;                     // !MG_EOK start: let the scan decide
-    else {
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        w.C[k] = ld3(A.xyz, w.t.v[k]);
-        w.I[k] = w.t.v[k];
-        w.NB[k] = w.t.nb[k];
-      }
-      r = slot_walk<CW>(A, p, w, K);
-    }
-    if (r == SW_PAUSE) paused = true;
-    else slot_finish<LAYOUT, S, TIES>(A, i, p, w, r == SW_CAND, s_cnt, s_sum, s_max, s_min);
-  }
-  // the walks still going, counted per wave, moved to the first waves
-  const unsigned long long bal = __ballot(paused);
-  if (lane == 0) sh.wcnt[wv] = (int)__popcll(bal);
-  __syncthreads();
-  int total = 0, off = 0;
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const int c = sh.wcnt[q];
-    off += q < wv ? c : 0;
-    total += c;
-  }
-  if (paused) {
-    const int s = off + (int)__popcll(bal & ((1ull << lane) - 1ull));
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      sh.I[k][s] = w.I[k];
-      sh.NB[k][s] = w.NB[k];
-      sh.ring[k][s] = w.ring[k];
-    }
-    // the current tet's vertex order as slots (t.v[l] = I[perm_l])
-    int perm = 0;
-#pragma unroll
-    for (int l = 0; l < 4; l++) {
-      const int k = (w.t.v[l] == w.I[0]) ? 0 : (w.t.v[l] == w.I[1]) ? 1 : (w.t.v[l] == w.I[2]) ? 2 : 3;
-      perm |= k << (2 * l);
-    }
-    sh.idx[s] = (int)i;
-    sh.cur[s] = w.cur;
-    sh.misc[s] = w.step | (w.neg ? 1 << 16 : 0) | (perm << 20);
-  }
-  __syncthreads();
-  const int t = threadIdx.x;
-  if (t < total) {
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      w.I[k] = sh.I[k][t];
-      w.NB[k] = sh.NB[k][t];
-      w.ring[k] = sh.ring[k][t];
-    }
-    i = sh.idx[t];
-    w.cur = sh.cur[t];
-    const int m = sh.misc[t];
-    w.step = m & 0xffff;
-    w.neg = (m >> 16) & 1;
-#pragma unroll
-    for (int l = 0; l < 4; l++) {
-      const int k = (m >> (20 + 2 * l)) & 3;
-      w.t.v[l] = pick4(w.I, k);
-      w.t.nb[l] = pick4(w.NB, k);
-    }
-    const D3 p{A.q[3 * i], A.q[3 * i + 1], A.q[3 * i + 2]};
-#pragma unroll
-    for (int k = 0; k < 4; k++) w.C[k] = ld3(A.xyz, w.I[k]);
-    const int r = slot_walk<CW>(A, p, w, 0x7fffffff);
-    slot_finish<LAYOUT, S, TIES>(A, i, p, w, r == SW_CAND, s_cnt, s_sum, s_max, s_min);
-  }
-  wave_stats_w(A.wstats + (b * blockDim.x + threadIdx.x) / 64, s_cnt, s_sum, s_max, s_min);
-}
-
-template <int LAYOUT, int S, bool TIES, int K>
-static void launch_walkc(const VolArgs &a, unsigned nb, hipStream_t s) {
-  hipLaunchKernelGGL((k_walkc<LAYOUT, S, TIES, true, K>), dim3(nb), dim3(256), 0, s, a);
-}
-
 template <int LAYOUT, int S>
 static void launch_walk_t(const VolArgs &a, int64_t nb, hipStream_t s) {
   if (a.ref_walk) {
     if (a.inline_ties) hipLaunchKernelGGL((k_walk<LAYOUT, S, true>), dim3((unsigned)nb), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_walk<LAYOUT, S, false>), dim3((unsigned)nb), dim3(256), 0, s, a);
-  } else if (a.wrec && a.exp >= 13 && a.exp <= 15) {
-    // exp 13 / 14 / 15: k_walkc, compaction after 2 / 3 / 4 steps (A/B)
-    const unsigned nbb = (unsigned)((a.nlist + 255) / 256);
-    const bool ti = a.inline_ties != 0;
-    if (a.exp == 13) ti ? launch_walkc<LAYOUT, S, true, 2>(a, nbb, s) : launch_walkc<LAYOUT, S, false, 2>(a, nbb, s);
-    else if (a.exp == 14) ti ? launch_walkc<LAYOUT, S, true, 3>(a, nbb, s) : launch_walkc<LAYOUT, S, false, 3>(a, nbb, s);
-    else ti ? launch_walkc<LAYOUT, S, true, 4>(a, nbb, s) : launch_walkc<LAYOUT, S, false, 4>(a, nbb, s);
   } else if (a.wrec && a.exp != 6) {           // exp 6: walk on the 32-B records (A/B)
     // exp 11 / 12: 128- / 64-thread workgroups (A/B of the dispatch granularity)
     const unsigned bs = a.exp == 11 ? 128u : a.exp == 12 ? 64u : 256u;

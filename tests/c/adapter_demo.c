@@ -18,7 +18,16 @@
  * Outputs: <dir>/out_{met,fld,qual}.bin and, on stdout, what the adapter
  * handed Mmg's display functions (one JSON object per line).
  *
- * usage: adapter_demo <dir> full|refuse_ani|refuse_les
+ * Mode "iterate": two ParMmg iterations.  Iteration 1 as above up to :845;
+ * then iteration 2 with TWO groups (a group context each, kept from
+ * iteration 1): group 0's background is iteration 1's new mesh with its
+ * interpolated metric and field (PMMG_update_oldGrps, :653), its new mesh
+ * <dir>/new2_*; group 1 repeats iteration 1's inputs.  Every PMMG_tetraQual
+ * (:845) on the device-resident new meshes is followed by a second call that
+ * takes the re-upload path (the resident state is used once): both written
+ * out (out_q{1,2a,2b}_{res,upl}.bin) for a bit-for-bit comparison.
+ *
+ * usage: adapter_demo <dir> full|refuse_ani|refuse_les|iterate
  */
 #include "parmmg.h"
 #include "pmx_transfer.h"
@@ -85,6 +94,11 @@ int MPI_Bcast(void *buf, int count, int type, int root, MPI_Comm comm) {
   fprintf(stderr, "MPI_Bcast reached with one rank\n");
   exit(3);
 }
+int MPI_Allreduce(const void *sendbuf, void *recvbuf, int count, int type, int op, MPI_Comm comm) {
+  (void)sendbuf; (void)recvbuf; (void)count; (void)type; (void)op; (void)comm;
+  fprintf(stderr, "MPI_Allreduce reached with one rank\n");
+  exit(3);
+}
 
 /* ---- mesh assembly ----------------------------------------------------------- */
 static MMG5_pMesh make_mesh(int64_t np, int64_t ne, const double *xyz, const int *tet, const uint16_t *tag) {
@@ -101,6 +115,117 @@ static MMG5_pMesh make_mesh(int64_t np, int64_t ne, const double *xyz, const int
   m->info.hausd = 0.01;
   m->info.hsiz = 0.0;
   return m;
+}
+
+/* :845 twice: the device-resident new mesh, then the re-upload path */
+static int qual_twice(const char *dir, const char *tag, PMMG_pParMesh pm) {
+  char name[64];
+  int g, k, ier;
+  for (int pass = 0; pass < 2; pass++) {
+    ier = PMMG_tetraQual(pm, 1);
+    printf("{\"call\": \"tetraqual_%s_%s\", \"ret\": %d}\n", tag, pass ? "upl" : "res", ier);
+    if (!ier) return 0;
+    for (g = 0; g < pm->ngrp; g++) {
+      MMG5_pMesh m = pm->listgrp[g].mesh;
+      double *q = calloc((size_t)m->ne + 1, sizeof(double));
+      for (k = 1; k <= m->ne; k++) q[k] = m->tetra[k].qual;
+      snprintf(name, sizeof name, "out_q%s%c_%s.bin", tag, pm->ngrp > 1 ? 'a' + g : '_', pass ? "upl" : "res");
+      wr(dir, name, q, (size_t)(m->ne + 1) * 8);
+      for (k = 1; k <= m->ne; k++) m->tetra[k].qual = -1.0;
+      free(q);
+    }
+  }
+  return 1;
+}
+
+static int iterate(const char *dir, PMMG_pParMesh pm, MMG5_pMesh mesh, MMG5_pMesh old, MMG5_pSol met,
+                   MMG5_pSol fld, MMG5_pSol oldmet, MMG5_pSol oldfld, int msize, int fsize) {
+  long long np3, ne3;
+  char path[1024];
+  FILE *f;
+  int ier, g;
+  int64_t i;
+  if (!qual_twice(dir, "1", pm)) return 1;
+  /* iteration 2 (:653): iteration 1's new mesh, metric and field become group
+   * 0's background (a snapshot copy, as PMMG_update_oldGrps makes) */
+  snprintf(path, sizeof path, "%s/sizes2.txt", dir);
+  f = fopen(path, "r");
+  if (!f || fscanf(f, "%lld %lld", &np3, &ne3) != 2) return 2;
+  fclose(f);
+  double *xyz1 = calloc((size_t)mesh->np + 1, 24);
+  int *tet1 = calloc((size_t)mesh->ne + 1, 16);
+  uint16_t *tag1 = calloc((size_t)mesh->np + 1, 2);
+  for (i = 1; i <= mesh->np; i++) {
+    memcpy(xyz1 + 3 * i, mesh->point[i].c, 24);
+    tag1[i] = mesh->point[i].tag;
+  }
+  for (i = 1; i <= mesh->ne; i++) memcpy(tet1 + 4 * i, mesh->tetra[i].v, 16);
+  MMG5_pMesh bg = make_mesh(mesh->np, mesh->ne, xyz1, tet1, tag1);
+  {
+    pmx_ctx *topo = pmx_create(0);
+    int *adja = calloc((size_t)(4 * bg->ne + 5), sizeof(int));
+    int *tria = calloc((size_t)(4 * bg->ne + 1) * 3, sizeof(int));
+    int *adjt = calloc((size_t)(12 * bg->ne + 4), sizeof(int));
+    int64_t nt;
+    if (!topo || !pmx_build_adja(topo, bg->ne, bg->np, tet1, 16, adja)) return 4;
+    nt = pmx_build_bdry(topo, bg->ne, bg->np, tet1, 16, adja, tria, 4 * bg->ne, adjt);
+    if (nt < 0) return 4;
+    bg->nt = (int)nt;
+    bg->tria = calloc((size_t)nt + 1, sizeof(MMG5_Tria));
+    for (i = 1; i <= nt; i++) memcpy(bg->tria[i].v, tria + 3 * i, 3 * sizeof(int));
+    bg->adjt = adjt;
+    bg->adja = adja;
+    free(tria);
+    pmx_destroy(topo);
+  }
+  MMG5_Sol bgmet = {mesh->np, msize, calloc((size_t)(mesh->np + 1) * msize, 8)};
+  MMG5_Sol bgfld = {mesh->np, fsize, calloc((size_t)(mesh->np + 1) * fsize, 8)};
+  memcpy(bgmet.m, met->m, (size_t)(mesh->np + 1) * msize * 8);
+  memcpy(bgfld.m, fld->m, (size_t)(mesh->np + 1) * fsize * 8);
+  double *x3 = rd(dir, "new2_xyz.bin", (size_t)(np3 + 1) * 24);
+  int *t3 = rd(dir, "new2_tet.bin", (size_t)(ne3 + 1) * 16);
+  uint16_t *g3 = rd(dir, "new2_tag.bin", (size_t)(np3 + 1) * 2);
+  MMG5_pMesh m3 = make_mesh(np3, ne3, x3, t3, g3);
+  m3->nsols = 1;
+  MMG5_Sol met3 = {(int)np3, msize, calloc((size_t)(np3 + 1) * msize, 8)};
+  MMG5_Sol fld3 = {(int)np3, fsize, calloc((size_t)(np3 + 1) * fsize, 8)};
+  for (i = 0; i < (np3 + 1) * msize; i++) met3.m[i] = -7.0;
+  for (i = 0; i < (np3 + 1) * fsize; i++) fld3.m[i] = -7.0;
+  /* group 1: iteration 1's inputs again, fresh output arrays */
+  MMG5_Sol met1 = {mesh->np, msize, calloc((size_t)(mesh->np + 1) * msize, 8)};
+  MMG5_Sol fld1 = {mesh->np, fsize, calloc((size_t)(mesh->np + 1) * fsize, 8)};
+  for (i = 0; i < (mesh->np + 1) * msize; i++) met1.m[i] = -7.0;
+  for (i = 0; i < (mesh->np + 1) * fsize; i++) fld1.m[i] = -7.0;
+  PMMG_Grp grps[2], ogrps[2];
+  memset(grps, 0, sizeof grps);
+  memset(ogrps, 0, sizeof ogrps);
+  grps[0].mesh = m3; grps[0].met = &met3; grps[0].field = &fld3;
+  ogrps[0].mesh = bg; ogrps[0].met = &bgmet; ogrps[0].field = &bgfld;
+  grps[1].mesh = mesh; grps[1].met = &met1; grps[1].field = &fld1;
+  ogrps[1].mesh = old; ogrps[1].met = oldmet; ogrps[1].field = oldfld;
+  pm->ngrp = 2;
+  pm->listgrp = grps;
+  pm->old_listgrp = ogrps;
+  for (g = 0; g < 2; g++) {
+    ier = PMMG_copyMetricsAndFields_point(grps[g].mesh, ogrps[g].mesh, grps[g].met, ogrps[g].met,
+                                          grps[g].field, ogrps[g].field, NULL, pm->info.inputMet);
+    if (!ier) return 1;
+  }
+  ier = PMMG_interpMetricsAndFields(pm, NULL);
+  printf("{\"call\": \"interp2\", \"ret\": %d}\n", ier);
+  if (!ier) return 1;
+  wr(dir, "out2_met.bin", met3.m, (size_t)(np3 + 1) * msize * 8);
+  wr(dir, "out2_fld.bin", fld3.m, (size_t)(np3 + 1) * fsize * 8);
+  wr(dir, "out2b_met.bin", met1.m, (size_t)(mesh->np + 1) * msize * 8);
+  wr(dir, "out2b_fld.bin", fld1.m, (size_t)(mesh->np + 1) * fsize * 8);
+  wr(dir, "bg2_met.bin", bgmet.m, (size_t)(mesh->np + 1) * msize * 8);
+  wr(dir, "bg2_fld.bin", bgfld.m, (size_t)(mesh->np + 1) * fsize * 8);
+  if (!qual_twice(dir, "2", pm)) return 1;
+  /* more than one group: PMMG_prilen fails as the reference's does (:623-627) */
+  ier = PMMG_prilen(pm, 1, 0);
+  printf("{\"call\": \"prilen_2grp\", \"ret\": %d}\n", ier);
+  printf("{\"adapter\": \"ok\"}\n");
+  return 0;
 }
 
 int main(int argc, char **argv) {
@@ -189,6 +314,7 @@ int main(int argc, char **argv) {
     printf("{\"call\": \"tetraqual_ani_0\", \"ret\": %d}\n", ier);
     return 0;
   }
+  if (!strcmp(mode, "iterate")) return iterate(dir, &pm, mesh, old, &met, &fld, &oldmet, &oldfld, msize, fsize);
   /* :845 */
   ier = PMMG_tetraQual(&pm, 1);
   printf("{\"call\": \"tetraqual\", \"ret\": %d}\n", ier);

@@ -161,8 +161,14 @@ int  MMG5_displayLengthHisto_internal(int ned, int amin, int bmin, double lmin, 
 int  PMMG_hashPar(MMG5_pMesh mesh, MMG5_HGeom *pHash);
 int  PMMG_build_edgeComm(PMMG_pParMesh parmesh, MMG5_pMesh mesh, MMG5_HGeom *hpar);
 void PMMG_edge_comm_free(PMMG_pParMesh parmesh);
-/* MPI_Bcast of the RCCL id: never reached with one rank */
+/* the adapter's MPI calls (the RCCL id's broadcast, the ranks' agreement on
+ * their local results): implemented by the test driver (never reached with
+ * one rank; a socketpair shim for the two-process driver) */
 int  MPI_Bcast(void *buf, int count, int type, int root, MPI_Comm comm);
+int  MPI_Allreduce(const void *sendbuf, void *recvbuf, int count, int type, int op, MPI_Comm comm);
 #define MPI_BYTE 1
+#define MPI_INT 2
+#define MPI_MIN 1
+#define MPI_IN_PLACE ((void *)1)
 
 #endif

@@ -5,7 +5,9 @@ tests/c/adapter_demo.c in the reference's call order of one iteration:
 copy (src/libparmmg1.c:792, before any device context exists) -> interp
 (:829) -> tetraQual(parmesh, 1) (:845) -> qualhisto OUTQUA (:910) ->
 prilen(parmesh, 1, 0) (:964), then the centralized input-side calls
-(src/libparmmg.c:175,185).  Results against the oracle."""
+(src/libparmmg.c:175,185); and two iterations with group contexts kept
+across them (PMMG_tetraQual on the device-resident new mesh).  Results
+against the oracle."""
 import json
 import os
 import subprocess
@@ -13,7 +15,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from helpers import compare_volume
+from helpers import bits_equal, compare_volume
 from oracle import oracle as O
 from parmmg_amd import mesh as M
 
@@ -156,3 +158,77 @@ def test_adapter_refuses_optimles(tmp_path):
     calls = {c["call"]: c["ret"] for c in recs if "call" in c}
     assert calls["qualhisto_les"] == 0
     assert "optimLES" in r.stderr
+
+
+@pytest.mark.gpu
+def test_adapter_two_iterations_resident_quality(tmp_path):
+    """Two ParMmg iterations through the adapter (src/libparmmg1.c:653-845):
+    iteration 2 has two groups, each on the group context kept from iteration
+    1.  PMMG_tetraQual right after the interpolation runs on the device-resident
+    new mesh (only the metric rows the step did not write cross PCIe); it must
+    equal the re-upload path bit for bit, and the oracle's MMG3D_tetraQual.
+    Group 0's background is iteration 1's result (PMMG_update_oldGrps); its
+    interpolation must equal a direct step on that background; group 1 repeats
+    iteration 1's inputs and must reproduce its results bit for bit."""
+    d = str(tmp_path)
+    # new meshes on the background's lattice: a frozen point keeps its index
+    # and moves by less than the jitter, so iteration 1's new mesh -- the
+    # background of iteration 2 -- stays untangled (in a tangled background a
+    # point can lie in several overlapping tets and the answer depends on the
+    # walk)
+    old, new, otag, ntag, nxyz, omet, ofld, req = write_case(d, "iso", n=6, n2=6)
+    # iteration 2's new mesh keeps the frozen points of its background
+    # (iteration 1's new mesh): same index, same position, MG_REQ
+    new2 = M.kuhn_cube(6, seed=9)
+    ntag2 = np.zeros(new2.np + 1, np.uint16)
+    nb2 = np.any((new2.xyz[1:] == 0.0) | (new2.xyz[1:] == 1.0), axis=1)
+    ntag2[1:][nb2] = M.TAG_BDY
+    ntag2[req] = ntag[req]
+    xyz2 = new2.xyz.copy()
+    xyz2[req] = nxyz[req]
+    for k, a in dict(new2_xyz=xyz2, new2_tet=new2.tet, new2_tag=ntag2).items():
+        np.ascontiguousarray(a).tofile(os.path.join(d, k + ".bin"))
+    with open(os.path.join(d, "sizes2.txt"), "w") as fh:
+        fh.write(f"{new2.np} {new2.ne}\n")
+    r, recs = run_demo(d, "iterate")
+    assert r.returncode == 0, r.stdout + r.stderr
+    calls = {c["call"]: c["ret"] for c in recs if "call" in c}
+    assert calls == {"copy": 1, "interp": 1, "tetraqual_1_res": 1, "tetraqual_1_upl": 1, "interp2": 1,
+                     "tetraqual_2_res": 1, "tetraqual_2_upl": 1, "prilen_2grp": 0}, calls
+
+    def rd(name, shape=None):
+        a = np.fromfile(os.path.join(d, name))
+        return a if shape is None else a.reshape(shape)
+    # resident quality == re-upload quality, every group of both iterations
+    for tag in ("1_", "2a", "2b"):
+        qr, qu = rd(f"out_q{tag}_res.bin"), rd(f"out_q{tag}_upl.bin")
+        assert qr.view(np.int64)[1:].tolist() == qu.view(np.int64)[1:].tolist(), tag
+    mesh1 = M.Mesh(nxyz, new.tet, new.adja, new.tria, new.adjt)
+    qo = O.tetra_qual(mesh1, None)
+    assert np.array_equal(rd("out_q1__res.bin")[1:], qo[1:])
+    assert np.array_equal(rd("out_q2b_res.bin")[1:], qo[1:])
+    mesh2 = M.Mesh(xyz2, new2.tet, new2.adja, new2.tria, new2.adjt)
+    assert np.array_equal(rd("out_q2a_res.bin")[1:], O.tetra_qual(mesh2, None)[1:])
+    # group 1 of iteration 2 = iteration 1 (same inputs, its own context)
+    assert np.array_equal(rd("out2b_met.bin"), rd("out_met.bin"))
+    assert np.array_equal(rd("out2b_fld.bin"), rd("out_fld.bin"))
+    # group 0: a direct step on iteration 1's result as background
+    bgm, bgf = rd("bg2_met.bin", (new.np + 1, 1)), rd("bg2_fld.bin", (new.np + 1, 1))
+    from parmmg_amd.transfer import Transfer
+    tr = Transfer(0)
+    # the background's boundary trias numbered as the driver's snapshot builds
+    # them (pmx_build_adja / pmx_build_bdry; the surface walk depends on it)
+    adja1 = tr.build_adja(new.tet, new.np)
+    tria1, adjt1 = tr.build_bdry(new.tet, new.np, adja1)
+    tr.upload_background(M.Mesh(nxyz, new.tet, adja1, tria1, adjt1), [bgm, bgf], 0)
+    tr.upload_points(xyz2[1:], ntag2[1:], tets_mmg=new2.tet)
+    tr.run()
+    g = tr.download()
+    tr.close()
+    m2, f2 = rd("out2_met.bin", (new2.np + 1, 1)), rd("out2_fld.bin", (new2.np + 1, 1))
+    live = (ntag2[1:] & M.TAG_REQ) == 0
+    for a, b in ((g.sols[0], m2[1:]), (g.sols[1], f2[1:])):
+        bad = np.nonzero(live & ~bits_equal(a, b))[0]
+        assert len(bad) == 0, (bad[:10], a[bad[:10], 0], b[bad[:10], 0], ntag2[1:][bad[:10]], g.elem[bad[:10]])
+    # its frozen points: the background's values (PMMG_copyMetricsAndFields_point)
+    assert np.array_equal(m2[req], bgm[req]) and np.array_equal(f2[req], bgf[req])

@@ -257,6 +257,109 @@ def resident_cycle(m, sols, cfg: dict, local: int, iters: int = 4, warmup: int =
             "timing": f"best of {iters} iterations after {warmup}, wall clock"}
 
 
+MMG_POINT = np.dtype([("c", "f8", 3), ("n", "f8", 3), ("ref", "i4"), ("xp", "i4"), ("tmp", "i4"),
+                      ("flag", "i4"), ("s", "i4"), ("tag", "u2"), ("tagdel", "i1"), ("pad", "i1")])
+MMG_TETRA = np.dtype([("qual", "f8"), ("v", "i4", 4), ("ref", "i4"), ("base", "i4"), ("mark", "i4"),
+                      ("xt", "i4"), ("flag", "i4"), ("tag", "i2"), ("pad", "i2")])
+
+
+def binding_cycle(m, x, t, tv, sols, local: int, iters: int = 3) -> dict:
+    """The per-iteration device work of integration/pmmg_pmx.c at its two
+    ParMmg seams, through the same C-ABI calls on Mmg-shaped AoS records
+    (MMG5_Point 72 B, MMG5_Tetra 48 B, strided views): PMMG_interpMetricsAndFields
+    (src/libparmmg1.c:829 -> PMX_interpMetricsAndFields_groups: new points +
+    new tets up, background up with device face matching, step, fields down)
+    then PMMG_tetraQual(parmesh, 1) (:845 -> pmx_new_mesh_qual_synced on the
+    device-resident new mesh, qualities scattered into tetra[k].qual).
+    `reupload_ms`: the r03 binding's :845 (the whole new mesh uploaded again,
+    pmx_tetra_qual).  Wall clock, best of iters."""
+    import ctypes as C
+    from parmmg_amd import _native as N
+    from parmmg_amd.transfer import Transfer
+    n = len(x)
+    op = np.zeros(m.np + 1, MMG_POINT)
+    op["c"] = m.xyz
+    ot = np.zeros(m.ne + 1, MMG_TETRA)
+    ot["v"] = m.tet
+    npnt = np.zeros(n + 1, MMG_POINT)
+    npnt["c"][1:] = x
+    npnt["tag"][1:] = t
+    nt = np.zeros(tv.shape[0], MMG_TETRA)
+    nt["v"] = tv
+    olds = [np.ascontiguousarray(s) for s in sols]
+    news = [np.full((n + 1, s.shape[1]), -7.0) for s in sols]
+    tri = np.ascontiguousarray(m.tria, np.int32)
+    adjt = np.ascontiguousarray(m.adjt, np.int32)
+
+    def ptr(a, field=None, ct=C.c_double):
+        base = a.ctypes.data + (a.dtype.fields[field][1] if field else 0)
+        return C.cast(C.c_void_p(base), C.POINTER(ct))
+
+    def sv(a):
+        v = N.SolView()
+        v.size, v.m = a.shape[1], a.ctypes.data_as(N.dptr)
+        return v
+
+    g = N.Group()
+    g.mesh.np, g.mesh.ne = n, nt.shape[0] - 1
+    g.mesh.point_c, g.mesh.point_stride = ptr(npnt, "c"), MMG_POINT.itemsize
+    g.mesh.tetra_v, g.mesh.tetra_stride = ptr(nt, "v", C.c_int), MMG_TETRA.itemsize
+    g.points.first, g.points.last = 1, n
+    g.points.c, g.points.stride = ptr(npnt, "c"), MMG_POINT.itemsize
+    g.points.tag, g.points.tag_stride = ptr(npnt, "tag", C.c_uint16), MMG_POINT.itemsize
+    g.old_mesh.np, g.old_mesh.ne, g.old_mesh.nt = m.np, m.ne, m.nt
+    g.old_mesh.point_c, g.old_mesh.point_stride = ptr(op, "c"), MMG_POINT.itemsize
+    g.old_mesh.tetra_v, g.old_mesh.tetra_stride = ptr(ot, "v", C.c_int), MMG_TETRA.itemsize
+    g.old_mesh.adja = None                     # the adapter's choice: device face matching
+    g.old_mesh.tria_v, g.old_mesh.tria_stride = tri.ctypes.data_as(N.iptr), 12
+    g.old_mesh.adjt = adjt.ctypes.data_as(N.iptr)
+    g.old_mesh.hausd = m.hausd
+    met, omet = sv(news[0]), sv(olds[0])
+    fl = (N.SolView * max(1, len(sols) - 1))(*[sv(a) for a in news[1:]])
+    ofl = (N.SolView * max(1, len(sols) - 1))(*[sv(a) for a in olds[1:]])
+    g.met, g.old_met = C.pointer(met), C.pointer(omet)
+    g.fields, g.old_fields = C.cast(fl, C.POINTER(N.SolView)), C.cast(ofl, C.POINTER(N.SolView))
+    g.nsols = len(sols) - 1
+    tr = Transfer(local)
+    st = Transfer(local)                        # the adapter's statistics context
+    lib = tr.lib
+    ctxs = (C.c_void_p * 1)(tr.ctx)
+    q = np.zeros(nt.shape[0])
+    # :845 passes metRidTyp 1 (PMMG_tetraQual(parmesh,1))
+    mrt = 1
+    rows = []
+    for it in range(iters + 1):
+        t0 = time.perf_counter()
+        if not lib.PMX_interpMetricsAndFields_groups(ctxs, 1, C.byref(g), None, 1):
+            raise RuntimeError(lib.pmx_last_error(tr.ctx).decode())
+        t1 = time.perf_counter()
+        if not lib.pmx_new_mesh_qual_synced(tr.ctx, C.byref(met), N.INQUA, mrt, q.ctypes.data_as(N.dptr), None):
+            raise RuntimeError(lib.pmx_last_error(tr.ctx).decode())
+        nt["qual"][1:] = q[1:]
+        t2 = time.perf_counter()
+        # the r03 binding's PMMG_tetraQual: the new mesh uploaded again
+        mv = N.MeshView()
+        mv.np, mv.ne = n, nt.shape[0] - 1
+        mv.point_c, mv.point_stride = ptr(npnt, "c"), MMG_POINT.itemsize
+        mv.tetra_v, mv.tetra_stride = ptr(nt, "v", C.c_int), MMG_TETRA.itemsize
+        if not (lib.pmx_upload_background(st.ctx, C.byref(mv), 1, C.byref(met), 0) and
+                lib.pmx_upload_point_tags(st.ctx, ptr(npnt, "tag", C.c_uint16), MMG_POINT.itemsize) and
+                lib.pmx_tetra_qual(st.ctx, mrt, q.ctypes.data_as(N.dptr))):
+            raise RuntimeError(lib.pmx_last_error(st.ctx).decode())
+        nt["qual"][1:] = q[1:]
+        t3 = time.perf_counter()
+        if it:
+            rows.append((t2 - t0, t1 - t0, t2 - t1, t3 - t2))
+    tr.close()
+    st.close()
+    best = min(rows)
+    return {"value": n / best[0], "unit": "vertices/s", "ms": best[0] * 1e3,
+            "phases": {"interp_ms": best[1] * 1e3, "tetra_qual_ms": best[2] * 1e3},
+            "reupload_tetra_qual_ms": min(r[3] for r in rows) * 1e3,
+            "timing": f"best of {iters} iterations, wall clock, Mmg-shaped AoS records "
+                      f"({MMG_POINT.itemsize} / {MMG_TETRA.itemsize} B)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -370,6 +473,7 @@ def main():
     if world == 1 and not args.no_pcie:
         pcie = pcie_inclusive(tr, m, x, t, sols)
         pcie["resident_cycle"] = resident_cycle(m, sols, cfg, local)
+        pcie["binding_cycle"] = binding_cycle(m, x, t, tv, sols, local)
 
     if dist is not None:
         import torch

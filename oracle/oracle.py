@@ -52,6 +52,7 @@ def load():
                                           vp, vp, C.c_int, vp, vp, vp, vp, vp]
         lib.orc_constant_size.argtypes = [i64, C.c_int, C.c_double, vp]
         lib.orc_tetra_qual.argtypes = [i64, vp, vp, vp, C.c_int, vp]
+        lib.orc_tetra_qual_rid.argtypes = [i64, vp, vp, vp, C.c_int, vp, C.c_int, vp]
         lib.orc_qualhisto.argtypes = [i64, vp, vp, C.POINTER(QualStats)]
         lib.orc_qualhisto_tags.argtypes = [i64, vp, vp, vp, C.POINTER(QualStats)]
         lib.orc_prilen.restype = C.c_int
@@ -131,12 +132,15 @@ def invmat(m):
     return bool(ok), mi
 
 
-def tetra_qual(mesh, met=None):
+def tetra_qual(mesh, met=None, tags=None, met_rid_typ=0):
+    """MMG3D_tetraQual(mesh, met, metRidTyp); tags (np+1,) MMG5_Point.tag: the
+    ridge points MMG5_moymet leaves out for metRidTyp 1 with a tensor metric."""
     lib = load()
     q = np.zeros(mesh.ne + 1)
     msize = met.shape[1] if met is not None else 0
     m = np.ascontiguousarray(met, np.float64) if met is not None else None
-    lib.orc_tetra_qual(mesh.ne, _p(mesh.xyz), _p(mesh.tet), _p(m), msize, _p(q))
+    t = None if tags is None else np.ascontiguousarray(tags, np.uint16)
+    lib.orc_tetra_qual_rid(mesh.ne, _p(mesh.xyz), _p(mesh.tet), _p(m), msize, _p(t), int(met_rid_typ), _p(q))
     return q
 
 

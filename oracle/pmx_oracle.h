@@ -97,6 +97,8 @@ typedef struct {
 /* per-tet quality (MMG3D_tetraQual -> MMG5_caltet_iso / caltet33_ani) */
 void orc_tetra_qual(int64_t ne, const double *xyz, const int *tet,
                     const double *met, int msize, double *qual /* ne+1 */);
+void orc_tetra_qual_rid(int64_t ne, const double *xyz, const int *tet, const double *met, int msize,
+                        const uint16_t *tag, int metRidTyp, double *qual);
 /* histogram of MMG3D_computeInqua-style statistics over qual[1..ne]; with
  * point tags (np+1, or NULL), MMG3D_computeOutqua's nrid */
 void orc_qualhisto(int64_t ne, const int *tet, const double *qual, orc_qualstats *st);

@@ -5,6 +5,10 @@
  *
  *   orc_tetra_qual  MMG3D_tetraQual -> MMG5_caltet_iso / MMG5_caltet33_ani
  *                   (called from reference src/quality_pmmg.c:720-733)
+ *   orc_tetra_qual_rid  the same with metRidTyp: 1 with a size-6 metric is
+ *                   MMG5_orcal -> MMG5_caltet_ani, whose mean metric
+ *                   (MMG5_moymet) leaves out the non-singular ridge points
+ *                   (their stored metric is Mmg's two-sided ridge metric)
  *   orc_qualhisto   MMG3D_computeInqua statistics as aggregated by
  *                   PMMG_qualhisto (src/quality_pmmg.c:156-261)
  *   orc_prilen      MMG3D_computePrilen (centralized branch of PMMG_prilen,
@@ -53,15 +57,14 @@ static double mlen2(const double *m, double x, double y, double z) {
   return m[0]*x*x + m[3]*y*y + m[5]*z*z + 2.0*(m[1]*x*y + m[2]*x*z + m[4]*y*z);
 }
 
-static double caltet_ani(const double *a, const double *b, const double *c, const double *d,
-                         const double *ma, const double *mb, const double *mc, const double *md) {
-  double mm[6], det, rap, num, vol;
+/* MMG5_caltet33_ani / MMG5_caltet_ani past their mean metric mm */
+static double caltet_ani_mm(const double *a, const double *b, const double *c, const double *d,
+                            const double *mm) {
+  double det, rap, num, vol;
   double abx = b[0]-a[0], aby = b[1]-a[1], abz = b[2]-a[2];
   double acx = c[0]-a[0], acy = c[1]-a[1], acz = c[2]-a[2];
   double adx = d[0]-a[0], ady = d[1]-a[1], adz = d[2]-a[2];
   double bcx, bcy, bcz, bdx, bdy, bdz, cdx, cdy, cdz;
-  int i;
-  for (i = 0; i < 6; i++) mm[i] = 0.25 * (ma[i] + mb[i] + mc[i] + md[i]);
   vol = abx*(acy*adz - acz*ady) + aby*(acz*adx - acx*adz) + abz*(acx*ady - acy*adx);
   if (vol <= 0.) return 0.0;
   det = mm[0]*(mm[3]*mm[5] - mm[4]*mm[4]) - mm[1]*(mm[1]*mm[5] - mm[2]*mm[4])
@@ -80,6 +83,51 @@ static double caltet_ani(const double *a, const double *b, const double *c, cons
   if (rap < EPSD2) return 0.0;
   num = sqrt(rap) * rap;
   return det / num;
+}
+
+/* MMG5_caltet33_ani: the plain mean of the 4 vertex metrics */
+static double caltet_ani(const double *a, const double *b, const double *c, const double *d,
+                         const double *ma, const double *mb, const double *mc, const double *md) {
+  double mm[6];
+  int i;
+  for (i = 0; i < 6; i++) mm[i] = 0.25 * (ma[i] + mb[i] + mc[i] + md[i]);
+  return caltet_ani_mm(a, b, c, d, mm);
+}
+
+static int ridge_pt(unsigned tg);
+
+/* MMG5_caltet_ani (metRidTyp = 1): MMG5_moymet's mean over the vertices that
+ * are not non-singular ridge points (MG_SIN || MG_NOM || !MG_GEO), summed in
+ * vertex order and scaled by 1/n; no such vertex: quality 0 (moymet fails) */
+static double caltet_ani_rid(const double *xyz, const double *met, const int *v, const uint16_t *tag) {
+  double mm[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, dd;
+  int i, j, n = 0;
+  for (j = 0; j < 4; j++) {
+    if (tag && ridge_pt(tag[v[j]])) continue;
+    n++;
+    for (i = 0; i < 6; i++) mm[i] += met[6*(int64_t)v[j] + i];
+  }
+  if (!n) return 0.0;
+  dd = 1. / n;
+  for (i = 0; i < 6; i++) mm[i] = mm[i] * dd;
+  return caltet_ani_mm(&xyz[3*v[0]], &xyz[3*v[1]], &xyz[3*v[2]], &xyz[3*v[3]], mm);
+}
+
+void orc_tetra_qual_rid(int64_t ne, const double *xyz, const int *tet, const double *met, int msize,
+                        const uint16_t *tag, int metRidTyp, double *qual) {
+  int64_t k;
+  qual[0] = 0.0;
+  for (k = 1; k <= ne; k++) {
+    const int *v = &tet[4*k];
+    if (v[0] <= 0) { qual[k] = 0.0; continue; }
+    if (met && msize == 6 && metRidTyp)
+      qual[k] = caltet_ani_rid(xyz, met, v, tag);
+    else if (met && msize == 6)
+      qual[k] = caltet_ani(&xyz[3*v[0]], &xyz[3*v[1]], &xyz[3*v[2]], &xyz[3*v[3]],
+                           &met[6*v[0]], &met[6*v[1]], &met[6*v[2]], &met[6*v[3]]);
+    else
+      qual[k] = caltet_iso(&xyz[3*v[0]], &xyz[3*v[1]], &xyz[3*v[2]], &xyz[3*v[3]]);
+  }
 }
 
 void orc_tetra_qual(int64_t ne, const double *xyz, const int *tet, const double *met, int msize,

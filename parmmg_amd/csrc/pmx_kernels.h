@@ -129,6 +129,11 @@ struct StatArgs {
   const double *sol;
   int S, msize, moff;
   const uint16_t *ptag;         // point tags or null (no ridge points)
+  // quality with metRidTyp = 1 and a tensor metric (MMG5_caltet_ani): the
+  // mean metric leaves out the non-singular ridge points of these tags
+  // (null: every vertex counts)
+  const uint16_t *rtag;
+  int ridmet;
   // distributed prilen: sorted (min << 32 | max) keys of the parallel edges
   // the tet loop must skip, and a per-point prefilter
   const unsigned long long *par_key;

@@ -74,11 +74,8 @@ __device__ __forceinline__ double mlen2(const double *m, double x, double y, dou
   return m[0] * x * x + m[3] * y * y + m[5] * z * z + 2.0 * (m[1] * x * y + m[2] * x * z + m[4] * y * z);
 }
 
-// MMG5_caltet33_ani (restated): quality in the mean vertex metric
-__device__ double caltet_ani(D3 a, D3 b, D3 c, D3 d, const double *ma, const double *mb,
-                             const double *mc, const double *md) {
-  double mm[6];
-  for (int i = 0; i < 6; i++) mm[i] = 0.25 * (ma[i] + mb[i] + mc[i] + md[i]);
+// MMG5_caltet33_ani / MMG5_caltet_ani (restated) past their mean metric mm
+__device__ double caltet_ani_mm(D3 a, D3 b, D3 c, D3 d, const double mm[6]) {
   double abx = b.x - a.x, aby = b.y - a.y, abz = b.z - a.z;
   double acx = c.x - a.x, acy = c.y - a.y, acz = c.z - a.z;
   double adx = d.x - a.x, ady = d.y - a.y, adz = d.z - a.z;
@@ -100,6 +97,14 @@ __device__ double caltet_ani(D3 a, D3 b, D3 c, D3 d, const double *ma, const dou
   if (rap < PMX_EPSD2) return 0.0;
   double num = sqrt(rap) * rap;
   return det / num;
+}
+
+// MMG5_caltet33_ani: the plain mean of the 4 vertex metrics
+__device__ double caltet_ani(D3 a, D3 b, D3 c, D3 d, const double *ma, const double *mb,
+                             const double *mc, const double *md) {
+  double mm[6];
+  for (int i = 0; i < 6; i++) mm[i] = 0.25 * (ma[i] + mb[i] + mc[i] + md[i]);
+  return caltet_ani_mm(a, b, c, d, mm);
 }
 
 // vertex v of the statistics' mesh (the background: dense xyz; the new mesh:
@@ -128,9 +133,31 @@ __device__ __forceinline__ bool tet_4ridge(const StatArgs &A, const int v[4]) {
   return all;
 }
 
+// MMG5_caltet_ani (metRidTyp = 1): MMG5_moymet's mean over the vertices that
+// are not non-singular ridge points (their stored metric is Mmg's two-sided
+// ridge metric), summed in vertex order and scaled by 1/n; none: quality 0
+__device__ double caltet_ani_rid(const StatArgs &A, const int v[4], D3 a, D3 b, D3 c, D3 d) {
+  double mm[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  int n = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    if (A.rtag && ridge_pt(A.rtag[v[j] - A.vbase])) continue;
+    n++;
+    const double *m = smet(A, v[j]);
+#pragma unroll
+    for (int i = 0; i < 6; i++) mm[i] += m[i];
+  }
+  if (!n) return 0.0;
+  const double dd = 1. / n;
+#pragma unroll
+  for (int i = 0; i < 6; i++) mm[i] = mm[i] * dd;
+  return caltet_ani_mm(a, b, c, d, mm);
+}
+
 template <bool ANI>
 __device__ double tet_quality(const StatArgs &A, const int v[4]) {
   D3 a = sld3(A, v[0]), b = sld3(A, v[1]), c = sld3(A, v[2]), d = sld3(A, v[3]);
+  if (ANI && A.ridmet) return caltet_ani_rid(A, v, a, b, c, d);
   if (ANI) return caltet_ani(a, b, c, d, smet(A, v[0]), smet(A, v[1]), smet(A, v[2]), smet(A, v[3]));
   return caltet_iso(a, b, c, d);
 }
@@ -823,10 +850,19 @@ static int qual_partial(pmx_ctx *ctx, const StatArgs &A, int opt, double *qual_d
   hipStream_t s = ctx->stream;
   const bool ani = A.msize == 6, out = opt == PMX_OUTQUA && A.ptag;
   double *q = use_stored ? qual_dev : nullptr;
-  if (ani && out) hipLaunchKernelGGL((k_qual<true, true>), dim3(nb), dim3(256), 0, s, A, q, parts, use_stored);
-  else if (ani) hipLaunchKernelGGL((k_qual<true, false>), dim3(nb), dim3(256), 0, s, A, q, parts, use_stored);
-  else if (out) hipLaunchKernelGGL((k_qual<false, true>), dim3(nb), dim3(256), 0, s, A, q, parts, use_stored);
-  else hipLaunchKernelGGL((k_qual<false, false>), dim3(nb), dim3(256), 0, s, A, q, parts, use_stored);
+  // MMG3D_computeInqua takes MMG5_caltet33_ani (classic storage);
+  // MMG3D_computeOutqua MMG5_orcal -> MMG5_caltet_ani, the ridge-storage mean
+  // (ridge points left out, caltet_ani_rid) -- unless the caller's stored
+  // qualities are used
+  StatArgs B = A;
+  if (ani && opt == PMX_OUTQUA && !use_stored) {
+    B.ridmet = 1;
+    B.rtag = A.ptag;
+  }
+  if (ani && out) hipLaunchKernelGGL((k_qual<true, true>), dim3(nb), dim3(256), 0, s, B, q, parts, use_stored);
+  else if (ani) hipLaunchKernelGGL((k_qual<true, false>), dim3(nb), dim3(256), 0, s, B, q, parts, use_stored);
+  else if (out) hipLaunchKernelGGL((k_qual<false, true>), dim3(nb), dim3(256), 0, s, B, q, parts, use_stored);
+  else hipLaunchKernelGGL((k_qual<false, false>), dim3(nb), dim3(256), 0, s, B, q, parts, use_stored);
   QualPart *mid = parts + nb;
   hipLaunchKernelGGL(k_qual_final, dim3(FINAL_GRID), dim3(256), 0, s, parts, nb, mid,
                      (pmx_qual_part *)nullptr, 0LL);
@@ -875,19 +911,28 @@ int pmx_upload_point_tags(pmx_ctx *ctx, const uint16_t *tag, int64_t stride) {
   return 1;
 }
 
-// MMG3D_tetraQual(mesh, met, metRidTyp) (src/quality_pmmg.c:726): metRidTyp
-// selects Mmg's ridge-metric storage.  For a size-1 metric (or none) both
-// values take the same isotropic arithmetic and are accepted; for a size-6
-// metric only the classic storage (0) is restated -- 1 needs the ridge points'
-// normals (xPoint), which the ABI does not carry: refused, not approximated.
-static bool check_met_rid_typ(pmx_ctx *ctx, int metRidTyp, int msize, const char *who) {
+// metRidTyp selects Mmg's ridge-metric storage (src/quality_pmmg.c:462,527,
+// 726).  For a size-1 metric (or none) both values take the same isotropic
+// arithmetic.  With a size-6 metric:
+//  * the quality (MMG3D_tetraQual: 0 -> MMG5_caltet33_ani, 1 -> MMG5_orcal ->
+//    MMG5_caltet_ani) is restated for both: 1 averages the metric over the
+//    vertices that are not non-singular ridge points (MMG5_moymet), which
+//    needs the point tags only (caltet_ani_rid);
+//  * the edge lengths with 1 (MMG5_lenedg -> MMG5_lenedg_ani: surface edges
+//    measured along the curved surface, ridge metrics rebuilt from the
+//    xPoint normals, MMG5_buildridmet) need the xTetra edge tags and the
+//    xPoint / point normals, which the ABI does not carry: refused, not
+//    approximated (PMMG_prilen(parmesh,1,0) at src/libparmmg1.c:964 runs
+//    once, at the end of the run).
+static bool check_met_rid_typ(pmx_ctx *ctx, int metRidTyp, int msize, const char *who, bool lengths) {
   if (metRidTyp != 0 && metRidTyp != 1) {
     ctx->err = std::string(who) + ": metRidTyp must be 0 or 1";
     return false;
   }
-  if (metRidTyp == 1 && msize == 6) {
-    ctx->err = std::string(who) + ": metRidTyp = 1 with an anisotropic metric (Mmg's ridge metric storage, "
-                                  "needs the xPoint normals) is not supported";
+  if (lengths && metRidTyp == 1 && msize == 6) {
+    ctx->err = std::string(who) + ": metRidTyp = 1 with an anisotropic metric (Mmg's ridge metric storage: "
+                                  "curved surface edges and ridge metrics need the xTetra edge tags and the "
+                                  "xPoint normals) is not supported for edge lengths";
     return false;
   }
   return true;
@@ -898,7 +943,9 @@ int pmx_tetra_qual(pmx_ctx *ctx, int metRidTyp, double *qual) {
   hipSetDevice(ctx->device);
   StatArgs A;
   if (!stat_args(ctx, A)) return 0;
-  if (!check_met_rid_typ(ctx, metRidTyp, A.msize, "pmx_tetra_qual")) return 0;
+  if (!check_met_rid_typ(ctx, metRidTyp, A.msize, "pmx_tetra_qual", false)) return 0;
+  A.ridmet = metRidTyp == 1 && A.msize == 6;
+  A.rtag = A.ptag;
   if (!pmx_dgrow(ctx, ctx->d_qual, (size_t)(ctx->ne + 1))) return 0;
   if (A.msize == 6)
     hipLaunchKernelGGL((k_qual<true, false>), dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
@@ -1007,7 +1054,7 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
   // size-6 metric 1 selects Mmg's ridge storage: refused, not approximated
   if (!ctx || !dev_result) return 0;
   if (ctx->have_bg && ctx->sd.imet >= 0 &&
-      !check_met_rid_typ(ctx, metRidTyp, ctx->sd.size[ctx->sd.imet], "pmx_prilen"))
+      !check_met_rid_typ(ctx, metRidTyp, ctx->sd.size[ctx->sd.imet], "pmx_prilen", true))
     return 0;
   if (metRidTyp != 0 && metRidTyp != 1) { ctx->err = "pmx_prilen: metRidTyp must be 0 or 1"; return 0; }
   hipSetDevice(ctx->device);
@@ -1135,7 +1182,9 @@ static int new_mesh_qual_core(pmx_ctx *ctx, const char *who, int opt, int metRid
   A.msize = msize;
   A.moff = moff;
   A.ptag = (opt == PMX_OUTQUA && ctx->have_qtag) ? ctx->d_qtag.p : nullptr;
-  if (!check_met_rid_typ(ctx, metRidTyp, A.msize, who)) return 0;
+  if (!check_met_rid_typ(ctx, metRidTyp, A.msize, who, false)) return 0;
+  A.ridmet = metRidTyp == 1 && A.msize == 6;
+  A.rtag = ctx->have_qtag ? ctx->d_qtag.p : nullptr;
   if (dev_result && opt != PMX_INQUA && opt != PMX_OUTQUA) {
     ctx->err = std::string(who) + (opt == PMX_LESQUA ? ": the optimLES quality (MMG3D_computeLESqua) is not supported"
                                                       : ": opt must be PMX_INQUA or PMX_OUTQUA");

@@ -27,7 +27,7 @@
  * takes the re-upload path (the resident state is used once): both written
  * out (out_q{1,2a,2b}_{res,upl}.bin) for a bit-for-bit comparison.
  *
- * usage: adapter_demo <dir> full|refuse_ani|refuse_les|iterate
+ * usage: adapter_demo <dir> full|ani|refuse_les|iterate
  */
 #include "parmmg.h"
 #include "pmx_transfer.h"
@@ -304,14 +304,21 @@ int main(int argc, char **argv) {
   if (!ier) return 1;
   wr(dir, "out_met.bin", met.m, (size_t)(np2 + 1) * msize * 8);
   wr(dir, "out_fld.bin", fld.m, (size_t)(np2 + 1) * fsize * 8);
-  if (!strcmp(mode, "refuse_ani")) {
-    /* :845 with an anisotropic metric: Mmg's ridge metric storage, refused */
+  if (!strcmp(mode, "ani")) {
+    /* :845 with an anisotropic metric (Mmg's ridge metric storage): the
+     * quality on the device-resident new mesh; the lengths of :964 refused */
+    double *q = calloc((size_t)ne2 + 1, sizeof(double));
     ier = PMMG_tetraQual(&pm, 1);
     printf("{\"call\": \"tetraqual_ani_1\", \"ret\": %d}\n", ier);
+    for (i = 1; i <= ne2; i++) q[i] = mesh->tetra[i].qual;
+    wr(dir, "out_qual_ani1.bin", q, (size_t)(ne2 + 1) * 8);
     ier = PMMG_prilen(&pm, 1, 0);
     printf("{\"call\": \"prilen_ani_1\", \"ret\": %d}\n", ier);
     ier = PMMG_tetraQual(&pm, 0);
     printf("{\"call\": \"tetraqual_ani_0\", \"ret\": %d}\n", ier);
+    for (i = 1; i <= ne2; i++) q[i] = mesh->tetra[i].qual;
+    wr(dir, "out_qual_ani0.bin", q, (size_t)(ne2 + 1) * 8);
+    free(q);
     return 0;
   }
   if (!strcmp(mode, "iterate")) return iterate(dir, &pm, mesh, old, &met, &fld, &oldmet, &oldfld, msize, fsize);

@@ -134,17 +134,29 @@ def test_adapter_reference_call_order(tmp_path):
 
 
 @pytest.mark.gpu
-def test_adapter_refuses_ani_ridge_metric(tmp_path):
-    """metRidTyp = 1 with an anisotropic metric (Mmg's ridge metric storage,
-    needs the xPoint normals): PMMG_tetraQual and PMMG_prilen fail loudly;
-    metRidTyp = 0 succeeds."""
+def test_adapter_ani_ridge_metric(tmp_path):
+    """metRidTyp = 1 with an anisotropic metric (Mmg's ridge metric storage):
+    PMMG_tetraQual(parmesh,1) (src/libparmmg1.c:845) runs on the device-resident
+    new mesh and equals the oracle's MMG5_caltet_ani restatement (the mean
+    metric without the non-singular ridge points, from the new points' tags)
+    bit for bit; metRidTyp = 0 equals MMG5_caltet33_ani; PMMG_prilen(parmesh,1,0)
+    (:964: curved surface edges and ridge metrics, which need the xTetra edge
+    tags and xPoint normals the ABI does not carry) fails loudly."""
     d = str(tmp_path)
-    write_case(d, "ani")
-    r, recs = run_demo(d, "refuse_ani")
+    old, new, otag, ntag, nxyz, omet, ofld, req = write_case(d, "ani")
+    r, recs = run_demo(d, "ani")
     assert r.returncode == 0, r.stdout + r.stderr
     calls = {c["call"]: c["ret"] for c in recs if "call" in c}
-    assert calls["tetraqual_ani_1"] == 0 and calls["prilen_ani_1"] == 0 and calls["tetraqual_ani_0"] == 1
+    assert calls["tetraqual_ani_1"] == 1 and calls["prilen_ani_1"] == 0 and calls["tetraqual_ani_0"] == 1
     assert "metRidTyp = 1 with an anisotropic metric" in r.stderr
+    met = np.fromfile(os.path.join(d, "out_met.bin")).reshape(new.np + 1, 6)
+    mesh_new = M.Mesh(nxyz, new.tet, new.adja, new.tria, new.adjt)
+    q1 = np.fromfile(os.path.join(d, "out_qual_ani1.bin"))
+    q0 = np.fromfile(os.path.join(d, "out_qual_ani0.bin"))
+    o1 = O.tetra_qual(mesh_new, met, tags=ntag, met_rid_typ=1)
+    o0 = O.tetra_qual(mesh_new, met)
+    assert np.array_equal(q1[1:], o1[1:]) and np.array_equal(q0[1:], o0[1:])
+    assert np.count_nonzero(q1[1:] != q0[1:]) > 0       # the ridge points change the mean
 
 
 @pytest.mark.gpu

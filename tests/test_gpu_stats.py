@@ -79,13 +79,18 @@ def test_ridge_filter_and_outqua(transfer, metric):
     Lall = O.prilen(m, sols[0])
     assert Lo["ned"] + Lo["nullEdge"] < Lall["ned"] + Lall["nullEdge"], "the filter must bite"
     assert_len_equal(L, Lo)
-    qo = O.tetra_qual(m, sols[0] if metric == "ani" else None)
+    met = sols[0] if metric == "ani" else None
+    # OUTQUA: MMG3D_computeOutqua's MMG5_orcal (ridge-storage mean for a
+    # tensor metric); INQUA: MMG3D_computeInqua's MMG5_caltet33_ani
+    qr = O.tetra_qual(m, met, tags=tags, met_rid_typ=1)
+    qo = O.tetra_qual(m, met)
     h = transfer.qualhisto(N.OUTQUA)
-    ho = O.qualhisto(m, qo, tags=tags)
+    ho = O.qualhisto(m, qr, tags=tags)
     assert ho["nrid"] > 0
     assert_qual_equal(h, ho)
     hin = transfer.qualhisto(N.INQUA)
     assert hin["nrid"] == 0 and hin["ne"] == ho["ne"]
+    assert_qual_equal(hin, O.qualhisto(m, qo))
     # tags dropped: the filter is off again
     transfer.upload_point_tags(None)
     assert_len_equal(transfer.prilen(), Lall)
@@ -219,3 +224,41 @@ def test_rccl_single_rank_equals_fold(transfer):
     fl = shard.fold_len(dl.cpu().numpy()[None])
     assert rq == fq and rl == fl
     assert rq["ne"] == 2 * m.ne and rq["cpu"] == 0 and rq["iel_grp"] == 0
+
+
+@pytest.mark.parametrize("metric", ["iso", "ani"])
+def test_tetra_qual_ridge_metric_storage(transfer, metric):
+    """MMG3D_tetraQual(mesh, met, metRidTyp) (src/quality_pmmg.c:726; ParMmg's
+    own call is PMMG_tetraQual(parmesh,1), src/libparmmg1.c:845): with a
+    tensor metric, 1 averages it over the vertices that are not non-singular
+    ridge points (MMG5_moymet; quality 0 when all 4 are), 0 over all 4
+    (MMG5_caltet33_ani).  Bit-exact against the oracle's restatement, on the
+    background and on the new mesh of a step (the points view's tags)."""
+    m, x, t, sols = cube_case(7, metric=metric, fields=False)
+    tags = ridge_tags(m)
+    met = sols[0] if metric == "ani" else None
+    transfer.upload_background(m, sols, 0)
+    transfer.upload_point_tags(tags)
+    q1, q0 = transfer.tetra_qual(m.ne, 1), transfer.tetra_qual(m.ne, 0)
+    o1 = O.tetra_qual(m, met, tags=tags, met_rid_typ=1)
+    o0 = O.tetra_qual(m, met)
+    assert np.array_equal(q1.view(np.int64)[1:], o1.view(np.int64)[1:])
+    assert np.array_equal(q0.view(np.int64)[1:], o0.view(np.int64)[1:])
+    if metric == "ani":
+        assert np.count_nonzero(q1 != q0) > 0, "the ridge points must change the mean metric"
+        assert np.count_nonzero(o1[1:] == 0.0) > 0      # tets with 4 ridge points
+    else:
+        assert np.array_equal(q1, q0)
+    # the new mesh of a step: a jittered Kuhn mesh whose points are located in
+    # m, its tags the points view's
+    nm = M.kuhn_cube(6, seed=77)
+    ntags = ridge_tags(nm) & ~np.uint16(REQ)     # frozen points are not interpolated
+    transfer.upload_points(nm.xyz[1:], ntags[1:], tets_mmg=nm.tet)
+    transfer.run()
+    r = transfer.download()
+    qn = transfer.new_mesh_qual(None, met_rid_typ=1)
+    metn = None
+    if metric == "ani":
+        metn = np.concatenate([np.zeros((1, 6)), r.sols[0]])
+    on = O.tetra_qual(nm, metn, tags=ntags, met_rid_typ=1)
+    assert np.array_equal(qn.view(np.int64)[1:], on.view(np.int64)[1:])

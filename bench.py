@@ -372,6 +372,10 @@ def main():
     ap.add_argument("--no-new-tets", action="store_true",
                     help="ablation: upload the new points without the new mesh's tets (no vertex "
                          "enumeration through the tets / orphan marks in the step)")
+    ap.add_argument("--numbering", default="lex", choices=["lex", "shuffle", "appended"],
+                    help="background tet numbering (SURVEY.md 8(d)): lex = the generator's "
+                         "cell-lexicographic order (Scotch-like), shuffle = random order (seed 7), "
+                         "appended = 10%% of the tets moved to the end (Mmg insertions)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 process group backend (nccl = RCCL; gloo only to rehearse "
                          "the multi-rank path, e.g. several ranks on one GPU)")
@@ -402,6 +406,9 @@ def main():
     cfg = CONFIGS[args.config]
     ngrp = cfg.get("groups", 1)
     cases = [build_case(cfg, rank * ngrp + g) for g in range(ngrp)]
+    if args.numbering != "lex":
+        from parmmg_amd import mesh as M
+        cases = [(M.numbering(c[0], args.numbering)[0],) + tuple(c[1:]) for c in cases]
     # the CPU baseline first: its worker processes are forked before this
     # process touches the GPU
     cpu = None
@@ -458,6 +465,8 @@ def main():
                                                             "derive"])}
     st = tr.locate_stats()
     st["volume_waves"] = tr.wave_stats(0)
+    from parmmg_amd import mesh as M
+    st["wrec_escapes"] = M.wrec_escapes(m)
     # the same step on a background already prepared by an earlier step (what
     # repeated steps on one background cost; reported, never `value`)
     sync()
@@ -512,7 +521,8 @@ def main():
         "config": {"workload": f"{args.config}: {cfg['desc']}", "n_cells": cfg["n"], "ne": m.ne,
                    "np": m.np, "nt": m.nt,
                    "new_vertices_per_gpu": sum(len(c[1]) for c in cases), "S": S,
-                   "groups_per_gpu": ngrp, "parallelism": f"group-sharded x{world}"},
+                   "groups_per_gpu": ngrp, "parallelism": f"group-sharded x{world}",
+                   "numbering": args.numbering},
         "roofline": {"bound": "hbm", "kernel": "k_walks",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None,

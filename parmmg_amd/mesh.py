@@ -189,6 +189,69 @@ def count_inverted(m: Mesh) -> int:
 
 # ---- analytic fields ----------------------------------
 
+def renumber(m: Mesh, tperm: np.ndarray, vperm: np.ndarray | None = None):
+    """The same mesh with its tets (and vertices) renumbered: tperm / vperm
+    map new -> old (0-based over 1..ne / 1..np; vperm None: vertices kept).
+    The adjacency is permuted, not rebuilt.  Returns (mesh, tinv) with
+    tinv[old tet] = new tet."""
+    ne, np_ = m.ne, m.np
+    if vperm is None:
+        vinv = np.arange(np_ + 1, dtype=np.int32)
+        xyz = m.xyz
+    else:
+        vinv = np.zeros(np_ + 1, np.int32)
+        vinv[vperm + 1] = np.arange(1, np_ + 1, dtype=np.int32)
+        xyz = np.empty_like(m.xyz)
+        xyz[0] = m.xyz[0]
+        xyz[1:] = m.xyz[vperm + 1]
+    tinv = np.zeros(ne + 1, np.int64)
+    tinv[tperm + 1] = np.arange(1, ne + 1)
+    tet = np.zeros_like(m.tet)
+    tet[1:] = vinv[m.tet[tperm + 1]]
+    old = m.adja[1:4 * ne + 1].reshape(ne, 4)[tperm]
+    k, f = old >> 2, old & 3
+    adja = np.zeros_like(m.adja)
+    adja[1:4 * ne + 1] = np.where(old > 0, 4 * tinv[k] + f, 0).astype(np.int32).ravel()
+    tria = vinv[m.tria]
+    tria[0] = 0
+    return Mesh(xyz, tet, adja, tria, m.adjt.copy(), m.hausd), tinv
+
+
+def numbering(m: Mesh, kind: str, seed: int = 7):
+    """Background tet numberings of the bench: "lex" the
+    generator's cell-lexicographic order (a Scotch-renumbered Mmg mesh);
+    "shuffle" the tets in random order (seed 7, vertices kept); "appended" 10 %
+    of the tets, chosen at random, moved to the end in their order (what Mmg's
+    insertions do to a numbering between renumberings).  Returns (mesh, tinv
+    or None)."""
+    if kind == "lex":
+        return m, None
+    rng = np.random.default_rng(seed)
+    if kind == "shuffle":
+        tp = rng.permutation(m.ne)
+    elif kind == "appended":
+        moved = np.zeros(m.ne, bool)
+        moved[rng.choice(m.ne, m.ne // 10, replace=False)] = True
+        tp = np.concatenate([np.nonzero(~moved)[0], np.nonzero(moved)[0]])
+    else:
+        raise ValueError(f"unknown numbering {kind}")
+    return renumber(m, tp)
+
+
+def wrec_escapes(m: Mesh) -> int:
+    """Tets whose walk record does not fit the 24-B encoding (pmx_wrec.h): a
+    vertex delta from v[0] outside [-2^19, 2^19) or a neighbour delta from the
+    tet index outside (-2^23, 2^23); the walk reads those from the 32-B records."""
+    t = m.tet[1:].astype(np.int64)
+    valid = t[:, 0] > 0
+    dv = t[:, 1:] - t[:, :1]
+    esc = np.any((dv < -(1 << 19)) | (dv >= (1 << 19)), axis=1)
+    nb = (m.adja[1:4 * m.ne + 1].reshape(m.ne, 4) >> 2).astype(np.int64)
+    dn = nb - np.arange(1, m.ne + 1, dtype=np.int64)[:, None]
+    esc |= np.any((nb != 0) & ((dn <= -(1 << 23)) | (dn >= (1 << 23))), axis=1)
+    return int(np.count_nonzero(esc & valid))
+
+
 def iso_metric(x: np.ndarray) -> np.ndarray:
     """h(x) = 0.05 + 0.1 x0, shape (n, 1)."""
     return (0.05 + 0.1 * x[:, 0])[:, None]

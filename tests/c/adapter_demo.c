@@ -27,8 +27,13 @@
  * takes the re-upload path (the resident state is used once): both written
  * out (out_q{1,2a,2b}_{res,upl}.bin) for a bit-for-bit comparison.
  *
- * usage: adapter_demo <dir> full|ani|refuse_les|iterate
+ * usage: adapter_demo <dir> full|ani|refuse_les|iterate|twoproc_prilen|twoproc_qualhisto
  */
+#define _POSIX_C_SOURCE 200809L
+#include <signal.h>
+#include <sys/socket.h>
+#include <sys/wait.h>
+#include <unistd.h>
 #include "parmmg.h"
 #include "pmx_transfer.h"
 
@@ -89,15 +94,44 @@ int PMMG_build_edgeComm(PMMG_pParMesh parmesh, MMG5_pMesh mesh, MMG5_HGeom *hpar
   return 1;
 }
 void PMMG_edge_comm_free(PMMG_pParMesh parmesh) { parmesh->int_edge_comm = NULL; }
+/* MPI: never reached with one rank; for the two-process mode a shim over a
+ * socketpair (rank 0 = parent, rank 1 = forked child), blocking, in call order */
+static int mpi_fd = -1, mpi_rank = 0;
+static void xfer(void *out, const void *in, size_t n) {
+  /* rank 0 writes then reads, rank 1 reads then writes: no deadlock for n < the socket buffer */
+  if (mpi_rank == 0) {
+    if (write(mpi_fd, in, n) != (ssize_t)n || read(mpi_fd, out, n) != (ssize_t)n) exit(5);
+  } else {
+    if (read(mpi_fd, out, n) != (ssize_t)n || write(mpi_fd, in, n) != (ssize_t)n) exit(5);
+  }
+}
 int MPI_Bcast(void *buf, int count, int type, int root, MPI_Comm comm) {
-  (void)buf; (void)count; (void)type; (void)root; (void)comm;
-  fprintf(stderr, "MPI_Bcast reached with one rank\n");
-  exit(3);
+  char tmp[4096];
+  (void)type; (void)comm;
+  if (mpi_fd < 0) {
+    fprintf(stderr, "MPI_Bcast reached with one rank\n");
+    exit(3);
+  }
+  if (count > (int)sizeof tmp) exit(5);
+  xfer(tmp, buf, (size_t)count);
+  if (mpi_rank != root) memcpy(buf, tmp, (size_t)count);
+  printf("{\"mpi\": \"bcast\", \"rank\": %d}\n", mpi_rank);
+  return 0;
 }
 int MPI_Allreduce(const void *sendbuf, void *recvbuf, int count, int type, int op, MPI_Comm comm) {
-  (void)sendbuf; (void)recvbuf; (void)count; (void)type; (void)op; (void)comm;
-  fprintf(stderr, "MPI_Allreduce reached with one rank\n");
-  exit(3);
+  int mine[64], other[64], i;
+  (void)comm;
+  if (mpi_fd < 0) {
+    fprintf(stderr, "MPI_Allreduce reached with one rank\n");
+    exit(3);
+  }
+  if (type != MPI_INT || op != MPI_MIN || count > 64) exit(5);
+  memcpy(mine, sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, (size_t)count * sizeof(int));
+  xfer(other, mine, (size_t)count * sizeof(int));
+  for (i = 0; i < count; i++) ((int *)recvbuf)[i] = mine[i] < other[i] ? mine[i] : other[i];
+  printf("{\"mpi\": \"allreduce\", \"rank\": %d, \"value\": %d}\n", mpi_rank, ((int *)recvbuf)[0]);
+  fflush(stdout);
+  return 0;
 }
 
 /* ---- mesh assembly ----------------------------------------------------------- */
@@ -228,6 +262,55 @@ static int iterate(const char *dir, PMMG_pParMesh pm, MMG5_pMesh mesh, MMG5_pMes
   return 0;
 }
 
+/* Mode "twoproc_<case>": two ranks (fork + socketpair MPI shim) on the
+ * statistics seams; rank 1 fails locally (<case> = prilen: two groups, the
+ * reference's refusal; qualhisto: an upload it cannot do), rank 0 does not.
+ * Both must agree on the failure and return 0 without entering a collective
+ * the other rank skips (no hang: each rank has a 120 s alarm). */
+static int twoproc(const char *dir, const char *which, MMG5_pMesh mesh, MMG5_pSol met, MMG5_pSol fld) {
+  int sv[2], ier, status = 0;
+  pid_t pid;
+  if (socketpair(AF_UNIX, SOCK_STREAM, 0, sv) != 0) return 6;
+  fflush(stdout);
+  pid = fork();
+  if (pid < 0) return 6;
+  mpi_rank = pid == 0 ? 1 : 0;
+  mpi_fd = sv[mpi_rank];
+  close(sv[1 - mpi_rank]);
+  alarm(120);
+  {
+    PMMG_Grp grps[2];
+    PMMG_ParMesh pm;
+    memset(grps, 0, sizeof grps);
+    memset(&pm, 0, sizeof pm);
+    grps[0].mesh = mesh; grps[0].met = met; grps[0].field = fld;
+    grps[1] = grps[0];
+    pm.myrank = mpi_rank; pm.nprocs = 2; pm.ngrp = 1;
+    pm.listgrp = grps; pm.old_listgrp = grps;
+    pm.info.imprim = 5; pm.info.imprim0 = 5; pm.info.root = 0; pm.info.inputMet = 1;
+    if (!strcmp(which, "prilen")) {
+      if (mpi_rank == 1) pm.ngrp = 2;                  /* :623-627: fails on this rank */
+      ier = PMMG_prilen(&pm, 0, 0);
+    } else {
+      MMG5_Mesh bad;
+      if (mpi_rank == 1) {                             /* a tet with a vertex past np */
+        bad = *mesh;
+        bad.tetra = calloc((size_t)mesh->ne + 1, sizeof(MMG5_Tetra));
+        memcpy(bad.tetra, mesh->tetra, ((size_t)mesh->ne + 1) * sizeof(MMG5_Tetra));
+        bad.tetra[1].v[2] = mesh->np + 5;
+        grps[0].mesh = &bad;
+      }
+      ier = PMMG_qualhisto(&pm, PMMG_INQUA, 0);
+    }
+    printf("{\"call\": \"%s_rank%d\", \"ret\": %d}\n", which, mpi_rank, ier);
+    fflush(stdout);
+  }
+  (void)dir;
+  if (mpi_rank == 1) _exit(0);
+  if (waitpid(pid, &status, 0) != pid || !WIFEXITED(status) || WEXITSTATUS(status) != 0) return 7;
+  return 0;
+}
+
 int main(int argc, char **argv) {
   const char *dir = argc > 1 ? argv[1] : ".";
   const char *mode = argc > 2 ? argv[2] : "full";
@@ -250,6 +333,14 @@ int main(int argc, char **argv) {
   int *ntet = rd(dir, "new_tet.bin", (size_t)(ne2 + 1) * 16);
   uint16_t *ntag = rd(dir, "new_tag.bin", (size_t)(np2 + 1) * 2);
 
+  if (!strncmp(mode, "twoproc_", 8)) {
+    /* before any HIP call: the ranks are forked processes */
+    MMG5_pMesh m2 = make_mesh(np2, ne2, nxyz, ntet, ntag);
+    MMG5_Sol met2 = {(int)np2, msize, calloc((size_t)(np2 + 1) * msize, 8)};
+    MMG5_Sol fld2 = {(int)np2, fsize, calloc((size_t)(np2 + 1) * fsize, 8)};
+    for (i = 0; i < (np2 + 1) * msize; i++) met2.m[i] = msize == 1 ? 0.05 : ((i % 6 == 0 || i % 6 == 3 || i % 6 == 5) ? 400.0 : 0.0);
+    return twoproc(dir, mode + 8, m2, &met2, &fld2);
+  }
   /* the background group: its snapshot's boundary trias + adjacency, built
    * by the device builders (their own context) */
   MMG5_pMesh old = make_mesh(np, ne, oxyz, otet, otag);

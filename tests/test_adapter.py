@@ -244,3 +244,38 @@ def test_adapter_two_iterations_resident_quality(tmp_path):
         assert len(bad) == 0, (bad[:10], a[bad[:10], 0], b[bad[:10], 0], ntag2[1:][bad[:10]], g.elem[bad[:10]])
     # its frozen points: the background's values (PMMG_copyMetricsAndFields_point)
     assert np.array_equal(m2[req], bgm[req]) and np.array_equal(f2[req], bgf[req])
+
+
+def _twoproc(d, which):
+    r, recs = run_demo(d, "twoproc_" + which)
+    assert r.returncode == 0, r.stdout + r.stderr
+    calls = {c["call"]: c["ret"] for c in recs if "call" in c}
+    mpi = [c for c in recs if "mpi" in c]
+    return calls, mpi, r
+
+
+@pytest.mark.parametrize("which", ["prilen", "qualhisto"])
+def test_adapter_two_ranks_agree_on_failure_cpu(tmp_path, which):
+    """Two ranks (forked processes, a socketpair MPI shim) through the
+    statistics seams; without a device both fail locally: each reaches the
+    agreement (one MPI_Allreduce MIN) and returns 0 -- neither waits in a
+    collective the other skipped (the r03 advisor's finding)."""
+    d = str(tmp_path)
+    write_case(d, "iso")
+    calls, mpi, r = _twoproc(d, which)
+    assert calls == {f"{which}_rank0": 0, f"{which}_rank1": 0}
+    assert sorted((m["mpi"], m["rank"]) for m in mpi) == [("allreduce", 0), ("allreduce", 1)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["prilen", "qualhisto"])
+def test_adapter_two_ranks_agree_on_failure(tmp_path, which):
+    """The same on the GPU, where rank 0 succeeds locally and rank 1 fails
+    (prilen: two groups, the reference's refusal at src/quality_pmmg.c:623-627;
+    qualhisto: an upload it must refuse): both return 0 after the agreement,
+    and no rank enters the RCCL set-up (no MPI_Bcast of its id)."""
+    d = str(tmp_path)
+    write_case(d, "iso")
+    calls, mpi, r = _twoproc(d, which)
+    assert calls == {f"{which}_rank0": 0, f"{which}_rank1": 0}
+    assert sorted((m["mpi"], m["rank"], m.get("value")) for m in mpi) == [("allreduce", 0, 0), ("allreduce", 1, 0)]

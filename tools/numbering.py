@@ -34,26 +34,9 @@ def morton_keys(x: np.ndarray, bits: int = 21) -> np.ndarray:
     return key
 
 
-def renumber(m, tperm: np.ndarray, vperm: np.ndarray):
-    """tperm/vperm: new -> old (0-based over 1..ne / 1..np)."""
-    from parmmg_amd.mesh import Mesh
-    ne, np_ = m.ne, m.np
-    vinv = np.zeros(np_ + 1, np.int32)
-    vinv[vperm + 1] = np.arange(1, np_ + 1, dtype=np.int32)
-    tinv = np.zeros(ne + 1, np.int64)
-    tinv[tperm + 1] = np.arange(1, ne + 1)
-    xyz = np.empty_like(m.xyz)
-    xyz[0] = m.xyz[0]
-    xyz[1:] = m.xyz[vperm + 1]
-    tet = np.zeros_like(m.tet)
-    tet[1:] = vinv[m.tet[tperm + 1]]
-    old = m.adja[1:4 * ne + 1].reshape(ne, 4)[tperm]
-    k, f = old >> 2, old & 3
-    adja = np.zeros_like(m.adja)
-    adja[1:4 * ne + 1] = np.where(old > 0, 4 * tinv[k] + f, 0).astype(np.int32).ravel()
-    tria = vinv[m.tria]
-    tria[0] = 0
-    return Mesh(xyz, tet, adja, tria, m.adjt.copy(), m.hausd), tinv
+def renumber(m, tperm, vperm):
+    from parmmg_amd.mesh import renumber as R
+    return R(m, tperm, vperm)
 
 
 def main():

@@ -67,7 +67,11 @@ typedef struct {
  * (v[0] > 0) are located, as in the reference's vertex loop over the new tets
  * (src/interpmesh_pmmg.c:535-541); the others are left untouched (a constant
  * size metric is still written on every valid point).  NULL: every point.
- * The tets also stay on the device (pmx_new_mesh_qual, pmx_promote_background). */
+ * The tets also stay on the device (pmx_new_mesh_qual, pmx_promote_background).
+ * They are read, validated and sent by the first pmx_run on these points,
+ * once its step is enqueued (their DMA overlaps the step and the download; a
+ * vertex outside [first, last] fails that pmx_run): the array must stay
+ * valid until then. */
 typedef struct {
   int64_t         first, last;
   const double   *c;    int64_t stride;

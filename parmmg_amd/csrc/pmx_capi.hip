@@ -285,7 +285,9 @@ pmx_ctx *pmx_create(int device) {
   ctx->stream = ctx->own;
   if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->topo, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->up, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_topo, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_tets, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc((void **)&ctx->h_nbad, 2 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess ||
       [&] {
         for (auto &e : ctx->ev_dl)
@@ -323,6 +325,7 @@ void pmx_destroy(pmx_ctx *ctx) {
   hipStreamSynchronize(ctx->stream);
   if (ctx->side) hipStreamSynchronize(ctx->side);
   if (ctx->topo) hipStreamSynchronize(ctx->topo);
+  if (ctx->up) hipStreamSynchronize(ctx->up);
   ctx->free_all();
   for (auto &e : ctx->events) hipEventDestroy(e);
   if (ctx->ev_fork) hipEventDestroy(ctx->ev_fork);
@@ -331,6 +334,9 @@ void pmx_destroy(pmx_ctx *ctx) {
   if (ctx->side) hipStreamDestroy(ctx->side);
   if (ctx->topo) hipStreamDestroy(ctx->topo);
   if (ctx->ev_topo) hipEventDestroy(ctx->ev_topo);
+  if (ctx->ev_tets) hipEventDestroy(ctx->ev_tets);
+  if (ctx->up) hipStreamDestroy(ctx->up);
+  if (ctx->h_tets) hipHostFree(ctx->h_tets);
   for (auto &e : ctx->ev_dl)
     if (e) hipEventDestroy(e);
   if (ctx->h_nbad) hipHostFree(ctx->h_nbad);
@@ -595,6 +601,13 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
     CK(hipStreamSynchronize(ctx->topo));
     ctx->next_topo = false;
   }
+  if (ctx->tets_inflight) {                 // d_ntetv / h_tets are about to be reused
+    CK(hipEventSynchronize(ctx->ev_tets));
+    ctx->tets_inflight = false;
+  }
+  ctx->tets_pending = false;
+  ctx->norph = 0;
+  ctx->orph_fixed = true;
   if (!pv) { ctx->err = "pmx_upload_points: null view"; return 0; }
   hipSetDevice(ctx->device);
   const int64_t n = pv->last - pv->first + 1;
@@ -617,16 +630,12 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   // sizes (upper bounds: orphans are found on the device).
   const int64_t ntet = pv->tetra_v ? pv->ne : 0;
   const size_t o_x = 0, o_tg = o_x + al256(nn * 3 * sizeof(double)),
-               o_tv = o_tg + al256(pv->tag ? nn * 2 : 0),
-               o_mk = o_tv + al256(ntet ? (size_t)(ntet + 1) * sizeof(int4) : 0),
-               total = o_mk + al256(pv->tetra_v ? nn : 0);
+               total = o_tg + al256(pv->tag ? nn * 2 : 0);
   CK(hipStreamSynchronize(ctx->stream));   // the arena may still feed an earlier copy
   char *st = hstage(ctx, total);
   if (!st) return 0;
   double *hx = (double *)(st + o_x);
   uint16_t *htg = (uint16_t *)(st + o_tg);
-  int4 *htv = (int4 *)(st + o_tv);
-  uint8_t *hmk = (uint8_t *)(st + o_mk);
   const char *pc = (const char *)pv->c;
   const char *tg = (const char *)pv->tag;
   if (!dgrow(ctx, ctx->d_qxyz, nn * 3) || !dgrow(ctx, ctx->d_kind, nn) || !dgrow(ctx, ctx->d_qmark, nn) ||
@@ -678,60 +687,10 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
     if (tg) CK(hipMemcpyAsync(ctx->d_qtag.p, htg, (size_t)n * 2, hipMemcpyHostToDevice, ctx->stream));
   }
   tr.mark("coords");
-  // the new tets (vertex = view index - first + 1), validated, packed in
-  // chunks whose DMA overlaps the packing of the next.  The same pass is the
-  // reference's vertex loop over the new tets (src/interpmesh_pmmg.c:535-541):
-  // it marks the points of valid tets, so that points in no valid tet
-  // (orphans: untouched, as the reference never visits them) are known.
-  // Every tet must be read here anyway to pack it; a device pass over the
-  // 16-B tets would re-read them all (C3: 1.6 GB, 0.5 ms) to find, normally,
-  // no orphan at all.  The step applies the marks only when there are some.
-  int64_t norph = 0;
-  if (pv->tetra_v) {
-    uint8_t *mk = hmk;
-    memset(mk, 0, (size_t)n);
-    const char *tc = (const char *)pv->tetra_v;
-    bool bad = false;
-    if (ntet) htv[0] = make_int4(0, 0, 0, 0);
-    const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(8, ntet >> 20));
-    for (int64_t c = 0; ntet && c < nch; c++) {
-      const int64_t lo = (c == 0) ? 0 : 1 + ntet * c / nch, hi = 1 + ntet * (c + 1) / nch;
-      par_for(std::max<int64_t>(lo, 1), hi, [&](int64_t k0, int64_t k1) {
-        bool b = false;
-        for (int64_t k = k0; k < k1; k++) {
-          const int *v = (const int *)(tc + k * pv->tetra_stride);
-          if (v[0] <= 0) { htv[k] = make_int4(0, 0, 0, 0); continue; }   // !MG_EOK
-          int w[4];
-          for (int l = 0; l < 4; l++) {
-            int64_t jj = (int64_t)v[l] - pv->first;
-            if (jj < 0 || jj >= n) { b = true; jj = 0; }
-            w[l] = (int)(jj + 1);
-            __atomic_store_n(&mk[jj], (uint8_t)1, __ATOMIC_RELAXED);
-          }
-          htv[k] = make_int4(w[0], w[1], w[2], w[3]);
-        }
-        if (b) __atomic_store_n(&bad, true, __ATOMIC_RELAXED);
-      });
-      if (bad) break;
-      CK(hipMemcpyAsync(ctx->d_ntetv.p + lo, htv + lo, (size_t)(hi - lo) * sizeof(int4), hipMemcpyHostToDevice,
-                        ctx->stream));
-    }
-    if (bad) {
-      ctx->err = "pmx_upload_points: new tet vertex outside [first, last]";
-      return 0;
-    }
-    // orphans among the points a step would locate or give a constant size
-    int64_t no[64] = {};
-    const int Co = par_chunks(0, n, [&](int ci, int64_t j0, int64_t j1) {
-      int64_t c = 0;
-      for (int64_t j = j0; j < j1; j++)
-        c += (!mk[j] && !(tg && htg[j] >= PMX_TAG_NUL)) ? 1 : 0;
-      no[ci] = c;
-    });
-    for (int i = 0; i < Co; i++) norph += no[i];
-    if (norph && n) CK(hipMemcpyAsync(ctx->d_qmark.p, mk, (size_t)n, hipMemcpyHostToDevice, ctx->stream));
-  }
-  tr.mark("tets pack+dma");
+  // the new tets are packed and sent by the first step on these points
+  // (pack_new_tets): their DMA overlaps the step and the download
+  ctx->tview = *pv;
+  ctx->tets_pending = ntet > 0;
   ctx->nq = n;
   if (!dgrow(ctx, ctx->d_wmask, nn)) return 0;
   if (!dgrow(ctx, ctx->d_elem, nn)) return 0;
@@ -758,27 +717,135 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   tr.mark("sync");
   ctx->have_qtag = tg && n;
   ctx->pts_first = pv->first;
-  ctx->pts_mark = norph > 0;            // the step applies the orphan marks
+  // orphans (points in no valid new tet) are known once the tets are packed,
+  // after the step: the step locates them too and fix_orphans resets their
+  // rows before any consumer reads them (the reference never visits them,
+  // src/interpmesh_pmmg.c:535-541)
+  ctx->pts_mark = false;
   ctx->have_pts = true;
   ctx->have_ntet = ntet > 0;
   ctx->n_ntet = ntet;
-  // residency: the next background's tet records (face adjacency built on
-  // the device) on the topo stream, while the step on these points runs
-  if (ctx->residency && ntet > 0) {
-    const int64_t ns = (ntet + PMX_HINT_STRIDE - 1) / PMX_HINT_STRIDE;
-    if (!dgrow(ctx, ctx->d_adja, (size_t)(4 * ntet + 5)) || !dgrow(ctx, ctx->d_tets_next, (size_t)(ntet + 1)) ||
-        !dgrow(ctx, ctx->d_wrec_next, (size_t)(ntet + 1)) ||
-        !dgrow(ctx, ctx->d_tets_s_next, (size_t)std::max<int64_t>(ns, 1)))
-      return 0;
-    *ctx->h_nbad = 0;
-    if (!pmx_ctx_build_adja_device(ctx, ctx->d_ntetv.p, ntet, n, ctx->d_adja.p, ctx->topo, ctx->h_nbad)) return 0;
-    launch_build_tetrec(ctx->d_ntetv.p, ctx->d_adja.p, ntet, PMX_HINT_STRIDE, ctx->d_tets_next.p,
-                        ctx->d_tets_s_next.p, ctx->topo);
-    launch_build_wrec(ctx->d_tets_next.p, ntet, ctx->d_wrec_next.p, ctx->topo);
-    CK(hipEventRecord(ctx->ev_topo, ctx->topo));
-    ctx->next_topo = true;
-  }
   return 1;
+}
+
+// ---- the new tets, after the step (pack_new_tets) ------------------------------
+
+// The points view's new tets (vertex = view index - first + 1), validated and
+// packed in chunks into their own pinned staging (the shared arena serves the
+// download meanwhile), each chunk's DMA on `up` overlapping the packing of
+// the next.  The same pass is the reference's vertex loop over the new tets
+// (src/interpmesh_pmmg.c:535-541): it marks the points of valid tets, so that
+// the points in no valid tet (orphans: untouched, the reference never visits
+// them) are known.  With residency the next background's tet records are
+// built from them on the topo stream once they have arrived.
+bool pmx_ctx::pack_new_tets() {
+  pmx_ctx *ctx = this;                     // CK()
+  if (!tets_pending) return true;
+  tets_pending = false;
+  const pmx_points_view *pv = &tview;
+  const int64_t n = nq, ntet = pv->ne;
+  Trace tr("new tets");
+  const size_t bytes = (size_t)(ntet + 1) * sizeof(int4);
+  if (bytes > h_tets_cap) {
+    if (h_tets) hipHostFree(h_tets);
+    h_tets = nullptr;
+    h_tets_cap = 0;
+    if (hipHostMalloc((void **)&h_tets, bytes, hipHostMallocDefault) != hipSuccess) {
+      err = "pmx_run: pinned staging of the new tets";
+      return false;
+    }
+    h_tets_cap = bytes;
+  }
+  int4 *htv = (int4 *)h_tets;
+  h_mk.assign((size_t)std::max<int64_t>(n, 1), 0);
+  uint8_t *mk = h_mk.data();
+  const char *tc = (const char *)pv->tetra_v;
+  bool bad = false;
+  htv[0] = make_int4(0, 0, 0, 0);
+  const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(8, ntet >> 20));
+  for (int64_t c = 0; c < nch; c++) {
+    const int64_t lo = (c == 0) ? 0 : 1 + ntet * c / nch, hi = 1 + ntet * (c + 1) / nch;
+    par_for(std::max<int64_t>(lo, 1), hi, [&](int64_t k0, int64_t k1) {
+      bool b = false;
+      for (int64_t k = k0; k < k1; k++) {
+        const int *v = (const int *)(tc + k * pv->tetra_stride);
+        if (v[0] <= 0) { htv[k] = make_int4(0, 0, 0, 0); continue; }   // !MG_EOK
+        int w[4];
+        for (int l = 0; l < 4; l++) {
+          int64_t jj = (int64_t)v[l] - pv->first;
+          if (jj < 0 || jj >= n) { b = true; jj = 0; }
+          w[l] = (int)(jj + 1);
+          __atomic_store_n(&mk[jj], (uint8_t)1, __ATOMIC_RELAXED);
+        }
+        htv[k] = make_int4(w[0], w[1], w[2], w[3]);
+      }
+      if (b) __atomic_store_n(&bad, true, __ATOMIC_RELAXED);
+    });
+    if (bad) break;
+    CK(hipMemcpyAsync(d_ntetv.p + lo, htv + lo, (size_t)(hi - lo) * sizeof(int4), hipMemcpyHostToDevice, up));
+  }
+  CK(hipEventRecord(ev_tets, up));
+  tets_inflight = true;
+  if (bad) {
+    err = "pmx_run: new tet vertex outside [first, last] of the points view";
+    have_ntet = false;
+    return false;
+  }
+  tr.mark("pack + dma issued");
+  // orphans among the points a step would locate or give a constant size
+  const char *tg = (const char *)pv->tag;
+  int64_t no[64] = {};
+  const int Co = par_chunks(0, n, [&](int ci, int64_t j0, int64_t j1) {
+    int64_t cnt = 0;
+    for (int64_t j = j0; j < j1; j++) {
+      const unsigned t = tg ? *(const uint16_t *)(tg + (pv->first + j) * pv->tag_stride) : 0u;
+      cnt += (!mk[j] && t < PMX_TAG_NUL) ? 1 : 0;
+    }
+    no[ci] = cnt;
+  });
+  norph = 0;
+  for (int i = 0; i < Co; i++) norph += no[i];
+  // residency: the next background's tet records (face adjacency built on
+  // the device) on the topo stream, after the tets' DMA, while the step and
+  // the download go on
+  if (residency && ntet > 0) {
+    const int64_t ns = (ntet + PMX_HINT_STRIDE - 1) / PMX_HINT_STRIDE;
+    if (!dgrow(this, d_adja, (size_t)(4 * ntet + 5)) || !dgrow(this, d_tets_next, (size_t)(ntet + 1)) ||
+        !dgrow(this, d_wrec_next, (size_t)(ntet + 1)) ||
+        !dgrow(this, d_tets_s_next, (size_t)std::max<int64_t>(ns, 1)))
+      return false;
+    *h_nbad = 0;
+    CK(hipStreamWaitEvent(topo, ev_tets, 0));
+    if (!pmx_ctx_build_adja_device(this, d_ntetv.p, ntet, n, d_adja.p, topo, h_nbad)) return false;
+    launch_build_tetrec(d_ntetv.p, d_adja.p, ntet, PMX_HINT_STRIDE, d_tets_next.p, d_tets_s_next.p, topo);
+    launch_build_wrec(d_tets_next.p, ntet, d_wrec_next.p, topo);
+    CK(hipEventRecord(ev_topo, topo));
+    next_topo = true;
+  }
+  return true;
+}
+
+// the new tets on the device before work on stream s reads them
+bool pmx_ctx::ensure_tets(hipStream_t s) {
+  pmx_ctx *ctx = this;
+  if (tets_pending && !pack_new_tets()) return false;
+  if (tets_inflight) CK(hipStreamWaitEvent(s, ev_tets, 0));
+  return true;
+}
+
+// The last step located every live point; the orphans' rows go back to
+// "never visited" -- no written solution bit (a constant-size metric stays:
+// MMG3D_Set_constantSize writes every valid point), element / status / steps
+// 0 -- on the stream, before any consumer of the results.
+bool pmx_ctx::fix_orphans() {
+  pmx_ctx *ctx = this;
+  if (orph_fixed) return true;
+  orph_fixed = true;
+  if (!ran || norph == 0 || nq == 0) return true;
+  CK(hipMemcpyAsync(d_qmark.p, h_mk.data(), (size_t)nq, hipMemcpyHostToDevice, stream));
+  launch_orphans(d_qmark.p, nq, (uint8_t)last_const_bit, d_wmask.p, d_elem.p, d_status.p, d_steps.p, stream);
+  CK(hipGetLastError());
+  return true;
 }
 
 // ---- the step ---------------------------------------------------------------
@@ -955,6 +1022,12 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
       if (k != 7 && k != 3) CK(hipEventRecord(ev[k], st));
   }
   CK(hipGetLastError());
+  // the step located every live point: the orphans' rows are reset by the
+  // first consumer of these results (fix_orphans); the new tets are packed
+  // and sent now, while the device runs the step
+  ctx->last_const_bit = sd.metric_const ? (1u << sd.imet) : 0u;
+  ctx->orph_fixed = false;
+  if (ctx->tets_pending && !ctx->pack_new_tets()) return 0;
   ctx->out_S = S;
   ctx->out_n = n;
   ctx->ran = true;
@@ -974,6 +1047,7 @@ int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem, int *sta
   if (!ctx) return 0;
   if (!results_ready(ctx, "pmx_download")) return 0;
   hipSetDevice(ctx->device);
+  if (!ctx->fix_orphans()) return 0;
   const int64_t n = ctx->nq;
   const int S = ctx->sd.S;
   CK(hipStreamSynchronize(ctx->stream));
@@ -1048,6 +1122,7 @@ int pmx_download_border(pmx_ctx *ctx, int *edge, int *vertex) {
 int pmx_locate_stats_get(pmx_ctx *ctx, pmx_locate_stats *st) {
   if (!ctx || !st) return 0;
   if (!results_ready(ctx, "pmx_locate_stats_get")) return 0;
+  if (!ctx->fix_orphans()) return 0;
   unsigned cnt[8];
   int nsel[2] = {0, 0};
   CK(hipStreamSynchronize(ctx->stream));
@@ -1095,6 +1170,7 @@ int pmx_locate_wave_stats(pmx_ctx *ctx, int path, pmx_wave_stats *st) {
     return 0;
   }
   if (!results_ready(ctx, "pmx_locate_wave_stats")) return 0;
+  if (!ctx->fix_orphans()) return 0;
   int nsel[2] = {0, 0};
   CK(hipStreamSynchronize(ctx->stream));
   if (!ctx->check_device_errors()) return 0;
@@ -1221,6 +1297,11 @@ int pmx_upload_new_tets(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, 
     CK(hipStreamSynchronize(ctx->topo));
     ctx->next_topo = false;
   }
+  ctx->tets_pending = false;                // these tets replace the points view's
+  if (ctx->tets_inflight) {
+    CK(hipEventSynchronize(ctx->ev_tets));
+    ctx->tets_inflight = false;
+  }
   if (!ctx->have_pts) { ctx->err = "pmx_upload_new_tets: upload the new points first"; return 0; }
   if (!tetra_v || ne < 1 || tetra_stride < 16 || 4 * ne >= (1LL << 31)) {
     ctx->err = "pmx_upload_new_tets: bad new tets";
@@ -1312,6 +1393,7 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
   hipSetDevice(ctx->device);
   Trace tr("promote");
   hipStream_t st = ctx->stream;
+  if (!ctx->fix_orphans() || !ctx->ensure_tets(st)) return 0;
   CK(hipStreamSynchronize(st));
   if (!ctx->check_device_errors()) return 0;
   tr.mark("sync");

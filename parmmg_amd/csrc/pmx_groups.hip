@@ -243,6 +243,7 @@ extern "C" int pmx_copy_required(pmx_ctx *ctx, const int *permNodGlob, int copy_
     return 0;
   }
   if (!ctx->have_ptag) { ctx->err = "pmx_copy_required: the background's point tags are not on the device"; return 0; }
+  if (!ctx->fix_orphans()) return 0;
   const int64_t np = ctx->np;
   hipStream_t s = ctx->stream;
   if (permNodGlob) {

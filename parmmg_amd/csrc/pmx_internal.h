@@ -141,6 +141,21 @@ struct pmx_ctx {
   DevBuf<uint16_t> d_qtag;
   int64_t pts_first = 0;                // points view's first index
   bool pts_mark = false;                // d_qmark holds the host's orphan marks (some point is in no valid new tet)
+  // the new tets of the points view: packed (validated, orphan marks) and
+  // sent by the first pmx_run after the upload, once its step is enqueued --
+  // their DMA on `up` overlaps the step and the results' download (the step
+  // itself never reads them); consumers wait for ev_tets (ensure_tets)
+  hipStream_t up = nullptr;
+  hipEvent_t ev_tets = nullptr;
+  char *h_tets = nullptr;               // pinned staging of the tets (not the shared arena)
+  size_t h_tets_cap = 0;
+  bool tets_pending = false;            // view kept, not packed yet
+  bool tets_inflight = false;           // DMA issued on `up`, ev_tets recorded
+  pmx_points_view tview{};
+  std::vector<uint8_t> h_mk;            // 1: the point is in a valid new tet
+  int64_t norph = 0;                    // live points in no valid new tet (known once packed)
+  bool orph_fixed = true;               // the last step's orphan rows reset (fix_orphans)
+  unsigned last_const_bit = 0;          // wmask bit of the last step's constant-size metric
   DevBuf<double> d_gather;              // all-gathered partials
 
   // timing
@@ -154,6 +169,9 @@ struct pmx_ctx {
   bool classify(hipStream_t s);           // the new points: kinds, lists, marks (pmx_capi.hip)
   bool launch_bdy(const VolArgs &a, hipStream_t s);
   bool size_tria_grid();
+  bool pack_new_tets();                   // the pending new tets: pack, send on `up`, residency build
+  bool ensure_tets(hipStream_t s);        // d_ntetv valid for work on stream s
+  bool fix_orphans();                     // the last step's rows of orphan points: untouched
   // device error word of the last step (after a stream sync): 0 = none
   bool check_device_errors();
 };

@@ -471,6 +471,26 @@ void launch_prologue(const ZeroRanges &z, hipStream_t s) {
   hipLaunchKernelGGL(k_prologue, dim3((unsigned)nb), dim3(256), 0, s, z);
 }
 
+// the rows of points in no valid new tet, after a step that located them:
+// back to untouched (the constant-size bit kept), element / status / steps 0
+__global__ __launch_bounds__(256) void k_orphans(const uint8_t *__restrict__ mk, int64_t n, uint8_t keep,
+                                                 uint8_t *__restrict__ wmask, int *__restrict__ elem,
+                                                 int *__restrict__ status, int *__restrict__ steps) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    if (mk[j]) continue;
+    wmask[j] &= keep;
+    elem[j] = 0;
+    status[j] = 0;
+    steps[j] = 0;
+  }
+}
+void launch_orphans(const uint8_t *mk, int64_t n, uint8_t keep, uint8_t *wmask, int *elem, int *status, int *steps,
+                    hipStream_t s) {
+  if (n < 1) return;
+  const int64_t nb = std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_orphans, dim3((unsigned)nb), dim3(256), 0, s, mk, n, keep, wmask, elem, status, steps);
+}
+
 // ---- device residency across iterations (pmx_promote_background) ----------------
 
 // the last step's new points and results become the background: vertex ip

@@ -1223,6 +1223,8 @@ int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, in
   } else if (!ctx->have_ntet) {
     ctx->err = "pmx_new_mesh_qual: no new tets uploaded";
     return 0;
+  } else if (!ctx->ensure_tets(ctx->stream)) {
+    return 0;
   }
   // the interpolated metric, in the step's output rows (a constant-size
   // metric of the step is there too)
@@ -1247,6 +1249,7 @@ int pmx_new_mesh_qual_synced(pmx_ctx *ctx, const pmx_sol_view *met, int opt, int
     return 0;
   }
   if (!ctx->have_ntet) { ctx->err = std::string(who) + ": the step's points view had no new tets"; return 0; }
+  if (!ctx->ensure_tets(ctx->stream) || !ctx->fix_orphans()) return 0;
   const int64_t n = ctx->nq, first = ctx->pts_first;
   hipStream_t s = ctx->stream;
   if (!met || !met->m) return new_mesh_qual_core(ctx, who, opt, metRidTyp, qual, dev_result, nullptr, 0, 0, 0);

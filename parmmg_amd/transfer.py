@@ -162,6 +162,9 @@ class Transfer:
             pv.tetra_v, pv.tetra_stride, pv.ne = _ip(tv), 16, tv.shape[0] - 1
         self._chk(self.lib.pmx_upload_points(self.ctx, C.byref(pv)), "pmx_upload_points")
         self.npts = xyz.shape[0]
+        # the view's tets are the device's new tets (read by the first run):
+        # new_mesh_qual(None) sizes its output by them
+        self.n_new_tets = int(pv.ne) if pv.tetra_v else 0
 
     def run(self, hsiz: float = 0.0, timing: bool = False, max_walk: int = 0, hint_stride: int = 0,
             flags: int = 0, record_starts: bool = False):

@@ -257,10 +257,7 @@ def resident_cycle(m, sols, cfg: dict, local: int, iters: int = 4, warmup: int =
             "timing": f"best of {iters} iterations after {warmup}, wall clock"}
 
 
-MMG_POINT = np.dtype([("c", "f8", 3), ("n", "f8", 3), ("ref", "i4"), ("xp", "i4"), ("tmp", "i4"),
-                      ("flag", "i4"), ("s", "i4"), ("tag", "u2"), ("tagdel", "i1"), ("pad", "i1")])
-MMG_TETRA = np.dtype([("qual", "f8"), ("v", "i4", 4), ("ref", "i4"), ("base", "i4"), ("mark", "i4"),
-                      ("xt", "i4"), ("flag", "i4"), ("tag", "i2"), ("pad", "i2")])
+from parmmg_amd.mesh import MMG_POINT, MMG_TETRA  # noqa: E402  (Mmg's AoS records)
 
 
 def binding_cycle(m, x, t, tv, sols, local: int, iters: int = 3) -> dict:
@@ -333,9 +330,10 @@ def binding_cycle(m, x, t, tv, sols, local: int, iters: int = 3) -> dict:
         if not lib.PMX_interpMetricsAndFields_groups(ctxs, 1, C.byref(g), None, 1):
             raise RuntimeError(lib.pmx_last_error(tr.ctx).decode())
         t1 = time.perf_counter()
-        if not lib.pmx_new_mesh_qual_synced(tr.ctx, C.byref(met), N.INQUA, mrt, q.ctypes.data_as(N.dptr), None):
+        # straight into tetra[k].qual, as the binding does
+        if not lib.pmx_new_mesh_qual_synced(tr.ctx, C.byref(met), N.INQUA, mrt, ptr(nt, "qual"),
+                                            MMG_TETRA.itemsize, None):
             raise RuntimeError(lib.pmx_last_error(tr.ctx).decode())
-        nt["qual"][1:] = q[1:]
         t2 = time.perf_counter()
         # the r03 binding's PMMG_tetraQual: the new mesh uploaded again
         mv = N.MeshView()

@@ -433,8 +433,8 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
 int pmx_prilen(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, pmx_len_stats *st);
 
 /* PMMG_tetraQual(parmesh, metRidTyp) on the NEW mesh right after the
- * interpolation (src/libparmmg1.c:845, metRidTyp = 1; refused for a size-6
- * metric as in pmx_tetra_qual): the new tets (1-based records through a stride,
+ * interpolation (src/libparmmg1.c:845, metRidTyp = 1; a size-6 metric
+ * takes MMG5_caltet_ani's ridge-aware mean as in pmx_tetra_qual): the new tets (1-based records through a stride,
  * vertex indices in the last points view's numbering) are uploaded as by
  * pmx_upload_new_tets -- or tetra_v = NULL: the ones already uploaded; the
  * coordinates and the interpolated metric are the step's device-resident
@@ -452,9 +452,14 @@ int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, in
  * metric; only the rows the step did not write -- frozen points the caller
  * filled (PMMG_copyMetricsAndFields_point), failed tensor inversions -- are
  * sent, or the whole array when the step interpolated no metric (-hsiz, Mmg's
- * own metric).  qual / dev_result as in pmx_new_mesh_qual. */
+ * own metric).  dev_result as in pmx_new_mesh_qual.  qual: the qualities of
+ * tets 1..ne through qual_stride bytes -- 0 or 8: a dense array of ne+1
+ * doubles, every entry written (deleted tets 0, qual[0] = 0); any larger
+ * stride: an AoS field such as &mesh->tetra[0].qual with sizeof(MMG5_Tetra),
+ * written for the valid tets only (MMG3D_tetraQual skips !MG_EOK) -- straight
+ * from pinned staging, no intermediate array. */
 int pmx_new_mesh_qual_synced(pmx_ctx *ctx, const pmx_sol_view *met, int opt, int metRidTyp, double *qual,
-                             void *dev_result);
+                             int64_t qual_stride, void *dev_result);
 
 /* The reduction across groups and ranks (the reference's MPI_Reduce with its
  * custom operators, src/quality_pmmg.c:82-144, :265-307, :661-676), as host

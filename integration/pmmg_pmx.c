@@ -223,31 +223,33 @@ static int pmx_resident(int igrp, MMG5_pMesh mesh) {
  * any other mesh is uploaded. */
 int PMMG_tetraQual(PMMG_pParMesh parmesh, int8_t metRidTyp) {
   int igrp, k, ok;
-  double *q;
+  double *q = NULL;
   for (igrp = 0; igrp < parmesh->ngrp; igrp++) {
     PMMG_pGrp grp = &parmesh->listgrp[igrp];
     MMG5_pMesh mesh = grp->mesh;
     pmx_ctx *ctx;
-    PMMG_MALLOC(parmesh, q, mesh->ne + 1, double, "qual", return 0);
     if (pmx_resident(igrp, mesh)) {
+      /* the qualities straight into tetra[k].qual (valid tets only) */
       pmx_sol_view mv;
       ctx = PMMG_pmx_grp[igrp];
       PMMG_pmx_state[igrp].valid = 0;            /* one use per interpolation */
       if (grp->met && grp->met->m) view_sol(grp->met, &mv);
-      ok = pmx_new_mesh_qual_synced(ctx, grp->met && grp->met->m ? &mv : NULL, PMX_INQUA, metRidTyp, q, NULL);
+      ok = pmx_new_mesh_qual_synced(ctx, grp->met && grp->met->m ? &mv : NULL, PMX_INQUA, metRidTyp,
+                                    &mesh->tetra[0].qual, sizeof(MMG5_Tetra), NULL);
     } else {
       ctx = pmx(parmesh);
+      PMMG_MALLOC(parmesh, q, mesh->ne + 1, double, "qual", return 0);
       ok = ctx && upload_stats_group(ctx, mesh, grp->met) && pmx_tetra_qual(ctx, metRidTyp, q);
+      if (ok)
+        for (k = 1; k <= mesh->ne; k++)
+          if (MG_EOK(&mesh->tetra[k])) mesh->tetra[k].qual = q[k];
+      PMMG_DEL_MEM(parmesh, q, double, "qual");
     }
     if (!ok) {
-      PMMG_DEL_MEM(parmesh, q, double, "qual");
       if (ctx) pmx_fail(ctx, __func__);
       fprintf(stderr, "\n  ## Quality computation problem.\n");
       return 0;
     }
-    for (k = 1; k <= mesh->ne; k++)
-      if (MG_EOK(&mesh->tetra[k])) mesh->tetra[k].qual = q[k];
-    PMMG_DEL_MEM(parmesh, q, double, "qual");
   }
   return 1;
 }

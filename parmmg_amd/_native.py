@@ -168,7 +168,8 @@ SIGNATURES = {
     "pmx_prilen_device": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(ParEdges), C.c_void_p]),
     "pmx_prilen": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(ParEdges), C.POINTER(LenStats)]),
     "pmx_new_mesh_qual": (C.c_int, [C.c_void_p, iptr, i64, i64, C.c_int, C.c_int, dptr, C.c_void_p]),
-    "pmx_new_mesh_qual_synced": (C.c_int, [C.c_void_p, C.POINTER(SolView), C.c_int, C.c_int, dptr, C.c_void_p]),
+    "pmx_new_mesh_qual_synced": (C.c_int, [C.c_void_p, C.POINTER(SolView), C.c_int, C.c_int, dptr, i64,
+                                          C.c_void_p]),
     "pmx_upload_new_tets": (C.c_int, [C.c_void_p, iptr, i64, i64]),
     "pmx_set_residency": (C.c_int, [C.c_void_p, C.c_int]),
     "pmx_copy_required": (C.c_int, [C.c_void_p, iptr, C.c_int]),

@@ -76,6 +76,26 @@ static unsigned host_threads() {
   }();
   return T;
 }
+// streaming (non-temporal) 16-B stores into the pinned staging: the host
+// never reads those lines again, and a plain store first reads each line for
+// ownership (a third of the packing traffic).  PMX_NT_STORES=0: plain stores,
+// for the A/B.  A pass ends with a full fence before its DMA is issued.
+typedef int pmx_v4i __attribute__((ext_vector_type(4)));
+static bool nt_stores() {
+  static const bool on = [] {
+    const char *e = getenv("PMX_NT_STORES");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+static inline void st4(int4 *p, int a, int b, int c, int d, bool nt) {
+  if (nt) {
+    const pmx_v4i v = {a, b, c, d};
+    __builtin_nontemporal_store(v, (pmx_v4i *)p);
+  } else {
+    *p = make_int4(a, b, c, d);
+  }
+}
 static int64_t host_threads_min() {
   static const int64_t M = [] {
     const char *e = getenv("PMX_HOST_THREADS_MIN");
@@ -190,6 +210,59 @@ template <class F> static int par_chunks(int64_t lo, int64_t hi, F f) {
 }
 template <class F> static void par_for(int64_t lo, int64_t hi, F f) {
   par_chunks(lo, hi, [&](int, int64_t a, int64_t b) { if (a < b) f(a, b); });
+}
+void pmx_par_for(int64_t lo, int64_t hi, const std::function<void(int64_t, int64_t)> &f) {
+  par_for(lo, hi, f);
+}
+
+bool pmx_download_qual(pmx_ctx *ctx, const double *dev, int64_t ne, double *qual, int64_t stride) {
+  const bool dense = stride == (int64_t)sizeof(double);
+  const int4 *htv = (const int4 *)ctx->h_tets;
+  if (!dense && (!htv || ctx->h_tets_cap < (size_t)(ne + 1) * sizeof(int4))) {
+    ctx->err = "qualities: strided output needs the new tets' host copy";
+    return false;
+  }
+  hipStream_t s = ctx->stream;
+  char *st = hstage(ctx, (size_t)(ne + 1) * sizeof(double));
+  if (!st) return false;
+  const double *h = (const double *)st;
+  char *out = (char *)qual;
+  const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(8, (ne + 1) >> 20));
+  for (int64_t c = 0; c < nch; c++) {
+    const int64_t lo = (ne + 1) * c / nch, hi = (ne + 1) * (c + 1) / nch;
+    CK(hipMemcpyAsync(st + lo * 8, dev + lo, (size_t)(hi - lo) * 8, hipMemcpyDeviceToHost, s));
+    CK(hipEventRecord(ctx->ev_dl[c], s));
+  }
+  for (int64_t c = 0; c < nch; c++) {
+    const int64_t lo = (ne + 1) * c / nch, hi = (ne + 1) * (c + 1) / nch;
+    CK(hipEventSynchronize(ctx->ev_dl[c]));
+    if (dense) {
+      par_for(lo, hi, [&](int64_t k0, int64_t k1) { memcpy(qual + k0, h + k0, (size_t)(k1 - k0) * 8); });
+    } else {
+      par_for(std::max<int64_t>(lo, 1), hi, [&](int64_t k0, int64_t k1) {
+        for (int64_t k = k0; k < k1; k++)
+          if (htv[k].x) *(double *)(out + k * stride) = h[k];
+      });
+    }
+  }
+  if (dense) qual[0] = 0.0;
+  return true;
+}
+
+// the pinned copy of the new tets, ne + 1 records
+int4 *pmx_ctx::grow_htets(int64_t ne) {
+  const size_t bytes = (size_t)(ne + 1) * sizeof(int4);
+  if (bytes > h_tets_cap) {
+    if (h_tets) hipHostFree(h_tets);
+    h_tets = nullptr;
+    h_tets_cap = 0;
+    if (hipHostMalloc((void **)&h_tets, bytes, hipHostMallocDefault) != hipSuccess) {
+      err = "pinned staging of the new tets";
+      return nullptr;
+    }
+    h_tets_cap = bytes;
+  }
+  return (int4 *)h_tets;
 }
 
 template <class T> static void dfree(DevBuf<T> &b) {
@@ -494,6 +567,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   const char *tc = (const char *)m->tetra_v;
   const int *adja_in = m->adja;
   bool bad = false;
+  const bool ntst = nt_stores();
   const int64_t ntc = std::max<int64_t>(1, std::min<int64_t>(8, ne >> 20));
   for (int64_t c = 0; c < ntc; c++) {
     const int64_t klo = (c == 0) ? 0 : 1 + ne * c / ntc, khi = 1 + ne * (c + 1) / ntc;
@@ -505,11 +579,11 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
         // MG_EOK) must name vertices 1..np and neighbours 0..ne
         const bool valid = v[0] > 0;
         if (dev_adja) {
-          if (!valid) { htv[k] = make_int4(0, 0, 0, 0); }
+          if (!valid) { st4(&htv[k], 0, 0, 0, 0, ntst); }
           else {
             for (int l = 0; l < 4; l++)
               if (v[l] < 1 || v[l] > np) b = true;
-            htv[k] = make_int4(v[0], v[1], v[2], v[3]);
+            st4(&htv[k], v[0], v[1], v[2], v[3], ntst);
           }
         } else {
           TetRec &r = ht[(size_t)k];
@@ -523,6 +597,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
         if ((k - 1) % PMX_HINT_STRIDE == 0) hh[(k - 1) / PMX_HINT_STRIDE] = make_int4(v[0], v[1], v[2], v[3]);
       }
       if (b) __atomic_store_n(&bad, true, __ATOMIC_RELAXED);
+      std::atomic_thread_fence(std::memory_order_seq_cst);
     });
     if (bad) break;
     if (dev_adja)
@@ -745,23 +820,14 @@ bool pmx_ctx::pack_new_tets() {
   const pmx_points_view *pv = &tview;
   const int64_t n = nq, ntet = pv->ne;
   Trace tr("new tets");
-  const size_t bytes = (size_t)(ntet + 1) * sizeof(int4);
-  if (bytes > h_tets_cap) {
-    if (h_tets) hipHostFree(h_tets);
-    h_tets = nullptr;
-    h_tets_cap = 0;
-    if (hipHostMalloc((void **)&h_tets, bytes, hipHostMallocDefault) != hipSuccess) {
-      err = "pmx_run: pinned staging of the new tets";
-      return false;
-    }
-    h_tets_cap = bytes;
-  }
-  int4 *htv = (int4 *)h_tets;
+  int4 *htv = grow_htets(ntet);
+  if (!htv) return false;
   h_mk.assign((size_t)std::max<int64_t>(n, 1), 0);
   uint8_t *mk = h_mk.data();
   const char *tc = (const char *)pv->tetra_v;
   bool bad = false;
   htv[0] = make_int4(0, 0, 0, 0);
+  const bool nt = nt_stores();
   const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(8, ntet >> 20));
   for (int64_t c = 0; c < nch; c++) {
     const int64_t lo = (c == 0) ? 0 : 1 + ntet * c / nch, hi = 1 + ntet * (c + 1) / nch;
@@ -769,7 +835,7 @@ bool pmx_ctx::pack_new_tets() {
       bool b = false;
       for (int64_t k = k0; k < k1; k++) {
         const int *v = (const int *)(tc + k * pv->tetra_stride);
-        if (v[0] <= 0) { htv[k] = make_int4(0, 0, 0, 0); continue; }   // !MG_EOK
+        if (v[0] <= 0) { st4(&htv[k], 0, 0, 0, 0, nt); continue; }   // !MG_EOK
         int w[4];
         for (int l = 0; l < 4; l++) {
           int64_t jj = (int64_t)v[l] - pv->first;
@@ -777,9 +843,10 @@ bool pmx_ctx::pack_new_tets() {
           w[l] = (int)(jj + 1);
           __atomic_store_n(&mk[jj], (uint8_t)1, __ATOMIC_RELAXED);
         }
-        htv[k] = make_int4(w[0], w[1], w[2], w[3]);
+        st4(&htv[k], w[0], w[1], w[2], w[3], nt);
       }
       if (b) __atomic_store_n(&bad, true, __ATOMIC_RELAXED);
+      std::atomic_thread_fence(std::memory_order_seq_cst);
     });
     if (bad) break;
     CK(hipMemcpyAsync(d_ntetv.p + lo, htv + lo, (size_t)(hi - lo) * sizeof(int4), hipMemcpyHostToDevice, up));
@@ -1309,29 +1376,31 @@ int pmx_upload_new_tets(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, 
   }
   hipSetDevice(ctx->device);
   const int64_t first = ctx->pts_first, n = ctx->nq;
-  CK(hipStreamSynchronize(ctx->stream));   // the arena may still feed an earlier copy
-  char *st = hstage(ctx, (size_t)(ne + 1) * sizeof(int4));
-  if (!st) return 0;
-  int4 *h = (int4 *)st;
+  // packed into the pinned copy of the new tets (a strided quality output
+  // reads their validity there)
+  int4 *h = ctx->grow_htets(ne);
+  if (!h) return 0;
   h[0] = make_int4(0, 0, 0, 0);
   const char *tc = (const char *)tetra_v;
   bool bad = false;
+  const bool nt = nt_stores();
   // vertices renumbered from the points view (first..last) to 1..n: the
   // numbering of a promoted background
   par_for(1, ne + 1, [&](int64_t k0, int64_t k1) {
     bool b = false;
     for (int64_t k = k0; k < k1; k++) {
       const int *v = (const int *)(tc + k * tetra_stride);
-      if (v[0] <= 0) { h[k] = make_int4(0, 0, 0, 0); continue; }   // !MG_EOK
+      if (v[0] <= 0) { st4(&h[k], 0, 0, 0, 0, nt); continue; }   // !MG_EOK
       int w[4];
       for (int l = 0; l < 4; l++) {
         const int64_t j = (int64_t)v[l] - first;
         if (j < 0 || j >= n) b = true;
         w[l] = (int)(j + 1);
       }
-      h[k] = make_int4(w[0], w[1], w[2], w[3]);
+      st4(&h[k], w[0], w[1], w[2], w[3], nt);
     }
     if (b) __atomic_store_n(&bad, true, __ATOMIC_RELAXED);
+    std::atomic_thread_fence(std::memory_order_seq_cst);
   });
   if (bad) { ctx->err = "pmx_upload_new_tets: tet vertex outside the uploaded points"; return 0; }
   if (!dgrow(ctx, ctx->d_ntetv, (size_t)(ne + 1))) return 0;

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <functional>
 #include <string>
 #include <vector>
 #include "pmx_transfer.h"
@@ -147,8 +148,8 @@ struct pmx_ctx {
   // itself never reads them); consumers wait for ev_tets (ensure_tets)
   hipStream_t up = nullptr;
   hipEvent_t ev_tets = nullptr;
-  char *h_tets = nullptr;               // pinned staging of the tets (not the shared arena)
-  size_t h_tets_cap = 0;
+  char *h_tets = nullptr;               // pinned copy of the current new tets (int4, 0 = deleted);
+  size_t h_tets_cap = 0;                // not the shared arena: it outlives the step (qualities' validity)
   bool tets_pending = false;            // view kept, not packed yet
   bool tets_inflight = false;           // DMA issued on `up`, ev_tets recorded
   pmx_points_view tview{};
@@ -172,6 +173,7 @@ struct pmx_ctx {
   bool pack_new_tets();                   // the pending new tets: pack, send on `up`, residency build
   bool ensure_tets(hipStream_t s);        // d_ntetv valid for work on stream s
   bool fix_orphans();                     // the last step's rows of orphan points: untouched
+  int4 *grow_htets(int64_t ne);           // h_tets for ne + 1 records (ev_tets already waited)
   // device error word of the last step (after a stream sync): 0 = none
   bool check_device_errors();
 };
@@ -193,6 +195,15 @@ template <class T> inline bool pmx_dgrow(pmx_ctx *ctx, DevBuf<T> &b, size_t n) {
 }
 // the context's pinned staging arena, at least `bytes` (pmx_capi.hip)
 char *pmx_hstage(pmx_ctx *ctx, size_t bytes);
+// qualities dev[0..ne] (stream order) into the caller's array: stride 8
+// (dense) writes qual[0..ne] with qual[0] = 0; any other stride (bytes, an
+// AoS field such as &MMG5_Tetra[0].qual) writes only the tets that are valid
+// in h_tets (deleted tets keep their value, as MMG3D_tetraQual skips
+// !MG_EOK).  Chunked through the pinned arena, each chunk's host scatter
+// overlapping the next one's DMA (pmx_capi.hip).
+bool pmx_download_qual(pmx_ctx *ctx, const double *dev, int64_t ne, double *qual, int64_t stride);
+// f(i0, i1) over [lo, hi) on the host pool (pmx_capi.hip)
+void pmx_par_for(int64_t lo, int64_t hi, const std::function<void(int64_t, int64_t)> &f);
 
 // face adjacency of device connectivity (1-based int4, slot 0 unused) into
 // dadja (Mmg layout, 4 ne + 5 ints), context-owned scratch; false on a

@@ -34,6 +34,7 @@
 #include <cstring>
 #include <unordered_set>
 #include <type_traits>
+#include <mutex>
 #include <vector>
 #include "pmx_internal.h"
 
@@ -1166,7 +1167,7 @@ int pmx_prilen(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, pmx_len_st
 // the quality pass over the device-resident new mesh (the step's points and
 // the uploaded new tets), in the metric at sol[S * j + moff] (msize 0: none)
 static int new_mesh_qual_core(pmx_ctx *ctx, const char *who, int opt, int metRidTyp, double *qual,
-                              void *dev_result, const double *sol, int S, int msize, int moff) {
+                              int64_t qstride, void *dev_result, const double *sol, int S, int msize, int moff) {
   const int64_t ne = ctx->n_ntet;
   const int64_t n = ctx->nq;
   hipStream_t s = ctx->stream;
@@ -1197,13 +1198,9 @@ static int new_mesh_qual_core(pmx_ctx *ctx, const char *who, int opt, int metRid
     hipLaunchKernelGGL((k_qual<false, false>), dim3(nb), dim3(256), 0, s, A, ctx->d_nqual.p, (QualPart *)nullptr, 0);
   if (dev_result && !qual_partial(ctx, A, opt, ctx->d_nqual.p, 1, (pmx_qual_part *)dev_result, n)) return 0;
   if (hipGetLastError() != hipSuccess) { ctx->err = std::string(who) + ": launch"; return 0; }
-  if (qual) {
-    if (hipMemcpyAsync(qual, ctx->d_nqual.p, (size_t)(ne + 1) * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess) {
-      ctx->err = std::string(who) + ": download";
-      return 0;
-    }
-    qual[0] = 0.0;
+  if (qual && !pmx_download_qual(ctx, ctx->d_nqual.p, ne, qual, qstride)) {
+    ctx->err = std::string(who) + ": " + ctx->err;
+    return 0;
   }
   return 1;
 }
@@ -1230,7 +1227,7 @@ int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, in
   // metric of the step is there too)
   const int msize = ctx->sd.imet >= 0 ? ctx->sd.size[ctx->sd.imet] : 0;
   const int moff = ctx->sd.imet >= 0 ? ctx->sd.off[ctx->sd.imet] : 0;
-  return new_mesh_qual_core(ctx, "pmx_new_mesh_qual", opt, metRidTyp, qual, dev_result, ctx->d_out.p, ctx->sd.S,
+  return new_mesh_qual_core(ctx, "pmx_new_mesh_qual", opt, metRidTyp, qual, 8, dev_result, ctx->d_out.p, ctx->sd.S,
                             msize, moff);
 }
 
@@ -1240,10 +1237,12 @@ int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, in
 // the host, failed tensor inversions) sent to the device; a metric the step
 // did not interpolate (-hsiz constant size, or Mmg's own) is sent whole.
 int pmx_new_mesh_qual_synced(pmx_ctx *ctx, const pmx_sol_view *met, int opt, int metRidTyp, double *qual,
-                             void *dev_result) {
+                             int64_t qual_stride, void *dev_result) {
   if (!ctx) return 0;
   hipSetDevice(ctx->device);
   const char *who = "pmx_new_mesh_qual_synced";
+  const int64_t qs = qual_stride ? qual_stride : (int64_t)sizeof(double);
+  if (qs < (int64_t)sizeof(double)) { ctx->err = std::string(who) + ": bad quality stride"; return 0; }
   if (!ctx->ran || !ctx->have_pts || ctx->out_n != ctx->nq) {
     ctx->err = std::string(who) + ": run a step on the new points first";
     return 0;
@@ -1252,7 +1251,7 @@ int pmx_new_mesh_qual_synced(pmx_ctx *ctx, const pmx_sol_view *met, int opt, int
   if (!ctx->ensure_tets(ctx->stream) || !ctx->fix_orphans()) return 0;
   const int64_t n = ctx->nq, first = ctx->pts_first;
   hipStream_t s = ctx->stream;
-  if (!met || !met->m) return new_mesh_qual_core(ctx, who, opt, metRidTyp, qual, dev_result, nullptr, 0, 0, 0);
+  if (!met || !met->m) return new_mesh_qual_core(ctx, who, opt, metRidTyp, qual, qs, dev_result, nullptr, 0, 0, 0);
   const int sz = met->size;
   if (sz != 1 && sz != 6) { ctx->err = std::string(who) + ": metric size must be 1 or 6"; return 0; }
   const double *hm = met->m + first * sz;      // Mmg layout: entry of point `first`
@@ -1265,12 +1264,28 @@ int pmx_new_mesh_qual_synced(pmx_ctx *ctx, const pmx_sol_view *met, int opt, int
       ctx->err = std::string(who) + ": write masks";
       return 0;
     }
+    // the unwritten rows, found by the host pool (per-chunk lists joined in order)
     std::vector<int4> ent;
     std::vector<double> val;
-    for (int64_t j = 0; j < n; j++) {
-      if (wm[(size_t)j] & (1u << im)) continue;
-      ent.push_back(make_int4((int)j, ctx->sd.off[im], sz, 0));
-      for (int c = 0; c < 6; c++) val.push_back(c < sz ? hm[j * sz + c] : 0.0);
+    {
+      std::mutex mu;
+      std::vector<std::pair<int64_t, std::vector<int>>> rows;
+      pmx_par_for(0, n, [&](int64_t j0, int64_t j1) {
+        std::vector<int> r;
+        for (int64_t j = j0; j < j1; j++)
+          if (!(wm[(size_t)j] & (1u << im))) r.push_back((int)j);
+        std::lock_guard<std::mutex> g(mu);
+        rows.emplace_back(j0, std::move(r));
+      });
+      std::sort(rows.begin(), rows.end(),
+                [](const std::pair<int64_t, std::vector<int>> &a, const std::pair<int64_t, std::vector<int>> &b) {
+                  return a.first < b.first;
+                });
+      for (const auto &r : rows)
+        for (int j : r.second) {
+          ent.push_back(make_int4(j, ctx->sd.off[im], sz, 0));
+          for (int c = 0; c < 6; c++) val.push_back(c < sz ? hm[(int64_t)j * sz + c] : 0.0);
+        }
     }
     const int64_t ne_ = (int64_t)ent.size();
     if (ne_) {
@@ -1293,7 +1308,7 @@ int pmx_new_mesh_qual_synced(pmx_ctx *ctx, const pmx_sol_view *met, int opt, int
         return 0;
       }
     }
-    return new_mesh_qual_core(ctx, who, opt, metRidTyp, qual, dev_result, ctx->d_out.p, ctx->sd.S, sz,
+    return new_mesh_qual_core(ctx, who, opt, metRidTyp, qual, qs, dev_result, ctx->d_out.p, ctx->sd.S, sz,
                               ctx->sd.off[im]);
   }
   // no metric in the step: the caller's whole array
@@ -1304,7 +1319,7 @@ int pmx_new_mesh_qual_synced(pmx_ctx *ctx, const pmx_sol_view *met, int opt, int
     ctx->err = std::string(who) + ": metric upload";
     return 0;
   }
-  return new_mesh_qual_core(ctx, who, opt, metRidTyp, qual, dev_result, ctx->d_cmet.p, sz, sz, 0);
+  return new_mesh_qual_core(ctx, who, opt, metRidTyp, qual, qs, dev_result, ctx->d_cmet.p, sz, sz, 0);
 }
 
 // ---- the reduction across ranks (host folds + RCCL) --------------------------------

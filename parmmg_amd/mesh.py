@@ -22,6 +22,13 @@ MESHGEN_PATH = os.path.join(_HERE, "libpmx_meshgen.so")
 
 TAG_REQ, TAG_BDY, TAG_NUL = 4, 16, 16384
 
+# Mmg's point and tet records (MMG5_Point 72 B, MMG5_Tetra 48 B, libmmgtypes.h)
+# for the AoS views of the binding
+MMG_POINT = np.dtype([("c", "f8", 3), ("n", "f8", 3), ("ref", "i4"), ("xp", "i4"), ("tmp", "i4"),
+                      ("flag", "i4"), ("s", "i4"), ("tag", "u2"), ("tagdel", "i1"), ("pad", "i1")])
+MMG_TETRA = np.dtype([("qual", "f8"), ("v", "i4", 4), ("ref", "i4"), ("base", "i4"), ("mark", "i4"),
+                      ("xt", "i4"), ("flag", "i4"), ("tag", "i2"), ("pad", "i2")])
+
 _mg = None
 
 

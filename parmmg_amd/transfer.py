@@ -435,6 +435,30 @@ class Transfer:
             self.n_new_tets = tv.shape[0] - 1
         return q
 
+    def new_mesh_qual_synced(self, met: np.ndarray | None, opt: int = N.INQUA, met_rid_typ: int = 1,
+                             out: np.ndarray | None = None) -> np.ndarray:
+        """PMMG_tetraQual after the interpolation on the caller's metric
+        (Mmg layout, (np+1, size), entry 0 unused; None: no metric), the new
+        tets being the last points view's.  out: None -> a dense (ne+1,) array;
+        a structured array with a "qual" field (MMG_TETRA records) -> written
+        in place for the valid tets only (pmx_new_mesh_qual_synced, strided)."""
+        mv = None
+        if met is not None:
+            met = np.ascontiguousarray(met, np.float64)
+            mv = N.SolView()
+            mv.size, mv.m = met.shape[1], _dp(met)
+        if out is None:
+            q = np.zeros(self.n_new_tets + 1)
+            ptr, stride = _dp(q), 8
+        else:
+            q = out
+            base = out.ctypes.data + out.dtype.fields["qual"][1]
+            ptr, stride = C.cast(C.c_void_p(base), N.dptr), out.dtype.itemsize
+        self._chk(self.lib.pmx_new_mesh_qual_synced(self.ctx, C.byref(mv) if mv is not None else None, opt,
+                                                    met_rid_typ, ptr, stride, None),
+                  "pmx_new_mesh_qual_synced")
+        return q
+
     def comm_init(self, nranks: int, uid: bytes, rank: int) -> int:
         c = C.c_void_p()
         self._chk(self.lib.pmx_comm_init(self.ctx, C.byref(c), nranks, uid, rank), "pmx_comm_init")

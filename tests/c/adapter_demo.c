@@ -155,6 +155,9 @@ static MMG5_pMesh make_mesh(int64_t np, int64_t ne, const double *xyz, const int
 static int qual_twice(const char *dir, const char *tag, PMMG_pParMesh pm) {
   char name[64];
   int g, k, ier;
+  /* the deleted tets keep the -1 (MMG3D_tetraQual skips !MG_EOK) */
+  for (g = 0; g < pm->ngrp; g++)
+    for (k = 1; k <= pm->listgrp[g].mesh->ne; k++) pm->listgrp[g].mesh->tetra[k].qual = -1.0;
   for (int pass = 0; pass < 2; pass++) {
     ier = PMMG_tetraQual(pm, 1);
     printf("{\"call\": \"tetraqual_%s_%s\", \"ret\": %d}\n", tag, pass ? "upl" : "res", ier);

@@ -202,6 +202,39 @@ def test_new_mesh_quality_deleted_tets_and_bad_index(transfer):
         transfer.new_mesh_qual(bad)
 
 
+@pytest.mark.parametrize("metric", ["iso", "ani"])
+def test_new_mesh_quality_synced_into_tetra_records(transfer, metric):
+    """PMMG_tetraQual at :845 through pmx_new_mesh_qual_synced, the qualities
+    written straight into MMG5_Tetra.qual (stride 48 B) for the valid tets
+    only -- a deleted tet keeps its value, as MMG3D_tetraQual skips !MG_EOK --
+    equal to the dense output and to the oracle.  Sizes past 2^20 tets run
+    the chunked download (several chunks)."""
+    m, _, _, sols = cube_case(6, metric=metric, fields=False)
+    new = M.kuhn_cube(56, seed=3)                  # 56^3 * 6 = 1.05M tets: 2 chunks
+    x = new.xyz[1:].copy()
+    t = np.zeros(len(x), np.uint16)
+    tv = new.tet.copy()
+    tv[0] = 0
+    tv[7, 0] = 0                                   # deleted (!MG_EOK)
+    transfer.upload_background(m, sols, 0)
+    transfer.upload_points(x, t, tets_mmg=tv)
+    transfer.run()
+    r = transfer.download()
+    met = np.concatenate([np.zeros((1, sols[0].shape[1])), r.sols[0]])
+    rec = np.zeros(tv.shape[0], M.MMG_TETRA)
+    rec["v"] = tv
+    rec["qual"] = -1.0
+    transfer.new_mesh_qual_synced(met, out=rec)
+    qd = transfer.new_mesh_qual_synced(met)
+    qo = O.tetra_qual(M.Mesh(new.xyz, tv, new.adja, new.tria, new.adjt), met if metric == "ani" else None,
+                      tags=np.zeros(new.np + 1, np.uint16), met_rid_typ=1)
+    assert rec["qual"][7] == -1.0 and qd[7] == 0.0
+    ok = np.arange(tv.shape[0]) != 7
+    ok[0] = False
+    assert np.array_equal(rec["qual"][ok], qd[ok])
+    assert np.array_equal(qd.view(np.int64)[ok], qo.view(np.int64)[ok])
+
+
 def test_rccl_single_rank_equals_fold(transfer):
     """pmx_qualhisto_allreduce / pmx_prilen_allreduce over a 1-rank RCCL
     communicator: the all-gather + fold of the group partials equals the

@@ -4,6 +4,7 @@
 // layout of pmx_device.h, owns the device buffers of one GPU, and sequences
 // the kernels of one transfer step on one HIP stream.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -63,16 +64,34 @@ char *pmx_hstage(pmx_ctx *ctx, size_t bytes) {
 static char *hstage(pmx_ctx *ctx, size_t bytes) { return pmx_hstage(ctx, bytes); }
 static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-// host gathers/scatters of large AoS arrays split over a few threads
-// (PMX_HOST_THREADS, default min(8, hardware threads); 16 measured slower on a
-// GPU box's 16-CPU share); ranges below
-// PMX_HOST_THREADS_MIN elements (default 2^18) stay serial
+// The process's CPU share: the CPUs it may run on, capped by a cgroup v2 CPU
+// quota (cpu.max "quota period"; a GPU box of this pool: 16 of 256).
+static unsigned cpu_share() {
+  cpu_set_t set;
+  unsigned n = 0;
+  if (sched_getaffinity(0, sizeof set, &set) == 0) n = (unsigned)CPU_COUNT(&set);
+  if (!n) n = std::max(1u, std::thread::hardware_concurrency());
+  if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    long long period = 0;
+    if (fscanf(f, "%31s %lld", q, &period) == 2 && period > 0 && strcmp(q, "max") != 0) {
+      const long long quota = atoll(q);
+      if (quota > 0) n = std::min<unsigned>(n, (unsigned)std::max(1LL, (quota + period - 1) / period));
+    }
+    fclose(f);
+  }
+  return n;
+}
+// host gathers/scatters of large AoS arrays split over the CPU share
+// (PMX_HOST_THREADS overrides; at most 32).  Measured on a GPU box (16-CPU
+// quota of 256, C3 resident cycle, tools/trace_resident.py): 8 threads 89-95
+// ms, 16 threads 67-71 ms, 24 threads (throttled by the quota) 77 ms.
+// Ranges below PMX_HOST_THREADS_MIN elements (default 2^18) stay serial.
 static unsigned host_threads() {
   static const unsigned T = [] {
     const char *e = getenv("PMX_HOST_THREADS");
-    unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    unsigned t = e ? (unsigned)std::max(1, atoi(e)) : std::min(8u, hw);
-    return std::min(t, 64u);
+    unsigned t = e ? (unsigned)std::max(1, atoi(e)) : cpu_share();
+    return std::min(t, 32u);
   }();
   return T;
 }

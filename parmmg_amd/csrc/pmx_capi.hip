@@ -50,8 +50,12 @@ template <class T> static bool dgrow(pmx_ctx *ctx, DevBuf<T> &b, size_t n) {
   return pmx_dgrow(ctx, b, n);
 }
 // pinned staging of at least `bytes`, 25 % slack so that a slowly growing
-// ParMmg group does not re-pin every iteration
+// ParMmg group does not re-pin every iteration.  Every arena copy is on the
+// context's stream and no call waits for its last one (pmx_upload_points
+// returns with its coordinates still in flight): the arena is handed out only
+// once that stream has drained, so no host write, read or re-pin races a DMA.
 char *pmx_hstage(pmx_ctx *ctx, size_t bytes) {
+  if (!ok(ctx, hipStreamSynchronize(ctx->stream), "pmx_hstage: stream")) return nullptr;
   if (bytes <= ctx->h_stage_cap && ctx->h_stage) return (char *)ctx->h_stage;
   if (ctx->h_stage) hipHostFree(ctx->h_stage);
   ctx->h_stage = nullptr;
@@ -806,9 +810,8 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   // one record per wave (sized for every point on one path)
   if (!dgrow(ctx, ctx->d_vstat, (nn + 255) / 256 * 4 + 4)) return 0;
   if (!dgrow(ctx, ctx->d_bstat, (nn + 255) / 256 * 4 + 4)) return 0;
-  ctx->have_qtag = false;
-  CK(hipStreamSynchronize(ctx->stream));
-  tr.mark("sync");
+  // no wait for the copies: the step queues behind them, and the next host
+  // use of the arena waits for the stream (pmx_hstage)
   ctx->have_qtag = tg && n;
   ctx->pts_first = pv->first;
   // orphans (points in no valid new tet) are known once the tets are packed,

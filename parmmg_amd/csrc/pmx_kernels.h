@@ -142,4 +142,8 @@ struct StatArgs {
   const unsigned long long *par_key;
   int64_t npar;
   const uint8_t *par_pt;
+  // k_prilen's tet schedule: 0 = one contiguous range per workgroup; C > 0 =
+  // a moving front (each XCD's range dealt out in chunks of C batches,
+  // round-robin over that XCD's workgroups, all co-resident)
+  int sched_chunk;
 };

@@ -608,12 +608,39 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
   __shared__ long long kbase[2];                 // first tet of each LDS buffer
   __shared__ unsigned lcnt[10];
   LenAcc acc(lcnt);
-  // XCD-contiguous chunks: the shells and points of the next z-layer of
-  // cells are another chunk's, read by the same L2
-  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
-  const int64_t per = (A.ne + gridDim.x - 1) / gridDim.x;
-  const int64_t k0 = 1 + lb * per, k1 = min(A.ne, k0 + per - 1);
+  // The tets a workgroup takes, batch by batch (kb = first tet of a batch,
+  // valid while kb <= k1):
+  //  * contiguous (sched_chunk 0): XCD-contiguous ranges, one per workgroup;
+  //    the shells and points of the next z-layer of cells are another
+  //    range's, read by the same L2;
+  //  * front (sched_chunk C): each XCD's eighth of the tets is dealt out in
+  //    chunks of C batches, round-robin over the XCD's co-resident
+  //    workgroups, so the XCD works on one contiguous window that moves
+  //    forward: a +y shell (a few batches ahead) is a batch another
+  //    workgroup of the same L2 loads about then.
+  // Either way a workgroup's batches come in increasing tet order (the ring's
+  // keys stay ordered).
   const unsigned tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t C = A.sched_chunk;
+  int64_t lb, k0, k1, jump = 0, xlo = 1;
+  if (C == 0) {
+    lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t per = (A.ne + gridDim.x - 1) / gridDim.x;
+    k0 = 1 + lb * per;
+    k1 = min(A.ne, k0 + per - 1);
+  } else {
+    lb = blockIdx.x;
+    const int64_t x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int64_t G = ((int64_t)gridDim.x - x + 7) >> 3;     // this XCD's workgroups
+    xlo = 1 + x * A.ne / 8;
+    k1 = (x + 1) * A.ne / 8;
+    k0 = xlo + j * C * 256;
+    jump = (G - 1) * C * 256;
+  }
+  auto next_batch = [&](int64_t kb) -> int64_t {
+    if (C == 0) return kb + 256;
+    return kb + 256 + (((kb - xlo) >> 8) % C == C - 1 ? jump : 0);
+  };
   unsigned head = 0, tail = 0;                   // ring positions (uniform)
   // each batch's records go to an LDS buffer; the next batch's are loaded at
   // the start of the batch and written to the other buffer after its rounds,
@@ -621,7 +648,7 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
   // merge copy that would wait for it; records past k1 are never used)
   const int4 *recs = reinterpret_cast<const int4 *>(A.tets);
   {
-    const int64_t kn = min(k0 + (int64_t)tid, A.ne);
+    const int64_t kn = max<int64_t>(1, min(k0 + (int64_t)tid, A.ne));
     int4 *srow = reinterpret_cast<int4 *>(&srec[0][tid]);
     srow[0] = recs[2 * kn];
     srow[1] = recs[2 * kn + 1];
@@ -631,11 +658,12 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
   }
 
   int buf = 0;
-  for (int64_t kb = k0;; kb += 256, buf ^= 1) {
+  for (int64_t kb = k0;; buf ^= 1) {
     const bool more = kb <= k1;
     if (!more && head == tail) break;
     const unsigned prev_end = tail;              // entries before it: the previous batch
-    const int64_t kn = min(kb + 256 + (int64_t)tid, A.ne);
+    const int64_t kbn = next_batch(kb);
+    const int64_t kn = max<int64_t>(1, min(kbn + (int64_t)tid, A.ne));
     const int4 pv = recs[2 * kn], pn = recs[2 * kn + 1];
     if (more) {
       const int64_t k = kb + tid;
@@ -715,9 +743,10 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
       int4 *srow = reinterpret_cast<int4 *>(&srec[buf ^ 1][tid]);
       srow[0] = pv;
       srow[1] = pn;
-      if (tid == 0) kbase[buf ^ 1] = kb + 256;
+      if (tid == 0) kbase[buf ^ 1] = kbn;
     }
     __syncthreads();                             // srec, wcnt, kbase rewritten next
+    kb = kbn;
   }
   acc.store(parts + lb);
 }
@@ -1095,7 +1124,46 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
       ppt[(size_t)(key & 0xffffffffu)] = 1;
     }
   }
-  const int nb = stat_blocks(ctx->ne);
+  // the schedule (PMX_PRILEN_SCHED=C: the moving front in chunks of C
+  // batches, grid = the co-resident workgroups; unset: contiguous ranges)
+  static const int sched = [] {
+    const char *e = getenv("PMX_PRILEN_SCHED");
+    return e ? std::max(0, atoi(e)) : 0;
+  }();
+  using KFn = void (*)(StatArgs, LenPart *);
+  // variants: metric kind x point tags x parallel edges (each drops the
+  // other paths' registers and branches)
+  // the isotropic variants held to 5 waves per SIMD (96 VGPRs, a few
+  // spills): 2 % faster at the C5 share; the anisotropic ones spill too
+  // much there (4.46 instead of 3.63 ms) and keep the compiler's choice
+  static const KFn kfn[16] = {
+      k_prilen<false, false, false, 5>,        k_prilen<false, false, true, 5>,
+      k_prilen<false, true, false, 5>,         k_prilen<false, true, true, 5>,
+      k_prilen<true, false, false>,            k_prilen<true, false, true>,
+      k_prilen<true, true, false>,             k_prilen<true, true, true>,
+      k_prilen<false, false, false, 5, true>,  k_prilen<false, false, true, 5, true>,
+      k_prilen<false, true, false, 5, true>,   k_prilen<false, true, true, 5, true>,
+      k_prilen<true, false, false, 1, true>,   k_prilen<true, false, true, 1, true>,
+      k_prilen<true, true, false, 1, true>,    k_prilen<true, true, true, 1, true>};
+  // lean 32-bit index arithmetic while 6 ne + 5 fits 32 bits (PMX_PRILEN_WIDE=1:
+  // the 64-bit variant, for the A/B)
+  static const bool wide = getenv("PMX_PRILEN_WIDE") != nullptr;
+  const bool lean = !wide && A.ne < 700000000LL;
+  const int sel = (lean ? 8 : 0) | (ctx->sd.size[ctx->sd.imet] == 6 ? 4 : 0) | (A.ptag ? 2 : 0) |
+                  (par && par->n > 0 && !excl.empty() ? 1 : 0);
+  int nb = stat_blocks(ctx->ne);
+  A.sched_chunk = 0;
+  if (sched > 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn[sel], 256, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess ||
+        per_cu < 1 || cus < 8) {
+      ctx->err = "pmx_prilen: occupancy query";
+      return 0;
+    }
+    nb = per_cu * cus / 8 * 8;
+    A.sched_chunk = sched;
+  }
   if (!ensure_red(ctx, sizeof(LenPart) * ((size_t)nb + 1 + FINAL_GRID + 1))) return 0;
   LenPart *parts = (LenPart *)ctx->d_red.p;
   A.npar = (int64_t)excl.size();
@@ -1117,29 +1185,7 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
     hipLaunchKernelGGL(k_prilen_par, dim3(1), dim3(256), 0, s, A, ctx->d_pedge.p, (int64_t)own.size(), parts);
   else
     hipLaunchKernelGGL(k_prilen_par, dim3(1), dim3(256), 0, s, A, (const int2 *)nullptr, (int64_t)0, parts);
-  {
-    // variants: metric kind x point tags x parallel edges (each drops the
-    // other paths' registers and branches)
-    using KFn = void (*)(StatArgs, LenPart *);
-    // the isotropic variants held to 5 waves per SIMD (96 VGPRs, a few
-    // spills): 2 % faster at the C5 share; the anisotropic ones spill too
-    // much there (4.46 instead of 3.63 ms) and keep the compiler's choice
-    static const KFn kfn[16] = {
-        k_prilen<false, false, false, 5>,        k_prilen<false, false, true, 5>,
-        k_prilen<false, true, false, 5>,         k_prilen<false, true, true, 5>,
-        k_prilen<true, false, false>,            k_prilen<true, false, true>,
-        k_prilen<true, true, false>,             k_prilen<true, true, true>,
-        k_prilen<false, false, false, 5, true>,  k_prilen<false, false, true, 5, true>,
-        k_prilen<false, true, false, 5, true>,   k_prilen<false, true, true, 5, true>,
-        k_prilen<true, false, false, 1, true>,   k_prilen<true, false, true, 1, true>,
-        k_prilen<true, true, false, 1, true>,    k_prilen<true, true, true, 1, true>};
-    // lean 32-bit index arithmetic while 6 ne + 5 fits 32 bits (PMX_PRILEN_WIDE=1:
-    // the 64-bit variant, for the A/B)
-    static const bool wide = getenv("PMX_PRILEN_WIDE") != nullptr;
-    const bool lean = !wide && A.ne < 700000000LL;
-    const int sel = (lean ? 8 : 0) | (A.msize == 6 ? 4 : 0) | (A.ptag ? 2 : 0) | (A.npar ? 1 : 0);
-    hipLaunchKernelGGL(kfn[sel], dim3(nb), dim3(256), 0, s, A, parts + 1);
-  }
+  hipLaunchKernelGGL(kfn[sel], dim3(nb), dim3(256), 0, s, A, parts + 1);
   LenPart *mid = parts + 1 + nb;
   hipLaunchKernelGGL(k_prilen_final, dim3(FINAL_GRID), dim3(256), 0, s, parts, nb + 1, mid,
                      (pmx_len_part *)nullptr, ctx->d_tets.p, (const int2 *)ctx->d_pedge.p);

@@ -76,7 +76,10 @@ def main():
                       "frac_hbm_peak": Bq / tq / 8e12, "alg_bytes": Bq, "ne": q["ne"], "his": q["his"],
                       "min": q["min"], "max": q["max"]},
         "prilen": {"ms": tl * 1e3, "tets_per_s": m.ne / tl, "alg_GBs": B / tl / 1e9,
-                   "frac_hbm_peak": B / tl / 8e12, "alg_bytes": B, "ned": ln["ned"], "hl": ln["hl"]},
+                   "frac_hbm_peak": B / tl / 8e12, "alg_bytes": B, "ned": ln["ned"], "hl": ln["hl"],
+                   "sched": os.environ.get("PMX_PRILEN_SCHED", "0"),
+                   **{k: ln[k] for k in ("avlen", "lmin", "lmax", "amin", "bmin", "amax", "bmax", "nullEdge")
+                      if k in ln}},
         "setup_s": t_setup,
         "dtype": "f64", "data": "synthetic (jittered Kuhn cube, analytic metric)",
     }

@@ -213,6 +213,7 @@ def resident_cycle(m, sols, cfg: dict, local: int, iters: int = 4, warmup: int =
     mesh + results to the next background (only its boundary trias and Mmg
     adjacency cross PCIe).  Two jittered Kuhn meshes of the config's size
     alternate as background and new mesh; wall clock per iteration."""
+    from parmmg_amd import _native as N
     from parmmg_amd import mesh as M
     from parmmg_amd.transfer import Result, Transfer
     mb = M.kuhn_cube(cfg["n"], seed=777)
@@ -238,7 +239,9 @@ def resident_cycle(m, sols, cfg: dict, local: int, iters: int = 4, warmup: int =
         t0 = time.perf_counter()
         tr.upload_points(x, t, tets_mmg=tets1)
         t1 = time.perf_counter()
-        tr.run()
+        # the ParMmg seam's step: its fields always come down, so they start
+        # down at once (overlapping the new tets' packing)
+        tr.run(flags=N.RUN_EAGER_DOWNLOAD)
         tr.synchronize()
         t2 = time.perf_counter()
         tr.download(into=out, sols_only=True)

@@ -143,6 +143,13 @@ typedef struct {
 #define PMX_RUN_DEBUG_BARRIER_TIMEOUT 0x100 /* test hook: the fallback's grid
                                          barriers do not wait (the step must
                                          then fail, never return silently)   */
+#define PMX_RUN_EAGER_DOWNLOAD   0x20 /* the step's fields start down into
+                                         pinned staging as soon as it ends
+                                         (overlapping the host work that
+                                         follows pmx_run); pmx_download then
+                                         only scatters them.  For callers that
+                                         always download (the ParMmg seam
+                                         sets it)                             */
 
 /* Locate every uploaded new point in the background group and interpolate all
  * background solutions onto it.  Results stay on the device.  Asynchronous:

@@ -67,6 +67,7 @@ RUN_RECORD_STARTS = 0x4
 RUN_SERIAL_SURFACE = 0x8
 RUN_FRESH_BACKGROUND = 0x10
 RUN_DEBUG_BARRIER_TIMEOUT = 0x100
+RUN_EAGER_DOWNLOAD = 0x20
 
 
 class Group(C.Structure):

@@ -388,6 +388,8 @@ pmx_ctx *pmx_create(int device) {
       [&] {
         for (auto &e : ctx->ev_dl)
           if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return true;
+        for (auto &e : ctx->ev_eg)
+          if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return true;
         return false;
       }() ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
@@ -435,6 +437,9 @@ void pmx_destroy(pmx_ctx *ctx) {
   if (ctx->h_tets) hipHostFree(ctx->h_tets);
   for (auto &e : ctx->ev_dl)
     if (e) hipEventDestroy(e);
+  for (auto &e : ctx->ev_eg)
+    if (e) hipEventDestroy(e);
+  if (ctx->h_out) hipHostFree(ctx->h_out);
   if (ctx->h_nbad) hipHostFree(ctx->h_nbad);
   if (ctx->own) hipStreamDestroy(ctx->own);
   delete ctx;
@@ -507,6 +512,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   // upload has completed (a failed call must not leave sizes that disagree
   // with the device buffers)
   ctx->have_bg = ctx->ran = ctx->have_derived = ctx->have_tetv = ctx->have_qual = false;
+  ctx->eager_nch = 0;
   ctx->have_ptag = ctx->have_csr = false;
   ctx->stat_np = -1;
   if (!m) { ctx->err = "pmx_upload_background: null mesh"; return 0; }
@@ -706,6 +712,7 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   ctx->tets_pending = false;
   ctx->norph = 0;
   ctx->orph_fixed = true;
+  ctx->eager_nch = 0;
   if (!pv) { ctx->err = "pmx_upload_points: null view"; return 0; }
   hipSetDevice(ctx->device);
   const int64_t n = pv->last - pv->first + 1;
@@ -966,7 +973,8 @@ static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &o
 // refused, so that a stray bit never changes results silently.
 static bool run_flags_valid(int flags, std::string *err) {
   const int pub = PMX_RUN_REFERENCE_WALK | PMX_RUN_NO_INLINE_TIES | PMX_RUN_RECORD_STARTS |
-                  PMX_RUN_SERIAL_SURFACE | PMX_RUN_FRESH_BACKGROUND | PMX_RUN_DEBUG_BARRIER_TIMEOUT;
+                  PMX_RUN_SERIAL_SURFACE | PMX_RUN_FRESH_BACKGROUND | PMX_RUN_DEBUG_BARRIER_TIMEOUT |
+                  PMX_RUN_EAGER_DOWNLOAD;
   if (flags & ~(pub | (0xff << PMX_RUN_EXP_SHIFT))) {
     *err = "pmx_run: unknown flag bits";
     return false;
@@ -990,6 +998,7 @@ static bool run_flags_valid(int flags, std::string *err) {
 int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   if (!ctx) return 0;
   ctx->ran = false;
+  ctx->eager_nch = 0;
   if (!ctx->have_bg || !ctx->have_pts) { ctx->err = "pmx_run: upload background and points first"; return 0; }
   hipSetDevice(ctx->device);
   pmx_run_opts opts{};
@@ -1116,11 +1125,46 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   // and sent now, while the device runs the step
   ctx->last_const_bit = sd.metric_const ? (1u << sd.imet) : 0u;
   ctx->orph_fixed = false;
-  if (ctx->tets_pending && !ctx->pack_new_tets()) return 0;
   ctx->out_S = S;
   ctx->out_n = n;
+  if ((opts.flags & PMX_RUN_EAGER_DOWNLOAD) && !ctx->eager_download()) return 0;
+  if (ctx->tets_pending && !ctx->pack_new_tets()) return 0;
   ctx->ran = true;
   return 1;
+}
+
+// The fields and write masks of the step just enqueued, down into h_out (its
+// own pinned buffer: the arena stays free for the calls in between) in chunks
+// on the step's stream.  The orphan reset (fix_orphans, later) is applied to
+// these masks by pmx_download on the host, from the same marks.
+bool pmx_ctx::eager_download() {
+  pmx_ctx *ctx = this;
+  eager_nch = 0;
+  const int64_t n = nq;
+  const int S = sd.S;
+  if (n == 0 || S == 0) return true;
+  const size_t o_wm = al256((size_t)(n * S) * sizeof(double)), bytes = o_wm + al256((size_t)n);
+  if (bytes > h_out_cap) {
+    CK(hipStreamSynchronize(stream));      // an earlier eager copy may still land in it
+    if (h_out) hipHostFree(h_out);
+    h_out = nullptr;
+    h_out_cap = 0;
+    if (hipHostMalloc((void **)&h_out, bytes + bytes / 4, hipHostMallocDefault) != hipSuccess) {
+      err = "pmx_run: pinned staging of the eager download";
+      return false;
+    }
+    h_out_cap = bytes + bytes / 4;
+  }
+  const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(4, (n * S) >> 21));
+  for (int c = 0; c < nch; c++) {
+    const int64_t lo = n * c / nch, hi = n * (c + 1) / nch;
+    CK(hipMemcpyAsync(h_out + (size_t)(lo * S) * sizeof(double), d_out.p + lo * S,
+                      (size_t)((hi - lo) * S) * sizeof(double), hipMemcpyDeviceToHost, stream));
+    CK(hipMemcpyAsync(h_out + o_wm + lo, d_wmask.p + lo, (size_t)(hi - lo), hipMemcpyDeviceToHost, stream));
+    CK(hipEventRecord(ev_eg[c], stream));
+  }
+  eager_nch = nch;
+  return true;
 }
 
 // results of the last step, consistent with the current uploads
@@ -1130,6 +1174,57 @@ static bool results_ready(pmx_ctx *ctx, const char *who) {
     return false;
   }
   return true;
+}
+
+// pmx_download after a PMX_RUN_EAGER_DOWNLOAD step: the fields are (being)
+// copied into h_out; each chunk is scattered once it has landed.  The write
+// masks are the step's: the orphan reset is applied here (a point in no valid
+// new tet keeps only a constant-size metric bit, as launch_orphans does on the
+// device).  elem / status / steps come down as usual (after fix_orphans).
+static int download_eager(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem, int *status, int *steps) {
+  const int64_t n = ctx->nq;
+  const int S = ctx->sd.S;
+  const double *h = (const double *)ctx->h_out;
+  const uint8_t *wm = (const uint8_t *)(ctx->h_out + al256((size_t)(n * S) * sizeof(double)));
+  const bool orph = ctx->norph > 0 && (int64_t)ctx->h_mk.size() >= n;
+  const uint8_t *mk = orph ? ctx->h_mk.data() : nullptr;
+  const unsigned keep = ctx->last_const_bit;
+  const bool want_int = elem || status || steps;
+  const size_t o_el = 0, o_st = o_el + al256((size_t)n * sizeof(int)), o_sp = o_st + al256((size_t)n * sizeof(int)),
+               total = o_sp + al256((size_t)n * sizeof(int));
+  char *st = nullptr;
+  if (want_int) {
+    st = hstage(ctx, total);               // waits for the stream: the eager chunks have landed
+    if (!st) return 0;
+    if (elem) CK(hipMemcpyAsync(st + o_el, ctx->d_elem.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    if (status) CK(hipMemcpyAsync(st + o_st, ctx->d_status.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    if (steps) CK(hipMemcpyAsync(st + o_sp, ctx->d_steps.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  }
+  const int nch = ctx->eager_nch;
+  for (int c = 0; c < nch; c++) {
+    const int64_t lo = n * c / nch, hi = n * (c + 1) / nch;
+    CK(hipEventSynchronize(ctx->ev_eg[c]));
+    par_for(lo, hi, [&](int64_t i0, int64_t i1) {
+      for (int s = 0; s < ctx->sd.nsol; s++) {
+        double *dst = new_sols[s].m;
+        const int sz = ctx->sd.size[s], off = ctx->sd.off[s];
+        if (!dst) continue;
+        const unsigned bit = 1u << s;
+        for (int64_t i = i0; i < i1; i++) {
+          const unsigned w = (mk && !mk[i]) ? (wm[i] & keep) : wm[i];
+          if (!(w & bit)) continue;
+          for (int j = 0; j < sz; j++) dst[i * sz + j] = h[(size_t)(i * S + off + j)];
+        }
+      }
+    });
+  }
+  if (want_int) {
+    CK(hipStreamSynchronize(ctx->stream));
+    if (elem) memcpy(elem, st + o_el, (size_t)n * sizeof(int));
+    if (status) memcpy(status, st + o_st, (size_t)n * sizeof(int));
+    if (steps) memcpy(steps, st + o_sp, (size_t)n * sizeof(int));
+  }
+  return 1;
 }
 
 int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem, int *status, int *steps) {
@@ -1145,6 +1240,7 @@ int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem, int *sta
   // every device -> host copy lands in the pinned arena (async DMA, one sync),
   // then the host scatters into the caller's (pageable, strided) arrays
   const bool want_sol = new_sols && S > 0;
+  if (want_sol && ctx->eager_nch > 0) return download_eager(ctx, new_sols, elem, status, steps);
   const size_t o_out = 0, o_wm = o_out + al256(want_sol ? (size_t)(n * S) * sizeof(double) : 0),
                o_el = o_wm + al256(want_sol ? (size_t)n : 0), o_st = o_el + al256((size_t)n * sizeof(int)),
                o_sp = o_st + al256((size_t)n * sizeof(int)), total = o_sp + al256((size_t)n * sizeof(int));

@@ -115,6 +115,7 @@ static int interp_groups(pmx_ctx *ectx, pmx_ctx *const *ctxs, int ngrp, pmx_grou
     if (!pmx_upload_background(X, &G.old_mesh, ns, olds, imet)) { fail(X); continue; }
     // the background upload invalidated nothing of the points; run the step
     pmx_run_opts o{};
+    o.flags = PMX_RUN_EAGER_DOWNLOAD;        // every group is downloaded below
     if (!pmx_run(X, &o)) { fail(X); continue; }
     // outputs in Mmg layout start at point index `first`
     for (int k = 0; k < ns; k++)
@@ -255,6 +256,7 @@ extern "C" int pmx_copy_required(pmx_ctx *ctx, const int *permNodGlob, int copy_
     }
   }
   if (!pmx_dgrow(ctx, ctx->d_ccnt, 1) || hipMemsetAsync(ctx->d_ccnt.p, 0, sizeof(int), s) != hipSuccess) return 0;
+  ctx->eager_nch = 0;                        // the results change: no eager copy of them
   unsigned smask = (1u << ctx->sd.nsol) - 1u;
   if (!copy_metric && ctx->sd.imet >= 0) smask &= ~(1u << ctx->sd.imet);
   const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((np + 255) / 256, 4096));

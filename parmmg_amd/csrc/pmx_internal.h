@@ -157,6 +157,13 @@ struct pmx_ctx {
   int64_t norph = 0;                    // live points in no valid new tet (known once packed)
   bool orph_fixed = true;               // the last step's orphan rows reset (fix_orphans)
   unsigned last_const_bit = 0;          // wmask bit of the last step's constant-size metric
+  // PMX_RUN_EAGER_DOWNLOAD: the last step's fields (n * S doubles) and write
+  // masks (n bytes) copied into h_out as soon as the step ends, in eager_nch
+  // chunks (ev_eg); 0 = no such copy, or the results changed since
+  char *h_out = nullptr;
+  size_t h_out_cap = 0;
+  int eager_nch = 0;
+  hipEvent_t ev_eg[4] = {};
   DevBuf<double> d_gather;              // all-gathered partials
 
   // timing
@@ -173,6 +180,7 @@ struct pmx_ctx {
   bool pack_new_tets();                   // the pending new tets: pack, send on `up`, residency build
   bool ensure_tets(hipStream_t s);        // d_ntetv valid for work on stream s
   bool fix_orphans();                     // the last step's rows of orphan points: untouched
+  bool eager_download();                  // issue the eager copies of the step just enqueued
   int4 *grow_htets(int64_t ne);           // h_tets for ne + 1 records (ev_tets already waited)
   // device error word of the last step (after a stream sync): 0 = none
   bool check_device_errors();

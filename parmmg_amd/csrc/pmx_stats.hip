@@ -1344,6 +1344,7 @@ int pmx_new_mesh_qual_synced(pmx_ctx *ctx, const pmx_sol_view *met, int opt, int
         return 0;
       }
       launch_patch_rows(ctx->d_pent.p, ctx->d_pval.p, ne_, ctx->sd.S, ctx->d_out.p, s);
+      ctx->eager_nch = 0;                    // the results changed
       // the rows are the caller's now (pmx_download / pmx_promote_background
       // then give the same values)
       const uint8_t bit = (uint8_t)(1u << im);

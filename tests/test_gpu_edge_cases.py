@@ -92,6 +92,48 @@ def test_orphan_points_untouched_and_constant_size(transfer):
         assert np.all(r2.sols[s][~used] == -7.0)
 
 
+@pytest.mark.parametrize("hsiz", [0.0, 0.05])
+def test_eager_download_equals_download(transfer, hsiz):
+    """PMX_RUN_EAGER_DOWNLOAD (the fields start down right after the step, the
+    orphan reset applied on the host) gives pmx_download's bytes: orphans
+    untouched (a constant-size metric still written on them), NUL points
+    untouched, elem / status / steps identical; a second download repeats
+    them."""
+    m, x, t, sols = cube_case(6, metric="iso", surface=True)
+    n = len(x)
+    t = t.copy()
+    t[5::41] = M.TAG_NUL
+    rng = np.random.default_rng(11)
+    used = np.zeros(n, bool)
+    used[: int(0.85 * n)] = True
+    pool = np.nonzero(used)[0]
+    tets = np.zeros((len(pool) + 1, 4), np.int32)
+    tets[1:] = rng.choice(pool, size=(len(pool), 4))
+    tets[1:, 0] = pool
+    tets[0] = -1
+
+    def go(flags):
+        init = [np.full((n, s.shape[1]), -7.0) for s in sols]
+        transfer.upload_background(m, sols, 0)
+        transfer.upload_points(x, t, tets)
+        transfer.run(flags=flags, hsiz=hsiz)
+        a = transfer.download(init=init)
+        b = transfer.download(init=[np.full((n, s.shape[1]), -7.0) for s in sols])
+        return a, b
+
+    ref, _ = go(0)
+    eg, eg2 = go(N.RUN_EAGER_DOWNLOAD)
+    for r in (eg, eg2):
+        for s in range(len(sols)):
+            assert bits_equal(r.sols[s], ref.sols[s]).all()
+        assert np.array_equal(r.elem, ref.elem) and np.array_equal(r.status, ref.status)
+        assert np.array_equal(r.steps, ref.steps)
+    for s in range(1, len(sols)):
+        assert np.all(eg.sols[s][~used] == -7.0)
+    if hsiz > 0:
+        assert np.all(eg.sols[0][t != M.TAG_NUL, 0] == hsiz)
+
+
 def delete_tets(m, dead):
     """Mark tets `dead` as deleted (v[0] = 0, the rest of the record kept) and
     cut the adjacency to and from them: Mmg's state of a hole."""

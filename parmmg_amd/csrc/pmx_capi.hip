@@ -1176,6 +1176,32 @@ static bool results_ready(pmx_ctx *ctx, const char *who) {
   return true;
 }
 
+// The step's rows [i0, i1) of the packed fields h (S doubles per point) into
+// the caller's per-solution arrays where the write mask has the solution's bit
+// (mk: orphan marks; a point without one keeps only the `keep` bits).  In
+// blocks of 1024 points, so that every solution reads a block of h from cache
+// (solution by solution over the whole range read h once per solution).
+static void scatter_rows(const pmx_ctx *ctx, const pmx_sol_view *new_sols, const double *h, const uint8_t *wm,
+                         const uint8_t *mk, unsigned keep, int64_t i0, int64_t i1) {
+  const int S = ctx->sd.S;
+  for (int64_t b0 = i0; b0 < i1; b0 += 1024) {
+    const int64_t b1 = std::min(i1, b0 + 1024);
+    for (int s = 0; s < ctx->sd.nsol; s++) {
+      double *dst = new_sols[s].m;
+      if (!dst) continue;
+      const int sz = ctx->sd.size[s], off = ctx->sd.off[s];
+      const unsigned bit = 1u << s;
+      for (int64_t i = b0; i < b1; i++) {
+        const unsigned w = (mk && !mk[i]) ? (wm[i] & keep) : wm[i];
+        if (!(w & bit)) continue;
+        const double *src = h + i * S + off;
+        double *d = dst + i * sz;
+        for (int j = 0; j < sz; j++) d[j] = src[j];
+      }
+    }
+  }
+}
+
 // pmx_download after a PMX_RUN_EAGER_DOWNLOAD step: the fields are (being)
 // copied into h_out; each chunk is scattered once it has landed.  The write
 // masks are the step's: the orphan reset is applied here (a point in no valid
@@ -1204,19 +1230,7 @@ static int download_eager(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem,
   for (int c = 0; c < nch; c++) {
     const int64_t lo = n * c / nch, hi = n * (c + 1) / nch;
     CK(hipEventSynchronize(ctx->ev_eg[c]));
-    par_for(lo, hi, [&](int64_t i0, int64_t i1) {
-      for (int s = 0; s < ctx->sd.nsol; s++) {
-        double *dst = new_sols[s].m;
-        const int sz = ctx->sd.size[s], off = ctx->sd.off[s];
-        if (!dst) continue;
-        const unsigned bit = 1u << s;
-        for (int64_t i = i0; i < i1; i++) {
-          const unsigned w = (mk && !mk[i]) ? (wm[i] & keep) : wm[i];
-          if (!(w & bit)) continue;
-          for (int j = 0; j < sz; j++) dst[i * sz + j] = h[(size_t)(i * S + off + j)];
-        }
-      }
-    });
+    par_for(lo, hi, [&](int64_t i0, int64_t i1) { scatter_rows(ctx, new_sols, h, wm, mk, keep, i0, i1); });
   }
   if (want_int) {
     CK(hipStreamSynchronize(ctx->stream));
@@ -1264,17 +1278,7 @@ int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem, int *sta
   for (int64_t c = 0; c < nch; c++) {
     const int64_t lo = n * c / nch, hi = n * (c + 1) / nch;
     CK(hipEventSynchronize(ctx->ev_dl[c]));
-    par_for(lo, hi, [&](int64_t i0, int64_t i1) {
-      for (int s = 0; s < ctx->sd.nsol; s++) {
-        double *dst = new_sols[s].m;
-        const int sz = ctx->sd.size[s], off = ctx->sd.off[s];
-        if (!dst) continue;
-        for (int64_t i = i0; i < i1; i++) {
-          if (!(wm[i] & (1u << s))) continue;
-          for (int j = 0; j < sz; j++) dst[i * sz + j] = h[(size_t)(i * S + off + j)];
-        }
-      }
-    });
+    par_for(lo, hi, [&](int64_t i0, int64_t i1) { scatter_rows(ctx, new_sols, h, wm, nullptr, 0u, i0, i1); });
   }
   CK(hipStreamSynchronize(ctx->stream));
   if (elem) memcpy(elem, st + o_el, (size_t)n * sizeof(int));

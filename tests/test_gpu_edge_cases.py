@@ -97,8 +97,7 @@ def test_eager_download_equals_download(transfer, hsiz):
     """PMX_RUN_EAGER_DOWNLOAD (the fields start down right after the step, the
     orphan reset applied on the host) gives pmx_download's bytes: orphans
     untouched (a constant-size metric still written on them), NUL points
-    untouched, elem / status / steps identical; a second download repeats
-    them."""
+    untouched, elem / status identical; a second download repeats them."""
     m, x, t, sols = cube_case(6, metric="iso", surface=True)
     n = len(x)
     t = t.copy()
@@ -127,7 +126,8 @@ def test_eager_download_equals_download(transfer, hsiz):
         for s in range(len(sols)):
             assert bits_equal(r.sols[s], ref.sols[s]).all()
         assert np.array_equal(r.elem, ref.elem) and np.array_equal(r.status, ref.status)
-        assert np.array_equal(r.steps, ref.steps)
+        # (walk lengths are a diagnostic: the hint grid keeps whichever sampled
+        # tet of a cell was stored last, so they vary from run to run)
     for s in range(1, len(sols)):
         assert np.all(eg.sols[s][~used] == -7.0)
     if hsiz > 0:

@@ -20,9 +20,12 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 #include <vector>
 #include "pmx_internal.h"
+
+static unsigned nblk_(int64_t n) { return (unsigned)std::max<int64_t>((n + 255) / 256, 1); }
 
 // MMG5_idir: local vertices of face f (opposite vertex f), outward order
 __constant__ int TOPO_IDIR[4][3] = {{1, 2, 3}, {0, 3, 2}, {0, 1, 3}, {0, 2, 1}};
@@ -133,6 +136,67 @@ __global__ __launch_bounds__(256) void k_face_match(const int4 *__restrict__ rec
   }
   adja[me.w - 3] = (n == 1) ? partner : 0;       // 4*(k-1)+1+f = owner - 3
   if (n > 1) atomicAdd(nbad, 1u);
+}
+
+// The same matching with the records staged in LDS: a workgroup owns
+// MATCH_R consecutive records and loads them with MATCH_PAD records on either
+// side (coalesced, 16 KB); a record whose bucket lies inside that window is
+// compared against the LDS copy, any other (a bucket longer than the pads)
+// against global memory.  One global read per record and window instead of
+// one per (record, bucket member): the global-scan variant re-reads every
+// bucket once per member (~24 x 16 B per record).
+#define MATCH_R 512
+#define MATCH_PAD 256
+__global__ __launch_bounds__(256) void k_face_match_lds(const int4 *__restrict__ rec, int64_t nb,
+                                                        const unsigned *__restrict__ off,
+                                                        int *__restrict__ adja,
+                                                        unsigned *__restrict__ nbad) {
+  __shared__ int4 win[MATCH_R + 2 * MATCH_PAD];
+  const int64_t nrec = (int64_t)off[nb];
+  const int64_t s0 = (int64_t)blockIdx.x * MATCH_R;
+  const int64_t w0 = s0 - MATCH_PAD;              // window start (may be negative)
+  for (int i = threadIdx.x; i < MATCH_R + 2 * MATCH_PAD; i += blockDim.x) {
+    const int64_t r = w0 + i;
+    win[i] = (r >= 0 && r < nrec) ? rec[r] : make_int4(-1, -1, -1, 0);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < MATCH_R; j += blockDim.x) {
+    const int64_t s = s0 + j;
+    if (s >= nrec) break;
+    const int4 me = win[MATCH_PAD + j];
+    const int64_t lo = off[me.x], hi = off[me.x + 1];
+    int partner = 0, n = 0;
+    if (lo >= w0 && hi <= w0 + MATCH_R + 2 * MATCH_PAD) {
+      for (int64_t r = lo; r < hi; r++) {
+        const int4 o = win[r - w0];
+        if (r != s && o.y == me.y && o.z == me.z) { partner = o.w; n++; }
+      }
+    } else {
+      for (int64_t r = lo; r < hi; r++) {
+        const int4 o = rec[r];
+        if (r != s && o.y == me.y && o.z == me.z) { partner = o.w; n++; }
+      }
+    }
+    adja[me.w - 3] = (n == 1) ? partner : 0;
+    if (n > 1) atomicAdd(nbad, 1u);
+  }
+}
+
+// PMX_TOPO_MATCH=global: the global-scan matching, for the A/B
+static bool topo_match_global() {
+  static const bool g = [] {
+    const char *e = getenv("PMX_TOPO_MATCH");
+    return e && std::string(e) == "global";
+  }();
+  return g;
+}
+static void launch_face_match(const int4 *rec, int64_t ne, int64_t np, const unsigned *off, int *dadja,
+                              unsigned *nbad, hipStream_t s) {
+  if (topo_match_global())
+    hipLaunchKernelGGL(k_face_match, dim3(nblk_(4 * ne)), dim3(256), 0, s, rec, np + 1, off, dadja, nbad);
+  else
+    hipLaunchKernelGGL(k_face_match_lds, dim3((unsigned)std::max<int64_t>((4 * ne + MATCH_R - 1) / MATCH_R, 1)),
+                       dim3(256), 0, s, rec, np + 1, off, dadja, nbad);
 }
 
 // ---- boundary trias and their edge adjacency -------------------------------------
@@ -291,8 +355,7 @@ bool build_adja_dev(pmx_ctx *ctx, const int4 *tv, int64_t ne, int64_t np, int *d
   if (!scan_counts(cnt, off, np + 1, s, sc)) return topo_fail(ctx, "pmx_build_adja: scan");
   hipMemcpyAsync(cnt, off, sizeof(unsigned) * (size_t)(np + 2), hipMemcpyDeviceToDevice, s);
   hipLaunchKernelGGL(k_face_scatter, dim3(nblk(ne)), dim3(256), 0, s, tv, ne, cnt, rec);
-  hipLaunchKernelGGL(k_face_match, dim3(nblk(4 * ne)), dim3(256), 0, s, rec, np + 1, off, dadja,
-                     nbad);
+  launch_face_match(rec, ne, np, off, dadja, nbad, s);
   if (hipMemcpyAsync(nbad_out, nbad, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return topo_fail(ctx, "pmx_build_adja: launch");
@@ -324,8 +387,7 @@ bool pmx_ctx_build_adja_device(pmx_ctx *ctx, const int4 *tv, int64_t ne, int64_t
     return topo_fail(ctx, "device adjacency: scan");
   hipMemcpyAsync(cnt, off, sizeof(unsigned) * (size_t)(np + 2), hipMemcpyDeviceToDevice, s);
   hipLaunchKernelGGL(k_face_scatter, dim3(nblk(ne)), dim3(256), 0, s, tv, ne, cnt, ctx->d_trec.p);
-  hipLaunchKernelGGL(k_face_match, dim3(nblk(4 * ne)), dim3(256), 0, s, ctx->d_trec.p, np + 1, off, dadja,
-                     nbad);
+  launch_face_match(ctx->d_trec.p, ne, np, off, dadja, nbad, s);
   if (h_nbad) {
     if (hipMemcpyAsync(h_nbad, nbad, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess)
       return topo_fail(ctx, "device adjacency: launch");

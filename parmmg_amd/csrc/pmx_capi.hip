@@ -660,19 +660,33 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     CK(hipEventRecord(ctx->ev_join, ctx->topo));
   }
   tr.mark("tets");
-  // solutions -> interleaved [np+1][S]
+  // solutions -> interleaved [np+1][S], in blocks of 1024 rows (each row's
+  // line written while it is in cache, not once per solution) and chunks
+  // whose DMA overlaps the packing of the next
   double *hs = (double *)(stg + o_s);
   memset(hs, 0, (size_t)std::max(S, 1) * sizeof(double));   // row 0 (unused slot)
-  if (S == 0) memset(hs, 0, hs_n * sizeof(double));
-  par_chunks(1, np + 1, [&](int, int64_t i0, int64_t i1) {
-    for (int s = 0; s < nsol; s++) {
-      const int sz = sols[s].size, off = sd.off[s];
-      const double *src = sols[s].m;
-      for (int64_t i = i0; i < i1; i++)
-        for (int j = 0; j < sz; j++) hs[(size_t)i * S + off + j] = src[i * sz + j];
+  if (S == 0) {
+    memset(hs, 0, hs_n * sizeof(double));
+    CK(hipMemcpyAsync(ctx->d_sol.p, hs, hs_n * sizeof(double), hipMemcpyHostToDevice, st));
+  } else {
+    const int64_t nsc = std::max<int64_t>(1, std::min<int64_t>(4, (np * S) >> 21));
+    for (int64_t c = 0; c < nsc; c++) {
+      const int64_t r0 = (c == 0) ? 0 : 1 + np * c / nsc, r1 = 1 + np * (c + 1) / nsc;
+      par_for(std::max<int64_t>(r0, 1), r1, [&](int64_t i0, int64_t i1) {
+        for (int64_t b0 = i0; b0 < i1; b0 += 1024) {
+          const int64_t b1 = std::min(i1, b0 + 1024);
+          for (int s = 0; s < nsol; s++) {
+            const int sz = sols[s].size, off = sd.off[s];
+            const double *src = sols[s].m;
+            for (int64_t i = b0; i < b1; i++)
+              for (int j = 0; j < sz; j++) hs[(size_t)i * S + off + j] = src[i * sz + j];
+          }
+        }
+      });
+      CK(hipMemcpyAsync(ctx->d_sol.p + r0 * S, hs + r0 * S, (size_t)((r1 - r0) * S) * sizeof(double),
+                        hipMemcpyHostToDevice, st));
     }
-  });
-  CK(hipMemcpyAsync(ctx->d_sol.p, hs, hs_n * sizeof(double), hipMemcpyHostToDevice, st));
+  }
   tr.mark("solutions");
   // boundary triangles
   std::vector<TriRec> htr;

@@ -193,9 +193,14 @@ __device__ __forceinline__ void qual_init(QualPart &p) {
 // scalar registers); sum and extrema per lane, reduced by a fixed shuffle
 // tree and the 4 waves in order (deterministic), so the workgroup needs no
 // 256-entry LDS reduction buffer (occupancy no longer LDS-bound).
-template <bool ANI, bool OUT>
-__global__ __launch_bounds__(256) void k_qual(StatArgs A, double *qual, QualPart *parts,
-                                              int use_stored) {
+// MODE (compiled apart, no run-time branches in the loop): QM_STORE every
+// tet's quality into qual, no partials (MMG3D_tetraQual); QM_HISTO the
+// partials of freshly computed qualities, nothing stored; QM_STORED the
+// partials of the qualities already in qual (OUTQUA after tetraQual).
+enum { QM_STORE = 0, QM_HISTO = 1, QM_STORED = 2 };
+template <bool ANI, bool OUT, int MODE>
+__global__ __launch_bounds__(256) void k_qual(StatArgs A, double *qual, QualPart *parts) {
+  constexpr bool use_stored = MODE == QM_STORED;
   __shared__ QualPart sh[4];
   double avg = 0.0, qmax = 0.0, qmin = 2.0;
   long long iel = 0x7fffffffffffffffLL;
@@ -215,17 +220,19 @@ __global__ __launch_bounds__(256) void k_qual(StatArgs A, double *qual, QualPart
     if (kn <= k1) cv = A.tetv[kn];
     const bool valid = in && v[0] > 0;
     // !MG_EOK: no quality (0, not a stale value)
-    if (in && !valid && !use_stored && qual) qual[k] = 0.0;
+    if (MODE == QM_STORE && in && !valid) qual[k] = 0.0;
     double rap = 0.0;
     if (valid) {
       const double q = use_stored ? qual[k] : tet_quality<ANI>(A, v);
-      if (!use_stored && qual) qual[k] = q;
+      if (MODE == QM_STORE) qual[k] = q;
       rap = ALPHAD * q;
-      if (rap < qmin || (rap == qmin && k < iel)) { qmin = rap; iel = k; }
-      avg += rap;
-      qmax = fmax(qmax, rap);
+      if (MODE != QM_STORE) {
+        if (rap < qmin || (rap == qmin && k < iel)) { qmin = rap; iel = k; }
+        avg += rap;
+        qmax = fmax(qmax, rap);
+      }
     }
-    if (!parts) continue;
+    if (MODE == QM_STORE) continue;
     cne += (unsigned)__popcll(__ballot(valid));
     cgood += (unsigned)__popcll(__ballot(valid && rap > 0.12));
     cmed += (unsigned)__popcll(__ballot(valid && rap > 0.5));
@@ -235,7 +242,7 @@ __global__ __launch_bounds__(256) void k_qual(StatArgs A, double *qual, QualPart
 #pragma unroll
     for (int i = 0; i < 5; i++) chis[i] += (unsigned)__popcll(__ballot(valid && ir == i));
   }
-  if (!parts) return;
+  if (MODE == QM_STORE) return;
   // the same tree on every lane (the lower lane's value first)
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -889,10 +896,13 @@ static int qual_partial(pmx_ctx *ctx, const StatArgs &A, int opt, double *qual_d
     B.ridmet = 1;
     B.rtag = A.ptag;
   }
-  if (ani && out) hipLaunchKernelGGL((k_qual<true, true>), dim3(nb), dim3(256), 0, s, B, q, parts, use_stored);
-  else if (ani) hipLaunchKernelGGL((k_qual<true, false>), dim3(nb), dim3(256), 0, s, B, q, parts, use_stored);
-  else if (out) hipLaunchKernelGGL((k_qual<false, true>), dim3(nb), dim3(256), 0, s, B, q, parts, use_stored);
-  else hipLaunchKernelGGL((k_qual<false, false>), dim3(nb), dim3(256), 0, s, B, q, parts, use_stored);
+  using KQ = void (*)(StatArgs, double *, QualPart *);
+  static const KQ kq[2][2][2] = {
+      {{k_qual<false, false, QM_HISTO>, k_qual<false, false, QM_STORED>},
+       {k_qual<false, true, QM_HISTO>, k_qual<false, true, QM_STORED>}},
+      {{k_qual<true, false, QM_HISTO>, k_qual<true, false, QM_STORED>},
+       {k_qual<true, true, QM_HISTO>, k_qual<true, true, QM_STORED>}}};
+  hipLaunchKernelGGL(kq[ani][out][use_stored ? 1 : 0], dim3(nb), dim3(256), 0, s, B, q, parts);
   QualPart *mid = parts + nb;
   hipLaunchKernelGGL(k_qual_final, dim3(FINAL_GRID), dim3(256), 0, s, parts, nb, mid,
                      (pmx_qual_part *)nullptr, 0LL);
@@ -978,11 +988,11 @@ int pmx_tetra_qual(pmx_ctx *ctx, int metRidTyp, double *qual) {
   A.rtag = A.ptag;
   if (!pmx_dgrow(ctx, ctx->d_qual, (size_t)(ctx->ne + 1))) return 0;
   if (A.msize == 6)
-    hipLaunchKernelGGL((k_qual<true, false>), dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
-                       ctx->d_qual.p, (QualPart *)nullptr, 0);
+    hipLaunchKernelGGL((k_qual<true, false, QM_STORE>), dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
+                       ctx->d_qual.p, (QualPart *)nullptr);
   else
-    hipLaunchKernelGGL((k_qual<false, false>), dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
-                       ctx->d_qual.p, (QualPart *)nullptr, 0);
+    hipLaunchKernelGGL((k_qual<false, false, QM_STORE>), dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
+                       ctx->d_qual.p, (QualPart *)nullptr);
   if (hipGetLastError() != hipSuccess) { ctx->err = "k_qual launch"; return 0; }
   ctx->have_qual = true;
   if (qual) {
@@ -1239,9 +1249,9 @@ static int new_mesh_qual_core(pmx_ctx *ctx, const char *who, int opt, int metRid
   }
   const int nb = stat_blocks(ne);
   if (A.msize == 6)
-    hipLaunchKernelGGL((k_qual<true, false>), dim3(nb), dim3(256), 0, s, A, ctx->d_nqual.p, (QualPart *)nullptr, 0);
+    hipLaunchKernelGGL((k_qual<true, false, QM_STORE>), dim3(nb), dim3(256), 0, s, A, ctx->d_nqual.p, (QualPart *)nullptr);
   else
-    hipLaunchKernelGGL((k_qual<false, false>), dim3(nb), dim3(256), 0, s, A, ctx->d_nqual.p, (QualPart *)nullptr, 0);
+    hipLaunchKernelGGL((k_qual<false, false, QM_STORE>), dim3(nb), dim3(256), 0, s, A, ctx->d_nqual.p, (QualPart *)nullptr);
   if (dev_result && !qual_partial(ctx, A, opt, ctx->d_nqual.p, 1, (pmx_qual_part *)dev_result, n)) return 0;
   if (hipGetLastError() != hipSuccess) { ctx->err = std::string(who) + ": launch"; return 0; }
   if (qual && !pmx_download_qual(ctx, ctx->d_nqual.p, ne, qual, qstride)) {

@@ -239,8 +239,16 @@ __global__ __launch_bounds__(256) void k_qual(StatArgs A, double *qual, QualPart
     if (OUT) cnrid += (unsigned)__popcll(__ballot(valid && tet_4ridge(A, v)));
     int ir = (int)(5.0 * rap);
     ir = ir < 4 ? ir : 4;
-#pragma unroll
-    for (int i = 0; i < 5; i++) chis[i] += (unsigned)__popcll(__ballot(valid && ir == i));
+    // the bin from three bit ballots (scalar mask algebra) instead of five
+    // per-bin ones
+    const unsigned long long V = __ballot(valid), B0 = __ballot(ir & 1), B1 = __ballot(ir & 2),
+                             B2 = __ballot(ir & 4);
+    const unsigned long long L = V & ~B2;            // bins 0-3
+    chis[0] += (unsigned)__popcll(L & ~B1 & ~B0);
+    chis[1] += (unsigned)__popcll(L & ~B1 & B0);
+    chis[2] += (unsigned)__popcll(L & B1 & ~B0);
+    chis[3] += (unsigned)__popcll(L & B1 & B0);
+    chis[4] += (unsigned)__popcll(V & B2);
   }
   if (MODE == QM_STORE) return;
   // the same tree on every lane (the lower lane's value first)

@@ -264,7 +264,7 @@ bool pmx_download_qual(pmx_ctx *ctx, const double *dev, int64_t ne, double *qual
     } else {
       par_for(std::max<int64_t>(lo, 1), hi, [&](int64_t k0, int64_t k1) {
         for (int64_t k = k0; k < k1; k++)
-          if (htv[k].x) *(double *)(out + k * stride) = h[k];
+          if (htv[k].x) memcpy(out + k * stride, &h[k], sizeof(double));   // any record alignment
       });
     }
   }

@@ -995,7 +995,7 @@ static bool run_flags_valid(int flags, std::string *err) {
   }
   const int e = (flags >> PMX_RUN_EXP_SHIFT) & 0xff;
   switch (e) {
-    case 0: case 6: case 9: case 10: case 11: case 12: case 13:
+    case 0: case 6: case 9: case 10: case 11: case 12:
       return true;
     case 4: case 5: {
       const char *v = getenv("PMX_EXPERIMENTS");
@@ -1062,12 +1062,10 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     if (!ctx->build_node_trias(ss)) return 0;
     ctx->have_csr = true;
   }
-  // exp 13 (A/B): hint cells from the double coordinates, no fixed-point copy
-  const bool hint_d = ((opts.flags >> PMX_RUN_EXP_SHIFT) & 0xff) == 13;
   if (derive) {
-    launch_bg_derive(ctx->d_xyz.p, ctx->np, ctx->grid, hint_d ? nullptr : ctx->d_xyzq.p, ctx->d_tris.p, ctx->nt,
+    launch_bg_derive(ctx->d_xyz.p, ctx->np, ctx->grid, ctx->d_xyzq.p, ctx->d_tris.p, ctx->nt,
                      ctx->d_trn.p, st);
-    ctx->have_derived = !hint_d;             // no fixed-point copy: the next step derives again
+    ctx->have_derived = true;
   }
   if (ev) CK(hipEventRecord(ev[7], st));
   if (!ctx->classify(st)) return 0;
@@ -1102,9 +1100,8 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     const bool early = A.exp != 9;
     if (early && !fork_surface()) return 0;
     const int stride = opts.hint_stride > 0 ? opts.hint_stride : PMX_HINT_STRIDE;
-    const bool packed = stride == PMX_HINT_STRIDE;
-    launch_hint_build(packed ? ctx->d_tets_s.p : nullptr, ctx->d_tets.p, ctx->ne, stride, ctx->d_grid.p, A.g,
-                      (hint_d && packed) ? nullptr : ctx->d_xyzq.p, st, ctx->d_xyz.p);
+    launch_hint_build(stride == PMX_HINT_STRIDE ? ctx->d_tets_s.p : nullptr, ctx->d_tets.p, ctx->ne,
+                      stride, ctx->d_grid.p, A.g, ctx->d_xyzq.p, st);
     if (ev) CK(hipEventRecord(ev[1], st));
     if (!early && !fork_surface()) return 0;
     if (ctx->nq_vol_ub) launch_walk(A, st);

@@ -74,8 +74,7 @@ struct ExhArgs {
 // connectivity of tets 1, 1+stride, ... (stride == PMX_HINT_STRIDE), else the
 // tet records are read strided
 void launch_hint_build(const int4 *packed, const TetRec *tets, int64_t ne, int stride, int *grid,
-                       GridDesc g, const unsigned long long *xyzq, hipStream_t s,
-                       const double *xyz = nullptr);
+                       GridDesc g, const unsigned long long *xyzq, hipStream_t s);
 // per-background derived data: fixed-point grid coordinates of the vertices
 // (hint centroids) and the unit normals of the boundary trias
 // (PMMG_precompute_triaNormals, src/locate_pmmg.c:68-90), one launch

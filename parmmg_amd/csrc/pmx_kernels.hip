@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void k_bg_derive(const double *__restrict__ xy
     return r;
   };
   // two vertices per thread: three 16-B loads, one 16-B store (rows 2m, 2m+1)
-  const int64_t npair = q ? (np + 2) / 2 : 0;   // vertices 0 .. np (no q: normals only)
+  const int64_t npair = (np + 2) / 2;           // vertices 0 .. np
   for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < npair; m += st) {
     if (2 * m + 1 <= np) {
       const double2 *p = reinterpret_cast<const double2 *>(xyz + 6 * m);
@@ -109,34 +109,10 @@ __global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ pac
   }
   grid[gcell(g, cq[0], cq[1], cq[2])] = (int)k;
 }
-// The same cells from the double coordinates (4 x 24-B gathers, the centroid
-// scaled into the grid): no fixed-point copy of the vertices is needed, so
-// the derived-data pass skips it (exp 13, A/B).
-__global__ __launch_bounds__(256) void k_hint_build_d(const int4 *__restrict__ packed, int64_t ne, int stride,
-                                                      int *__restrict__ grid, GridDesc g,
-                                                      const double *__restrict__ xyz) {
-  const int64_t n = (ne + stride - 1) / stride;
-  const int64_t t = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  const int4 v = packed[t];
-  if (v.x <= 0) return;
-  const D3 a = ld3(xyz, v.x), b = ld3(xyz, v.y), c = ld3(xyz, v.z), d = ld3(xyz, v.w);
-  const double m[3] = {0.25 * (a.x + b.x + c.x + d.x), 0.25 * (a.y + b.y + c.y + d.y),
-                       0.25 * (a.z + b.z + c.z + d.z)};
-  int cq[3];
-#pragma unroll
-  for (int ax = 0; ax < 3; ax++) cq[ax] = clampi((m[ax] - g.lo[ax]) * g.inv[ax], g.dim[ax]);
-  grid[gcell(g, cq[0], cq[1], cq[2])] = (int)(1 + t * stride);
-}
-
 void launch_hint_build(const int4 *packed, const TetRec *tets, int64_t ne, int stride, int *grid,
-                       GridDesc g, const unsigned long long *xyzq, hipStream_t s, const double *xyz) {
+                       GridDesc g, const unsigned long long *xyzq, hipStream_t s) {
   const int64_t n = (ne + stride - 1) / stride;
   const int64_t nb = std::max<int64_t>((n + 255) / 256, 1);
-  if (!xyzq && packed) {
-    hipLaunchKernelGGL(k_hint_build_d, dim3((unsigned)nb), dim3(256), 0, s, packed, ne, stride, grid, g, xyz);
-    return;
-  }
   if (packed)
     hipLaunchKernelGGL(k_hint_build<true>, dim3((unsigned)nb), dim3(256), 0, s, packed, tets, ne, stride,
                        grid, g, xyzq);

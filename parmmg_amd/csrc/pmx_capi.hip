@@ -724,7 +724,7 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
     ctx->tets_inflight = false;
   }
   ctx->tets_pending = false;
-  ctx->norph = 0;
+  ctx->orph_marks = false;
   ctx->orph_fixed = true;
   ctx->eager_nch = 0;
   if (!pv) { ctx->err = "pmx_upload_points: null view"; return 0; }
@@ -851,11 +851,12 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
 // The points view's new tets (vertex = view index - first + 1), validated and
 // packed in chunks into their own pinned staging (the shared arena serves the
 // download meanwhile), each chunk's DMA on `up` overlapping the packing of
-// the next.  The same pass is the reference's vertex loop over the new tets
-// (src/interpmesh_pmmg.c:535-541): it marks the points of valid tets, so that
-// the points in no valid tet (orphans: untouched, the reference never visits
-// them) are known.  With residency the next background's tet records are
-// built from them on the topo stream once they have arrived.
+// the next.  Once they are on the device, a kernel on the same stream marks
+// the points of valid tets -- the reference's vertex loop over the new tets
+// (src/interpmesh_pmmg.c:535-541) -- so that the points in no valid tet
+// (orphans: untouched, the reference never visits them) are known to
+// fix_orphans.  With residency the next background's tet records are built
+// from them on the topo stream once they have arrived.
 bool pmx_ctx::pack_new_tets() {
   pmx_ctx *ctx = this;                     // CK()
   if (!tets_pending) return true;
@@ -865,8 +866,6 @@ bool pmx_ctx::pack_new_tets() {
   Trace tr("new tets");
   int4 *htv = grow_htets(ntet);
   if (!htv) return false;
-  h_mk.assign((size_t)std::max<int64_t>(n, 1), 0);
-  uint8_t *mk = h_mk.data();
   const char *tc = (const char *)pv->tetra_v;
   bool bad = false;
   htv[0] = make_int4(0, 0, 0, 0);
@@ -884,7 +883,6 @@ bool pmx_ctx::pack_new_tets() {
           int64_t jj = (int64_t)v[l] - pv->first;
           if (jj < 0 || jj >= n) { b = true; jj = 0; }
           w[l] = (int)(jj + 1);
-          __atomic_store_n(&mk[jj], (uint8_t)1, __ATOMIC_RELAXED);
         }
         st4(&htv[k], w[0], w[1], w[2], w[3], nt);
       }
@@ -894,6 +892,14 @@ bool pmx_ctx::pack_new_tets() {
     if (bad) break;
     CK(hipMemcpyAsync(d_ntetv.p + lo, htv + lo, (size_t)(hi - lo) * sizeof(int4), hipMemcpyHostToDevice, up));
   }
+  if (!bad && n > 0) {
+    // the orphan marks, on the device once the tets are there (the host's
+    // byte stores into a point-sized array cost as much as the packing)
+    CK(hipMemsetAsync(d_qmark.p, 0, (size_t)n, up));
+    launch_mark_new_tets(d_ntetv.p, ntet, d_qmark.p, up);
+    CK(hipGetLastError());
+    orph_marks = true;
+  }
   CK(hipEventRecord(ev_tets, up));
   tets_inflight = true;
   if (bad) {
@@ -902,19 +908,6 @@ bool pmx_ctx::pack_new_tets() {
     return false;
   }
   tr.mark("pack + dma issued");
-  // orphans among the points a step would locate or give a constant size
-  const char *tg = (const char *)pv->tag;
-  int64_t no[64] = {};
-  const int Co = par_chunks(0, n, [&](int ci, int64_t j0, int64_t j1) {
-    int64_t cnt = 0;
-    for (int64_t j = j0; j < j1; j++) {
-      const unsigned t = tg ? *(const uint16_t *)(tg + (pv->first + j) * pv->tag_stride) : 0u;
-      cnt += (!mk[j] && t < PMX_TAG_NUL) ? 1 : 0;
-    }
-    no[ci] = cnt;
-  });
-  norph = 0;
-  for (int i = 0; i < Co; i++) norph += no[i];
   // residency: the next background's tet records (face adjacency built on
   // the device) on the topo stream, after the tets' DMA, while the step and
   // the download go on
@@ -951,8 +944,8 @@ bool pmx_ctx::fix_orphans() {
   pmx_ctx *ctx = this;
   if (orph_fixed) return true;
   orph_fixed = true;
-  if (!ran || norph == 0 || nq == 0) return true;
-  CK(hipMemcpyAsync(d_qmark.p, h_mk.data(), (size_t)nq, hipMemcpyHostToDevice, stream));
+  if (!ran || !orph_marks || nq == 0) return true;
+  if (tets_inflight) CK(hipStreamWaitEvent(stream, ev_tets, 0));   // the marks are written on `up`
   launch_orphans(d_qmark.p, nq, (uint8_t)last_const_bit, d_wmask.p, d_elem.p, d_status.p, d_steps.p, stream);
   CK(hipGetLastError());
   return true;
@@ -1149,8 +1142,8 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
 
 // The fields and write masks of the step just enqueued, down into h_out (its
 // own pinned buffer: the arena stays free for the calls in between) in chunks
-// on the step's stream.  The orphan reset (fix_orphans, later) is applied to
-// these masks by pmx_download on the host, from the same marks.
+// on the step's stream.  The orphan reset (fix_orphans, later) changes masks
+// only: pmx_download takes them again.
 bool pmx_ctx::eager_download() {
   pmx_ctx *ctx = this;
   eager_nch = 0;
@@ -1191,12 +1184,12 @@ static bool results_ready(pmx_ctx *ctx, const char *who) {
 }
 
 // The step's rows [i0, i1) of the packed fields h (S doubles per point) into
-// the caller's per-solution arrays where the write mask has the solution's bit
-// (mk: orphan marks; a point without one keeps only the `keep` bits).  In
-// blocks of 1024 points, so that every solution reads a block of h from cache
-// (solution by solution over the whole range read h once per solution).
+// the caller's per-solution arrays where the write mask has the solution's
+// bit.  In blocks of 1024 points, so that every solution reads a block of h
+// from cache (solution by solution over the whole range read h once per
+// solution).
 static void scatter_rows(const pmx_ctx *ctx, const pmx_sol_view *new_sols, const double *h, const uint8_t *wm,
-                         const uint8_t *mk, unsigned keep, int64_t i0, int64_t i1) {
+                         int64_t i0, int64_t i1) {
   const int S = ctx->sd.S;
   for (int64_t b0 = i0; b0 < i1; b0 += 1024) {
     const int64_t b1 = std::min(i1, b0 + 1024);
@@ -1206,8 +1199,7 @@ static void scatter_rows(const pmx_ctx *ctx, const pmx_sol_view *new_sols, const
       const int sz = ctx->sd.size[s], off = ctx->sd.off[s];
       const unsigned bit = 1u << s;
       for (int64_t i = b0; i < b1; i++) {
-        const unsigned w = (mk && !mk[i]) ? (wm[i] & keep) : wm[i];
-        if (!(w & bit)) continue;
+        if (!(wm[i] & bit)) continue;
         const double *src = h + i * S + off;
         double *d = dst + i * sz;
         for (int j = 0; j < sz; j++) d[j] = src[j];
@@ -1217,18 +1209,20 @@ static void scatter_rows(const pmx_ctx *ctx, const pmx_sol_view *new_sols, const
 }
 
 // pmx_download after a PMX_RUN_EAGER_DOWNLOAD step: the fields are (being)
-// copied into h_out; each chunk is scattered once it has landed.  The write
-// masks are the step's: the orphan reset is applied here (a point in no valid
-// new tet keeps only a constant-size metric bit, as launch_orphans does on the
-// device).  elem / status / steps come down as usual (after fix_orphans).
+// copied into h_out; each chunk is scattered once it has landed.  elem /
+// status / steps come down as usual (after fix_orphans).
 static int download_eager(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem, int *status, int *steps) {
   const int64_t n = ctx->nq;
   const int S = ctx->sd.S;
   const double *h = (const double *)ctx->h_out;
   const uint8_t *wm = (const uint8_t *)(ctx->h_out + al256((size_t)(n * S) * sizeof(double)));
-  const bool orph = ctx->norph > 0 && (int64_t)ctx->h_mk.size() >= n;
-  const uint8_t *mk = orph ? ctx->h_mk.data() : nullptr;
-  const unsigned keep = ctx->last_const_bit;
+  // the eager copy holds the step's masks; with new tets, the orphan reset
+  // (fix_orphans, enqueued by pmx_download after them) changed some: take the
+  // masks again (n bytes)
+  if (ctx->orph_marks) {
+    CK(hipMemcpyAsync(const_cast<uint8_t *>(wm), ctx->d_wmask.p, (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+    CK(hipStreamSynchronize(ctx->stream));
+  }
   const bool want_int = elem || status || steps;
   const size_t o_el = 0, o_st = o_el + al256((size_t)n * sizeof(int)), o_sp = o_st + al256((size_t)n * sizeof(int)),
                total = o_sp + al256((size_t)n * sizeof(int));
@@ -1244,7 +1238,7 @@ static int download_eager(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem,
   for (int c = 0; c < nch; c++) {
     const int64_t lo = n * c / nch, hi = n * (c + 1) / nch;
     CK(hipEventSynchronize(ctx->ev_eg[c]));
-    par_for(lo, hi, [&](int64_t i0, int64_t i1) { scatter_rows(ctx, new_sols, h, wm, mk, keep, i0, i1); });
+    par_for(lo, hi, [&](int64_t i0, int64_t i1) { scatter_rows(ctx, new_sols, h, wm, i0, i1); });
   }
   if (want_int) {
     CK(hipStreamSynchronize(ctx->stream));
@@ -1292,7 +1286,7 @@ int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem, int *sta
   for (int64_t c = 0; c < nch; c++) {
     const int64_t lo = n * c / nch, hi = n * (c + 1) / nch;
     CK(hipEventSynchronize(ctx->ev_dl[c]));
-    par_for(lo, hi, [&](int64_t i0, int64_t i1) { scatter_rows(ctx, new_sols, h, wm, nullptr, 0u, i0, i1); });
+    par_for(lo, hi, [&](int64_t i0, int64_t i1) { scatter_rows(ctx, new_sols, h, wm, i0, i1); });
   }
   CK(hipStreamSynchronize(ctx->stream));
   if (elem) memcpy(elem, st + o_el, (size_t)n * sizeof(int));

@@ -153,8 +153,7 @@ struct pmx_ctx {
   bool tets_pending = false;            // view kept, not packed yet
   bool tets_inflight = false;           // DMA issued on `up`, ev_tets recorded
   pmx_points_view tview{};
-  std::vector<uint8_t> h_mk;            // 1: the point is in a valid new tet
-  int64_t norph = 0;                    // live points in no valid new tet (known once packed)
+  bool orph_marks = false;              // d_qmark holds the device's marks of the packed new tets
   bool orph_fixed = true;               // the last step's orphan rows reset (fix_orphans)
   unsigned last_const_bit = 0;          // wmask bit of the last step's constant-size metric
   // PMX_RUN_EAGER_DOWNLOAD: the last step's fields (n * S doubles) and write

@@ -491,6 +491,24 @@ void launch_orphans(const uint8_t *mk, int64_t n, uint8_t keep, uint8_t *wmask, 
   hipLaunchKernelGGL(k_orphans, dim3((unsigned)nb), dim3(256), 0, s, mk, n, keep, wmask, elem, status, steps);
 }
 
+// the orphan marks from the new tets on the device: point j (0-based) is
+// marked when a valid new tet (1-based vertex j + 1) holds it -- the
+// reference's vertex loop over the new tets (src/interpmesh_pmmg.c:535-541)
+__global__ __launch_bounds__(256) void k_mark_new_tets(const int4 *__restrict__ tv, int64_t ne,
+                                                       uint8_t *__restrict__ mk) {
+  for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= ne;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int4 v = tv[k];
+    if (v.x <= 0) continue;
+    mk[v.x - 1] = 1; mk[v.y - 1] = 1; mk[v.z - 1] = 1; mk[v.w - 1] = 1;
+  }
+}
+void launch_mark_new_tets(const int4 *tv, int64_t ne, uint8_t *mk, hipStream_t s) {
+  if (ne < 1) return;
+  const int64_t nb = std::min<int64_t>((ne + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_mark_new_tets, dim3((unsigned)nb), dim3(256), 0, s, tv, ne, mk);
+}
+
 // ---- device residency across iterations (pmx_promote_background) ----------------
 
 // the last step's new points and results become the background: vertex ip

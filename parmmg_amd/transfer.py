@@ -451,6 +451,11 @@ class Transfer:
             q = np.zeros(self.n_new_tets + 1)
             ptr, stride = _dp(q), 8
         else:
+            if (out.ndim != 1 or not out.flags.c_contiguous or out.dtype.fields is None or "qual" not in
+                    out.dtype.fields or out.dtype.fields["qual"][0] != np.float64 or
+                    out.shape[0] < self.n_new_tets + 1):
+                raise ValueError("out: a contiguous 1-D record array with a float64 'qual' field, "
+                                 "one record per new tet plus slot 0")
             q = out
             base = out.ctypes.data + out.dtype.fields["qual"][1]
             ptr, stride = C.cast(C.c_void_p(base), N.dptr), out.dtype.itemsize

@@ -347,7 +347,8 @@ typedef struct {
  * vertex indices in the last points view's numbering, !MG_EOK entries kept
  * as deleted) -- after pmx_upload_points, once per iteration (they also
  * serve pmx_new_mesh_qual).  A points view with tetra_v uploads them too
- * (same pass as the orphan marking): no separate call needed then.
+ * (packed and sent by the first pmx_run, the orphan marks made from them on
+ * the device): no separate call needed then.
  *
  * pmx_promote_background: after a pmx_run on those points, the new points
  * (view first must be 1) become the background vertices 1..np, the step's

@@ -111,17 +111,6 @@ static bool nt_stores() {
   }();
   return on;
 }
-static inline void st3u(unsigned *p, unsigned a, unsigned b, unsigned c, bool nt) {
-  if (nt) {
-    __builtin_nontemporal_store(a, p);
-    __builtin_nontemporal_store(b, p + 1);
-    __builtin_nontemporal_store(c, p + 2);
-  } else {
-    p[0] = a;
-    p[1] = b;
-    p[2] = c;
-  }
-}
 static inline void st4(int4 *p, int a, int b, int c, int d, bool nt) {
   if (nt) {
     const pmx_v4i v = {a, b, c, d};
@@ -251,7 +240,8 @@ void pmx_par_for(int64_t lo, int64_t hi, const std::function<void(int64_t, int64
 
 bool pmx_download_qual(pmx_ctx *ctx, const double *dev, int64_t ne, double *qual, int64_t stride) {
   const bool dense = stride == (int64_t)sizeof(double);
-  if (!dense && (!ctx->h_tets || ctx->h_tets_cap < (size_t)(ne + 1) * (size_t)ctx->h_tets_rec)) {
+  const int4 *htv = (const int4 *)ctx->h_tets;
+  if (!dense && (!htv || ctx->h_tets_cap < (size_t)(ne + 1) * sizeof(int4))) {
     ctx->err = "qualities: strided output needs the new tets' host copy";
     return false;
   }
@@ -274,7 +264,7 @@ bool pmx_download_qual(pmx_ctx *ctx, const double *dev, int64_t ne, double *qual
     } else {
       par_for(std::max<int64_t>(lo, 1), hi, [&](int64_t k0, int64_t k1) {
         for (int64_t k = k0; k < k1; k++)
-          if (ctx->htet_valid(k)) memcpy(out + k * stride, &h[k], sizeof(double));   // any record alignment
+          if (htv[k].x) memcpy(out + k * stride, &h[k], sizeof(double));   // any record alignment
       });
     }
   }
@@ -282,10 +272,9 @@ bool pmx_download_qual(pmx_ctx *ctx, const double *dev, int64_t ne, double *qual
   return true;
 }
 
-// the pinned copy of the new tets, ne + 1 records of rec bytes
-char *pmx_ctx::grow_htets(int64_t ne, int rec) {
-  const size_t bytes = (size_t)(ne + 1) * (size_t)rec;
-  h_tets_rec = rec;
+// the pinned copy of the new tets, ne + 1 records
+int4 *pmx_ctx::grow_htets(int64_t ne) {
+  const size_t bytes = (size_t)(ne + 1) * sizeof(int4);
   if (bytes > h_tets_cap) {
     if (h_tets) hipHostFree(h_tets);
     h_tets = nullptr;
@@ -296,7 +285,7 @@ char *pmx_ctx::grow_htets(int64_t ne, int rec) {
     }
     h_tets_cap = bytes;
   }
-  return h_tets;
+  return (int4 *)h_tets;
 }
 
 template <class T> static void dfree(DevBuf<T> &b) {
@@ -875,82 +864,33 @@ bool pmx_ctx::pack_new_tets() {
   const pmx_points_view *pv = &tview;
   const int64_t n = nq, ntet = pv->ne;
   Trace tr("new tets");
-  // PCIe carries 12 B per tet (PMX_TPK: the first vertex, then the three
-  // others as 21-bit deltas from it; decoded on the device), 16 B with
-  // PMX_TPK=0 (the A/B)
-  static const bool tpk = [] {
-    const char *e = getenv("PMX_TPK");
-    return !(e && e[0] == '0');
-  }();
-  const int rec = tpk ? 12 : 16;
-  char *hb = grow_htets(ntet, rec);
-  if (!hb) return false;
-  if (tpk && !dgrow(this, d_tpk, (size_t)(3 * (ntet + 1)))) return false;
-  int4 *htv = (int4 *)hb;
-  unsigned *hpk = (unsigned *)hb;
+  int4 *htv = grow_htets(ntet);
+  if (!htv) return false;
   const char *tc = (const char *)pv->tetra_v;
   bool bad = false;
-  if (tpk) hpk[0] = hpk[1] = hpk[2] = 0u;
-  else htv[0] = make_int4(0, 0, 0, 0);
+  htv[0] = make_int4(0, 0, 0, 0);
   const bool nt = nt_stores();
-  h_tesc.clear();
-  std::mutex esc_m;
   const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(8, ntet >> 20));
   for (int64_t c = 0; c < nch; c++) {
     const int64_t lo = (c == 0) ? 0 : 1 + ntet * c / nch, hi = 1 + ntet * (c + 1) / nch;
     par_for(std::max<int64_t>(lo, 1), hi, [&](int64_t k0, int64_t k1) {
       bool b = false;
-      std::vector<int4> esc;
       for (int64_t k = k0; k < k1; k++) {
         const int *v = (const int *)(tc + k * pv->tetra_stride);
-        if (v[0] <= 0) {                                            // !MG_EOK
-          if (tpk) st3u(hpk + 3 * k, 0u, 0u, 0u, nt);
-          else st4(&htv[k], 0, 0, 0, 0, nt);
-          continue;
-        }
+        if (v[0] <= 0) { st4(&htv[k], 0, 0, 0, 0, nt); continue; }   // !MG_EOK
         int w[4];
         for (int l = 0; l < 4; l++) {
           int64_t jj = (int64_t)v[l] - pv->first;
           if (jj < 0 || jj >= n) { b = true; jj = 0; }
           w[l] = (int)(jj + 1);
         }
-        if (!tpk) { st4(&htv[k], w[0], w[1], w[2], w[3], nt); continue; }
-        unsigned long long bits = 0;
-        bool fits = true;
-        for (int l = 1; l < 4; l++) {
-          const int d = w[l] - w[0];
-          fits = fits && d >= -(1 << 20) && d < (1 << 20);
-          bits |= (unsigned long long)((unsigned)d & 0x1fffffu) << (21 * (l - 1));
-        }
-        if (!fits) {                                                 // escape: fixed on the device
-          bits = 1ull << 63;
-          esc.push_back(make_int4((int)k, w[1], w[2], w[3]));
-        }
-        st3u(hpk + 3 * k, (unsigned)w[0], (unsigned)bits, (unsigned)(bits >> 32), nt);
+        st4(&htv[k], w[0], w[1], w[2], w[3], nt);
       }
       if (b) __atomic_store_n(&bad, true, __ATOMIC_RELAXED);
-      if (!esc.empty()) {
-        std::lock_guard<std::mutex> g(esc_m);
-        h_tesc.insert(h_tesc.end(), esc.begin(), esc.end());
-      }
       std::atomic_thread_fence(std::memory_order_seq_cst);
     });
     if (bad) break;
-    if (tpk)
-      CK(hipMemcpyAsync(d_tpk.p + 3 * lo, hpk + 3 * lo, (size_t)(hi - lo) * 12, hipMemcpyHostToDevice, up));
-    else
-      CK(hipMemcpyAsync(d_ntetv.p + lo, htv + lo, (size_t)(hi - lo) * sizeof(int4), hipMemcpyHostToDevice, up));
-  }
-  if (!bad && tpk) {
-    // decode (+ the escapes' vertices) into the int4 records
-    int4 *desc = nullptr;
-    if (!h_tesc.empty()) {
-      if (!dgrow(this, d_tesc, h_tesc.size())) return false;
-      desc = d_tesc.p;
-      CK(hipMemcpyAsync(desc, h_tesc.data(), h_tesc.size() * sizeof(int4), hipMemcpyHostToDevice, up));
-    }
-    launch_decode_tpk(d_tpk.p, ntet, desc, (int64_t)h_tesc.size(), d_ntetv.p, up);
-    CK(hipGetLastError());
+    CK(hipMemcpyAsync(d_ntetv.p + lo, htv + lo, (size_t)(hi - lo) * sizeof(int4), hipMemcpyHostToDevice, up));
   }
   if (!bad && n > 0) {
     // the orphan marks, on the device once the tets are there (the host's
@@ -1568,7 +1508,7 @@ int pmx_upload_new_tets(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, 
   const int64_t first = ctx->pts_first, n = ctx->nq;
   // packed into the pinned copy of the new tets (a strided quality output
   // reads their validity there)
-  int4 *h = (int4 *)ctx->grow_htets(ne, (int)sizeof(int4));
+  int4 *h = ctx->grow_htets(ne);
   if (!h) return 0;
   h[0] = make_int4(0, 0, 0, 0);
   const char *tc = (const char *)tetra_v;
@@ -1801,7 +1741,7 @@ void pmx_ctx::free_all() {
   dfree(d_ptag); dfree(d_touch); dfree(d_cidx); dfree(d_intv); dfree(d_pub); dfree(d_pkey);
   dfree(d_ppt); dfree(d_pedge); dfree(d_ntetv); dfree(d_nqual); dfree(d_qtag); dfree(d_gather);
   dfree(d_adja); dfree(d_tcnt); dfree(d_toff); dfree(d_tbad); dfree(d_trec); dfree(d_ttmp);
-  dfree(d_pent); dfree(d_pval); dfree(d_tpk); dfree(d_tesc); dfree(d_tets_next); dfree(d_tets_s_next);
+  dfree(d_pent); dfree(d_pval); dfree(d_tets_next); dfree(d_tets_s_next);
   next_topo = false;
   dfree(d_cmet); dfree(d_cperm); dfree(d_ccnt);
   if (d_tgrid) hipFree(d_tgrid);

@@ -148,12 +148,8 @@ struct pmx_ctx {
   // itself never reads them); consumers wait for ev_tets (ensure_tets)
   hipStream_t up = nullptr;
   hipEvent_t ev_tets = nullptr;
-  char *h_tets = nullptr;               // pinned copy of the current new tets (0 = deleted);
+  char *h_tets = nullptr;               // pinned copy of the current new tets (int4, 0 = deleted);
   size_t h_tets_cap = 0;                // not the shared arena: it outlives the step (qualities' validity)
-  int h_tets_rec = 16;                  // its record: 16 (int4) or 12 (PMX_TPK: v0 + three 21-bit deltas)
-  DevBuf<unsigned> d_tpk;               // the 12-B records on the device, before the decode
-  std::vector<int4> h_tesc;             // PMX_TPK escapes: (k, w1, w2, w3) of tets whose deltas do not fit
-  DevBuf<int4> d_tesc;                  // the same on the device
   bool tets_pending = false;            // view kept, not packed yet
   bool tets_inflight = false;           // DMA issued on `up`, ev_tets recorded
   pmx_points_view tview{};
@@ -184,10 +180,7 @@ struct pmx_ctx {
   bool ensure_tets(hipStream_t s);        // d_ntetv valid for work on stream s
   bool fix_orphans();                     // the last step's rows of orphan points: untouched
   bool eager_download();                  // issue the eager copies of the step just enqueued
-  char *grow_htets(int64_t ne, int rec);  // h_tets for ne + 1 records of rec bytes (ev_tets already waited)
-  bool htet_valid(int64_t k) const {      // tet k of the pinned copy is valid (MG_EOK)
-    return h_tets_rec == 12 ? ((const unsigned *)h_tets)[3 * k] != 0u : ((const int4 *)h_tets)[k].x != 0;
-  }
+  int4 *grow_htets(int64_t ne);           // h_tets for ne + 1 records (ev_tets already waited)
   // device error word of the last step (after a stream sync): 0 = none
   bool check_device_errors();
 };

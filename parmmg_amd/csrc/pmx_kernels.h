@@ -100,7 +100,6 @@ void launch_tet_conn(const TetRec *src, int64_t n, int4 *dst, hipStream_t s);
 void launch_promote(const double *qxyz, const double *out, const uint16_t *qtag, int64_t n, int S, double *xyz,
                     double *sol, uint16_t *ptag, hipStream_t s);
 // points in no valid new tet (mk == 0) after a step: rows back to untouched
-void launch_decode_tpk(const unsigned *pk, int64_t ne, const int4 *esc, int64_t nesc, int4 *tv, hipStream_t s);
 void launch_mark_new_tets(const int4 *tv, int64_t ne, uint8_t *mk, hipStream_t s);
 void launch_orphans(const uint8_t *mk, int64_t n, uint8_t keep, uint8_t *wmask, int *elem, int *status, int *steps,
                     hipStream_t s);

@@ -509,40 +509,6 @@ void launch_mark_new_tets(const int4 *tv, int64_t ne, uint8_t *mk, hipStream_t s
   hipLaunchKernelGGL(k_mark_new_tets, dim3((unsigned)nb), dim3(256), 0, s, tv, ne, mk);
 }
 
-// PMX_TPK records (12 B: first vertex, three 21-bit signed deltas, bit 63 =
-// escape) -> int4; the escapes' vertices from their own list afterwards
-__global__ __launch_bounds__(256) void k_decode_tpk(const unsigned *__restrict__ pk, int64_t ne,
-                                                    int4 *__restrict__ tv) {
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= ne;
-       k += (int64_t)gridDim.x * blockDim.x) {
-    const int a = (int)pk[3 * k];
-    const unsigned long long b = (unsigned long long)pk[3 * k + 1] | ((unsigned long long)pk[3 * k + 2] << 32);
-    int d[3];
-#pragma unroll
-    for (int l = 0; l < 3; l++) {
-      const unsigned u = (unsigned)(b >> (21 * l)) & 0x1fffffu;
-      d[l] = (int)(u << 11) >> 11;                                 // sign-extend 21 bits
-    }
-    tv[k] = a ? make_int4(a, a + d[0], a + d[1], a + d[2]) : make_int4(0, 0, 0, 0);
-  }
-}
-__global__ __launch_bounds__(256) void k_tpk_escapes(const int4 *__restrict__ esc, int64_t n, int4 *__restrict__ tv) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int4 e = esc[i];
-    tv[e.x].y = e.y;
-    tv[e.x].z = e.z;
-    tv[e.x].w = e.w;
-  }
-}
-void launch_decode_tpk(const unsigned *pk, int64_t ne, const int4 *esc, int64_t nesc, int4 *tv, hipStream_t s) {
-  const int64_t nb = std::min<int64_t>((ne + 256) / 256, 16384);
-  hipLaunchKernelGGL(k_decode_tpk, dim3((unsigned)std::max<int64_t>(nb, 1)), dim3(256), 0, s, pk, ne, tv);
-  if (nesc > 0) {
-    const int64_t eb = std::min<int64_t>((nesc + 255) / 256, 4096);
-    hipLaunchKernelGGL(k_tpk_escapes, dim3((unsigned)eb), dim3(256), 0, s, esc, nesc, tv);
-  }
-}
-
 // ---- device residency across iterations (pmx_promote_background) ----------------
 
 // the last step's new points and results become the background: vertex ip

@@ -235,6 +235,36 @@ def test_new_mesh_quality_synced_into_tetra_records(transfer, metric):
     assert np.array_equal(qd.view(np.int64)[ok], qo.view(np.int64)[ok])
 
 
+def test_new_tets_shuffled_numbering(transfer):
+    """The points view's tets with a shuffled numbering of > 2^20 points (vertex
+    indices of one tet far apart) and a deleted tet: the device's copy must be
+    the caller's -- the new-mesh qualities (computed on it) bit-exact against
+    the oracle's on the caller's tets -- and exactly the points in no valid
+    tet are orphans (never visited)."""
+    m, _, _, sols = cube_case(6, metric="iso", fields=False)
+    n = 104
+    x, t = M.new_points(n, surface=False)                # 1.12 M volume points
+    tv = M.new_point_tets(n, x, t)
+    perm = np.random.default_rng(3).permutation(len(x))  # new index of point j
+    xs = np.empty_like(x)
+    xs[perm] = x
+    tvs = tv.copy()
+    tvs[1:] = perm[tv[1:] - 1] + 1
+    tvs[5, 0] = 0                                         # a deleted tet among them
+    transfer.upload_background(m, sols, 0)
+    transfer.upload_points(xs, np.zeros(len(x), np.uint16), tets_mmg=tvs)
+    transfer.run()
+    r = transfer.download()
+    used = np.zeros(len(x), bool)
+    used[tvs[1:][tvs[1:, 0] > 0].ravel() - 1] = True      # points of valid tets
+    assert np.all(r.status[used] == 1) and np.all(r.status[~used] == 0)
+    q = transfer.new_mesh_qual(None)
+    xyz1 = np.concatenate([np.zeros((1, 3)), xs])
+    qo = O.tetra_qual(M.Mesh(xyz1, tvs, None, np.zeros((1, 3), np.int32), None), None)
+    assert q[5] == 0.0
+    assert np.array_equal(q.view(np.int64)[1:], qo.view(np.int64)[1:])
+
+
 def test_rccl_single_rank_equals_fold(transfer):
     """pmx_qualhisto_allreduce / pmx_prilen_allreduce over a 1-rank RCCL
     communicator: the all-gather + fold of the group partials equals the

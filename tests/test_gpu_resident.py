@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 from helpers import bits_equal
+from parmmg_amd import _native as N
 from parmmg_amd import mesh as M
 from parmmg_amd.transfer import Transfer
 
@@ -150,7 +151,8 @@ def test_promote_requires_step_and_tets():
 
 
 @pytest.mark.parametrize("use_perm,copy_metric", [(False, True), (True, True), (True, False)])
-def test_copy_required_on_device(use_perm, copy_metric):
+@pytest.mark.parametrize("eager", [False, True])
+def test_copy_required_on_device(use_perm, copy_metric, eager):
     """pmx_copy_required: the frozen (MG_REQ) background points' values land
     in the rows of their new points that the step did not write -- the
     reference's PMMG_copySol_point (src/interpmesh_pmmg.c:311-358) before the
@@ -174,7 +176,8 @@ def test_copy_required_on_device(use_perm, copy_metric):
         tr.upload_background(m1, sols1, 0)
         tr.upload_point_tags(tags1)
         tr.upload_points(x2, t2, tets2)
-        tr.run()
+        # eager: the fields' copy started with the step is dropped by the copy
+        tr.run(flags=N.RUN_EAGER_DOWNLOAD if eager else 0)
         if copy:
             tr.copy_required(perm if use_perm else None, copy_metric)
         r = tr.download(init=init)

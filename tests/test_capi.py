@@ -107,3 +107,21 @@ def test_dropin_demo_runs():
     r = subprocess.run([build_dropin_demo()], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "dropin ok" in r.stdout
+
+
+def test_integration_makefile_matches_the_build():
+    """integration/Makefile (the Python-free build a ParMmg build links) lists
+    the same HIP sources as parmmg_amd/build.py and the flags bit parity needs
+    (-ffp-contract=off, gfx950); `make -n` resolves every rule."""
+    import re
+    import subprocess
+    from parmmg_amd import build
+    mk = open(os.path.join(ROOT, "integration", "Makefile")).read()
+    m = re.search(r"^SOURCES\s*:=\s*((?:.*\\\n)*.*)$", mk, re.M)
+    srcs = m.group(1).replace("\\\n", " ").split()
+    assert srcs == build.HIP_SOURCES
+    assert "-ffp-contract=off" in mk and "gfx950" in mk
+    r = subprocess.run(["make", "-n", "-C", os.path.join(ROOT, "integration"), "OUT=/tmp/pmx_make_n"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.count("-c ") == len(srcs) and "libpmx_transfer.so" in r.stdout

@@ -250,6 +250,7 @@ bool pmx_download_qual(pmx_ctx *ctx, const double *dev, int64_t ne, double *qual
   if (!st) return false;
   const double *h = (const double *)st;
   char *out = (char *)qual;
+  const bool nt_q = !dense && nt_stores() && ((uintptr_t)out % 8) == 0 && stride % 8 == 0;
   const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(8, (ne + 1) >> 20));
   for (int64_t c = 0; c < nch; c++) {
     const int64_t lo = (ne + 1) * c / nch, hi = (ne + 1) * (c + 1) / nch;
@@ -261,6 +262,18 @@ bool pmx_download_qual(pmx_ctx *ctx, const double *dev, int64_t ne, double *qual
     CK(hipEventSynchronize(ctx->ev_dl[c]));
     if (dense) {
       par_for(lo, hi, [&](int64_t k0, int64_t k1) { memcpy(qual + k0, h + k0, (size_t)(k1 - k0) * 8); });
+    } else if (nt_q) {
+      // streaming 8-B stores into the records (8-B aligned field and stride):
+      // no read for ownership of the caller's record lines
+      par_for(std::max<int64_t>(lo, 1), hi, [&](int64_t k0, int64_t k1) {
+        for (int64_t k = k0; k < k1; k++)
+          if (htv[k].x) {
+            long long bits;
+            memcpy(&bits, &h[k], sizeof bits);
+            __builtin_nontemporal_store(bits, (long long *)(out + k * stride));
+          }
+        std::atomic_thread_fence(std::memory_order_seq_cst);
+      });
     } else {
       par_for(std::max<int64_t>(lo, 1), hi, [&](int64_t k0, int64_t k1) {
         for (int64_t k = k0; k < k1; k++)

@@ -1204,6 +1204,9 @@ static bool results_ready(pmx_ctx *ctx, const char *who) {
 static void scatter_rows(const pmx_ctx *ctx, const pmx_sol_view *new_sols, const double *h, const uint8_t *wm,
                          int64_t i0, int64_t i1) {
   const int S = ctx->sd.S;
+  // streaming 8-B stores (no read for ownership of the caller's lines; the
+  // arrays are far larger than the caches anyway); PMX_NT_STORES=0: plain
+  const bool nt = nt_stores();
   for (int64_t b0 = i0; b0 < i1; b0 += 1024) {
     const int64_t b1 = std::min(i1, b0 + 1024);
     for (int s = 0; s < ctx->sd.nsol; s++) {
@@ -1215,10 +1218,19 @@ static void scatter_rows(const pmx_ctx *ctx, const pmx_sol_view *new_sols, const
         if (!(wm[i] & bit)) continue;
         const double *src = h + i * S + off;
         double *d = dst + i * sz;
-        for (int j = 0; j < sz; j++) d[j] = src[j];
+        if (nt) {
+          for (int j = 0; j < sz; j++) {
+            long long bits;
+            memcpy(&bits, &src[j], sizeof bits);
+            __builtin_nontemporal_store(bits, (long long *)&d[j]);
+          }
+        } else {
+          for (int j = 0; j < sz; j++) d[j] = src[j];
+        }
       }
     }
   }
+  if (nt) std::atomic_thread_fence(std::memory_order_seq_cst);   // the caller reads them next
 }
 
 // pmx_download after a PMX_RUN_EAGER_DOWNLOAD step: the fields are (being)

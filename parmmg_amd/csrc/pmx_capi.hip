@@ -111,15 +111,6 @@ static bool nt_stores() {
   }();
   return on;
 }
-static inline void st8d(double *p, double v, bool nt) {
-  if (nt) {
-    long long bits;
-    memcpy(&bits, &v, sizeof bits);
-    __builtin_nontemporal_store(bits, (long long *)p);
-  } else {
-    *p = v;
-  }
-}
 static inline void st4(int4 *p, int a, int b, int c, int d, bool nt) {
   if (nt) {
     const pmx_v4i v = {a, b, c, d};
@@ -589,19 +580,17 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   hp[0] = hp[1] = hp[2] = 0.0;
   const char *pc = (const char *)m->point_c;
   double blo[64][3], bhi[64][3];
-  const bool ntp = nt_stores();
   const int nch = par_chunks(1, np + 1, [&](int c, int64_t i0, int64_t i1) {
     double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
     for (int64_t i = i0; i < i1; i++) {
       const double *cc = (const double *)(pc + i * m->point_stride);
       for (int a = 0; a < 3; a++) {
-        st8d(&hp[3 * i + a], cc[a], ntp);
+        hp[3 * i + a] = cc[a];
         lo[a] = std::min(lo[a], cc[a]);
         hi[a] = std::max(hi[a], cc[a]);
       }
     }
     for (int a = 0; a < 3; a++) { blo[c][a] = lo[a]; bhi[c][a] = hi[a]; }
-    if (ntp) std::atomic_thread_fence(std::memory_order_seq_cst);
   });
   double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
   for (int c = 0; c < nch; c++)
@@ -790,14 +779,13 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   // (+ the per-path upper bounds)
   double qlo[64][3], qhi[64][3];
   int64_t cvol[64], cbdy[64];
-  const bool ntp = nt_stores();
   const int C = par_chunks(0, n, [&](int ci, int64_t j0, int64_t j1) {
     double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
     int64_t nv = 0, nb = 0;
     for (int64_t j = j0; j < j1; j++) {
       const double *c = (const double *)(pc + (pv->first + j) * pv->stride);
       for (int ax = 0; ax < 3; ax++) {
-        st8d(&hx[3 * j + ax], c[ax], ntp);
+        hx[3 * j + ax] = c[ax];
         lo[ax] = std::min(lo[ax], c[ax]);
         hi[ax] = std::max(hi[ax], c[ax]);
       }
@@ -812,7 +800,6 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
     for (int ax = 0; ax < 3; ax++) { qlo[ci][ax] = lo[ax]; qhi[ci][ax] = hi[ax]; }
     cvol[ci] = tg ? nv : j1 - j0;
     cbdy[ci] = nb;
-    if (ntp) std::atomic_thread_fence(std::memory_order_seq_cst);
   });
   ctx->nq_vol_ub = ctx->nq_bdy_ub = 0;
   for (int i = 0; i < C; i++) {

@@ -335,7 +335,7 @@ def binding_cycle(m, x, t, tv, sols, local: int, iters: int = 3) -> dict:
         t1 = time.perf_counter()
         # straight into tetra[k].qual, as the binding does
         if not lib.pmx_new_mesh_qual_synced(tr.ctx, C.byref(met), N.INQUA, mrt, ptr(nt, "qual"),
-                                            MMG_TETRA.itemsize, None):
+                                            MMG_TETRA.itemsize, nt.shape[0], None):
             raise RuntimeError(lib.pmx_last_error(tr.ctx).decode())
         t2 = time.perf_counter()
         # the r03 binding's PMMG_tetraQual: the new mesh uploaded again
@@ -345,7 +345,7 @@ def binding_cycle(m, x, t, tv, sols, local: int, iters: int = 3) -> dict:
         mv.tetra_v, mv.tetra_stride = ptr(nt, "v", C.c_int), MMG_TETRA.itemsize
         if not (lib.pmx_upload_background(st.ctx, C.byref(mv), 1, C.byref(met), 0) and
                 lib.pmx_upload_point_tags(st.ctx, ptr(npnt, "tag", C.c_uint16), MMG_POINT.itemsize) and
-                lib.pmx_tetra_qual(st.ctx, mrt, q.ctypes.data_as(N.dptr))):
+                lib.pmx_tetra_qual(st.ctx, mrt, q.ctypes.data_as(N.dptr), q.shape[0])):
             raise RuntimeError(lib.pmx_last_error(st.ctx).decode())
         nt["qual"][1:] = q[1:]
         t3 = time.perf_counter()

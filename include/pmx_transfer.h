@@ -159,15 +159,24 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *opts);
 
 /* Copy results to the host.  new_sols[s].m receives size*(npts) doubles in
  * point-list order (entries of REQ points and of failed tensor inversions are
- * left untouched).  elem/status/steps may be NULL. */
-int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem,
+ * left untouched).  elem/status/steps may be NULL.  Every host output call
+ * takes the capacity its arrays were allocated for and returns 0 (nothing
+ * written, pmx_last_error says why) when the device holds more: here
+ * npts_cap rows -- size*npts_cap doubles per solution, npts_cap ints for
+ * elem/status/steps -- with npts = last - first + 1 of the points view. */
+int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int64_t npts_cap, int *elem,
                  int *status, int *steps);
 /* Per-point start element used by the device walk (debug/parity).  Volume
  * points' starts are recorded only by a pmx_run with PMX_RUN_RECORD_STARTS;
- * surface points' always. */
-int pmx_download_starts(pmx_ctx *ctx, int *start);
-/* Per-point reference-style extras for boundary points: edge/vertex (-1 unset). */
-int pmx_download_border(pmx_ctx *ctx, int *edge, int *vertex);
+ * surface points' always.  cap: ints in start (>= npts). */
+int pmx_download_starts(pmx_ctx *ctx, int *start, int64_t cap);
+/* Per-point reference-style extras for boundary points: edge/vertex (-1
+ * unset).  cap: ints in each array (>= npts). */
+int pmx_download_border(pmx_ctx *ctx, int *edge, int *vertex, int64_t cap);
+/* 1 when the context holds a step's results on its current points (a pmx_run
+ * after the last pmx_upload_points), 0 otherwise -- e.g. a group whose
+ * interpolation had nothing to locate (src/interpmesh_pmmg.c:497-512). */
+int pmx_step_ready(pmx_ctx *ctx);
 int pmx_locate_stats_get(pmx_ctx *ctx, pmx_locate_stats *st);
 /* Lane utilisation of the last step's walks (path 0 volume, 1 surface): a
  * wave iterates until its longest walk ends, so step_sum / lane_steps is the
@@ -397,9 +406,10 @@ int pmx_upload_point_tags(pmx_ctx *ctx, const uint16_t *tag, int64_t tag_stride)
 /* Quality of every background tet in the uploaded metric
  * (MMG3D_tetraQual(mesh, met, metRidTyp), src/quality_pmmg.c:726).  metRidTyp
  * 0 or 1: identical arithmetic for a size-1 metric (or none); with a size-6
- * metric 1 (Mmg's ridge metric storage, needs the xPoint normals) is refused.
- * Result stays on the device; qual (ne+1 doubles) may be NULL. */
-int pmx_tetra_qual(pmx_ctx *ctx, int metRidTyp, double *qual);
+ * metric 1 is MMG5_caltet_ani's ridge-aware mean (needs the point tags,
+ * pmx_upload_point_tags: refused without them).  Result stays on the device;
+ * qual may be NULL, else it holds qual_cap doubles (>= ne+1). */
+int pmx_tetra_qual(pmx_ctx *ctx, int metRidTyp, double *qual, int64_t qual_cap);
 
 /* PMMG_count_nodes_par (src/quality_pmmg.c:33-80) for the uploaded group:
  * the group's points in the internal node communicator (idx_ip[i] -> slot
@@ -430,13 +440,43 @@ typedef struct {
   const int      *a, *b, *owner;
   int             myrank;
   int             exact_once;
+  /* the edge's tag from the parallel-edge hash (MMG5_hGet(&hpar, a, b, &ref,
+   * &tag), :456): its MG_GEO bit is the isedg of MMG5_lenSurfEdg33_ani for a
+   * tensor metric (:463).  NULL: 0 */
+  const uint16_t *tag;
 } pmx_par_edges;
+
+/* Mmg's surface data of the uploaded group, read through strides as Mmg holds
+ * it (1-based; pass &mesh->tetra[0].xt, sizeof(MMG5_Tetra);
+ * &mesh->xtetra[0].tag[0], sizeof(MMG5_xTetra); &mesh->point[0].n[0] and
+ * &mesh->point[0].xp, sizeof(MMG5_Point); &mesh->xpoint[0].n1[0] / .n2[0],
+ * sizeof(MMG5_xPoint)).  The edge lengths in a tensor metric need it
+ * (src/quality_pmmg.c:463,528,531 -> MMG5_lenedg33_ani / MMG5_lenedg_ani:
+ * an edge tagged MG_BDY in its tet's xTetra is measured along the curved
+ * surface from the point normals / ridge tangents, MMG5_lenSurfEdg33_ani /
+ * MMG5_lenSurfEdg_ani, and with metRidTyp = 1 a ridge point's metric is rebuilt
+ * per direction from its two xPoint normals, MMG5_buildridmet).  Never
+ * uploaded after the background (or a NULL view): no tet has an xTetra and
+ * every normal is 0 -- what Mmg holds for a mesh it never analysed.  Kept
+ * until the next background upload; refused (0) if an index is out of range. */
+typedef struct {
+  int64_t         nxt, nxp;                     /* xTetra / xPoint counts   */
+  const int      *tetra_xt;    int64_t tetra_stride;
+  const uint16_t *xtetra_tag;  int64_t xtetra_stride;
+  const double   *point_n;     const int *point_xp;  int64_t point_stride;
+  const double   *xpoint_n1;   const double *xpoint_n2;  int64_t xpoint_stride;
+} pmx_surface_view;
+int pmx_upload_surface(pmx_ctx *ctx, const pmx_surface_view *sv);
 
 /* PMMG_prilen on the uploaded group: centralized (par == NULL, the
  * MMG3D_computePrilen branch) or distributed (PMMG_computePrilen).  Tets whose
  * 4 vertices are ridge points (pmx_upload_point_tags) are skipped.  metRidTyp
- * (src/quality_pmmg.c:462,527): 0 or 1 for a size-1 metric (the same
- * lengths); a size-6 metric with 1 (ridge metric storage) is refused. */
+ * (src/quality_pmmg.c:462-466,527-531): 0 or 1 for a size-1 metric (the same
+ * lengths); with a size-6 metric 0 = classic storage (MMG5_lenedg33_ani /
+ * MMG5_lenSurfEdg33_ani), 1 = Mmg's ridge storage (MMG5_lenedg_ani; the
+ * parallel edges, as the reference writes them, MMG5_lenSurfEdg_iso on the
+ * metric array read as isotropic: h = met->m[ip]), which needs the point tags
+ * (refused without).  Surface edges use pmx_upload_surface's data. */
 int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, void *dev_result);
 int pmx_prilen(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, pmx_len_stats *st);
 
@@ -446,11 +486,11 @@ int pmx_prilen(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, pmx_len_st
  * vertex indices in the last points view's numbering) are uploaded as by
  * pmx_upload_new_tets -- or tetra_v = NULL: the ones already uploaded; the
  * coordinates and the interpolated metric are the step's device-resident
- * points and results.  qual (ne+1 doubles, host) and/or dev_result (the
- * qualhisto partial of the new mesh, opt as above; np = the points) may be
- * NULL.  Needs a pmx_run on those points. */
+ * points and results.  qual (host, qual_cap doubles >= ne+1) and/or
+ * dev_result (the qualhisto partial of the new mesh, opt as above; np = the
+ * points) may be NULL.  Needs a pmx_run on those points. */
 int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, int64_t ne, int opt,
-                      int metRidTyp, double *qual, void *dev_result);
+                      int metRidTyp, double *qual, int64_t qual_cap, void *dev_result);
 
 /* PMMG_tetraQual(parmesh, metRidTyp) on the new mesh of the last step
  * (src/libparmmg1.c:845, right after PMMG_interpMetricsAndFields) in the
@@ -465,9 +505,10 @@ int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, in
  * doubles, every entry written (deleted tets 0, qual[0] = 0); any larger
  * stride: an AoS field such as &mesh->tetra[0].qual with sizeof(MMG5_Tetra),
  * written for the valid tets only (MMG3D_tetraQual skips !MG_EOK) -- straight
- * from pinned staging, no intermediate array. */
+ * from pinned staging, no intermediate array.  qual_cap: the records the
+ * array holds (entries 0 .. qual_cap-1; >= ne+1, e.g. mesh->nemax+1). */
 int pmx_new_mesh_qual_synced(pmx_ctx *ctx, const pmx_sol_view *met, int opt, int metRidTyp, double *qual,
-                             int64_t qual_stride, void *dev_result);
+                             int64_t qual_stride, int64_t qual_cap, void *dev_result);
 
 /* The reduction across groups and ranks (the reference's MPI_Reduce with its
  * custom operators, src/quality_pmmg.c:82-144, :265-307, :661-676), as host

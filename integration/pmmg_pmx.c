@@ -179,11 +179,15 @@ int PMMG_interpMetricsAndFields(PMMG_pParMesh parmesh, int *permNodGlob) {
   }
   ier = PMX_interpMetricsAndFields_groups(ctxs, ngrp, g, permNodGlob, parmesh->info.inputMet);
   if (!ier) pmx_fail(ctxs[0], __func__);
+  /* resident only where the group's context ran a step: a group with nothing
+   * to locate (no metric and no field, or -hsiz and no field, reference
+   * :497-512) keeps no new mesh on the device, and its PMMG_tetraQual takes
+   * the upload path */
   for (igrp = 0; ier && igrp < ngrp; igrp++) {
     MMG5_pMesh mesh = parmesh->listgrp[igrp].mesh;
     pmx_grp_state *st = &PMMG_pmx_state[igrp];
     st->mesh = mesh; st->point = mesh->point; st->tetra = mesh->tetra;
-    st->np = mesh->np; st->ne = mesh->ne; st->valid = 1;
+    st->np = mesh->np; st->ne = mesh->ne; st->valid = pmx_step_ready(ctxs[igrp]);
   }
   PMMG_DEL_MEM(parmesh, sv, pmx_sol_view, "pmx sols");
   PMMG_DEL_MEM(parmesh, g, pmx_group, "pmx groups");
@@ -192,18 +196,35 @@ int PMMG_interpMetricsAndFields(PMMG_pParMesh parmesh, int *permNodGlob) {
 
 /* ---- the statistics seams --------------------------------------------------- */
 
-/* a group's mesh + metric on the device for the statistics (no surface: the
- * quality and length passes read tets, points, metric, point tags) */
+/* a group's mesh + metric on the device for the statistics: tets, points,
+ * metric, point tags and -- for the lengths in a tensor metric, which Mmg
+ * measures along the curved surface (MMG5_lenedg33_ani / MMG5_lenedg_ani) --
+ * Mmg's xTetra edge tags and point / xPoint normals, read in place */
 static int upload_stats_group(pmx_ctx *ctx, MMG5_pMesh mesh, MMG5_pSol met) {
   pmx_mesh_view v;
   pmx_sol_view s;
+  pmx_surface_view sv;
   int ns = 0;
   view_mesh(mesh, &v);
   v.nt = 0; v.tria_v = NULL; v.adjt = NULL;
   v.adja = mesh->adja;                       /* Mmg's, when it has one */
   if (met && met->m) { view_sol(met, &s); ns = 1; }
   if (!pmx_upload_background(ctx, &v, ns, &s, ns ? 0 : -1)) return 0;
-  return pmx_upload_point_tags(ctx, &mesh->point[0].tag, sizeof(MMG5_Point));
+  if (!pmx_upload_point_tags(ctx, &mesh->point[0].tag, sizeof(MMG5_Point))) return 0;
+  if (!(ns && met->size == 6 && (mesh->xtetra || mesh->xpoint))) return 1;
+  memset(&sv, 0, sizeof sv);
+  if (mesh->xtetra && mesh->xt > 0) {
+    sv.nxt = mesh->xt;
+    sv.tetra_xt = &mesh->tetra[0].xt;              sv.tetra_stride = sizeof(MMG5_Tetra);
+    sv.xtetra_tag = (const uint16_t *)&mesh->xtetra[0].tag[0]; sv.xtetra_stride = sizeof(MMG5_xTetra);
+  }
+  sv.point_n = &mesh->point[0].n[0];  sv.point_xp = &mesh->point[0].xp;  sv.point_stride = sizeof(MMG5_Point);
+  if (mesh->xpoint && mesh->xp > 0) {
+    sv.nxp = mesh->xp;
+    sv.xpoint_n1 = &mesh->xpoint[0].n1[0];  sv.xpoint_n2 = &mesh->xpoint[0].n2[0];
+    sv.xpoint_stride = sizeof(MMG5_xPoint);
+  }
+  return pmx_upload_surface(ctx, &sv);
 }
 
 /* the group's new mesh of the last interpolation is still the one the
@@ -235,11 +256,12 @@ int PMMG_tetraQual(PMMG_pParMesh parmesh, int8_t metRidTyp) {
       PMMG_pmx_state[igrp].valid = 0;            /* one use per interpolation */
       if (grp->met && grp->met->m) view_sol(grp->met, &mv);
       ok = pmx_new_mesh_qual_synced(ctx, grp->met && grp->met->m ? &mv : NULL, PMX_INQUA, metRidTyp,
-                                    &mesh->tetra[0].qual, sizeof(MMG5_Tetra), NULL);
+                                    &mesh->tetra[0].qual, sizeof(MMG5_Tetra), (int64_t)mesh->ne + 1, NULL);
     } else {
       ctx = pmx(parmesh);
       PMMG_MALLOC(parmesh, q, mesh->ne + 1, double, "qual", return 0);
-      ok = ctx && upload_stats_group(ctx, mesh, grp->met) && pmx_tetra_qual(ctx, metRidTyp, q);
+      ok = ctx && upload_stats_group(ctx, mesh, grp->met) &&
+           pmx_tetra_qual(ctx, metRidTyp, q, (int64_t)mesh->ne + 1);
       if (ok)
         for (k = 1; k <= mesh->ne; k++)
           if (MG_EOK(&mesh->tetra[k])) mesh->tetra[k].qual = q[k];
@@ -368,6 +390,7 @@ int PMMG_prilen(PMMG_pParMesh parmesh, int8_t metRidTyp, int isCentral) {
   MMG5_pSol met = NULL;
   void *d_part = NULL;
   int *pa = NULL, *pb = NULL, *po = NULL, *intvalues, hl[9];
+  uint16_t *pt = NULL;
   int i, k, ier = 1, dist = 0, have = 0;
   const int reduce = !isCentral && parmesh->nprocs > 1;
   pmx_ctx *ctx;
@@ -407,16 +430,23 @@ int PMMG_prilen(PMMG_pParMesh parmesh, int8_t metRidTyp, int isCentral) {
         PMMG_MALLOC(parmesh, pa, grp->nitem_int_edge_comm, int, "par a", ier = 0);
         PMMG_MALLOC(parmesh, pb, grp->nitem_int_edge_comm, int, "par b", ier = 0);
         PMMG_MALLOC(parmesh, po, grp->nitem_int_edge_comm, int, "par owner", ier = 0);
+        PMMG_MALLOC(parmesh, pt, grp->nitem_int_edge_comm, uint16_t, "par tag", ier = 0);
       }
       if (ier) {
         for (i = 0; i < grp->nitem_int_edge_comm; i++) {
           const int ia = grp->edge2int_edge_comm_index1[i];
+          int ref;
+          int16_t tag = 0;
           pa[i] = mesh->edge[ia].a;
           pb[i] = mesh->edge[ia].b;
           po[i] = intvalues[grp->edge2int_edge_comm_index2[i]];
+          /* :456: an edge missing from the parallel-edge hash is not measured
+           * in step 1 (it stays in the edge hash for the tet loop): no owner */
+          if (!MMG5_hGet(&hpar, pa[i], pb[i], &ref, &tag)) po[i] = -1;
+          pt[i] = (uint16_t)tag;
         }
         par.n = grp->nitem_int_edge_comm;
-        par.a = pa; par.b = pb; par.owner = po;
+        par.a = pa; par.b = pb; par.owner = po; par.tag = pt;
         par.myrank = parmesh->myrank;
         par.exact_once = 0;                         /* the reference's counts (:585-586) */
       }
@@ -451,6 +481,7 @@ int PMMG_prilen(PMMG_pParMesh parmesh, int8_t metRidTyp, int isCentral) {
   if (pa) PMMG_DEL_MEM(parmesh, pa, int, "par a");
   if (pb) PMMG_DEL_MEM(parmesh, pb, int, "par b");
   if (po) PMMG_DEL_MEM(parmesh, po, int, "par owner");
+  if (pt) PMMG_DEL_MEM(parmesh, pt, uint16_t, "par tag");
   if (dist) {
     /* the reference's cleanup (:566-571) */
     if (parmesh->int_edge_comm) PMMG_DEL_MEM(parmesh, parmesh->int_edge_comm->intvalues, int, "intvalues");

@@ -30,6 +30,12 @@ class LenStats(C.Structure):
                 ("hl", i64 * 9)]
 
 
+class Surface(C.Structure):
+    """orc_surface: Mmg's surface data (xTetra edge tags, point / xPoint normals)."""
+    _fields_ = [("xt", C.c_void_p), ("xtag", C.c_void_p), ("n", C.c_void_p), ("xp", C.c_void_p),
+                ("n1", C.c_void_p), ("n2", C.c_void_p)]
+
+
 def load():
     global _lib
     if _lib is None:
@@ -57,6 +63,9 @@ def load():
         lib.orc_qualhisto_tags.argtypes = [i64, vp, vp, vp, C.POINTER(QualStats)]
         lib.orc_prilen.restype = C.c_int
         lib.orc_prilen.argtypes = [i64, i64, vp, vp, vp, C.c_int, C.POINTER(LenStats)]
+        lib.orc_prilen_full.restype = C.c_int
+        lib.orc_prilen_full.argtypes = [i64, i64, vp, vp, vp, C.c_int, vp, C.c_int, C.POINTER(Surface), i64,
+                                        vp, vp, vp, vp, C.c_int, C.c_int, C.POINTER(LenStats)]
         lib.orc_prilen_dist.restype = C.c_int
         lib.orc_prilen_dist.argtypes = [i64, i64, vp, vp, vp, C.c_int, vp, i64, vp, vp, vp, C.c_int,
                                         C.c_int, C.POINTER(LenStats)]
@@ -155,23 +164,38 @@ def qualhisto(mesh, qual, tags=None):
     return d
 
 
-def prilen(mesh, met, tags=None, par=None):
+def prilen(mesh, met, tags=None, par=None, met_rid_typ=0, surface=None):
     """PMMG_prilen: centralized (par None) or PMMG_computePrilen with parallel
-    edges par = {"a", "b", "owner", "myrank", "exact_once"}."""
+    edges par = {"a", "b", "owner", "myrank", "exact_once", "tag" (optional)}.
+    surface: Mmg's surface data {"xt" (ne+1,), "xtag" (nxt+1, 6), "n" (np+1, 3),
+    "xp" (np+1,), "n1"/"n2" (nxp+1, 3)} (None: no xTetra, zero normals)."""
     lib = load()
     st = LenStats()
     m = np.ascontiguousarray(met, np.float64)
     t = None if tags is None else np.ascontiguousarray(tags, np.uint16)
     if par is None:
-        pa = pb = po = None
+        pa = pb = po = pt = None
         npar, myrank, once = 0, 0, 0
     else:
         pa = np.ascontiguousarray(par["a"], np.int32)
         pb = np.ascontiguousarray(par["b"], np.int32)
         po = np.ascontiguousarray(par["owner"], np.int32)
+        pt = None if par.get("tag") is None else np.ascontiguousarray(par["tag"], np.uint16)
         npar, myrank, once = len(pa), int(par.get("myrank", 0)), int(par.get("exact_once", 0))
-    lib.orc_prilen_dist(mesh.np, mesh.ne, _p(mesh.xyz), _p(mesh.tet), _p(m), m.shape[1], _p(t), npar,
-                        _p(pa), _p(pb), _p(po), myrank, once, C.byref(st))
+    keep = []
+    sp = None
+    if surface is not None:
+        sf = Surface()
+        for f, dt in (("xt", np.int32), ("xtag", np.uint16), ("n", np.float64), ("xp", np.int32),
+                      ("n1", np.float64), ("n2", np.float64)):
+            a = surface.get(f)
+            if a is not None:
+                a = np.ascontiguousarray(a, dt)
+                keep.append(a)
+                setattr(sf, f, a.ctypes.data)
+        sp = C.byref(sf)
+    lib.orc_prilen_full(mesh.np, mesh.ne, _p(mesh.xyz), _p(mesh.tet), _p(m), m.shape[1], _p(t), met_rid_typ,
+                        sp, npar, _p(pa), _p(pb), _p(po), _p(pt), myrank, once, C.byref(st))
     d = {f: getattr(st, f) for f, _ in LenStats._fields_}
     d["hl"] = list(st.hl)
     return d

@@ -124,6 +124,25 @@ int orc_prilen_dist(int64_t np, int64_t ne, const double *xyz, const int *tet,
                     const int *pa, const int *pb, const int *powner, int myrank, int exact_once,
                     orc_lenstats *st);
 
+/* Mmg's surface data, as Mmg holds it (all 1-based; NULL members: absent):
+ * xt[k] = tetra[k].xt (0: no xTetra), xtag[6*x + ia] = xtetra[x].tag[ia],
+ * n[3*ip] = point[ip].n, xp[ip] = point[ip].xp, n1/n2[3*x] = xpoint[x].n1/n2 */
+typedef struct {
+  const int      *xt;
+  const uint16_t *xtag;
+  const double   *n;
+  const int      *xp;
+  const double   *n1, *n2;
+} orc_surface;
+/* PMMG_computePrilen / MMG3D_computePrilen with metRidTyp and the surface
+ * data (NULL: no xTetra, zero normals); ptag[i] = the parallel edge's tag
+ * (MMG5_hGet on the parallel-edge hash, :456; NULL: 0) */
+int orc_prilen_full(int64_t np, int64_t ne, const double *xyz, const int *tet,
+                    const double *met, int msize, const uint16_t *tag, int metRidTyp,
+                    const orc_surface *sf, int64_t npar, const int *pa, const int *pb,
+                    const int *powner, const uint16_t *ptag, int myrank, int exact_once,
+                    orc_lenstats *st);
+
 #ifdef __cplusplus
 }
 #endif

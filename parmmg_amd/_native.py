@@ -116,7 +116,18 @@ class LenPart(C.Structure):
 class ParEdges(C.Structure):
     _fields_ = [
         ("n", i64), ("a", iptr), ("b", iptr), ("owner", iptr), ("myrank", C.c_int),
-        ("exact_once", C.c_int),
+        ("exact_once", C.c_int), ("tag", u16ptr),
+    ]
+
+
+class SurfaceView(C.Structure):
+    """pmx_surface_view: Mmg's surface data through strides."""
+    _fields_ = [
+        ("nxt", i64), ("nxp", i64),
+        ("tetra_xt", iptr), ("tetra_stride", i64),
+        ("xtetra_tag", u16ptr), ("xtetra_stride", i64),
+        ("point_n", dptr), ("point_xp", iptr), ("point_stride", i64),
+        ("xpoint_n1", dptr), ("xpoint_n2", dptr), ("xpoint_stride", i64),
     ]
 
 
@@ -139,9 +150,10 @@ SIGNATURES = {
     "pmx_upload_background": (C.c_int, [C.c_void_p, C.POINTER(MeshView), C.c_int, C.POINTER(SolView), C.c_int]),
     "pmx_upload_points": (C.c_int, [C.c_void_p, C.POINTER(PointsView)]),
     "pmx_run": (C.c_int, [C.c_void_p, C.POINTER(RunOpts)]),
-    "pmx_download": (C.c_int, [C.c_void_p, C.POINTER(SolView), iptr, iptr, iptr]),
-    "pmx_download_starts": (C.c_int, [C.c_void_p, iptr]),
-    "pmx_download_border": (C.c_int, [C.c_void_p, iptr, iptr]),
+    "pmx_download": (C.c_int, [C.c_void_p, C.POINTER(SolView), i64, iptr, iptr, iptr]),
+    "pmx_download_starts": (C.c_int, [C.c_void_p, iptr, i64]),
+    "pmx_download_border": (C.c_int, [C.c_void_p, iptr, iptr, i64]),
+    "pmx_step_ready": (C.c_int, [C.c_void_p]),
     "pmx_locate_stats_get": (C.c_int, [C.c_void_p, C.POINTER(LocateStats)]),
     "pmx_locate_wave_stats": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(WaveStats)]),
     "pmx_device_buffer": (C.c_void_p, [C.c_void_p, C.c_int]),
@@ -161,16 +173,17 @@ SIGNATURES = {
     "PMX_interpMetricsAndFields_groups": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.POINTER(Group), iptr,
                                                     C.c_int]),
     "PMX_copyMetricsAndFields_point": (C.c_int, [C.c_void_p, C.POINTER(Group), u16ptr, i64, iptr, C.c_int, C.c_int]),
-    "pmx_tetra_qual": (C.c_int, [C.c_void_p, C.c_int, dptr]),
+    "pmx_tetra_qual": (C.c_int, [C.c_void_p, C.c_int, dptr, i64]),
     "pmx_upload_point_tags": (C.c_int, [C.c_void_p, u16ptr, i64]),
+    "pmx_upload_surface": (C.c_int, [C.c_void_p, C.POINTER(SurfaceView)]),
     "pmx_count_nodes": (C.c_int, [C.c_void_p, iptr, iptr, i64, iptr, i64, C.c_int, C.POINTER(i64)]),
     "pmx_qualhisto_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     "pmx_qualhisto": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(QualStats)]),
     "pmx_prilen_device": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(ParEdges), C.c_void_p]),
     "pmx_prilen": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(ParEdges), C.POINTER(LenStats)]),
-    "pmx_new_mesh_qual": (C.c_int, [C.c_void_p, iptr, i64, i64, C.c_int, C.c_int, dptr, C.c_void_p]),
+    "pmx_new_mesh_qual": (C.c_int, [C.c_void_p, iptr, i64, i64, C.c_int, C.c_int, dptr, i64, C.c_void_p]),
     "pmx_new_mesh_qual_synced": (C.c_int, [C.c_void_p, C.POINTER(SolView), C.c_int, C.c_int, dptr, i64,
-                                          C.c_void_p]),
+                                          i64, C.c_void_p]),
     "pmx_upload_new_tets": (C.c_int, [C.c_void_p, iptr, i64, i64]),
     "pmx_set_residency": (C.c_int, [C.c_void_p, C.c_int]),
     "pmx_copy_required": (C.c_int, [C.c_void_p, iptr, C.c_int]),

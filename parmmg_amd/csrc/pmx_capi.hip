@@ -526,7 +526,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   // with the device buffers)
   ctx->have_bg = ctx->ran = ctx->have_derived = ctx->have_tetv = ctx->have_qual = false;
   ctx->eager_nch = 0;
-  ctx->have_ptag = ctx->have_csr = false;
+  ctx->have_ptag = ctx->have_csr = ctx->have_surf = false;
   ctx->stat_np = -1;
   if (!m) { ctx->err = "pmx_upload_background: null mesh"; return 0; }
   hipSetDevice(ctx->device);
@@ -823,6 +823,7 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   // (pack_new_tets): their DMA overlaps the step and the download
   ctx->tview = *pv;
   ctx->tets_pending = ntet > 0;
+  ctx->view_tets = ntet > 0;
   ctx->nq = n;
   if (!dgrow(ctx, ctx->d_wmask, nn)) return 0;
   if (!dgrow(ctx, ctx->d_elem, nn)) return 0;
@@ -959,7 +960,8 @@ bool pmx_ctx::fix_orphans() {
   orph_fixed = true;
   if (!ran || !orph_marks || nq == 0) return true;
   if (tets_inflight) CK(hipStreamWaitEvent(stream, ev_tets, 0));   // the marks are written on `up`
-  launch_orphans(d_qmark.p, nq, (uint8_t)last_const_bit, d_wmask.p, d_elem.p, d_status.p, d_steps.p, stream);
+  OrphanRows r{d_wmask.p, d_elem.p, d_status.p, d_steps.p, d_start.p, d_edge.p, d_vertex.p, d_kind.p};
+  launch_orphans(d_qmark.p, nq, (uint8_t)last_const_bit, r, stream);
   CK(hipGetLastError());
   return true;
 }
@@ -1274,9 +1276,21 @@ static int download_eager(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem,
   return 1;
 }
 
-int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem, int *status, int *steps) {
+// the caller's host arrays must hold the points of the step (npts rows):
+// refused before anything is written (r04: an output sized by a wrong count
+// was written past on the host)
+static bool check_cap(pmx_ctx *ctx, const char *who, int64_t cap, int64_t need) {
+  if (cap >= need) return true;
+  ctx->err = std::string(who) + ": output capacity " + std::to_string(cap) + " < " + std::to_string(need) +
+             " entries needed";
+  return false;
+}
+
+int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int64_t npts_cap, int *elem, int *status,
+                 int *steps) {
   if (!ctx) return 0;
   if (!results_ready(ctx, "pmx_download")) return 0;
+  if (!check_cap(ctx, "pmx_download", npts_cap, ctx->nq)) return 0;
   hipSetDevice(ctx->device);
   if (!ctx->fix_orphans()) return 0;
   const int64_t n = ctx->nq;
@@ -1320,9 +1334,12 @@ int pmx_download(pmx_ctx *ctx, const pmx_sol_view *new_sols, int *elem, int *sta
   return 1;
 }
 
-int pmx_download_starts(pmx_ctx *ctx, int *start) {
+int pmx_download_starts(pmx_ctx *ctx, int *start, int64_t cap) {
   if (!ctx || !start) return 0;
   if (!results_ready(ctx, "pmx_download_starts")) return 0;
+  if (!check_cap(ctx, "pmx_download_starts", cap, ctx->nq)) return 0;
+  hipSetDevice(ctx->device);
+  if (!ctx->fix_orphans()) return 0;
   CK(hipStreamSynchronize(ctx->stream));
   if (!ctx->check_device_errors()) return 0;
   if (ctx->nq == 0) return 1;
@@ -1330,9 +1347,12 @@ int pmx_download_starts(pmx_ctx *ctx, int *start) {
   return 1;
 }
 
-int pmx_download_border(pmx_ctx *ctx, int *edge, int *vertex) {
+int pmx_download_border(pmx_ctx *ctx, int *edge, int *vertex, int64_t cap) {
   if (!ctx) return 0;
   if (!results_ready(ctx, "pmx_download_border")) return 0;
+  if (!check_cap(ctx, "pmx_download_border", cap, ctx->nq)) return 0;
+  hipSetDevice(ctx->device);
+  if (!ctx->fix_orphans()) return 0;
   CK(hipStreamSynchronize(ctx->stream));
   if (!ctx->check_device_errors()) return 0;
   if (ctx->nq == 0) return 1;
@@ -1344,45 +1364,42 @@ int pmx_download_border(pmx_ctx *ctx, int *edge, int *vertex) {
 int pmx_locate_stats_get(pmx_ctx *ctx, pmx_locate_stats *st) {
   if (!ctx || !st) return 0;
   if (!results_ready(ctx, "pmx_locate_stats_get")) return 0;
+  hipSetDevice(ctx->device);
   if (!ctx->fix_orphans()) return 0;
-  unsigned cnt[8];
-  int nsel[2] = {0, 0};
   CK(hipStreamSynchronize(ctx->stream));
   if (!ctx->check_device_errors()) return 0;
-  CK(hipMemcpy(cnt, ctx->d_counts.p, sizeof cnt, hipMemcpyDeviceToHost));
-  if (ctx->nq) CK(hipMemcpy(nsel, ctx->d_nsel.p, sizeof nsel, hipMemcpyDeviceToHost));
+  // per point, over the points the reference visits (kind VOL / BDY; orphans
+  // are KIND_ORPH once fix_orphans has run, NUL / frozen points never
+  // located): steps > 0 located by a walk, steps < 0 by an exhaustive scan
+  // (the reference's ppt->s sign, src/locate_pmmg.c:840-844), status 0 the
+  // closest element (not contained anywhere)
+  const int64_t n = ctx->nq;
+  std::vector<int> status((size_t)std::max<int64_t>(n, 1)), steps((size_t)std::max<int64_t>(n, 1));
+  std::vector<int8_t> kind((size_t)std::max<int64_t>(n, 1));
+  if (n) {
+    CK(hipMemcpy(status.data(), ctx->d_status.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(steps.data(), ctx->d_steps.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(kind.data(), ctx->d_kind.p, (size_t)n, hipMemcpyDeviceToHost));
+  }
   memset(st, 0, sizeof *st);
-  st->nvol = nsel[0];
-  st->nbdy = nsel[1];
-  st->nexhaust = cnt[0] + cnt[1];
-  // reduce the per-wave records of both walks
-  unsigned long long located = 0, sum = 0;
-  unsigned mx = 0, mn = 0xffffffffu;
-  for (int path = 0; path < 2; path++) {
-    int64_t npath = path ? nsel[1] : nsel[0];
-    if (!npath) continue;
-    std::vector<uint4> w((size_t)((npath + 255) / 256 * 4));
-    CK(hipMemcpy(w.data(), path ? ctx->d_bstat.p : ctx->d_vstat.p, w.size() * sizeof(uint4),
-                 hipMemcpyDeviceToHost));
-    for (const uint4 &r : w) {
-      located += r.x;
-      sum += r.y;
-      mx = std::max(mx, r.z);
-      if (r.x) mn = std::min(mn, r.w);
+  int64_t located = 0, sum = 0, mx = 0, mn = INT64_MAX;
+  for (int64_t i = 0; i < n; i++) {
+    const int8_t k = kind[(size_t)i];
+    if (k != KIND_VOL && k != KIND_BDY) continue;
+    (k == KIND_VOL ? st->nvol : st->nbdy)++;
+    const int s = steps[(size_t)i];
+    if (s < 0) st->nexhaust++;
+    if (status[(size_t)i] == 0) st->nclosest++;
+    if (s > 0) {
+      located++;
+      sum += s;
+      mx = std::max<int64_t>(mx, s);
+      mn = std::min<int64_t>(mn, s);
     }
   }
   st->stepmax = mx;
-  st->stepmin = located ? (int64_t)mn : 0;
+  st->stepmin = located ? mn : 0;
   st->stepav = located ? (double)sum / (double)located : 0.0;
-  // points resolved by the exhaustive scans and still not contained anywhere
-  std::vector<int> status((size_t)std::max<int64_t>(ctx->nq, 1));
-  if (ctx->nq) CK(hipMemcpy(status.data(), ctx->d_status.p, (size_t)ctx->nq * sizeof(int), hipMemcpyDeviceToHost));
-  std::vector<int8_t> kind((size_t)std::max<int64_t>(ctx->nq, 1));
-  if (ctx->nq) CK(hipMemcpy(kind.data(), ctx->d_kind.p, (size_t)ctx->nq, hipMemcpyDeviceToHost));
-  int64_t nc = 0;
-  for (int64_t i = 0; i < ctx->nq; i++)
-    if ((kind[(size_t)i] == KIND_VOL || kind[(size_t)i] == KIND_BDY) && status[(size_t)i] == 0) nc++;
-  st->nclosest = nc;
   return 1;
 }
 
@@ -1414,8 +1431,18 @@ int pmx_locate_wave_stats(pmx_ctx *ctx, int path, pmx_wave_stats *st) {
   return 1;
 }
 
+int pmx_step_ready(pmx_ctx *ctx) {
+  return ctx && ctx->ran && ctx->have_pts && ctx->have_bg && ctx->out_n == ctx->nq && ctx->out_S == ctx->sd.S;
+}
+
 void *pmx_device_buffer(pmx_ctx *ctx, int which) {
   if (!ctx) return nullptr;
+  // the orphan rows reset before a caller chains on the results (enqueued on
+  // the context stream, which the caller orders its own work after)
+  if (ctx->ran && (which == 0 || which == 1 || which == 2)) {
+    hipSetDevice(ctx->device);
+    if (!ctx->fix_orphans()) return nullptr;
+  }
   switch (which) {
     case 0: return ctx->d_out.p;
     case 1: return ctx->d_elem.p;
@@ -1560,6 +1587,17 @@ int pmx_upload_new_tets(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, 
   if (bad) { ctx->err = "pmx_upload_new_tets: tet vertex outside the uploaded points"; return 0; }
   if (!dgrow(ctx, ctx->d_ntetv, (size_t)(ne + 1))) return 0;
   CK(hipMemcpyAsync(ctx->d_ntetv.p, h, (size_t)(ne + 1) * sizeof(int4), hipMemcpyHostToDevice, ctx->stream));
+  if (ctx->view_tets && n > 0) {
+    // these tets replace the points view's: the reference visits the points
+    // of THEIR valid tets (src/interpmesh_pmmg.c:535-541), so the orphan
+    // marks come from them (a step already run has its orphan rows reset
+    // from these marks by the next consumer of its results)
+    CK(hipMemsetAsync(ctx->d_qmark.p, 0, (size_t)n, ctx->stream));
+    launch_mark_new_tets(ctx->d_ntetv.p, ne, ctx->d_qmark.p, ctx->stream);
+    CK(hipGetLastError());
+    ctx->orph_marks = true;
+    if (ctx->ran) ctx->orph_fixed = false;
+  }
   CK(hipStreamSynchronize(ctx->stream));
   ctx->n_ntet = ne;
   ctx->have_ntet = true;
@@ -1663,7 +1701,7 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
   if (!stage_trias(ctx, m, n, htr)) return 0;
   tr.mark("trias");
   // the background invalid until this completes
-  ctx->have_bg = ctx->have_derived = ctx->have_tetv = ctx->have_qual = ctx->have_ptag = ctx->have_csr = false;
+  ctx->have_bg = ctx->have_derived = ctx->have_tetv = ctx->have_qual = ctx->have_ptag = ctx->have_csr = ctx->have_surf = false;
   ctx->stat_np = -1;
   const int64_t ns = (ne + PMX_HINT_STRIDE - 1) / PMX_HINT_STRIDE;
   if (!dgrow(ctx, ctx->d_xyz, (size_t)(n + 1) * 3) || !dgrow(ctx, ctx->d_sol, (size_t)(n + 1) * std::max(S, 1)) ||
@@ -1773,6 +1811,8 @@ void pmx_ctx::free_all() {
   d_tgrid = nullptr;
   d_tgrid_cap = 0;
   have_bg = have_pts = ran = have_derived = have_tetv = have_qual = have_ptag = have_qtag = have_csr = false;
+  have_surf = false;
+  dfree(d_etag); dfree(d_pn); dfree(d_xpn); dfree(d_pxp); dfree(d_pedge_tag);
   have_ntet = false;
   stat_np = -1;
 }

@@ -60,13 +60,14 @@ static int interp_groups(pmx_ctx *ectx, pmx_ctx *const *ctxs, int ngrp, pmx_grou
   struct Pending {
     bool on = false;
     int ns = 0;
+    int64_t cap = 0;                       // rows the caller's arrays hold from `first` on
     pmx_sol_view news[PMX_MAX_SOLS];
   };
   std::vector<Pending> pend((size_t)std::max(ngrp, 1));
   auto finish = [&](int g) {
     if (!pend[g].on) return;
     pend[g].on = false;
-    if (!pmx_download(ctxs[g], pend[g].news, nullptr, nullptr, nullptr)) fail(ctxs[g]);
+    if (!pmx_download(ctxs[g], pend[g].news, pend[g].cap, nullptr, nullptr, nullptr)) fail(ctxs[g]);
   };
   for (int g = 0; g < ngrp; g++) {
     pmx_ctx *X = ctxs[g];
@@ -121,6 +122,9 @@ static int interp_groups(pmx_ctx *ectx, pmx_ctx *const *ctxs, int ngrp, pmx_grou
     for (int k = 0; k < ns; k++)
       if (P.news[k].m) P.news[k].m += (int64_t)P.news[k].size * G.points.first;
     P.ns = ns;
+    // Mmg's arrays hold entries 0..np of the new mesh (its view's np when
+    // given, else the points view's last)
+    P.cap = (G.mesh.np > 0 ? G.mesh.np : G.points.last) + 1 - G.points.first;
     P.on = true;
   }
   for (int g = 0; g < ngrp; g++) finish(g);

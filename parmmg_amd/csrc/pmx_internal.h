@@ -108,6 +108,14 @@ struct pmx_ctx {
   bool have_qual = false;
   bool have_ptag = false;               // background point tags (pmx_upload_point_tags)
   DevBuf<uint16_t> d_ptag;
+  // Mmg's surface data of the background (pmx_upload_surface): per tet the
+  // xTetra edge tags packed 2 bits per edge (BDY, GEO); per point MMG5_Point.n
+  // and its xPoint index; per xPoint n1, n2
+  bool have_surf = false;
+  DevBuf<uint16_t> d_etag;
+  DevBuf<double> d_pn, d_xpn;
+  DevBuf<int> d_pxp;
+  DevBuf<uint16_t> d_pedge_tag;         // prilen: tags of the owned parallel edges
   int64_t stat_np = -1;                 // node count of pmx_count_nodes (-1: np)
   DevBuf<uint8_t> d_touch;
   DevBuf<int> d_cidx, d_intv;
@@ -151,6 +159,7 @@ struct pmx_ctx {
   char *h_tets = nullptr;               // pinned copy of the current new tets (int4, 0 = deleted);
   size_t h_tets_cap = 0;                // not the shared arena: it outlives the step (qualities' validity)
   bool tets_pending = false;            // view kept, not packed yet
+  bool view_tets = false;               // the points view carried new tets (orphans exist by definition)
   bool tets_inflight = false;           // DMA issued on `up`, ev_tets recorded
   pmx_points_view tview{};
   bool orph_marks = false;              // d_qmark holds the device's marks of the packed new tets

@@ -101,8 +101,12 @@ void launch_promote(const double *qxyz, const double *out, const uint16_t *qtag,
                     double *sol, uint16_t *ptag, hipStream_t s);
 // points in no valid new tet (mk == 0) after a step: rows back to untouched
 void launch_mark_new_tets(const int4 *tv, int64_t ne, uint8_t *mk, hipStream_t s);
-void launch_orphans(const uint8_t *mk, int64_t n, uint8_t keep, uint8_t *wmask, int *elem, int *status, int *steps,
-                    hipStream_t s);
+struct OrphanRows {
+  uint8_t *wmask;
+  int *elem, *status, *steps, *start, *edge, *vertex;
+  int8_t *kind;
+};
+void launch_orphans(const uint8_t *mk, int64_t n, uint8_t keep, const OrphanRows &r, hipStream_t s);
 void launch_patch_rows(const int4 *ent, const double *vals, int64_t n, int S, double *sol, hipStream_t s);
 // new points, every step (the tag dispatch of the reference's vertex loop,
 // src/interpmesh_pmmg.c:541-560): kinds (mark != NULL: the host's orphan
@@ -138,6 +142,13 @@ struct StatArgs {
   // (null: every vertex counts)
   const uint16_t *rtag;
   int ridmet;
+  // edge lengths in a tensor metric along the curved surface (pmx_upload_surface;
+  // null: no xTetra, zero normals): per tet the xTetra edge tags (bit 2 ia
+  // MG_BDY, 2 ia + 1 MG_GEO), per point MMG5_Point.n and its xPoint index,
+  // per xPoint n1 | n2 (6 doubles, entry 0 zero)
+  const uint16_t *etag;
+  const double *pn, *xpn;
+  const int *pxp;
   // distributed prilen: sorted (min << 32 | max) keys of the parallel edges
   // the tet loop must skip, and a per-point prefilter
   const unsigned long long *par_key;

@@ -472,23 +472,29 @@ void launch_prologue(const ZeroRanges &z, hipStream_t s) {
 }
 
 // the rows of points in no valid new tet, after a step that located them:
-// back to untouched (the constant-size bit kept), element / status / steps 0
+// back to untouched (the constant-size bit kept), element / status / steps /
+// start 0, edge / vertex unset (-1), and their kind KIND_ORPH, so that the
+// locate statistics count only the points the reference visits (a NUL or
+// frozen point keeps its kind: the step never located it)
 __global__ __launch_bounds__(256) void k_orphans(const uint8_t *__restrict__ mk, int64_t n, uint8_t keep,
-                                                 uint8_t *__restrict__ wmask, int *__restrict__ elem,
-                                                 int *__restrict__ status, int *__restrict__ steps) {
+                                                 OrphanRows r) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
     if (mk[j]) continue;
-    wmask[j] &= keep;
-    elem[j] = 0;
-    status[j] = 0;
-    steps[j] = 0;
+    r.wmask[j] &= keep;
+    r.elem[j] = 0;
+    r.status[j] = 0;
+    r.steps[j] = 0;
+    r.start[j] = 0;
+    r.edge[j] = -1;
+    r.vertex[j] = -1;
+    const int8_t k = r.kind[j];
+    if (k == KIND_VOL || k == KIND_BDY) r.kind[j] = KIND_ORPH;
   }
 }
-void launch_orphans(const uint8_t *mk, int64_t n, uint8_t keep, uint8_t *wmask, int *elem, int *status, int *steps,
-                    hipStream_t s) {
+void launch_orphans(const uint8_t *mk, int64_t n, uint8_t keep, const OrphanRows &r, hipStream_t s) {
   if (n < 1) return;
   const int64_t nb = std::min<int64_t>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_orphans, dim3((unsigned)nb), dim3(256), 0, s, mk, n, keep, wmask, elem, status, steps);
+  hipLaunchKernelGGL(k_orphans, dim3((unsigned)nb), dim3(256), 0, s, mk, n, keep, r);
 }
 
 // the orphan marks from the new tets on the device: point j (0-based) is

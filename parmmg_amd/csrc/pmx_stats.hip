@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <unordered_set>
@@ -43,6 +44,7 @@
 #define TAG_REQ 4
 #define TAG_NOM 8
 #define TAG_CRN 32
+#define TAG_REF 1
 #define LEN_STEP2 (1LL << 40)      // keys of tet edges: LEN_STEP2 + 6*k + ia
 
 __constant__ int IARE[6][2] = {{0, 1}, {0, 2}, {0, 3}, {1, 2}, {1, 3}, {2, 3}};
@@ -381,6 +383,177 @@ __device__ double edge_len(const StatArgs &A, int p1, int p2) {
   return A.msize == 6 ? edge_len_t<true>(A, p1, p2) : edge_len_t<false>(A, p1, p2);
 }
 
+// ---- Mmg's surface-aware lengths in a tensor metric (restated from the public
+// Mmg sources, unpinned; the oracle's orc_prilen_full, oracle/pmx_oracle_stats.c,
+// is the same restatement in C).  The background's arrays: vbase 0, xstride 3.
+
+// MG_SIN(tag) || (tag & MG_NOM): the stored metric is a plain tensor
+__device__ __forceinline__ bool sin_or_nom(unsigned tg) { return (tg & (TAG_CRN | TAG_REQ | TAG_NOM)) != 0; }
+__device__ __forceinline__ unsigned ptag_or0(const StatArgs &A, int ip) { return A.ptag ? A.ptag[ip] : 0u; }
+// MMG5_Point.n (a ridge point's tangent, in mmg3d); zeros without surface data
+__device__ __forceinline__ D3 pn_of(const StatArgs &A, int ip) {
+  if (!A.pn) return D3{0.0, 0.0, 0.0};
+  const double *r = A.pn + 3 * (int64_t)ip;
+  return D3{r[0], r[1], r[2]};
+}
+// mesh->xpoint[p->xp].n1 / .n2 (entry 0: zeros)
+__device__ __forceinline__ D3 xn_of(const StatArgs &A, int ip, int which) {
+  if (!A.pxp) return D3{0.0, 0.0, 0.0};
+  const double *r = A.xpn + 6 * (int64_t)A.pxp[ip] + 3 * which;
+  return D3{r[0], r[1], r[2]};
+}
+
+// MMG5_buildridmet: ridge point np0's metric in the direction u, from its
+// ridge storage m = (tangent size, in-surface sizes of sides 1 / 2, normal
+// sizes of sides 1 / 2): the side whose normal is the more orthogonal to u,
+// basis (t, n x t, n), mr = R diag(m0, dv, dn) R^T
+__device__ void buildridmet(const StatArgs &A, int np0, double ux, double uy, double uz, double mr[6]) {
+  const double *m = smet(A, np0);
+  const D3 t = pn_of(A, np0);
+  D3 n1 = xn_of(A, np0, 0);
+  const D3 n2 = xn_of(A, np0, 1);
+  const double ps1 = ux * n1.x + uy * n1.y + uz * n1.z;
+  const double ps2 = ux * n2.x + uy * n2.y + uz * n2.z;
+  double dv, dn;
+  if (fabs(ps2) < fabs(ps1)) {
+    n1 = n2;
+    dv = m[2];
+    dn = m[4];
+  } else {
+    dv = m[1];
+    dn = m[3];
+  }
+  double r[3][3];
+  r[0][0] = t.x; r[1][0] = t.y; r[2][0] = t.z;
+  r[0][1] = n1.y * t.z - n1.z * t.y;
+  r[1][1] = n1.z * t.x - n1.x * t.z;
+  r[2][1] = n1.x * t.y - n1.y * t.x;
+  r[0][2] = n1.x; r[1][2] = n1.y; r[2][2] = n1.z;
+  mr[0] = m[0] * r[0][0] * r[0][0] + dv * r[0][1] * r[0][1] + dn * r[0][2] * r[0][2];
+  mr[1] = m[0] * r[0][0] * r[1][0] + dv * r[0][1] * r[1][1] + dn * r[0][2] * r[1][2];
+  mr[2] = m[0] * r[0][0] * r[2][0] + dv * r[0][1] * r[2][1] + dn * r[0][2] * r[2][2];
+  mr[3] = m[0] * r[1][0] * r[1][0] + dv * r[1][1] * r[1][1] + dn * r[1][2] * r[1][2];
+  mr[4] = m[0] * r[1][0] * r[2][0] + dv * r[1][1] * r[2][1] + dn * r[1][2] * r[2][2];
+  mr[5] = m[0] * r[2][0] * r[2][0] + dv * r[2][1] * r[2][1] + dn * r[2][2] * r[2][2];
+}
+
+// the tangent at ip of the curve under the edge [ip, ip + u] (MMG5_lenEdg's
+// gammaprim): u at a singular / non-manifold point; along the point's tangent
+// on a ridge edge (isedg); else u projected on the tangent plane of the side
+// nearest to it (ridge point), of its xPoint normal (MG_REF), of its normal
+__device__ D3 gammaprim(const StatArgs &A, int ip, double ux, double uy, double uz, bool isedg) {
+  const unsigned tg = ptag_or0(A, ip);
+  if (sin_or_nom(tg)) return D3{ux, uy, uz};
+  if (isedg) {
+    const D3 t = pn_of(A, ip);
+    const double ps1 = ux * t.x + uy * t.y + uz * t.z;
+    return D3{ps1 * t.x, ps1 * t.y, ps1 * t.z};
+  }
+  D3 n1;
+  double ps1;
+  if (TAG_GEO & tg) {
+    n1 = xn_of(A, ip, 0);
+    const D3 n2 = xn_of(A, ip, 1);
+    ps1 = ux * n1.x + uy * n1.y + uz * n1.z;
+    const double ps2 = ux * n2.x + uy * n2.y + uz * n2.z;
+    if (fabs(ps2) < fabs(ps1)) {
+      n1 = n2;
+      ps1 = ps2;
+    }
+  } else if (TAG_REF & tg) {
+    n1 = xn_of(A, ip, 0);
+    ps1 = ux * n1.x + uy * n1.y + uz * n1.z;
+  } else {
+    n1 = pn_of(A, ip);
+    ps1 = ux * n1.x + uy * n1.y + uz * n1.z;
+  }
+  return D3{ux - ps1 * n1.x, uy - ps1 * n1.y, uz - ps1 * n1.z};
+}
+
+__device__ __forceinline__ double qform(const double *m, D3 g) {
+  return m[0] * g.x * g.x + m[3] * g.y * g.y + m[5] * g.z * g.z + 2.0 * m[1] * g.x * g.y + 2.0 * m[2] * g.x * g.z +
+         2.0 * m[4] * g.y * g.z;
+}
+
+// MMG5_lenSurfEdg33_ani (ridmet 0, classic storage) / MMG5_lenSurfEdg_ani
+// (ridmet 1: a non-singular ridge endpoint's metric rebuilt per direction),
+// both through MMG5_lenEdg: the mean of the end tangents' lengths, a negative
+// quadratic form counting as 1
+__device__ double len_surf_ani(const StatArgs &A, int np0, int np1, bool isedg, bool ridmet) {
+  const D3 c0 = sld3(A, np0), c1 = sld3(A, np1);
+  const double ux = c1.x - c0.x, uy = c1.y - c0.y, uz = c1.z - c0.z;
+  double m0[6], m1[6];
+  const double *s0 = smet(A, np0), *s1 = smet(A, np1);
+#pragma unroll
+  for (int i = 0; i < 6; i++) { m0[i] = s0[i]; m1[i] = s1[i]; }
+  if (ridmet) {
+    const unsigned t0 = ptag_or0(A, np0), t1 = ptag_or0(A, np1);
+    if (!sin_or_nom(t0) && (TAG_GEO & t0)) buildridmet(A, np0, ux, uy, uz, m0);
+    if (!sin_or_nom(t1) && (TAG_GEO & t1)) buildridmet(A, np1, ux, uy, uz, m1);
+  }
+  const D3 g0 = gammaprim(A, np0, ux, uy, uz, isedg);
+  const D3 g1 = gammaprim(A, np1, -ux, -uy, -uz, isedg);
+  double l0 = qform(m0, g0), l1 = qform(m1, g1);
+  if (l0 < 0.) l0 = 1.;
+  if (l1 < 0.) l1 = 1.;
+  return 0.5 * (sqrt(l0) + sqrt(l1));
+}
+
+// MMG5_moymet: the mean metric of tet v over its vertices that are not
+// non-singular ridge points (false if none)
+__device__ bool moymet(const StatArgs &A, const int *v, double mm[6]) {
+  int n = 0;
+#pragma unroll
+  for (int i = 0; i < 6; i++) mm[i] = 0.0;
+  for (int j = 0; j < 4; j++) {
+    if (ridge_pt(ptag_or0(A, v[j]))) continue;
+    n++;
+    const double *m = smet(A, v[j]);
+#pragma unroll
+    for (int i = 0; i < 6; i++) mm[i] += m[i];
+  }
+  if (!n) return false;
+  const double dd = 1. / n;
+#pragma unroll
+  for (int i = 0; i < 6; i++) mm[i] = mm[i] * dd;
+  return true;
+}
+
+// MMG5_lenedg_ani (ridmet) / MMG5_lenedg33_ani of local edge ia = (ip1, ip2)
+// of tet v (its packed xTetra edge tags et): a boundary edge of the xTetra along the
+// surface, any other straight (MMG5_lenedgCoor_ani), a non-singular ridge
+// endpoint then taking the tet's mean metric (MMG5_lenedgspl_ani)
+__device__ double len_tet_ani(const StatArgs &A, const int *v, int ia, int ip1, int ip2, unsigned et) {
+  if ((et >> (2 * ia)) & 1u) return len_surf_ani(A, ip1, ip2, ((et >> (2 * ia + 1)) & 1u) != 0, A.ridmet != 0);
+  double m1[6], m2[6];
+  const double *s1 = smet(A, ip1), *s2 = smet(A, ip2);
+#pragma unroll
+  for (int i = 0; i < 6; i++) { m1[i] = s1[i]; m2[i] = s2[i]; }
+  if (A.ridmet) {
+    if (ridge_pt(ptag_or0(A, ip1)) && !moymet(A, v, m1)) return 0.0;
+    if (ridge_pt(ptag_or0(A, ip2)) && !moymet(A, v, m2)) return 0.0;
+  }
+  const D3 c1 = sld3(A, ip1), c2 = sld3(A, ip2);
+  const double ux = c2.x - c1.x, uy = c2.y - c1.y, uz = c2.z - c1.z;
+  double dd1 = mlen2(m1, ux, uy, uz), dd2 = mlen2(m2, ux, uy, uz);
+  if (dd1 <= 0.0) dd1 = 0.0;
+  if (dd2 <= 0.0) dd2 = 0.0;
+  return (sqrt(dd1) + sqrt(dd2) + 4.0 * sqrt(0.5 * (dd1 + dd2))) / 6.0;
+}
+
+// MMG5_lenSurfEdg_iso on a size-6 metric as the reference calls it for the
+// parallel edges with metRidTyp = 1 (src/quality_pmmg.c:466): h = met->m[ip],
+// the Mmg array (6 per point) read flat, i.e. component ip % 6 of point ip / 6
+__device__ double len_iso_flat(const StatArgs &A, int p1, int p2) {
+  const D3 c1 = sld3(A, p1), c2 = sld3(A, p2);
+  const double h1 = A.sol[(int64_t)(p1 / 6) * A.S + A.moff + p1 % 6];
+  const double h2 = A.sol[(int64_t)(p2 / 6) * A.S + A.moff + p2 % 6];
+  double l = (c2.x - c1.x) * (c2.x - c1.x) + (c2.y - c1.y) * (c2.y - c1.y) + (c2.z - c1.z) * (c2.z - c1.z);
+  l = sqrt(l);
+  const double r = h2 / h1 - 1.0;
+  return (fabs(r) < PMX_EPS) ? (l / h1) : (l / (h2 - h1) * log1p(r));
+}
+
 __device__ __forceinline__ void len_merge(LenPart &x, const LenPart &y) {
   x.avlen += y.avlen;
   if (y.lmin < x.lmin || (y.lmin == x.lmin && y.kmin < x.kmin)) { x.lmin = y.lmin; x.kmin = y.kmin; }
@@ -615,7 +788,9 @@ __device__ __forceinline__ bool owns_edge(const StatArgs &A, const TetRec (*srec
 // 125M tets; a fused version with one round trip per dependent load and
 // partial rounds after every batch: 7.2 ms.)
 #define LEN_QCAP 2048                 // > 255 left over + 6 * 256 queued
-template <bool ANI, bool TAGS, bool PAR, int W = 1, bool L = false>
+// SURF (tensor metrics with surface data or ridge storage): every length by
+// len_tet_ani from the owner tet's xTetra edge tags and vertices.
+template <bool ANI, bool TAGS, bool PAR, int W = 1, bool L = false, bool SURF = false>
 __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
   __shared__ TetRec srec[2][256];
   __shared__ unsigned short q[LEN_QCAP];
@@ -743,7 +918,12 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
         TetRec r0{}, r1{};
         if (c0) r0 = shell_rec<L>(A, srec, kb0, kb1, c0);
         if (c1) r1 = shell_rec<L>(A, srec, kb0, kb1, c1);
-        len = edge_len_t<ANI>(A, a, b);
+        if constexpr (SURF) {
+          const int vv[4] = {sv[0], sv[1], sv[2], sv[3]};
+          len = len_tet_ani(A, vv, ia, a, b, A.etag ? (unsigned)A.etag[kk] : 0u);
+        } else {
+          len = edge_len_t<ANI>(A, a, b);
+        }
         on = owns_edge<TAGS, L>(A, srec, kb0, kb1, kk, a, b, c0, c1, keep0, keep1, r0, r1) &&
              !(PAR && par_excluded(A, a, b));
         if constexpr (L) key = LEN_STEP2 + (long long)(6u * (unsigned)kk + (unsigned)ia);   // 6 ne < 2^32
@@ -767,9 +947,12 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
 }
 
 // step 1 of the distributed prilen: the owned parallel edges, in list order,
-// each once (src/quality_pmmg.c:445-502); one workgroup
-__global__ __launch_bounds__(256) void k_prilen_par(StatArgs A, const int2 *edges, int64_t n,
-                                                    LenPart *part) {
+// each once (src/quality_pmmg.c:445-502); one workgroup.  The kernel the
+// reference selects at :462-466: MMG5_lenSurfEdg33_ani for a tensor metric in
+// classic storage (isedg from the edge's hash tag), else MMG5_lenSurfEdg_iso
+// -- for a tensor metric with metRidTyp = 1 on the flat array, as written
+__global__ __launch_bounds__(256) void k_prilen_par(StatArgs A, const int2 *edges, const uint16_t *etags,
+                                                    int64_t n, LenPart *part) {
   __shared__ unsigned lcnt[10];
   LenAcc acc(lcnt);
   for (int64_t base = 0; base < n; base += blockDim.x) {
@@ -778,7 +961,9 @@ __global__ __launch_bounds__(256) void k_prilen_par(StatArgs A, const int2 *edge
     double len = 0.0;
     if (on) {
       const int2 e = edges[i];
-      len = edge_len(A, e.x, e.y);
+      if (A.msize != 6) len = edge_len(A, e.x, e.y);
+      else if (A.ridmet) len = len_iso_flat(A, e.x, e.y);
+      else len = len_surf_ani(A, e.x, e.y, etags && (etags[i] & TAG_GEO), false);
     }
     acc.add(on, len, i);
   }
@@ -959,41 +1144,111 @@ int pmx_upload_point_tags(pmx_ctx *ctx, const uint16_t *tag, int64_t stride) {
   return 1;
 }
 
+// Mmg's surface data of the background: packed on the host (the xTetra edge
+// tags to 2 bits per edge of each tet, the normals and xPoint indices as
+// arrays), checked, uploaded.  Replaces the previous upload's.
+int pmx_upload_surface(pmx_ctx *ctx, const pmx_surface_view *sv) {
+  if (!ctx) return 0;
+  ctx->have_surf = false;
+  if (!ctx->have_bg) { ctx->err = "pmx_upload_surface: upload a background first"; return 0; }
+  if (!sv) return 1;                        // no surface data: no xTetra, zero normals
+  const char *who = "pmx_upload_surface";
+  const int64_t np = ctx->np, ne = ctx->ne, nxt = sv->nxt, nxp = sv->nxp;
+  if (nxt < 0 || nxp < 0 || (nxt > 0 && (!sv->tetra_xt || !sv->xtetra_tag || sv->tetra_stride < 4 ||
+                                        sv->xtetra_stride < 12)) ||
+      (!sv->point_n != !sv->point_xp) || (sv->point_n && sv->point_stride < 24) ||
+      (nxp > 0 && (!sv->xpoint_n1 || !sv->xpoint_n2 || sv->xpoint_stride < 48))) {
+    ctx->err = std::string(who) + ": bad view";
+    return 0;
+  }
+  hipSetDevice(ctx->device);
+  std::vector<uint16_t> et((size_t)(ne + 1), 0);
+  std::vector<double> pn((size_t)(np + 1) * 3, 0.0), xpn((size_t)(nxp + 1) * 6, 0.0);
+  std::vector<int> pxp((size_t)(np + 1), 0);
+  std::atomic<bool> bad{false};
+  if (nxt > 0)
+    pmx_par_for(1, ne + 1, [&](int64_t k0, int64_t k1) {
+      for (int64_t k = k0; k < k1; k++) {
+        const int xt = *(const int *)((const char *)sv->tetra_xt + k * sv->tetra_stride);
+        if (xt == 0) continue;
+        if (xt < 0 || xt > nxt) { bad = true; continue; }
+        const uint16_t *tg = (const uint16_t *)((const char *)sv->xtetra_tag + (int64_t)xt * sv->xtetra_stride);
+        unsigned b = 0;
+        for (int ia = 0; ia < 6; ia++)
+          b |= ((tg[ia] & PMX_TAG_BDY) ? 1u : 0u) << (2 * ia) | ((tg[ia] & PMX_TAG_GEO) ? 1u : 0u) << (2 * ia + 1);
+        et[(size_t)k] = (uint16_t)b;
+      }
+    });
+  if (sv->point_n)
+    pmx_par_for(1, np + 1, [&](int64_t i0, int64_t i1) {
+      for (int64_t i = i0; i < i1; i++) {
+        const double *n = (const double *)((const char *)sv->point_n + i * sv->point_stride);
+        const int xp = *(const int *)((const char *)sv->point_xp + i * sv->point_stride);
+        if (xp < 0 || xp > nxp) { bad = true; continue; }
+        pxp[(size_t)i] = xp;
+        for (int c = 0; c < 3; c++) pn[(size_t)(3 * i + c)] = n[c];
+      }
+    });
+  for (int64_t x = 1; x <= nxp; x++) {
+    const double *n1 = (const double *)((const char *)sv->xpoint_n1 + x * sv->xpoint_stride);
+    const double *n2 = (const double *)((const char *)sv->xpoint_n2 + x * sv->xpoint_stride);
+    for (int c = 0; c < 3; c++) { xpn[(size_t)(6 * x + c)] = n1[c]; xpn[(size_t)(6 * x + 3 + c)] = n2[c]; }
+  }
+  if (bad) { ctx->err = std::string(who) + ": an xTetra or xPoint index is out of range"; return 0; }
+  hipStream_t s = ctx->stream;
+  if (!pmx_dgrow(ctx, ctx->d_etag, et.size()) || !pmx_dgrow(ctx, ctx->d_pn, pn.size()) ||
+      !pmx_dgrow(ctx, ctx->d_pxp, pxp.size()) || !pmx_dgrow(ctx, ctx->d_xpn, xpn.size()))
+    return 0;
+  if (hipMemcpyAsync(ctx->d_etag.p, et.data(), et.size() * 2, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(ctx->d_pn.p, pn.data(), pn.size() * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(ctx->d_pxp.p, pxp.data(), pxp.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(ctx->d_xpn.p, xpn.data(), xpn.size() * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    ctx->err = std::string(who) + ": copy";
+    return 0;
+  }
+  ctx->have_surf = true;
+  return 1;
+}
+
 // metRidTyp selects Mmg's ridge-metric storage (src/quality_pmmg.c:462,527,
 // 726).  For a size-1 metric (or none) both values take the same isotropic
 // arithmetic.  With a size-6 metric:
 //  * the quality (MMG3D_tetraQual: 0 -> MMG5_caltet33_ani, 1 -> MMG5_orcal ->
 //    MMG5_caltet_ani) is restated for both: 1 averages the metric over the
 //    vertices that are not non-singular ridge points (MMG5_moymet), which
-//    needs the point tags only (caltet_ani_rid);
-//  * the edge lengths with 1 (MMG5_lenedg -> MMG5_lenedg_ani: surface edges
-//    measured along the curved surface, ridge metrics rebuilt from the
-//    xPoint normals, MMG5_buildridmet) need the xTetra edge tags and the
-//    xPoint / point normals, which the ABI does not carry: refused, not
-//    approximated (PMMG_prilen(parmesh,1,0) at src/libparmmg1.c:964 runs
-//    once, at the end of the run).
+//    needs the point tags (caltet_ani_rid);
+//  * the edge lengths (0: MMG5_lenedg33_ani, 1: MMG5_lenedg_ani) measure the
+//    xTetra's boundary edges along the curved surface (pmx_upload_surface),
+//    and 1 rebuilds a ridge point's metric per direction (MMG5_buildridmet)
+//    or takes the tet's mean (MMG5_lenedgspl_ani): len_tet_ani.
 static bool check_met_rid_typ(pmx_ctx *ctx, int metRidTyp, int msize, const char *who, bool lengths) {
   if (metRidTyp != 0 && metRidTyp != 1) {
     ctx->err = std::string(who) + ": metRidTyp must be 0 or 1";
     return false;
   }
-  if (lengths && metRidTyp == 1 && msize == 6) {
-    ctx->err = std::string(who) + ": metRidTyp = 1 with an anisotropic metric (Mmg's ridge metric storage: "
-                                  "curved surface edges and ridge metrics need the xTetra edge tags and the "
-                                  "xPoint normals) is not supported for edge lengths";
-    return false;
-  }
+  (void)msize;
+  (void)lengths;
   return true;
 }
 
-int pmx_tetra_qual(pmx_ctx *ctx, int metRidTyp, double *qual) {
+int pmx_tetra_qual(pmx_ctx *ctx, int metRidTyp, double *qual, int64_t qual_cap) {
   if (!ctx) return 0;
   hipSetDevice(ctx->device);
   StatArgs A;
   if (!stat_args(ctx, A)) return 0;
   if (!check_met_rid_typ(ctx, metRidTyp, A.msize, "pmx_tetra_qual", false)) return 0;
+  if (qual && qual_cap < ctx->ne + 1) {
+    ctx->err = "pmx_tetra_qual: qual holds " + std::to_string(qual_cap) + " doubles, ne+1 = " +
+               std::to_string(ctx->ne + 1) + " needed";
+    return 0;
+  }
   A.ridmet = metRidTyp == 1 && A.msize == 6;
   A.rtag = A.ptag;
+  if (A.ridmet && !A.rtag) {
+    ctx->err = "pmx_tetra_qual: metRidTyp = 1 with a tensor metric needs the point tags (pmx_upload_point_tags)";
+    return 0;
+  }
   if (!pmx_dgrow(ctx, ctx->d_qual, (size_t)(ctx->ne + 1))) return 0;
   if (A.msize == 6)
     hipLaunchKernelGGL((k_qual<true, false, QM_STORE>), dim3(stat_blocks(ctx->ne)), dim3(256), 0, ctx->stream, A,
@@ -1110,10 +1365,23 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
   if (!stat_args(ctx, A)) return 0;
   if (ctx->sd.imet < 0) { ctx->err = "pmx_prilen: no metric"; return 0; }
   if (ctx->ne >= (1LL << 29)) { ctx->err = "pmx_prilen: ne >= 2^29 per group"; return 0; }
+  const bool ani = ctx->sd.size[ctx->sd.imet] == 6;
+  A.ridmet = metRidTyp == 1 && ani;
+  if (A.ridmet && !A.ptag) {
+    ctx->err = "pmx_prilen: metRidTyp = 1 with a tensor metric needs the point tags (pmx_upload_point_tags)";
+    return 0;
+  }
+  if (ctx->have_surf) {
+    A.etag = ctx->d_etag.p;
+    A.pn = ctx->d_pn.p;
+    A.pxp = ctx->d_pxp.p;
+    A.xpn = ctx->d_xpn.p;
+  }
   hipStream_t s = ctx->stream;
   // parallel edges (host): step-1 list (owned, first occurrence, list order)
   // and the sorted keys of the edges step 2 must not count
   std::vector<int2> own;
+  std::vector<uint16_t> own_tag;
   std::vector<unsigned long long> excl;
   std::vector<uint8_t> ppt;
   if (par && par->n > 0) {
@@ -1128,7 +1396,10 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
       const unsigned long long key = ((unsigned long long)(unsigned)std::min(a, b) << 32) | (unsigned)std::max(a, b);
       if (par->owner[i] == par->myrank) {
         // MMG5_hashPop succeeds once per edge: a repeated entry is not counted
-        if (popped.insert(key).second) own.push_back(make_int2(a, b));
+        if (popped.insert(key).second) {
+          own.push_back(make_int2(a, b));
+          own_tag.push_back(par->tag ? par->tag[i] : (uint16_t)0);
+        }
         excl.push_back(key);
       } else if (par->exact_once) {
         excl.push_back(key);
@@ -1167,13 +1438,22 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
   // the 64-bit variant, for the A/B)
   static const bool wide = getenv("PMX_PRILEN_WIDE") != nullptr;
   const bool lean = !wide && A.ne < 700000000LL;
-  const int sel = (lean ? 8 : 0) | (ctx->sd.size[ctx->sd.imet] == 6 ? 4 : 0) | (A.ptag ? 2 : 0) |
+  const int sel = (lean ? 8 : 0) | (ani ? 4 : 0) | (A.ptag ? 2 : 0) |
                   (par && par->n > 0 && !excl.empty() ? 1 : 0);
+  // tensor metrics measured along the surface / in ridge storage
+  // (len_tet_ani): the owner tet's xTetra tags and vertices per edge
+  static const KFn kfs[8] = {
+      k_prilen<true, false, false, 1, false, true>, k_prilen<true, false, true, 1, false, true>,
+      k_prilen<true, true, false, 1, false, true>,  k_prilen<true, true, true, 1, false, true>,
+      k_prilen<true, false, false, 1, true, true>,  k_prilen<true, false, true, 1, true, true>,
+      k_prilen<true, true, false, 1, true, true>,   k_prilen<true, true, true, 1, true, true>};
+  const bool surf = ani && (ctx->have_surf || A.ridmet);
+  const KFn kern = surf ? kfs[(lean ? 4 : 0) | (sel & 3)] : kfn[sel];
   int nb = stat_blocks(ctx->ne);
   A.sched_chunk = 0;
   if (sched > 0) {
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn[sel], 256, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess ||
         per_cu < 1 || cus < 8) {
       ctx->err = "pmx_prilen: occupancy query";
@@ -1187,11 +1467,14 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
   A.npar = (int64_t)excl.size();
   if (A.npar) {
     if (!pmx_dgrow(ctx, ctx->d_pkey, excl.size()) || !pmx_dgrow(ctx, ctx->d_ppt, ppt.size()) ||
-        !pmx_dgrow(ctx, ctx->d_pedge, std::max<size_t>(own.size(), 1)))
+        !pmx_dgrow(ctx, ctx->d_pedge, std::max<size_t>(own.size(), 1)) ||
+        !pmx_dgrow(ctx, ctx->d_pedge_tag, std::max<size_t>(own.size(), 1)))
       return 0;
     if (hipMemcpyAsync(ctx->d_pkey.p, excl.data(), excl.size() * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(ctx->d_ppt.p, ppt.data(), ppt.size(), hipMemcpyHostToDevice, s) != hipSuccess ||
-        (!own.empty() && hipMemcpyAsync(ctx->d_pedge.p, own.data(), own.size() * sizeof(int2), hipMemcpyHostToDevice, s) != hipSuccess)) {
+        (!own.empty() && hipMemcpyAsync(ctx->d_pedge.p, own.data(), own.size() * sizeof(int2), hipMemcpyHostToDevice, s) != hipSuccess) ||
+        (!own.empty() && hipMemcpyAsync(ctx->d_pedge_tag.p, own_tag.data(), own_tag.size() * sizeof(uint16_t),
+                                        hipMemcpyHostToDevice, s) != hipSuccess)) {
       ctx->err = "pmx_prilen: parallel edge upload";
       return 0;
     }
@@ -1200,10 +1483,12 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
   }
   // partials: [0] step 1 (owned parallel edges), [1..nb] step 2 (tet edges)
   if (!own.empty())
-    hipLaunchKernelGGL(k_prilen_par, dim3(1), dim3(256), 0, s, A, ctx->d_pedge.p, (int64_t)own.size(), parts);
+    hipLaunchKernelGGL(k_prilen_par, dim3(1), dim3(256), 0, s, A, ctx->d_pedge.p,
+                       (const uint16_t *)ctx->d_pedge_tag.p, (int64_t)own.size(), parts);
   else
-    hipLaunchKernelGGL(k_prilen_par, dim3(1), dim3(256), 0, s, A, (const int2 *)nullptr, (int64_t)0, parts);
-  hipLaunchKernelGGL(kfn[sel], dim3(nb), dim3(256), 0, s, A, parts + 1);
+    hipLaunchKernelGGL(k_prilen_par, dim3(1), dim3(256), 0, s, A, (const int2 *)nullptr, (const uint16_t *)nullptr,
+                       (int64_t)0, parts);
+  hipLaunchKernelGGL(kern, dim3(nb), dim3(256), 0, s, A, parts + 1);
   LenPart *mid = parts + 1 + nb;
   hipLaunchKernelGGL(k_prilen_final, dim3(FINAL_GRID), dim3(256), 0, s, parts, nb + 1, mid,
                      (pmx_len_part *)nullptr, ctx->d_tets.p, (const int2 *)ctx->d_pedge.p);
@@ -1250,6 +1535,12 @@ static int new_mesh_qual_core(pmx_ctx *ctx, const char *who, int opt, int metRid
   if (!check_met_rid_typ(ctx, metRidTyp, A.msize, who, false)) return 0;
   A.ridmet = metRidTyp == 1 && A.msize == 6;
   A.rtag = ctx->have_qtag ? ctx->d_qtag.p : nullptr;
+  if (A.ridmet && !A.rtag) {
+    // MMG5_moymet leaves the ridge points out: without their tags the mean
+    // would silently be the plain one
+    ctx->err = std::string(who) + ": metRidTyp = 1 with a tensor metric needs the new points' tags (points view tag)";
+    return 0;
+  }
   if (dev_result && opt != PMX_INQUA && opt != PMX_OUTQUA) {
     ctx->err = std::string(who) + (opt == PMX_LESQUA ? ": the optimLES quality (MMG3D_computeLESqua) is not supported"
                                                       : ": opt must be PMX_INQUA or PMX_OUTQUA");
@@ -1270,7 +1561,7 @@ static int new_mesh_qual_core(pmx_ctx *ctx, const char *who, int opt, int metRid
 }
 
 int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, int64_t ne, int opt,
-                      int metRidTyp, double *qual, void *dev_result) {
+                      int metRidTyp, double *qual, int64_t qual_cap, void *dev_result) {
   if (!ctx) return 0;
   hipSetDevice(ctx->device);
   if (!ctx->ran || !ctx->have_pts || ctx->out_n != ctx->nq) {
@@ -1287,6 +1578,11 @@ int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, in
   } else if (!ctx->ensure_tets(ctx->stream)) {
     return 0;
   }
+  if (qual && qual_cap < ctx->n_ntet + 1) {
+    ctx->err = "pmx_new_mesh_qual: qual holds " + std::to_string(qual_cap) + " doubles, ne+1 = " +
+               std::to_string(ctx->n_ntet + 1) + " needed";
+    return 0;
+  }
   // the interpolated metric, in the step's output rows (a constant-size
   // metric of the step is there too)
   const int msize = ctx->sd.imet >= 0 ? ctx->sd.size[ctx->sd.imet] : 0;
@@ -1301,7 +1597,7 @@ int pmx_new_mesh_qual(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, in
 // the host, failed tensor inversions) sent to the device; a metric the step
 // did not interpolate (-hsiz constant size, or Mmg's own) is sent whole.
 int pmx_new_mesh_qual_synced(pmx_ctx *ctx, const pmx_sol_view *met, int opt, int metRidTyp, double *qual,
-                             int64_t qual_stride, void *dev_result) {
+                             int64_t qual_stride, int64_t qual_cap, void *dev_result) {
   if (!ctx) return 0;
   hipSetDevice(ctx->device);
   const char *who = "pmx_new_mesh_qual_synced";
@@ -1312,6 +1608,11 @@ int pmx_new_mesh_qual_synced(pmx_ctx *ctx, const pmx_sol_view *met, int opt, int
     return 0;
   }
   if (!ctx->have_ntet) { ctx->err = std::string(who) + ": the step's points view had no new tets"; return 0; }
+  if (qual && qual_cap < ctx->n_ntet + 1) {
+    ctx->err = std::string(who) + ": qual holds " + std::to_string(qual_cap) + " records, ne+1 = " +
+               std::to_string(ctx->n_ntet + 1) + " needed";
+    return 0;
+  }
   if (!ctx->ensure_tets(ctx->stream) || !ctx->fix_orphans()) return 0;
   const int64_t n = ctx->nq, first = ctx->pts_first;
   hipStream_t s = ctx->stream;

@@ -206,21 +206,21 @@ class Transfer:
         for i, (a, sz) in enumerate(zip(outs, self.sizes)):
             views[i].size, views[i].m = sz, _dp(a)
         if sols_only:
-            self._chk(self.lib.pmx_download(self.ctx, views, None, None, None), "pmx_download")
+            self._chk(self.lib.pmx_download(self.ctx, views, n, None, None, None), "pmx_download")
         else:
-            self._chk(self.lib.pmx_download(self.ctx, views, _ip(elem), _ip(status), _ip(steps)),
+            self._chk(self.lib.pmx_download(self.ctx, views, n, _ip(elem), _ip(status), _ip(steps)),
                       "pmx_download")
         return Result(outs, elem, status, steps)
 
     def starts(self) -> np.ndarray:
         s = np.zeros(self.npts, np.int32)
-        self._chk(self.lib.pmx_download_starts(self.ctx, _ip(s)), "pmx_download_starts")
+        self._chk(self.lib.pmx_download_starts(self.ctx, _ip(s), len(s)), "pmx_download_starts")
         return s
 
     def border(self) -> tuple[np.ndarray, np.ndarray]:
         e = np.zeros(self.npts, np.int32)
         v = np.zeros(self.npts, np.int32)
-        self._chk(self.lib.pmx_download_border(self.ctx, _ip(e), _ip(v)), "pmx_download_border")
+        self._chk(self.lib.pmx_download_border(self.ctx, _ip(e), _ip(v), len(e)), "pmx_download_border")
         return e, v
 
     def locate_stats(self) -> dict:
@@ -332,7 +332,7 @@ class Transfer:
     def tetra_qual(self, ne: int, met_rid_typ: int = 0) -> np.ndarray:
         """MMG3D_tetraQual(mesh, met, metRidTyp) of the uploaded group."""
         q = np.zeros(ne + 1)
-        self._chk(self.lib.pmx_tetra_qual(self.ctx, met_rid_typ, _dp(q)), "pmx_tetra_qual")
+        self._chk(self.lib.pmx_tetra_qual(self.ctx, met_rid_typ, _dp(q), len(q)), "pmx_tetra_qual")
         return q
 
     def count_nodes(self, idx_ip=None, idx_comm=None, intvalues=None, base: int = 1) -> int:
@@ -378,7 +378,40 @@ class Transfer:
         pe = N.ParEdges()
         pe.n, pe.a, pe.b, pe.owner = len(a), _ip(a), _ip(b), _ip(o)
         pe.myrank, pe.exact_once = int(par.get("myrank", 0)), int(par.get("exact_once", 0))
-        return C.byref(pe), [a, b, o, pe]
+        keep = [a, b, o, pe]
+        if par.get("tag") is not None:
+            t = np.ascontiguousarray(par["tag"], np.uint16)
+            pe.tag = t.ctypes.data_as(N.u16ptr)
+            keep.append(t)
+        return C.byref(pe), keep
+
+    def upload_surface(self, surface: dict | None):
+        """Mmg's surface data of the uploaded group (pmx_upload_surface):
+        {"xt" (ne+1,) tetra[k].xt, "xtag" (nxt+1, 6) xtetra[x].tag, "n" (np+1, 3)
+        point[i].n, "xp" (np+1,) point[i].xp, "n1"/"n2" (nxp+1, 3) xpoint[x].n1/n2};
+        None: no surface data (no xTetra, zero normals)."""
+        if surface is None:
+            self._chk(self.lib.pmx_upload_surface(self.ctx, None), "pmx_upload_surface")
+            return
+        xt = np.ascontiguousarray(surface["xt"], np.int32)
+        xtag = np.ascontiguousarray(surface["xtag"], np.uint16).reshape(-1, 6)
+        n = np.ascontiguousarray(surface["n"], np.float64).reshape(-1, 3)
+        xp = np.ascontiguousarray(surface["xp"], np.int32)
+        n1 = np.ascontiguousarray(surface["n1"], np.float64).reshape(-1, 3)
+        n2 = np.ascontiguousarray(surface["n2"], np.float64).reshape(-1, 3)
+        sv = N.SurfaceView()
+        sv.nxt, sv.nxp = xtag.shape[0] - 1, n1.shape[0] - 1
+        sv.tetra_xt, sv.tetra_stride = _ip(xt), 4
+        sv.xtetra_tag, sv.xtetra_stride = xtag.ctypes.data_as(N.u16ptr), 12
+        sv.point_n, sv.point_xp, sv.point_stride = _dp(n), _ip(xp), 24
+        # point_n / point_xp share one stride in the ABI (MMG5_Point): pack them
+        rec = np.zeros(n.shape[0], dtype=[("n", np.float64, 3), ("xp", np.int32), ("pad", np.int32)])
+        rec["n"], rec["xp"] = n, xp
+        sv.point_n = C.cast(C.c_void_p(rec.ctypes.data), N.dptr)
+        sv.point_xp = C.cast(C.c_void_p(rec.ctypes.data + 24), N.iptr)
+        sv.point_stride = rec.dtype.itemsize
+        sv.xpoint_n1, sv.xpoint_n2, sv.xpoint_stride = _dp(n1), _dp(n2), 24
+        self._chk(self.lib.pmx_upload_surface(self.ctx, C.byref(sv)), "pmx_upload_surface")
 
     def prilen(self, met_rid_typ: int = 0, par: dict | None = None) -> dict:
         """par: {"a", "b", "owner", "myrank", "exact_once"} (distributed PMMG_prilen)."""
@@ -429,7 +462,7 @@ class Transfer:
         tv = _tets_1based(tets) if tets is not None else None
         q = np.zeros((tv.shape[0] if tv is not None else self.n_new_tets + 1))
         self._chk(self.lib.pmx_new_mesh_qual(self.ctx, _ip(tv), 16, tv.shape[0] - 1 if tv is not None else 0,
-                                             opt, met_rid_typ, _dp(q), C.c_void_p(dev_ptr or None)),
+                                             opt, met_rid_typ, _dp(q), len(q), C.c_void_p(dev_ptr or None)),
                   "pmx_new_mesh_qual")
         if tv is not None:
             self.n_new_tets = tv.shape[0] - 1
@@ -460,7 +493,7 @@ class Transfer:
             base = out.ctypes.data + out.dtype.fields["qual"][1]
             ptr, stride = C.cast(C.c_void_p(base), N.dptr), out.dtype.itemsize
         self._chk(self.lib.pmx_new_mesh_qual_synced(self.ctx, C.byref(mv) if mv is not None else None, opt,
-                                                    met_rid_typ, ptr, stride, None),
+                                                    met_rid_typ, ptr, stride, q.shape[0], None),
                   "pmx_new_mesh_qual_synced")
         return q
 

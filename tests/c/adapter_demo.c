@@ -27,7 +27,7 @@
  * takes the re-upload path (the resident state is used once): both written
  * out (out_q{1,2a,2b}_{res,upl}.bin) for a bit-for-bit comparison.
  *
- * usage: adapter_demo <dir> full|ani|refuse_les|iterate|twoproc_prilen|twoproc_qualhisto
+ * usage: adapter_demo <dir> full|ani|refuse_les|iterate|nolocate|hsiz_nofield|twoproc_prilen|twoproc_qualhisto
  */
 #define _POSIX_C_SOURCE 200809L
 #include <signal.h>
@@ -85,6 +85,11 @@ int MMG5_displayLengthHisto_internal(int ned, int amin, int bmin, double lmin, i
 /* one rank: no parallel edges */
 static PMMG_Int_comm edge_comm;
 int PMMG_hashPar(MMG5_pMesh mesh, MMG5_HGeom *pHash) { (void)mesh; pHash->geom = NULL; return PMMG_SUCCESS; }
+int MMG5_hGet(MMG5_HGeom *hash, int a, int b, int *ref, int16_t *tag) {
+  (void)hash; (void)a; (void)b;
+  *ref = 0; *tag = 0;
+  return 0;
+}
 int PMMG_build_edgeComm(PMMG_pParMesh parmesh, MMG5_pMesh mesh, MMG5_HGeom *hpar) {
   (void)mesh; (void)hpar;
   memset(&edge_comm, 0, sizeof edge_comm);
@@ -382,6 +387,27 @@ int main(int argc, char **argv) {
   pm.listgrp = &grp; pm.old_listgrp = &ogrp;
   pm.info.imprim = 5; pm.info.imprim0 = 5; pm.info.root = 0; pm.info.inputMet = 1;
 
+  if (!strcmp(mode, "nolocate") || !strcmp(mode, "hsiz_nofield")) {
+    /* a group whose interpolation has nothing to locate (reference
+     * src/interpmesh_pmmg.c:497-512): no input metric and no field, or -hsiz
+     * and no field.  Its context runs no step, so :845 must take the upload
+     * path (and not fail on a "resident" mesh the device does not hold). */
+    double *q = calloc((size_t)ne2 + 1, sizeof(double));
+    mesh->nsols = 0;
+    if (!strcmp(mode, "nolocate")) pm.info.inputMet = 0;
+    else mesh->info.hsiz = 0.05;
+    for (i = 0; i < (np2 + 1) * msize; i++) met.m[i] = 0.05;   /* Mmg's own metric */
+    ier = PMMG_interpMetricsAndFields(&pm, NULL);
+    printf("{\"call\": \"interp\", \"ret\": %d}\n", ier);
+    for (i = 1; i <= ne2; i++) mesh->tetra[i].qual = -1.0;
+    ier = PMMG_tetraQual(&pm, 1);
+    printf("{\"call\": \"tetraqual\", \"ret\": %d}\n", ier);
+    for (i = 1; i <= ne2; i++) q[i] = mesh->tetra[i].qual;
+    wr(dir, "out_qual.bin", q, (size_t)(ne2 + 1) * 8);
+    wr(dir, "out_met.bin", met.m, (size_t)(np2 + 1) * msize * 8);
+    free(q);
+    return 0;
+  }
   if (!strcmp(mode, "refuse_les")) {
     mesh->info.optimLES = 1;
     ier = PMMG_qualhisto(&pm, PMMG_INQUA, 1);
@@ -400,14 +426,37 @@ int main(int argc, char **argv) {
   wr(dir, "out_fld.bin", fld.m, (size_t)(np2 + 1) * fsize * 8);
   if (!strcmp(mode, "ani")) {
     /* :845 with an anisotropic metric (Mmg's ridge metric storage): the
-     * quality on the device-resident new mesh; the lengths of :964 refused */
+     * quality on the device-resident new mesh; then the lengths of :964 with
+     * the new mesh's surface data (xTetra edge tags, point / xPoint normals,
+     * as MMG3D_analys leaves them; files written by the test) */
     double *q = calloc((size_t)ne2 + 1, sizeof(double));
+    long long nxt, nxp;
     ier = PMMG_tetraQual(&pm, 1);
     printf("{\"call\": \"tetraqual_ani_1\", \"ret\": %d}\n", ier);
     for (i = 1; i <= ne2; i++) q[i] = mesh->tetra[i].qual;
     wr(dir, "out_qual_ani1.bin", q, (size_t)(ne2 + 1) * 8);
+    snprintf(path, sizeof path, "%s/surf_sizes.txt", dir);
+    f = fopen(path, "r");
+    if (!f || fscanf(f, "%lld %lld", &nxt, &nxp) != 2) return 2;
+    fclose(f);
+    {
+      int *xt = rd(dir, "new_xt.bin", (size_t)(ne2 + 1) * 4);
+      uint16_t *xtag = rd(dir, "new_xtag.bin", (size_t)(nxt + 1) * 12);
+      double *pn = rd(dir, "new_pn.bin", (size_t)(np2 + 1) * 24);
+      int *xp = rd(dir, "new_xp.bin", (size_t)(np2 + 1) * 4);
+      double *n1 = rd(dir, "new_n1.bin", (size_t)(nxp + 1) * 24), *n2 = rd(dir, "new_n2.bin", (size_t)(nxp + 1) * 24);
+      mesh->xt = (int)nxt; mesh->xp = (int)nxp;
+      mesh->xtetra = calloc((size_t)nxt + 1, sizeof(MMG5_xTetra));
+      mesh->xpoint = calloc((size_t)nxp + 1, sizeof(MMG5_xPoint));
+      for (i = 1; i <= ne2; i++) mesh->tetra[i].xt = xt[i];
+      for (i = 1; i <= nxt; i++) memcpy(mesh->xtetra[i].tag, xtag + 6 * i, 12);
+      for (i = 1; i <= np2; i++) { memcpy(mesh->point[i].n, pn + 3 * i, 24); mesh->point[i].xp = xp[i]; }
+      for (i = 1; i <= nxp; i++) { memcpy(mesh->xpoint[i].n1, n1 + 3 * i, 24); memcpy(mesh->xpoint[i].n2, n2 + 3 * i, 24); }
+    }
     ier = PMMG_prilen(&pm, 1, 0);
     printf("{\"call\": \"prilen_ani_1\", \"ret\": %d}\n", ier);
+    ier = PMMG_prilen(&pm, 0, 1);
+    printf("{\"call\": \"prilen_ani_0_central\", \"ret\": %d}\n", ier);
     ier = PMMG_tetraQual(&pm, 0);
     printf("{\"call\": \"tetraqual_ani_0\", \"ret\": %d}\n", ier);
     for (i = 1; i <= ne2; i++) q[i] = mesh->tetra[i].qual;

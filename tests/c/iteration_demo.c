@@ -99,7 +99,7 @@ int main(void) {
   double *h2 = calloc((size_t)m2.np + 1, sizeof(double)), *ls2 = calloc((size_t)m2.np + 1, sizeof(double));
   /* pmx_download writes in point-list order: entry 0 = point 1 (Mmg's m[1]) */
   pmx_sol_view new2[2] = {{1, h2 + 1}, {1, ls2 + 1}};
-  CK(pmx_download(ctx, new2, NULL, NULL, NULL));
+  CK(pmx_download(ctx, new2, m2.np, NULL, NULL, NULL));
   /* quality of the new mesh in the interpolated metric, reduced over the
    * (one-rank) RCCL communicator */
   const int stats = getenv("PMX_DEMO_NO_STATS") == NULL;
@@ -113,7 +113,7 @@ int main(void) {
   CK(pmx_comm_init(ctx, &comm, 1, id, 0));
   void *d = NULL;
   if (!(d = pmx_device_alloc(ctx, sizeof(pmx_qual_part)))) { fprintf(stderr, "%s\n", pmx_last_error(ctx)); return 1; }
-  CK(pmx_new_mesh_qual(ctx, NULL, 0, 0, PMX_INQUA, 1, NULL, d));
+  CK(pmx_new_mesh_qual(ctx, NULL, 0, 0, PMX_INQUA, 1, NULL, 0, d));
   CK(pmx_qualhisto_allreduce(ctx, comm, 1, d, 1, &qs));
   if (qs.ne != m2.ne || qs.np != m2.np || qs.min <= 0.0 || qs.max > 1.0 + 1e-12) {
     fprintf(stderr, "new-mesh statistics: ne %lld np %lld min %g max %g\n", (long long)qs.ne,
@@ -129,13 +129,13 @@ int main(void) {
   CK(pmx_run(ctx, &o));
   double *h3 = calloc((size_t)m3.np + 1, sizeof(double)), *ls3 = calloc((size_t)m3.np + 1, sizeof(double));
   pmx_sol_view new3[2] = {{1, h3 + 1}, {1, ls3 + 1}};
-  CK(pmx_download(ctx, new3, NULL, NULL, NULL));
+  CK(pmx_download(ctx, new3, m3.np, NULL, NULL, NULL));
   /* the same iteration 2 from a host upload of M2 and iteration 1's fields */
   pmx_ctx *ref = pmx_create(0);
   double *h3r = calloc((size_t)m3.np + 1, sizeof(double)), *ls3r = calloc((size_t)m3.np + 1, sizeof(double));
   pmx_sol_view new3r[2] = {{1, h3r + 1}, {1, ls3r + 1}};
   if (!ref || !pmx_upload_background(ref, &v2, 2, (pmx_sol_view[2]){{1, h2}, {1, ls2}}, 0) || !pmx_upload_points(ref, &p3) ||
-      !pmx_run(ref, &o) || !pmx_download(ref, new3r, NULL, NULL, NULL)) {
+      !pmx_run(ref, &o) || !pmx_download(ref, new3r, m3.np, NULL, NULL, NULL)) {
     fprintf(stderr, "reference context: %s\n", ref ? pmx_last_error(ref) : "create");
     return 1;
   }

@@ -24,6 +24,8 @@
 #define MG_REQ    ((int16_t)1 << 2)
 #define MG_BDY    ((int16_t)1 << 4)
 #define MG_NUL    ((int16_t)1 << 14)
+#define MG_NOM    ((int16_t)1 << 3)
+#define MG_CRN    ((int16_t)1 << 5)
 #define MG_EOK(pt) (pt && ((pt)->v[0] > 0))
 
 typedef struct {
@@ -57,6 +59,20 @@ typedef struct {
 typedef MMG5_Edge *MMG5_pEdge;
 
 typedef struct {
+  int      ref[4], edg[6];
+  int16_t  ftag[4];
+  uint16_t tag[6];
+  int8_t   ori;
+} MMG5_xTetra;
+typedef MMG5_xTetra *MMG5_pxTetra;
+
+typedef struct {
+  double  n1[3], n2[3];
+  int8_t  nnor;
+} MMG5_xPoint;
+typedef MMG5_xPoint *MMG5_pxPoint;
+
+typedef struct {
   double  hsiz, hausd;
   int     imprim, renum;
   int8_t  optimLES;
@@ -64,8 +80,11 @@ typedef struct {
 
 typedef struct {
   int         np, ne, nt, na, nsols, base;
+  int         xt, xp;                  /* xTetra / xPoint counts */
   MMG5_pPoint point;
   MMG5_pTetra tetra;
+  MMG5_pxTetra xtetra;
+  MMG5_pxPoint xpoint;
   MMG5_pTria  tria;
   MMG5_pEdge  edge;
   int        *adja, *adjt;
@@ -159,6 +178,7 @@ int  MMG5_displayLengthHisto_internal(int ned, int amin, int bmin, double lmin, 
                                       double lmax, int nullEdge, double *bd, int *hl, int8_t shift,
                                       int imprim);
 int  PMMG_hashPar(MMG5_pMesh mesh, MMG5_HGeom *pHash);
+int  MMG5_hGet(MMG5_HGeom *hash, int a, int b, int *ref, int16_t *tag);
 int  PMMG_build_edgeComm(PMMG_pParMesh parmesh, MMG5_pMesh mesh, MMG5_HGeom *hpar);
 void PMMG_edge_comm_free(PMMG_pParMesh parmesh);
 /* the adapter's MPI calls (the RCCL id's broadcast, the ranks' agreement on

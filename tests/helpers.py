@@ -125,3 +125,93 @@ def compare_exact(gpu, ref, idx, nsol):
     for s in range(nsol):
         ok = bits_equal(outs_g[s][idx], outs_r[s][idx])
         assert ok.all(), f"sol {s}: {np.count_nonzero(~ok)} points differ bitwise"
+
+
+# Mmg tags (libmmgtypes.h, restated): MG_REF, MG_GEO, MG_REQ, MG_NOM, MG_BDY, MG_CRN
+TAG_REF, TAG_GEO, TAG_REQ, TAG_NOM, TAG_BDY, TAG_CRN = 1, 2, 4, 8, 16, 32
+IARE = [(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)]
+
+
+def cube_surface(m, seed: int = 5, noise: float = 0.05, ridge_frac: float = 1.0):
+    """Mmg-like surface data of a Kuhn mesh of the unit cube, the way
+    MMG3D_analys leaves it (synthetic: the kernels only read it):
+
+    * point tags: MG_BDY on the faces, MG_GEO on the 12 cube edges (ridges),
+      MG_CRN | MG_REQ | MG_GEO at the 8 corners, a few ridge points MG_NOM
+      (non-manifold: their metric is a plain tensor);
+    * per tet an xTetra when it has a boundary face: tag[ia] = MG_BDY for the
+      edges of its boundary faces, | MG_GEO for those along a cube edge;
+    * per point p->n (the outward normal of a face point, the tangent of a
+      ridge point) and an xPoint with n1 (face normal) / n1, n2 (the two face
+      normals of a ridge point), all perturbed by `noise` and renormalised so
+      that the curved-length formulas see non-trivial normals;
+    * the metric in Mmg's ridge storage at the non-singular ridge points
+      ((tangent, in-surface 1 / 2, normal 1 / 2) sizes^-2), a shock tensor
+      elsewhere (ridge_frac < 1: only that fraction of the ridge points).
+
+    Returns (tags (np+1,), surface dict for Transfer.upload_surface /
+    oracle.prilen, met (np+1, 6))."""
+    rng = np.random.default_rng(seed)
+    x = m.xyz
+    onb = np.stack([(x[:, a] == 0.0) | (x[:, a] == 1.0) for a in range(3)], 1)
+    onb[0] = False
+    cnt = onb.sum(1)
+    tag = np.zeros(m.np + 1, np.uint16)
+    tag[cnt >= 1] |= TAG_BDY
+    tag[cnt >= 2] |= TAG_GEO
+    tag[cnt == 3] |= TAG_CRN | TAG_REQ
+    ridge = np.nonzero(cnt == 2)[0]
+    tag[ridge[:: 17]] |= TAG_NOM
+
+    def face_normal(ip, a):
+        v = np.zeros(3)
+        v[a] = 1.0 if x[ip, a] == 1.0 else -1.0
+        return v
+
+    def noisy(v):
+        w = v + noise * rng.standard_normal(3)
+        return w / np.sqrt((w * w).sum())
+
+    n = np.zeros((m.np + 1, 3))
+    xp = np.zeros(m.np + 1, np.int32)
+    n1, n2 = [np.zeros(3)], [np.zeros(3)]
+    for ip in np.nonzero((cnt == 1) | (cnt == 2))[0]:
+        axes = np.nonzero(onb[ip])[0]
+        a = face_normal(ip, axes[0])
+        if cnt[ip] == 1:
+            n[ip] = noisy(a)
+            n1.append(noisy(a))
+            n2.append(np.zeros(3))
+        else:
+            b = face_normal(ip, axes[1])
+            n[ip] = noisy(np.cross(a, b))
+            n1.append(noisy(a))
+            n2.append(noisy(b))
+        xp[ip] = len(n1) - 1
+    # xTetras of the tets with a boundary face (face f opposite vertex f)
+    ne = m.ne
+    adj = m.adja[1:4 * ne + 1].reshape(ne, 4)
+    xt = np.zeros(ne + 1, np.int32)
+    xtag = [np.zeros(6, np.uint16)]
+    for k in np.nonzero((adj == 0).any(1))[0] + 1:
+        v = m.tet[k]
+        t6 = np.zeros(6, np.uint16)
+        for f in np.nonzero(adj[k - 1] == 0)[0]:
+            for ia, (i, j) in enumerate(IARE):
+                if f in (i, j):
+                    continue
+                t6[ia] |= TAG_BDY
+                p, q = v[i], v[j]
+                common = onb[p] & onb[q] & (x[p] == x[q])
+                if common.sum() >= 2:
+                    t6[ia] |= TAG_GEO
+        xtag.append(t6)
+        xt[k] = len(xtag) - 1
+    met = M.on_vertices(m, M.shock_metric)
+    rid = np.nonzero(((tag & TAG_GEO) != 0) & ((tag & (TAG_CRN | TAG_REQ | TAG_NOM)) == 0))[0]
+    rid = rid[: int(len(rid) * ridge_frac)]
+    h = rng.uniform(0.02, 0.2, size=(len(rid), 5))
+    met[rid, :5] = 1.0 / (h * h)
+    met[rid, 5] = 0.0
+    surf = dict(xt=xt, xtag=np.array(xtag), n=n, xp=xp, n1=np.array(n1), n2=np.array(n2))
+    return tag, surf, met

@@ -139,24 +139,63 @@ def test_adapter_ani_ridge_metric(tmp_path):
     PMMG_tetraQual(parmesh,1) (src/libparmmg1.c:845) runs on the device-resident
     new mesh and equals the oracle's MMG5_caltet_ani restatement (the mean
     metric without the non-singular ridge points, from the new points' tags)
-    bit for bit; metRidTyp = 0 equals MMG5_caltet33_ani; PMMG_prilen(parmesh,1,0)
-    (:964: curved surface edges and ridge metrics, which need the xTetra edge
-    tags and xPoint normals the ABI does not carry) fails loudly."""
+    bit for bit; metRidTyp = 0 equals MMG5_caltet33_ani.  PMMG_prilen(parmesh,1,0)
+    (:964) -- ParMmg's output call -- measures the new mesh's edges in its
+    interpolated tensor metric along the curved surface (the mesh's xTetra
+    edge tags and point / xPoint normals, read in place by the binding,
+    MMG5_lenedg_ani) and PMMG_prilen(parmesh,0,1) (src/libparmmg.c:185) in
+    classic storage (MMG5_lenedg33_ani): both equal the oracle's restatement
+    bit for bit."""
+    from helpers import cube_surface
     d = str(tmp_path)
     old, new, otag, ntag, nxyz, omet, ofld, req = write_case(d, "ani")
+    stag, surf, _ = cube_surface(new, noise=0.08)
+    for k, a in dict(new_xt=surf["xt"].astype(np.int32), new_xtag=surf["xtag"].astype(np.uint16),
+                     new_pn=surf["n"], new_xp=surf["xp"].astype(np.int32), new_n1=surf["n1"],
+                     new_n2=surf["n2"]).items():
+        np.ascontiguousarray(a).tofile(os.path.join(d, k + ".bin"))
+    with open(os.path.join(d, "surf_sizes.txt"), "w") as fh:
+        fh.write(f"{surf['xtag'].shape[0] - 1} {surf['n1'].shape[0] - 1}\n")
     r, recs = run_demo(d, "ani")
     assert r.returncode == 0, r.stdout + r.stderr
     calls = {c["call"]: c["ret"] for c in recs if "call" in c}
-    assert calls["tetraqual_ani_1"] == 1 and calls["prilen_ani_1"] == 0 and calls["tetraqual_ani_0"] == 1
-    assert "metRidTyp = 1 with an anisotropic metric" in r.stderr
+    assert calls["tetraqual_ani_1"] == 1 and calls["tetraqual_ani_0"] == 1, calls
+    assert calls["prilen_ani_1"] == 1 and calls["prilen_ani_0_central"] == 1, (calls, r.stderr)
     met = np.fromfile(os.path.join(d, "out_met.bin")).reshape(new.np + 1, 6)
     mesh_new = M.Mesh(nxyz, new.tet, new.adja, new.tria, new.adjt)
+    pl = [c["prilen"] for c in recs if "prilen" in c]
+    assert len(pl) == 2
+    for got, mrt in zip(pl, (1, 0)):
+        ref = O.prilen(mesh_new, met, tags=ntag, met_rid_typ=mrt, surface=surf)
+        for k in ("ned", "nullEdge", "amin", "bmin", "amax", "bmax", "hl", "lmin", "lmax"):
+            assert got[k] == ref[k], (mrt, k, got[k], ref[k])
     q1 = np.fromfile(os.path.join(d, "out_qual_ani1.bin"))
     q0 = np.fromfile(os.path.join(d, "out_qual_ani0.bin"))
     o1 = O.tetra_qual(mesh_new, met, tags=ntag, met_rid_typ=1)
     o0 = O.tetra_qual(mesh_new, met)
     assert np.array_equal(q1[1:], o1[1:]) and np.array_equal(q0[1:], o0[1:])
     assert np.count_nonzero(q1[1:] != q0[1:]) > 0       # the ridge points change the mean
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["nolocate", "hsiz_nofield"])
+def test_adapter_quality_when_nothing_located(tmp_path, mode):
+    """A group whose interpolation locates nothing (src/interpmesh_pmmg.c:
+    497-512: no input metric and no field, or -hsiz and no field) keeps no
+    step on its context: PMMG_tetraQual (src/libparmmg1.c:845) must then take
+    the upload path and still set every valid tet's quality (the r04 advisor's
+    finding: the binding had marked every group resident)."""
+    d = str(tmp_path)
+    old, new, otag, ntag, nxyz, omet, ofld, req = write_case(d, "iso")
+    r, recs = run_demo(d, mode)
+    assert r.returncode == 0, r.stdout + r.stderr
+    calls = {c["call"]: c["ret"] for c in recs if "call" in c}
+    assert calls == {"interp": 1, "tetraqual": 1}, (calls, r.stderr)
+    qual = np.fromfile(os.path.join(d, "out_qual.bin"))
+    mesh_new = M.Mesh(nxyz, new.tet, new.adja, new.tria, new.adjt)
+    assert np.array_equal(qual[1:], O.tetra_qual(mesh_new, None)[1:])
+    met = np.fromfile(os.path.join(d, "out_met.bin"))
+    assert np.all(met[1:] == 0.05)                 # Mmg's metric, or the constant size
 
 
 @pytest.mark.gpu

@@ -283,3 +283,102 @@ def test_threaded_host_paths_bit_identical(tmp_path):
     for k in a.files:
         if k != "steps":
             assert np.array_equal(a[k].view(np.uint8), b[k].view(np.uint8)), k
+
+
+def test_orphan_locate_stats_and_rows(transfer):
+    """Orphans (points in no valid new tet) are located by the step (their
+    marks come with the new tets, after it) but then reset everywhere: kind,
+    element, status, steps, start 0, edge / vertex -1 -- so the locate
+    statistics count only the points the reference visits (an orphan outside
+    the domain adds no exhaustive scan, no closest element), and the
+    starts / border downloads show them as never visited.  New tets uploaded
+    after such a points view replace its tets for the orphan marks too."""
+    m, x, t, sols = cube_case(6, metric="iso", surface=True)
+    n = len(x)
+    x = x.copy()
+    rng = np.random.default_rng(21)
+    used = np.zeros(n, bool)
+    used[: int(0.75 * n)] = True
+    orph = np.nonzero(~used)[0]
+    x[orph[:5]] = [2.0, 2.0, 2.0]              # orphans outside the domain
+    pool = np.nonzero(used)[0]
+    tets = np.zeros((len(pool) + 1, 4), np.int32)
+    tets[1:] = rng.choice(pool, size=(len(pool), 4))
+    tets[1:, 0] = pool
+    tets[0] = -1
+    transfer.upload_background(m, sols, 0)
+    transfer.upload_points(x, t, tets)
+    transfer.run(record_starts=True)
+    st = transfer.locate_stats()
+    live = used & (t != M.TAG_NUL) & ((t & M.TAG_REQ) == 0)
+    bdy = (t & M.TAG_BDY) != 0
+    assert st["nvol"] == int((live & ~bdy).sum())
+    assert st["nbdy"] == int((live & bdy).sum())
+    assert st["nclosest"] == 0 and st["nexhaust"] == 0
+    starts = transfer.starts()
+    edge, vert = transfer.border()
+    r = transfer.download()
+    assert np.all(starts[~used] == 0) and np.all(edge[~used] == -1) and np.all(vert[~used] == -1)
+    assert np.all(r.elem[~used] == 0) and np.all(r.status[~used] == 0) and np.all(r.steps[~used] == 0)
+    assert np.all(r.status[live] != 0)
+    # the same points with the tets given afterwards (pmx_upload_new_tets
+    # before the step): the same orphans
+    transfer.upload_points(x, t, tets)
+    transfer.upload_new_tets(tets)
+    transfer.run()
+    st2 = transfer.locate_stats()
+    assert (st2["nvol"], st2["nbdy"], st2["nclosest"]) == (st["nvol"], st["nbdy"], 0)
+    r2 = transfer.download()
+    assert np.all(r2.elem[~used] == 0) and np.array_equal(r2.elem, r.elem)
+
+
+def test_undersized_host_outputs_refused(transfer):
+    """Every host-output call checks the caller's capacity before writing:
+    an array one entry short returns 0 with the reason and stays untouched
+    (r04: an output sized by a wrong tet count was written past)."""
+    import ctypes as C
+    m, x, t, sols = cube_case(5, metric="iso", surface=True)
+    n = len(x)
+    pool = np.arange(n)
+    rng = np.random.default_rng(3)
+    tets = np.zeros((n + 1, 4), np.int32)
+    tets[1:] = rng.choice(pool, size=(n, 4))
+    tets[1:, 0] = pool
+    tets[0] = -1
+    transfer.upload_background(m, sols, 0)
+    transfer.upload_points(x, t, tets)
+    transfer.run()
+    lib, ctx = transfer.lib, transfer.ctx
+    ip = lambda a: a.ctypes.data_as(N.iptr)
+    dp = lambda a: a.ctypes.data_as(N.dptr)
+    short = np.full(n - 1 + 8, -5, np.int32)        # room for n-1 (+ a guard)
+    views = (N.SolView * len(sols))()
+    arrs = [np.full((n - 1 + 8) * s.shape[1], -5.0) for s in sols]
+    for i, (a, s) in enumerate(zip(arrs, sols)):
+        views[i].size, views[i].m = s.shape[1], dp(a)
+
+    def refused(rc, what):
+        assert rc == 0, what
+        err = lib.pmx_last_error(ctx).decode()
+        assert "capacity" in err or "holds" in err, err
+
+    refused(lib.pmx_download(ctx, views, n - 1, ip(short), None, None), "pmx_download")
+    assert np.all(short == -5) and all(np.all(a == -5.0) for a in arrs)
+    refused(lib.pmx_download_starts(ctx, ip(short), n - 1), "pmx_download_starts")
+    refused(lib.pmx_download_border(ctx, ip(short), ip(short), n - 1), "pmx_download_border")
+    assert np.all(short == -5)
+    q = np.full(n + 8, -5.0)
+    refused(lib.pmx_new_mesh_qual(ctx, None, 0, 0, N.INQUA, 0, dp(q), n, None), "pmx_new_mesh_qual")
+    refused(lib.pmx_new_mesh_qual_synced(ctx, None, N.INQUA, 1, dp(q), 8, n, None), "pmx_new_mesh_qual_synced")
+    assert np.all(q == -5.0)
+    # the right sizes work
+    full = np.zeros(n, np.int32)
+    assert lib.pmx_download_starts(ctx, ip(full), n) == 1
+    q2 = np.full(n + 1, -5.0)
+    assert lib.pmx_new_mesh_qual(ctx, None, 0, 0, N.INQUA, 0, dp(q2), n + 1, None) == 1
+    assert np.all(q2[1:] >= 0.0)             # (random tets: many inverted, quality 0)
+    # the background's qualities
+    qb = np.full(m.ne + 8, -5.0)
+    refused(lib.pmx_tetra_qual(ctx, 0, dp(qb), m.ne), "pmx_tetra_qual")
+    assert np.all(qb == -5.0)
+    assert lib.pmx_tetra_qual(ctx, 0, dp(qb), m.ne + 1) == 1

@@ -325,3 +325,73 @@ def test_tetra_qual_ridge_metric_storage(transfer, metric):
         metn = np.concatenate([np.zeros((1, 6)), r.sols[0]])
     on = O.tetra_qual(nm, metn, tags=ntags, met_rid_typ=1)
     assert np.array_equal(qn.view(np.int64)[1:], on.view(np.int64)[1:])
+
+
+def assert_len_exact(L, Lo):
+    """Tensor-metric lengths: sqrt and divisions correctly rounded on both
+    sides, no log1p -- counts, bins, extrema and their endpoints bit for bit."""
+    for f in ("ned", "nullEdge", "amin", "bmin", "amax", "bmax"):
+        assert L[f] == Lo[f], (f, L[f], Lo[f])
+    assert L["hl"] == Lo["hl"], (L["hl"], Lo["hl"])
+    assert L["lmin"] == Lo["lmin"] and L["lmax"] == Lo["lmax"], (L, Lo)
+    assert abs(L["avlen"] - Lo["avlen"]) <= 1e-12 * abs(Lo["avlen"])
+
+
+@pytest.mark.parametrize("mrt", [0, 1])
+@pytest.mark.parametrize("with_surface", [False, True])
+def test_prilen_tensor_surface_and_ridge_storage(transfer, mrt, with_surface):
+    """PMMG_prilen with a tensor metric, centralized (MMG3D_computePrilen):
+    metRidTyp 0 = MMG5_lenedg33_ani, 1 = MMG5_lenedg_ani -- ParMmg's own output
+    call PMMG_prilen(parmesh,1,0) (src/libparmmg1.c:964) -- with Mmg's surface
+    data (xTetra edge tags, point / xPoint normals: MMG5_lenSurfEdg*_ani,
+    MMG5_buildridmet) or without (no xTetra): bit-exact against the oracle's
+    restatement."""
+    from helpers import cube_surface
+    m = M.kuhn_cube(9)
+    tags, surf, met = cube_surface(m, noise=0.08)
+    met = met * 0.01                       # lengths spread over the bins
+    transfer.upload_background(m, [met], 0)
+    transfer.upload_point_tags(tags)
+    if with_surface:
+        transfer.upload_surface(surf)
+    L = transfer.prilen(met_rid_typ=mrt)
+    Lo = O.prilen(m, met, tags=tags, met_rid_typ=mrt, surface=surf if with_surface else None)
+    assert_len_exact(L, Lo)
+    assert sum(1 for h in Lo["hl"] if h) >= 4
+
+
+@pytest.mark.parametrize("mrt", [0, 1])
+def test_distributed_prilen_tensor_surface(transfer, mrt):
+    """The distributed PMMG_computePrilen with a tensor metric on two
+    partitions: the owned parallel edges by MMG5_lenSurfEdg33_ani (isedg from
+    the edge's hash tag) or, with metRidTyp 1, by MMG5_lenSurfEdg_iso on the
+    metric array read as isotropic (src/quality_pmmg.c:462-466, as written),
+    then the tet edges along the surface; every rank's partial bit-exact
+    against the oracle, and the RCCL-free fold of both equals the oracle's."""
+    from helpers import cube_surface
+    full = M.kuhn_cube(7)
+    parts, nshared = split_partitions(full)
+    rng = np.random.default_rng(8)
+    for rank, (mr, glob, par) in enumerate(parts):
+        tags, surf, met = cube_surface(mr, noise=0.08, seed=rank + 1)
+        met = np.abs(met) * 0.01 + 1e-3    # positive everywhere: the flat read stays finite
+        met[0] = 1.0
+        ptag = np.where(rng.random(len(par["a"])) < 0.3, 2, 0).astype(np.uint16)
+        p = dict(par, myrank=rank, owner=np.zeros(len(par["a"]), np.int32), exact_once=0, tag=ptag)
+        transfer.upload_background(mr, [met], 0)
+        transfer.upload_point_tags(tags)
+        transfer.upload_surface(surf)
+        L = transfer.prilen(met_rid_typ=mrt, par=p)
+        Lo = O.prilen(mr, met, tags=tags, par=p, met_rid_typ=mrt, surface=surf)
+        assert_len_exact(L, Lo)
+
+
+def test_prilen_ridge_storage_needs_tags(transfer):
+    """metRidTyp 1 with a tensor metric reads the point tags (ridge points):
+    without them the call is refused, not computed as if there were none."""
+    m, x, t, sols = cube_case(5, metric="ani", fields=False)
+    transfer.upload_background(m, sols, 0)
+    with pytest.raises(RuntimeError, match="point tags"):
+        transfer.prilen(met_rid_typ=1)
+    with pytest.raises(RuntimeError, match="point tags"):
+        transfer.tetra_qual(m.ne, 1)

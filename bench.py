@@ -110,24 +110,74 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def cpu_share() -> tuple[int, list[int]]:
+    """The CPUs this process may use: its affinity set, capped by the cgroup
+    quota (cpu.max "quota period"; a GPU box of this pool: 16 of 256)."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        cpus = list(range(os.cpu_count() or 1))
+    k = len(cpus)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            k = min(k, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return k, cpus
+
+
+def mem_budget() -> float:
+    """Bytes the CPU baseline may allocate: 60 % of min(MemAvailable, the
+    cgroup's memory.max minus its current use)."""
+    avail = None
+    try:
+        for line in open("/proc/meminfo"):
+            if line.startswith("MemAvailable:"):
+                avail = int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    try:
+        mx = open("/sys/fs/cgroup/memory.max").read().strip()
+        cur = int(open("/sys/fs/cgroup/memory.current").read().strip())
+        if mx != "max":
+            room = int(mx) - cur
+            avail = room if avail is None else min(avail, room)
+    except (OSError, ValueError):
+        pass
+    return 0.6 * (avail if avail is not None else 64e9)
+
+
+def _cpu_rank_pinned(args):
+    """A forked child pinned to one core of the share, then one oracle 'rank'."""
+    r, core = args
+    os.sched_setaffinity(0, {core})
+    return _cpu_rank(r)
+
+
 def cpu_baseline_node(m, x, t, sols, budget_s: float = 20.0) -> dict:
     """K concurrent single-core oracle processes on the same workload, the
     ParMmg model of one MPI rank per core: each measures its
     own step rate while the others run (shared memory bandwidth included);
     the node rate is their sum.  Forked BEFORE any GPU initialisation.  K =
-    the cores this process may use, at most 16 (a GPU box's CPU share), and
-    bounded by memory (the oracle's per-process precompute ~110 B/tet)."""
+    the process's CPU share (affinity and cgroup quota), each child pinned to
+    its own core of it (os.sched_setaffinity, the `taskset` of SURVEY.md 8(d)),
+    fewer only if the oracle's per-process memory (faceAreas & co., ~110 B
+    per tet, the reference's own PMMG_precompute_faceAreas footprint) would not
+    fit the memory left (MemAvailable, cgroup memory.max)."""
     import multiprocessing as mp
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except AttributeError:
-        avail = os.cpu_count() or 1
-    K = max(1, min(16, avail, int(100e9 // max(1, m.ne * 110))))
+    share, cpus = cpu_share()
+    per_proc = max(1, m.ne * 110 + len(x) * 64)
+    budget = mem_budget()
+    K = max(1, min(share, len(cpus), int(budget // per_proc)))
     _CPU_CASE["case"] = (m, x, t, sols, budget_s)
     with mp.get_context("fork").Pool(K) as pool:
-        res = pool.map(_cpu_rank, range(K))
+        res = pool.map(_cpu_rank_pinned, [(r, cpus[r % len(cpus)]) for r in range(K)])
     rates = [r[0] for r in res]
     return {"value": float(sum(rates)), "unit": "vertices/s", "cores": K, "kind": "port",
+            "cpu_share": share, "pinning": f"one process per core, os.sched_setaffinity to cores "
+                                           f"{cpus[:K][0]}..{cpus[:K][-1]} of the affinity set",
+            "memory_bound": K < share, "mem_budget_GB": budget / 1e9, "per_process_GB": per_proc / 1e9,
             "per_core": float(np.mean(rates)), "cpu_model": _cpu_model(),
             "sample": f"{K} concurrent processes, each: {res[0][1]}; node rate = sum of the "
                       f"{K} per-process rates (min {min(rates):.3g}, max {max(rates):.3g})"}
@@ -490,9 +540,18 @@ def main():
         tt = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
-        # one RCCL all-reduce of the quality histogram (the path's only collective)
+        # the statistics reduction, the path's only collective: with RCCL (the
+        # driver's multi-GPU runs) through the C ABI's communicator and
+        # pmx_qualhisto_allreduce / pmx_prilen_allreduce -- what the ParMmg
+        # binding links -- checked on every rank against the rank-ordered fold;
+        # the gloo rehearsal (several ranks on one GPU, where RCCL cannot run)
+        # all-gathers over torch.distributed instead
         from parmmg_amd import shard
-        qs = shard.qualhisto_allreduce(tr, dist, local)
+        if args.dist_backend == "nccl":
+            qs = shard.binding_collectives(trs, dist, rank, world, local)
+        else:
+            qs = shard.qualhisto_allreduce(tr, dist, local)
+            qs["path"] = "torch.distributed all-gather (gloo rehearsal)"
     npts = len(x)
     total_pts = sum(len(c[1]) for c in cases) * world * args.steps
     value = total_pts / el
@@ -545,6 +604,12 @@ def main():
         "locate": st,
     }
     if cpu is not None:
+        if pcie is not None:
+            # what ParMmg sees (the binding's two seams per iteration, host
+            # buffers in and out) against the CPU node and one CPU core
+            b = pcie["binding_cycle"]["value"]
+            cpu["binding_cycle"] = {"vertices_per_s": b, "speedup_vs_node": b / cpu["value"],
+                                    "speedup_vs_core": b / cpu["per_core"]}
         out["cpu_baseline"] = cpu
     if pcie is not None:
         out["pcie_inclusive"] = pcie

@@ -677,7 +677,13 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   // line written while it is in cache, not once per solution) and chunks
   // whose DMA overlaps the packing of the next
   double *hs = (double *)(stg + o_s);
-  memset(hs, 0, (size_t)std::max(S, 1) * sizeof(double));   // row 0 (unused slot)
+  // row 0: Mmg's unused slot, as the caller holds it (no kernel reads a
+  // vertex 0 -- but PMMG_prilen's parallel edges with a tensor metric and
+  // metRidTyp = 1 read met->m[ip] flat, src/quality_pmmg.c:466, i.e. row 0
+  // for ip < 6)
+  memset(hs, 0, (size_t)std::max(S, 1) * sizeof(double));
+  for (int s = 0; s < nsol; s++)
+    for (int j = 0; j < sols[s].size; j++) hs[sd.off[s] + j] = sols[s].m[j];
   if (S == 0) {
     memset(hs, 0, hs_n * sizeof(double));
     CK(hipMemcpyAsync(ctx->d_sol.p, hs, hs_n * sizeof(double), hipMemcpyHostToDevice, st));
@@ -1003,9 +1009,9 @@ static bool run_flags_valid(int flags, std::string *err) {
   }
   const int e = (flags >> PMX_RUN_EXP_SHIFT) & 0xff;
   switch (e) {
-    case 0: case 6: case 9: case 10: case 11: case 12:
+    case 0: case 6: case 9: case 10: case 11: case 12: case 13: case 15:
       return true;
-    case 4: case 5: {
+    case 4: case 5: case 14: {
       const char *v = getenv("PMX_EXPERIMENTS");
       if (v && v[0] == '1') return true;
       *err = "pmx_run: measurement switch needs PMX_EXPERIMENTS=1";
@@ -1070,10 +1076,19 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     if (!ctx->build_node_trias(ss)) return 0;
     ctx->have_csr = true;
   }
+  // exp 15 (A/B): no fixed-point copy of the vertices -- the hint build
+  // quantises the sampled tets' vertices itself -- and the tria normals on
+  // the surface stream
+  const int exp = (opts.flags >> PMX_RUN_EXP_SHIFT) & 0xff;
+  const bool hint_xyz = exp == 15 && (opts.hint_stride == 0 || opts.hint_stride == PMX_HINT_STRIDE);
   if (derive) {
-    launch_bg_derive(ctx->d_xyz.p, ctx->np, ctx->grid, ctx->d_xyzq.p, ctx->d_tris.p, ctx->nt,
-                     ctx->d_trn.p, st);
-    ctx->have_derived = true;
+    if (hint_xyz)
+      launch_bg_derive(ctx->d_xyz.p, 0, ctx->grid, ctx->d_xyzq.p, ctx->d_tris.p, ctx->nt, ctx->d_trn.p,
+                       (bdy && !serial) ? side : st);
+    else
+      launch_bg_derive(ctx->d_xyz.p, ctx->np, ctx->grid, ctx->d_xyzq.p, ctx->d_tris.p, ctx->nt,
+                       ctx->d_trn.p, st);
+    ctx->have_derived = !hint_xyz;
   }
   if (ev) CK(hipEventRecord(ev[7], st));
   if (!ctx->classify(st)) return 0;
@@ -1109,7 +1124,12 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     if (early && !fork_surface()) return 0;
     const int stride = opts.hint_stride > 0 ? opts.hint_stride : PMX_HINT_STRIDE;
     launch_hint_build(stride == PMX_HINT_STRIDE ? ctx->d_tets_s.p : nullptr, ctx->d_tets.p, ctx->ne,
-                      stride, ctx->d_grid.p, A.g, ctx->d_xyzq.p, st);
+                      stride, ctx->d_grid.p, A.g, hint_xyz ? nullptr : ctx->d_xyzq.p, ctx->d_xyz.p, st);
+    if (exp == 13 && ctx->d_wrec.p) {
+      if (!dgrow(ctx, ctx->d_hrec, (size_t)(2 * ctx->gcells))) return 0;
+      launch_hint_inline(ctx->d_grid.p, ctx->gcells, ctx->d_wrec.p, ctx->d_hrec.p, st);
+      A.hrec = ctx->d_hrec.p;
+    }
     if (ev) CK(hipEventRecord(ev[1], st));
     if (!early && !fork_surface()) return 0;
     if (ctx->nq_vol_ub) launch_walk(A, st);
@@ -1799,7 +1819,7 @@ void pmx_ctx::free_all() {
   dfree(d_kind); dfree(d_qmark); dfree(d_ctile); dfree(d_nsel); dfree(d_wmask); dfree(d_out); dfree(d_elem); dfree(d_status);
   dfree(d_steps); dfree(d_start); dfree(d_edge); dfree(d_vertex); dfree(d_list); dfree(d_found);
   dfree(d_bestk); dfree(d_best); dfree(d_ties); dfree(d_counts); dfree(d_vollist); dfree(d_bdylist);
-  dfree(d_vstat); dfree(d_bstat);
+  dfree(d_vstat); dfree(d_bstat); dfree(d_hrec);
   dfree(d_qual); dfree(d_red); dfree(d_blist); dfree(d_olist); dfree(d_ows);
   dfree(d_ptag); dfree(d_touch); dfree(d_cidx); dfree(d_intv); dfree(d_pub); dfree(d_pkey);
   dfree(d_ppt); dfree(d_pedge); dfree(d_ntetv); dfree(d_nqual); dfree(d_qtag); dfree(d_gather);

@@ -91,6 +91,7 @@ struct pmx_ctx {
   DevBuf<int> d_nsel;                   // compaction counts: volume, surface
   DevBuf<int2> d_ctile;                 // classification tile counts
   DevBuf<uint4> d_vstat, d_bstat;       // per-wave walk statistics
+  DevBuf<uint4> d_hrec;                 // exp 13: hint cells with their start record inline
   DevBuf<int> d_blist, d_olist, d_ows;
   int *d_tgrid = nullptr;
   size_t d_tgrid_cap = 0;

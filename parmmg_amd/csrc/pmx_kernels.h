@@ -34,6 +34,7 @@ struct VolArgs {
   const int8_t *kind;
   int64_t nq, ne;
   const int *grid;
+  const uint4 *hrec;            // exp 13: the hint cells with their start record inline
   GridDesc g;
   double *out;
   uint8_t *wmask;
@@ -74,7 +75,8 @@ struct ExhArgs {
 // connectivity of tets 1, 1+stride, ... (stride == PMX_HINT_STRIDE), else the
 // tet records are read strided
 void launch_hint_build(const int4 *packed, const TetRec *tets, int64_t ne, int stride, int *grid,
-                       GridDesc g, const unsigned long long *xyzq, hipStream_t s);
+                       GridDesc g, const unsigned long long *xyzq, const double *xyz, hipStream_t s);
+void launch_hint_inline(const int *grid, int64_t cells, const WRec *wr, uint4 *hrec, hipStream_t s);
 // per-background derived data: fixed-point grid coordinates of the vertices
 // (hint centroids) and the unit normals of the boundary trias
 // (PMMG_precompute_triaNormals, src/locate_pmmg.c:68-90), one launch

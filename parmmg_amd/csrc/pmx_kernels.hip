@@ -31,22 +31,25 @@ __device__ __forceinline__ int clampi(double t, int n) {
 // the fixed-point walk of k_walkq): q = (x - lo) * inv * 2^qf, clamped to
 // [0, dim * 2^qf - 1] (21 bits per axis), packed x | y << 21 | z << 42; and
 // the tria normals + areas
+// a vertex's grid coordinates in fixed point, packed x | y << 21 | z << 42
+__device__ __forceinline__ unsigned long long quant_xyz(const double *c, const GridDesc &g) {
+  unsigned long long r = 0;
+#pragma unroll
+  for (int a = 0; a < 3; a++) {
+    const double t = (c[a] - g.lo[a]) * g.inv[a] * (double)(1 << g.qf[a]);
+    const long long hi = ((long long)g.dim[a] << g.qf[a]) - 1;
+    const long long u = !(t > 0.0) ? 0 : (t >= (double)hi ? hi : (long long)t);
+    r |= (unsigned long long)u << (21 * a);
+  }
+  return r;
+}
+
 __global__ __launch_bounds__(256) void k_bg_derive(const double *__restrict__ xyz, int64_t np, GridDesc g,
                                                    unsigned long long *__restrict__ q,
                                                    const TriRec *__restrict__ tris, int64_t nt,
                                                    Pt4 *__restrict__ trn) {
   const int64_t st = (int64_t)gridDim.x * blockDim.x;
-  auto quant = [&](const double *c) {
-    unsigned long long r = 0;
-#pragma unroll
-    for (int a = 0; a < 3; a++) {
-      const double t = (c[a] - g.lo[a]) * g.inv[a] * (double)(1 << g.qf[a]);
-      const long long hi = ((long long)g.dim[a] << g.qf[a]) - 1;
-      const long long u = !(t > 0.0) ? 0 : (t >= (double)hi ? hi : (long long)t);
-      r |= (unsigned long long)u << (21 * a);
-    }
-    return r;
-  };
+  auto quant = [&](const double *c) { return quant_xyz(c, g); };
   // two vertices per thread: three 16-B loads, one 16-B store (rows 2m, 2m+1)
   const int64_t npair = (np + 2) / 2;           // vertices 0 .. np
   for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < npair; m += st) {
@@ -86,18 +89,31 @@ void launch_bg_derive(const double *xyz, int64_t np, GridDesc g, unsigned long l
 // any sampled tet of the cell is a valid start, the located tet does not
 // depend on the start (unique containing tet, or the canonical min-index tet
 // of a tie, see canonical_tet).
-template <bool PACKED>
+// FROM_XYZ (run flag exp 15, A/B of the r04 verdict's "derive fused into
+// the hint build"): the four vertices' fixed-point coordinates computed here
+// from their double rows (the same quant_xyz, so the same cells) instead of
+// gathered from the derived xyzq array -- no separate pass over the vertices
+template <bool PACKED, bool FROM_XYZ = false>
 __global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ packed,
                                                     const TetRec *__restrict__ tets, int64_t ne,
                                                     int stride, int *__restrict__ grid, GridDesc g,
-                                                    const unsigned long long *__restrict__ xyzq) {
+                                                    const unsigned long long *__restrict__ xyzq,
+                                                    const double *__restrict__ xyz) {
   const int64_t n = (ne + stride - 1) / stride;
   const int64_t t = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (t >= n) return;
   const int64_t k = 1 + t * stride;
   const int4 v = PACKED ? packed[t] : *reinterpret_cast<const int4 *>(tets + k);
   if (v.x <= 0) return;
-  const unsigned long long a = xyzq[v.x], b = xyzq[v.y], c = xyzq[v.z], d = xyzq[v.w];
+  unsigned long long a, b, c, d;
+  if constexpr (FROM_XYZ) {
+    a = quant_xyz(xyz + 3 * (int64_t)v.x, g);
+    b = quant_xyz(xyz + 3 * (int64_t)v.y, g);
+    c = quant_xyz(xyz + 3 * (int64_t)v.z, g);
+    d = quant_xyz(xyz + 3 * (int64_t)v.w, g);
+  } else {
+    a = xyzq[v.x]; b = xyzq[v.y]; c = xyzq[v.z]; d = xyzq[v.w];
+  }
   const unsigned long long M = (1ull << 21) - 1;
   int cq[3];
 #pragma unroll
@@ -110,15 +126,42 @@ __global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ pac
   grid[gcell(g, cq[0], cq[1], cq[2])] = (int)k;
 }
 void launch_hint_build(const int4 *packed, const TetRec *tets, int64_t ne, int stride, int *grid,
-                       GridDesc g, const unsigned long long *xyzq, hipStream_t s) {
+                       GridDesc g, const unsigned long long *xyzq, const double *xyz, hipStream_t s) {
   const int64_t n = (ne + stride - 1) / stride;
   const int64_t nb = std::max<int64_t>((n + 255) / 256, 1);
-  if (packed)
-    hipLaunchKernelGGL(k_hint_build<true>, dim3((unsigned)nb), dim3(256), 0, s, packed, tets, ne, stride,
-                       grid, g, xyzq);
+  if (packed && !xyzq)
+    hipLaunchKernelGGL((k_hint_build<true, true>), dim3((unsigned)nb), dim3(256), 0, s, packed, tets, ne, stride,
+                       grid, g, xyzq, xyz);
+  else if (packed)
+    hipLaunchKernelGGL((k_hint_build<true, false>), dim3((unsigned)nb), dim3(256), 0, s, packed, tets, ne, stride,
+                       grid, g, xyzq, xyz);
   else
-    hipLaunchKernelGGL(k_hint_build<false>, dim3((unsigned)nb), dim3(256), 0, s, packed, tets, ne, stride,
-                       grid, g, xyzq);
+    hipLaunchKernelGGL((k_hint_build<false, false>), dim3((unsigned)nb), dim3(256), 0, s, packed, tets, ne, stride,
+                       grid, g, xyzq, xyz);
+}
+
+// the hint cells with their start tet's compact record inline (run flag exp
+// 13, A/B of the r04 verdict's item 2a): cell c -> {k, w0, w1, w2},
+// {w3, w4, w5, 0}; the walk's first record comes with the cell (a read of
+// neighbouring cells) instead of a dependent gather of a random tet line
+__global__ __launch_bounds__(256) void k_hint_inline(const int *__restrict__ grid, int64_t cells,
+                                                     const WRec *__restrict__ wr, uint4 *__restrict__ hrec) {
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < cells;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    const int k = grid[c];
+    uint4 a = make_uint4(0u, 0u, 0u, 0u), b = make_uint4(0u, 0u, 0u, 0u);
+    if (k) {
+      const WRec r = wr[k];
+      a = make_uint4((unsigned)k, r.w[0], r.w[1], r.w[2]);
+      b = make_uint4(r.w[3], r.w[4], r.w[5], 0u);
+    }
+    hrec[2 * c] = a;
+    hrec[2 * c + 1] = b;
+  }
+}
+void launch_hint_inline(const int *grid, int64_t cells, const WRec *wr, uint4 *hrec, hipStream_t s) {
+  const int64_t nb = std::min<int64_t>(std::max<int64_t>((cells + 255) / 256, 1), 65536);
+  hipLaunchKernelGGL(k_hint_inline, dim3((unsigned)nb), dim3(256), 0, s, grid, cells, wr, hrec);
 }
 
 // the walk's compact records (WRec, pmx_device.h) from the tet records, built

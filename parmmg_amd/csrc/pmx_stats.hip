@@ -1157,7 +1157,7 @@ int pmx_upload_surface(pmx_ctx *ctx, const pmx_surface_view *sv) {
   if (nxt < 0 || nxp < 0 || (nxt > 0 && (!sv->tetra_xt || !sv->xtetra_tag || sv->tetra_stride < 4 ||
                                         sv->xtetra_stride < 12)) ||
       (!sv->point_n != !sv->point_xp) || (sv->point_n && sv->point_stride < 24) ||
-      (nxp > 0 && (!sv->xpoint_n1 || !sv->xpoint_n2 || sv->xpoint_stride < 48))) {
+      (nxp > 0 && (!sv->xpoint_n1 || !sv->xpoint_n2 || sv->xpoint_stride < 24))) {
     ctx->err = std::string(who) + ": bad view";
     return 0;
   }

@@ -247,12 +247,19 @@ __device__ __forceinline__ void walk_finish(const VolArgs &A, int64_t i, D3 p, b
       return;
     }
     A.elem[i] = cur;
-    A.status[i] = 1;
-    A.steps[i] = step;
     const int v[4] = {t.v[0], t.v[1], t.v[2], t.v[3]};
-    if (A.exp == 4) return;                      // measurement: no interpolation
-    unsigned wm = interp_layout<LAYOUT, S>(A.sol, A.sd, v, lam, A.out + i * A.sd.S);
-    A.wmask[i] = (uint8_t)(wm | A.const_bit);
+    if (A.exp == 14) {
+      // measurement (r04 verdict item 2b): status, write mask and steps in
+      // one 4-B word -- two stores fewer per point (not decoded downstream)
+      const unsigned wm = interp_layout<LAYOUT, S>(A.sol, A.sd, v, lam, A.out + i * A.sd.S);
+      A.status[i] = (int)(1u | ((wm | A.const_bit) << 2) | ((unsigned)step << 10));
+    } else {
+      A.status[i] = 1;
+      A.steps[i] = step;
+      if (A.exp == 4) return;                      // measurement: no interpolation
+      unsigned wm = interp_layout<LAYOUT, S>(A.sol, A.sd, v, lam, A.out + i * A.sd.S);
+      A.wmask[i] = (uint8_t)(wm | A.const_bit);
+    }
     s_cnt += 1; s_sum += step;
     s_max = max(s_max, (unsigned)step); s_min = min(s_min, (unsigned)step);
   } else {
@@ -414,7 +421,27 @@ __device__ __forceinline__ TetRec walk_rec(const VolArgs &A, int k) {
   else return A.tets[k];
 }
 
-template <int LAYOUT, int S, bool TIES, bool CW>
+// exp 13: the start tet and its compact record from the hint cell itself
+// (k_hint_inline), one read of neighbouring cells instead of cell -> record
+__device__ __forceinline__ int hint_with_rec(const VolArgs &A, D3 p, TetRec &t) {
+  const int cx = wclamp((p.x - A.g.lo[0]) * A.g.inv[0], A.g.dim[0]);
+  const int cy = wclamp((p.y - A.g.lo[1]) * A.g.inv[1], A.g.dim[1]);
+  const int cz = wclamp((p.z - A.g.lo[2]) * A.g.inv[2], A.g.dim[2]);
+  const int64_t c = gcell(A.g, cx, cy, cz);
+  const uint4 a = A.hrec[2 * c], b = A.hrec[2 * c + 1];
+  int k = (int)a.x;
+  if (k) {
+    WRec r;
+    r.w[0] = a.y; r.w[1] = a.z; r.w[2] = a.w; r.w[3] = b.x; r.w[4] = b.y; r.w[5] = b.z;
+    t = wrec_decode(r, A.tets, k);
+    return k;
+  }
+  k = hint_search(A.grid, A.g.dim[0], A.g.dim[1], A.g.dim[2], cx, cy, cz);
+  t = wrec_load(A.wrec, A.tets, k);
+  return k;
+}
+
+template <int LAYOUT, int S, bool TIES, bool CW, bool HREC = false>
 __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
   const int64_t b = walk_xcd_remap(blockIdx.x, gridDim.x);
   const int64_t j = b * blockDim.x + threadIdx.x;
@@ -427,14 +454,20 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
     // classification 0.15 ms of copying)
     const int64_t i = A.list[j];
     const D3 p{A.q[3 * i], A.q[3 * i + 1], A.q[3 * i + 2]};
-    int cur = walk_hint(A.grid, A.g, p);
+    TetRec t;
+    int cur;
+    if constexpr (HREC) {
+      cur = hint_with_rec(A, p, t);
+    } else {
+      cur = walk_hint(A.grid, A.g, p);
+      t = walk_rec<CW>(A, cur);
+    }
     if (A.rec_start) A.start[i] = cur;
     int ring[WALK_RING];
 #pragma unroll
     for (int r = 0; r < WALK_RING; r++) ring[r] = 0;
     int step = 0;
     bool found = false;
-    TetRec t = walk_rec<CW>(A, cur);
     double lam[4];
     // measurement switch (PMX_EXPERIMENTS=1 only): hint + its record, no walk
     const bool hint_only = A.exp == 5;
@@ -556,7 +589,9 @@ static void launch_walk_t(const VolArgs &a, int64_t nb, hipStream_t s) {
     // exp 11 / 12: 128- / 64-thread workgroups (A/B of the dispatch granularity)
     const unsigned bs = a.exp == 11 ? 128u : a.exp == 12 ? 64u : 256u;
     const unsigned nbb = (unsigned)((a.nlist + bs - 1) / bs);
-    if (a.inline_ties) hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true>), dim3(nbb), dim3(bs), 0, s, a);
+    if (a.exp == 13 && a.hrec && a.inline_ties)
+      hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true, true>), dim3(nbb), dim3(bs), 0, s, a);
+    else if (a.inline_ties) hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true>), dim3(nbb), dim3(bs), 0, s, a);
     else hipLaunchKernelGGL((k_walks<LAYOUT, S, false, true>), dim3(nbb), dim3(bs), 0, s, a);
   } else {
     if (a.inline_ties) hipLaunchKernelGGL((k_walks<LAYOUT, S, true, false>), dim3((unsigned)nb), dim3(256), 0, s, a);

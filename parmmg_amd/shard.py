@@ -125,3 +125,53 @@ def qualhisto_allreduce(tr, dist, local: int) -> dict:
     torch.cuda.synchronize()
     res["allreduce_ms"] = (time.perf_counter() - t0) * 1e3
     return res
+
+
+def binding_collectives(trs, dist, rank: int, world: int, local: int) -> dict:
+    """The statistics reduction exactly as the ParMmg binding links it
+    (integration/pmmg_pmx.c: PMMG_qualhisto / PMMG_prilen over
+    pmx_qualhisto_allreduce / pmx_prilen_allreduce, reference
+    src/quality_pmmg.c:275-306,629-678): an RCCL communicator of the C ABI
+    (pmx_comm_unique_id on rank 0, the id broadcast over the torch process
+    group as the binding broadcasts it over MPI, pmx_comm_init on every rank),
+    this rank's group partials (PMMG_qualhisto OUTQUA over all groups,
+    PMMG_prilen(parmesh,1,0) on group 0) all-gathered on the device and folded
+    in rank order.  Every rank checks its result against the rank-ordered fold
+    of the same partials gathered over the torch process group."""
+    import time
+    from .transfer import Transfer, comm_unique_id
+    obj = [comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    tr0 = trs[0]
+    comm = tr0.comm_init(world, obj[0], rank)
+    dev = torch.device("cuda", local)
+    ngrp = len(trs)
+    qp = torch.zeros((ngrp, QUAL_WORDS), dtype=torch.float64, device=dev)
+    lp = torch.zeros(LEN_WORDS, dtype=torch.float64, device=dev)
+    for g, tr in enumerate(trs):
+        tr.qualhisto_device(qp[g].data_ptr(), opt=N.OUTQUA)
+    tr0.prilen_device(lp.data_ptr(), met_rid_typ=1)
+    for tr in trs:
+        tr.synchronize()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    q = tr0.qualhisto_allreduce(comm, world, qp.data_ptr(), ngrp)
+    ln = tr0.prilen_allreduce(comm, world, lp.data_ptr())
+    ms = (time.perf_counter() - t0) * 1e3
+    Transfer.comm_destroy(comm)
+    # the check: the same partials over the torch process group, folded here
+    allq = [None] * world
+    alll = [None] * world
+    dist.all_gather_object(allq, qp.cpu().numpy())
+    dist.all_gather_object(alll, lp.cpu().numpy())
+    ref_q = fold_qual(np.concatenate(allq), np.repeat(np.arange(world, dtype=np.int32), ngrp))
+    ref_l = fold_len(np.stack(alll))
+    for k, v in ref_q.items():
+        if q[k] != v:
+            raise AssertionError(f"rank {rank}: pmx_qualhisto_allreduce {k} = {q[k]}, fold = {v}")
+    for k, v in ref_l.items():
+        if ln[k] != v:
+            raise AssertionError(f"rank {rank}: pmx_prilen_allreduce {k} = {ln[k]}, fold = {v}")
+    return {"path": "C ABI RCCL (pmx_comm_init, pmx_qualhisto_allreduce, pmx_prilen_allreduce)",
+            "ranks_checked": world, "allreduce_ms": ms, "qualhisto": q, "prilen": ln}

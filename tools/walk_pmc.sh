@@ -12,7 +12,7 @@ for v in "$@"; do
   i=0
   for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum" "SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAVE_CYCLES"; do
     i=$((i+1))
-    timeout -s KILL 150 rocprofv3 --pmc $grp --kernel-include-regex "k_walk" -f csv -d $out/v${v}_p$i -o run -- \
+    timeout -s KILL 150 rocprofv3 --pmc $grp --kernel-include-regex "${PMC_REGEX:-k_walk}" -f csv -d $out/v${v}_p$i -o run -- \
       python3 tools/sweep.py --config $cfg --rounds 1 --reps 2 --opt flags=$v > $out/v${v}_p$i.log 2>&1
     rc=$?
     echo "variant $v pmc$i [$grp] rc=$rc"

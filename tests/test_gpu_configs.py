@@ -2,8 +2,8 @@
 
 * C2 / C3 at their full benchmark sizes (the meshes bench.py builds): every
   volume point bit-exact vs the oracle's sequential run in the reference's
-  own vertex order (first visit through the new tets) or a documented tie; a
-  sample of the surface points bit-exact vs the oracle in device semantics;
+  own vertex order (first visit through the new tets) or a documented tie;
+  every surface point bit-exact vs the oracle in device semantics;
   every surface point that differs from the reference's SEQUENTIAL run falls
   in a documented class (a containing tria, or a shadow wedge/cone acceptance
   within hausd of the returned edge/vertex).
@@ -61,7 +61,7 @@ def test_full_size_parity(cfg):
 
     Volume: every point bit-exact against that run or a verified tie.
     Surface (src/locate_pmmg.c:209-334,587-723, path dependent): bit-exact in
-    device semantics on >= 5 % of the points; against the sequential run,
+    device semantics on every surface point; against the sequential run,
     every point where the two differ is checked on BOTH sides -- each answer
     is a containing tria or a wedge/cone acceptance within hausd of its
     edge/vertex -- and where both contain the point a linear field is
@@ -97,9 +97,8 @@ def test_full_size_parity(cfg):
         assert c["same"] >= c["nvol"] - max(3, c["nvol"] // 1000)
         assert np.all(r.status[vol] == 1)
         # surface, device semantics (each query from the device's start tria, the
-        # point flags as PMMG_precompute_nodeTrias leaves them): 5 % sample
-        rng = np.random.default_rng(1)
-        sample = np.sort(rng.choice(bdy, max(len(bdy) // 20, min(len(bdy), 600)), replace=False))
+        # point flags as PMMG_precompute_nodeTrias leaves them): every surface point
+        sample = bdy
         so, se, ss, _, sed, sve = o.interp(x, t, s2, imet=0, order=sample, fresh=True,
                                            start_vol=starts, start_bdy=starts)
         compare_exact((r.sols, r.elem, r.status, edge, vert), (so, se, ss, sed, sve), sample, len(s2))
@@ -118,6 +117,13 @@ def test_full_size_parity(cfg):
               f"{len(diff)} differ from the sequential run (device: {int(in_dev.sum())} containing tria, "
               f"{int(sh_dev.sum())} wedge/cone within hausd; reference: {int(in_ref.sum())} / "
               f"{int(sh_ref.sum())})")
+        # the interpolated metric where the answers differ:
+        # relative difference device vs sequential run, by class
+        rel = np.abs(r.sols[0][diff] - qo[0][diff]).max(axis=1) / np.abs(qo[0][diff]).max(axis=1)
+        for name, sel in (("both containing", in_dev & in_ref), ("wedge/cone on a side", ~(in_dev & in_ref))):
+            if sel.any():
+                print(f"{cfg} group {g}: metric rel. difference, {name}: max {rel[sel].max():.3e}, "
+                      f"median {np.median(rel[sel]):.3e} ({int(sel.sum())} points)")
         assert np.all(in_dev | sh_dev), diff[~(in_dev | sh_dev)][:10]
         assert np.all(in_ref | sh_ref), diff[~(in_ref | sh_ref)][:10]
         assert len(diff) <= 0.05 * len(bdy)
@@ -178,20 +184,50 @@ def kuhn_edges(n):
 @pytest.mark.timeout(900)
 def test_c5_share_stats_counts():
     """C5's per-GPU share (1B tets over 8 GPUs, Kuhn n = 275 = 124.8M tets):
-    element and edge counts are exact against the analytic Kuhn-cube counts."""
+    counts exact against the analytic Kuhn-cube counts, and every statistic
+    against the oracle's sequential restatement on the same mesh
+    (tests/golden/c5share_stats.json, tools/make_c5_golden.py: MMG3D_tetraQual
+    + computeInqua, MMG3D_computePrilen with its edge hash): the 5-bin
+    histogram, good / med, min / max and the element of the min, and -- for
+    the iso metric and a graded one that fills all nine bins -- ned, the
+    length histogram, lmin / lmax and their endpoints.  Sums within 1e-12;
+    the length bins allow a couple of edges within an ulp of a bound (log1p:
+    ocml vs glibc)."""
+    import json
+    gold = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                       "c5share_stats.json")))
     n = 275
     m = M.kuhn_cube(n)
+    assert (m.ne, m.np) == (gold["ne"], gold["np"])
     tr = Transfer(0)
     tr.upload_background(m, [M.on_vertices(m, M.iso_metric)], 0)
     q = tr.qualhisto()
     assert q["ne"] == 6 * n ** 3 and sum(q["his"]) == q["ne"]
     assert 0 < q["min"] <= q["max"] <= 1.0 + 1e-12
+    g = gold["qualhisto"]
+    for f in ("ne", "good", "med", "his", "min", "max", "iel"):
+        assert q[f] == g[f], (f, q[f], g[f])
+    assert abs(q["avg"] - g["avg"]) <= 1e-12 * g["avg"]
     L = tr.prilen()
     assert L["ned"] + L["nullEdge"] == kuhn_edges(n)
     assert sum(L["hl"]) == L["ned"]
     # deterministic: the same partials and the same fixed-order reduction
     for _ in range(3):
         assert tr.prilen() == L and tr.qualhisto() == q
+
+    def same_len(L, g):
+        assert (L["ned"], L["nullEdge"]) == (g["ned"], g["nullEdge"])
+        assert sum(abs(a - b) for a, b in zip(L["hl"], g["hl"])) <= 2, (L["hl"], g["hl"])
+        assert abs(L["avlen"] - g["avlen"]) <= 1e-12 * g["avlen"]
+        for e in ("lmin", "lmax"):
+            assert abs(L[e] - g[e]) <= 1e-14 * g[e], (e, L[e], g[e])
+        if L["lmin"] == g["lmin"]:
+            assert (L["amin"], L["bmin"]) == (g["amin"], g["bmin"])
+        if L["lmax"] == g["lmax"]:
+            assert (L["amax"], L["bmax"]) == (g["amax"], g["bmax"])
+    same_len(L, gold["prilen_iso"])
+    tr.upload_background(m, [M.on_vertices(m, M.graded_iso_metric(n))], 0)
+    same_len(tr.prilen(), gold["prilen_graded"])
     tr.close()
 
 

@@ -128,7 +128,7 @@ def cpu_share() -> tuple[int, list[int]]:
 
 
 def mem_budget() -> float:
-    """Bytes the CPU baseline may allocate: 60 % of min(MemAvailable, the
+    """Bytes the CPU baseline may allocate: 75 % of min(MemAvailable, the
     cgroup's memory.max minus its current use)."""
     avail = None
     try:
@@ -145,7 +145,7 @@ def mem_budget() -> float:
             avail = room if avail is None else min(avail, room)
     except (OSError, ValueError):
         pass
-    return 0.6 * (avail if avail is not None else 64e9)
+    return 0.75 * (avail if avail is not None else 64e9)
 
 
 def _cpu_rank_pinned(args):
@@ -167,7 +167,10 @@ def cpu_baseline_node(m, x, t, sols, budget_s: float = 20.0) -> dict:
     fit the memory left (MemAvailable, cgroup memory.max)."""
     import multiprocessing as mp
     share, cpus = cpu_share()
-    per_proc = max(1, m.ne * 110 + len(x) * 64)
+    # the oracle context's arrays (oracle/pmx_oracle.c orc_create: 12 face
+    # normal components, volume and flag per tet; four int arrays per vertex)
+    # plus its sample's outputs; the mesh itself is the parent's (copy on write)
+    per_proc = max(1, m.ne * 110 + m.np * 24 + len(x) * 64)
     budget = mem_budget()
     K = max(1, min(share, len(cpus), int(budget // per_proc)))
     _CPU_CASE["case"] = (m, x, t, sols, budget_s)

@@ -93,7 +93,10 @@ void launch_bg_derive(const double *xyz, int64_t np, GridDesc g, unsigned long l
 // the hint build"): the four vertices' fixed-point coordinates computed here
 // from their double rows (the same quant_xyz, so the same cells) instead of
 // gathered from the derived xyzq array -- no separate pass over the vertices
-template <bool PACKED, bool FROM_XYZ = false>
+// V0 (run flag exp 16, A/B): the cell of the sample's first vertex instead
+// of its centroid -- one 8-B gather per sample instead of four; any tet of
+// the neighbourhood is a valid start (a longer walk at most)
+template <bool PACKED, bool FROM_XYZ = false, bool V0 = false>
 __global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ packed,
                                                     const TetRec *__restrict__ tets, int64_t ne,
                                                     int stride, int *__restrict__ grid, GridDesc g,
@@ -105,6 +108,15 @@ __global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ pac
   const int64_t k = 1 + t * stride;
   const int4 v = PACKED ? packed[t] : *reinterpret_cast<const int4 *>(tets + k);
   if (v.x <= 0) return;
+  if constexpr (V0) {
+    const unsigned long long a = xyzq[v.x];
+    const unsigned long long M = (1ull << 21) - 1;
+    int cq[3];
+#pragma unroll
+    for (int ax = 0; ax < 3; ax++) cq[ax] = min((int)(((a >> (21 * ax)) & M) >> g.qf[ax]), g.dim[ax] - 1);
+    grid[gcell(g, cq[0], cq[1], cq[2])] = (int)k;
+    return;
+  }
   unsigned long long a, b, c, d;
   if constexpr (FROM_XYZ) {
     a = quant_xyz(xyz + 3 * (int64_t)v.x, g);
@@ -126,10 +138,17 @@ __global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ pac
   grid[gcell(g, cq[0], cq[1], cq[2])] = (int)k;
 }
 void launch_hint_build(const int4 *packed, const TetRec *tets, int64_t ne, int stride, int *grid,
-                       GridDesc g, const unsigned long long *xyzq, const double *xyz, hipStream_t s) {
+                       GridDesc g, const unsigned long long *xyzq, const double *xyz, hipStream_t s,
+                       bool v0) {
   const int64_t n = (ne + stride - 1) / stride;
   const int64_t nb = std::max<int64_t>((n + 255) / 256, 1);
-  if (packed && !xyzq)
+  if (v0 && xyzq && packed)
+    hipLaunchKernelGGL((k_hint_build<true, false, true>), dim3((unsigned)nb), dim3(256), 0, s, packed, tets, ne,
+                       stride, grid, g, xyzq, xyz);
+  else if (v0 && xyzq)
+    hipLaunchKernelGGL((k_hint_build<false, false, true>), dim3((unsigned)nb), dim3(256), 0, s, packed, tets, ne,
+                       stride, grid, g, xyzq, xyz);
+  else if (packed && !xyzq)
     hipLaunchKernelGGL((k_hint_build<true, true>), dim3((unsigned)nb), dim3(256), 0, s, packed, tets, ne, stride,
                        grid, g, xyzq, xyz);
   else if (packed)

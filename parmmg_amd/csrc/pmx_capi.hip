@@ -1834,6 +1834,7 @@ void pmx_ctx::free_all() {
   have_bg = have_pts = ran = have_derived = have_tetv = have_qual = have_ptag = have_qtag = have_csr = false;
   have_surf = false;
   dfree(d_etag); dfree(d_pn); dfree(d_xpn); dfree(d_pxp); dfree(d_pedge_tag);
+  dfree(d_pbcnt); dfree(d_pboff); dfree(d_pbrec); dfree(d_pbtmp);
   have_ntet = false;
   stat_np = -1;
 }

@@ -117,6 +117,11 @@ struct pmx_ctx {
   DevBuf<double> d_pn, d_xpn;
   DevBuf<int> d_pxp;
   DevBuf<uint16_t> d_pedge_tag;         // prilen: tags of the owned parallel edges
+  // prilen, edge-bucket variant (PMX_PRILEN_BUCKETS=1, A/B of the shell
+  // rotation): per-vertex counts / offsets / cursors and the candidate records
+  DevBuf<unsigned> d_pbcnt, d_pboff;
+  DevBuf<int4> d_pbrec;
+  DevBuf<char> d_pbtmp;
   int64_t stat_np = -1;                 // node count of pmx_count_nodes (-1: np)
   DevBuf<uint8_t> d_touch;
   DevBuf<int> d_cidx, d_intv;

@@ -29,6 +29,7 @@
 // hash-pop order, so endpoints and orientation of every length match it.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <hipcub/hipcub.hpp>
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
@@ -946,6 +947,119 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
   acc.store(parts + lb);
 }
 
+// ---- prilen, edge-bucket variant (A/B of the shell rotation) --------------------
+//
+// The r04 verdict's alternative to the rotation: unique edges through buckets
+// of the smaller endpoint instead of shell walks.  The face-neighbour filter
+// of k_prilen keeps the candidates (a tet's edge no smaller face neighbour
+// disowns: 1.0015 per unique edge on Kuhn meshes); each candidate goes to the
+// bucket of its smaller endpoint (counts and placement aggregated per
+// workgroup in an LDS hash, one global atomic per distinct bucket -- the
+// LDS-aggregated bucketing of pmx_topo.hip); an edge's owner is its candidate
+// with the smallest key 6 k + ia in the bucket (the reference's first
+// occurrence), found by scanning the bucket.  Point tags (the 4-ridge
+// filter disables the face filter) and the surface-aware tensor lengths keep
+// the rotation.  Selected by PMX_PRILEN_BUCKETS=1.
+#define PB_HT 2048
+__device__ __forceinline__ int pb_slot(int *keys, int a) {
+  unsigned h = ((unsigned)a * 2654435761u) >> (32 - 11);
+  for (;;) {
+    const int old = atomicCAS(&keys[h], -1, a);
+    if (old == -1 || old == a) return (int)h;
+    h = (h + 1) & (PB_HT - 1);
+  }
+}
+// the candidate edges of tet k (bit ia): valid tet, no smaller face neighbour
+// on either face containing the edge
+__device__ __forceinline__ unsigned pb_cands(const TetRec &t, int64_t k) {
+  unsigned m = 0;
+  if (t.v[0] <= 0) return 0;
+#pragma unroll
+  for (int ia = 0; ia < 6; ia++) {
+    const int n0 = pick_nb(t, oth0(ia)), n1 = pick_nb(t, oth1(ia));
+    if ((n0 && n0 < k) || (n1 && n1 < k)) continue;
+    m |= 1u << ia;
+  }
+  return m;
+}
+// PASS 0 counts, PASS 1 places: records {a, b, 6 k + ia, 0} in the reference's
+// orientation (a = v[IARE[ia][0]]), bucket = min(a, b)
+template <int PASS>
+__global__ __launch_bounds__(256) void k_pb_bucket(const TetRec *__restrict__ tets, int64_t ne,
+                                                   unsigned *__restrict__ cnt, int4 *__restrict__ rec) {
+  __shared__ int keys[PB_HT];
+  __shared__ unsigned cnts[PB_HT];
+  for (int i = threadIdx.x; i < PB_HT; i += blockDim.x) { keys[i] = -1; cnts[i] = 0u; }
+  __syncthreads();
+  const int64_t k = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x + 1;
+  TetRec t{};
+  unsigned m = 0;
+  int slot[6];
+  unsigned rank[6];
+  if (k <= ne) {
+    t = tets[k];
+    m = pb_cands(t, k);
+#pragma unroll
+    for (int ia = 0; ia < 6; ia++) {
+      slot[ia] = 0;
+      rank[ia] = 0;
+      if (!((m >> ia) & 1u)) continue;
+      const int a = pick_v(t, iare0(ia)), b = pick_v(t, iare1(ia));
+      slot[ia] = pb_slot(keys, min(a, b));
+      rank[ia] = atomicAdd(&cnts[slot[ia]], 1u);
+    }
+  }
+  __syncthreads();
+  if (PASS == 0) {
+    for (int i = threadIdx.x; i < PB_HT; i += blockDim.x)
+      if (keys[i] >= 0) atomicAdd(cnt + keys[i], cnts[i]);
+    return;
+  }
+  // one reservation per bucket: the workgroup's run starts there
+  for (int i = threadIdx.x; i < PB_HT; i += blockDim.x)
+    if (keys[i] >= 0) cnts[i] = atomicAdd(cnt + keys[i], cnts[i]);
+  __syncthreads();
+#pragma unroll
+  for (int ia = 0; ia < 6; ia++) {
+    if (!((m >> ia) & 1u)) continue;
+    const int a = pick_v(t, iare0(ia)), b = pick_v(t, iare1(ia));
+    rec[cnts[slot[ia]] + rank[ia]] = make_int4(a, b, (int)(6u * (unsigned)k + (unsigned)ia), 0);
+  }
+}
+// one thread per candidate: the owner (smallest key among the bucket's
+// candidates of the same edge) measures it
+template <bool ANI, bool PAR>
+__global__ __launch_bounds__(256) void k_pb_edges(StatArgs A, const int4 *__restrict__ rec, int64_t nrec,
+                                                  const unsigned *__restrict__ off, LenPart *parts) {
+  __shared__ unsigned lcnt[10];
+  LenAcc acc(lcnt);
+  const int64_t lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t per = ((nrec + gridDim.x - 1) / gridDim.x + 255) / 256 * 256;
+  const int64_t r0 = lb * per, r1 = min(nrec, r0 + per);
+  for (int64_t rb = r0; rb < r0 + per; rb += blockDim.x) {   // uniform trip count
+    const int64_t r = rb + threadIdx.x;
+    bool on = false;
+    double len = 0.0;
+    long long key = 0;
+    if (r < r1) {
+      const int4 e = rec[r];
+      const int lo = min(e.x, e.y), hi = max(e.x, e.y);
+      const unsigned me = (unsigned)e.z;
+      const unsigned b0 = off[lo], b1 = off[lo + 1];
+      bool own = true;
+      for (unsigned q = b0; q < b1; q++) {
+        const int4 o = rec[q];
+        own = own && !(max(o.x, o.y) == hi && (unsigned)o.z < me);
+      }
+      on = own && !(PAR && par_excluded(A, e.x, e.y));
+      if (on) len = edge_len_t<ANI>(A, e.x, e.y);
+      key = LEN_STEP2 + (long long)me;
+    }
+    acc.add(on, len, key);
+  }
+  acc.store(parts + lb);
+}
+
 // step 1 of the distributed prilen: the owned parallel edges, in list order,
 // each once (src/quality_pmmg.c:445-502); one workgroup.  The kernel the
 // reference selects at :462-466: MMG5_lenSurfEdg33_ani for a tensor metric in
@@ -1462,6 +1576,43 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
     nb = per_cu * cus / 8 * 8;
     A.sched_chunk = sched;
   }
+  // the edge-bucket variant (A/B): no point tags, no surface-aware tensor path
+  static const bool buckets = [] {
+    const char *e = getenv("PMX_PRILEN_BUCKETS");
+    return e && e[0] == '1';
+  }();
+  const bool use_pb = buckets && !A.ptag && !surf;
+  int64_t npb = 0;
+  if (use_pb) {
+    const int64_t np = ctx->np;
+    if (!pmx_dgrow(ctx, ctx->d_pbcnt, (size_t)(np + 2)) || !pmx_dgrow(ctx, ctx->d_pboff, (size_t)(np + 2)))
+      return 0;
+    size_t tb = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ctx->d_pbcnt.p, ctx->d_pboff.p, (int)(np + 2), s);
+    if (!pmx_dgrow(ctx, ctx->d_pbtmp, tb)) return 0;
+    const unsigned nbt = (unsigned)std::max<int64_t>((ctx->ne + 255) / 256, 1);
+    if (hipMemsetAsync(ctx->d_pbcnt.p, 0, (size_t)(np + 2) * sizeof(unsigned), s) != hipSuccess) return 0;
+    hipLaunchKernelGGL(k_pb_bucket<0>, dim3(nbt), dim3(256), 0, s, (const TetRec *)ctx->d_tets.p, ctx->ne,
+                       ctx->d_pbcnt.p, (int4 *)nullptr);
+    if (hipcub::DeviceScan::ExclusiveSum(ctx->d_pbtmp.p, tb, ctx->d_pbcnt.p, ctx->d_pboff.p, (int)(np + 2), s) !=
+        hipSuccess) {
+      ctx->err = "pmx_prilen: bucket scan";
+      return 0;
+    }
+    unsigned tot = 0;
+    if (hipMemcpyAsync(&tot, ctx->d_pboff.p + np + 1, sizeof tot, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      ctx->err = "pmx_prilen: bucket total";
+      return 0;
+    }
+    npb = tot;
+    if (!pmx_dgrow(ctx, ctx->d_pbrec, (size_t)std::max<int64_t>(npb, 1)) ||
+        hipMemcpyAsync(ctx->d_pbcnt.p, ctx->d_pboff.p, (size_t)(np + 2) * sizeof(unsigned), hipMemcpyDeviceToDevice,
+                       s) != hipSuccess)
+      return 0;
+    hipLaunchKernelGGL(k_pb_bucket<1>, dim3(nbt), dim3(256), 0, s, (const TetRec *)ctx->d_tets.p, ctx->ne,
+                       ctx->d_pbcnt.p, ctx->d_pbrec.p);
+  }
   if (!ensure_red(ctx, sizeof(LenPart) * ((size_t)nb + 1 + FINAL_GRID + 1))) return 0;
   LenPart *parts = (LenPart *)ctx->d_red.p;
   A.npar = (int64_t)excl.size();
@@ -1488,7 +1639,15 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
   else
     hipLaunchKernelGGL(k_prilen_par, dim3(1), dim3(256), 0, s, A, (const int2 *)nullptr, (const uint16_t *)nullptr,
                        (int64_t)0, parts);
-  hipLaunchKernelGGL(kern, dim3(nb), dim3(256), 0, s, A, parts + 1);
+  if (use_pb) {
+    using KP = void (*)(StatArgs, const int4 *, int64_t, const unsigned *, LenPart *);
+    static const KP kp[2][2] = {{k_pb_edges<false, false>, k_pb_edges<false, true>},
+                                {k_pb_edges<true, false>, k_pb_edges<true, true>}};
+    hipLaunchKernelGGL(kp[ani ? 1 : 0][A.npar ? 1 : 0], dim3(nb), dim3(256), 0, s, A, (const int4 *)ctx->d_pbrec.p,
+                       npb, (const unsigned *)ctx->d_pboff.p, parts + 1);
+  } else {
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(256), 0, s, A, parts + 1);
+  }
   LenPart *mid = parts + 1 + nb;
   hipLaunchKernelGGL(k_prilen_final, dim3(FINAL_GRID), dim3(256), 0, s, parts, nb + 1, mid,
                      (pmx_len_part *)nullptr, ctx->d_tets.p, (const int2 *)ctx->d_pedge.p);

@@ -19,7 +19,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
   "TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum" \
   "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_THREAD_CYCLES_VALU SQ_CYCLES"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-include-regex "k_qual|k_prilen" -f csv -d $out/pmc$i -o run -- \
+  timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-include-regex "k_qual|k_prilen|k_pb_" -f csv -d $out/pmc$i -o run -- \
     python3 tools/bench_stats.py --reps 2 $args > $out/pmc$i.log 2>&1
   rc=$?
   echo "pmc$i [$grp] rc=$rc"

@@ -521,6 +521,7 @@ def main():
     st["volume_waves"] = tr.wave_stats(0)
     from parmmg_amd import mesh as M
     st["wrec_escapes"] = M.wrec_escapes(m)
+    st["wrec_far_fields"], st["wrec_tets_with_far_fields"] = M.wrec_far_fields(m)
     # the same step on a background already prepared by an earlier step (what
     # repeated steps on one background cost; reported, never `value`)
     sync()

@@ -55,7 +55,8 @@ struct VolArgs {
   int ref_walk;                 // 1: k_walk (reference-order walk) instead of k_walks
   int rec_start;                // write the start tet of every point (diagnostics)
   int exp;                      // measurement switch (tools/walk_pmc.sh): 0 production,
-                                // 4 no interpolation, 5 hint + hint record only
+                                // 4 no interpolation, 5 hint + hint record only,
+                                // 17 a record with a far neighbour field read whole
 };
 
 struct ExhArgs {

@@ -212,7 +212,7 @@ __device__ __forceinline__ bool face_tie(const VolArgs &A, D3 p, int &cur, TetRe
   }
   if (nnear == 0) return false;
   if (nnear > 1) return true;
-  const int n = pick4(t.nb, f1);
+  const int n = wrec_resolve(pick4(t.nb, f1), A.tets, cur);   // a far field of a compact record
   const TetRec u = A.tets[n];
   if (u.v[0] <= 0) return false;
   const D3 Q[4] = {ld3(A.xyz, u.v[0]), ld3(A.xyz, u.v[1]), ld3(A.xyz, u.v[2]), ld3(A.xyz, u.v[3])};
@@ -415,10 +415,17 @@ __device__ __forceinline__ int exact_next(const TetRec &t, const double lam[4], 
 }
 
 // the walk's tet record: through the compact copy (CW) or the full record
+// (whole: exp 17, A/B of the per-field escapes -- a record with a far field
+// is read whole from the 32-B records, the r04 rule)
 template <bool CW>
-__device__ __forceinline__ TetRec walk_rec(const VolArgs &A, int k) {
-  if constexpr (CW) return wrec_load(A.wrec, A.tets, k);
-  else return A.tets[k];
+__device__ __forceinline__ TetRec walk_rec(const VolArgs &A, int k, bool whole = false) {
+  if constexpr (CW) {
+    TetRec t = wrec_load(A.wrec, A.tets, k);
+    if (whole && (t.nb[0] | t.nb[1] | t.nb[2] | t.nb[3]) < 0) t = A.tets[k];
+    return t;
+  } else {
+    return A.tets[k];
+  }
 }
 
 // exp 13: the start tet and its compact record from the hint cell itself
@@ -460,7 +467,7 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
       cur = hint_with_rec(A, p, t);
     } else {
       cur = walk_hint(A.grid, A.g, p);
-      t = walk_rec<CW>(A, cur);
+      t = walk_rec<CW>(A, cur, A.exp == 17);
     }
     if (A.rec_start) A.start[i] = cur;
     int ring[WALK_RING];
@@ -499,21 +506,31 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
         ring[0] = cur;
         // the admissible slot (interior, not recently visited neighbour) with
         // the smallest barycentric
+        // smallest barycentric; a far field (< 0, pmx_wrec.h) counts as
+        // admissible until it is chosen, then is resolved from the full record
+        // and the choice made again (the same choice as on resolved fields)
         int sb = -1;
-        double wb = 0.0;
+        for (int it = 0; it < 5; it++) {
+          sb = -1;
+          double wb = 0.0;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const int nb = NB[k];
-          bool seen = false;
+          for (int k = 0; k < 4; k++) {
+            const int nb = NB[k];
+            bool seen = false;
 #pragma unroll
-          for (int q = 0; q < WALK_RING; q++) seen |= (ring[q] == nb);
-          const bool take = nb && !seen && (sb < 0 || w[k] < wb);
-          sb = take ? k : sb;
-          wb = take ? w[k] : wb;
+            for (int q = 0; q < WALK_RING; q++) seen |= (ring[q] == nb);
+            const bool take = nb && !seen && (sb < 0 || w[k] < wb);
+            sb = take ? k : sb;
+            wb = take ? w[k] : wb;
+          }
+          if (sb < 0 || pick4(NB, sb) > 0) break;
+          const int r = wrec_resolve(pick4(NB, sb), A.tets, cur);
+#pragma unroll
+          for (int k = 0; k < 4; k++) NB[k] = (k == sb) ? r : NB[k];
         }
         if (sb < 0) break;
         const int next = pick4(NB, sb);
-        const TetRec u = walk_rec<CW>(A, next);
+        const TetRec u = walk_rec<CW>(A, next, A.exp == 17);
         cur = next;
         t = u;
         if (u.v[0] <= 0) break;                            // !MG_EOK: let the scan decide
@@ -564,6 +581,7 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
           const double lmin = fmin(fmin(lam[0], lam[1]), fmin(lam[2], lam[3]));
           if (lmin > -PMX_EPS) { found = true; break; }    // src/barycoord_pmmg.c:102-107
           if (step >= A.max_walk) break;
+          if ((t.nb[0] | t.nb[1] | t.nb[2] | t.nb[3]) < 0) t = A.tets[cur];   // far fields
           const int next = exact_next(t, lam, ring, cur);
           if (!next) break;
           t = A.tets[next];

@@ -20,10 +20,16 @@ struct alignas(32) TetRec { int v[4]; int nb[4]; };
 //   w0 = v0            w1 = dn0 | dv1[0:8)<<24   w2 = dn1 | dv1[8:16)<<24
 //   w3 = dn2 | dv1[16:20)<<24 | flags<<28       w4 = dn3 | dv2[0:8)<<24
 //   w5 = dv2[8:20) | dv3<<12
-// A tet whose deltas do not fit gets WREC_ESC and is read from tets[] (a
-// Mmg mesh after its Scotch renumbering, like the generator's, has none).
+// A neighbour delta that does not fit escapes only its own field: the field
+// holds WREC_FAR and decodes to -(f+1), "read tets[k].nb[f]" -- the walk
+// resolves it (one 4-B read) only when it crosses that face (an Mmg-appended
+// numbering puts 10 % of the tets far from their neighbours, which flags 41 %
+// of the records in one face or more, r04 verdict).  A tet whose VERTEX
+// deltas do not fit gets WREC_ESC and is read whole from tets[] (a Mmg mesh
+// after its Scotch renumbering, like the generator's, has neither).
 struct alignas(8) WRec { unsigned w[6]; };
 #define WREC_NONE (-(1 << 23))
+#define WREC_FAR (-(1 << 23) + 1)
 #define WREC_ESC 1u
 
 PMX_HD void wrec_encode(const TetRec &t, int64_t k, WRec &r) {
@@ -39,8 +45,8 @@ PMX_HD void wrec_encode(const TetRec &t, int64_t k, WRec &r) {
   }
   for (int f = 0; f < 4; f++) {
     const int64_t d = (int64_t)t.nb[f] - k;
-    esc = esc || (t.nb[f] != 0 && (d <= WREC_NONE || d >= (1 << 23)));
-    dn[f] = t.nb[f] ? (int)d : WREC_NONE;
+    const bool far = t.nb[f] != 0 && (d <= WREC_FAR || d >= (1 << 23));
+    dn[f] = !t.nb[f] ? WREC_NONE : far ? WREC_FAR : (int)d;
   }
   if (esc) { r.w[3] = WREC_ESC << 28; return; }
   const unsigned m24 = 0xffffffu;
@@ -51,14 +57,21 @@ PMX_HD void wrec_encode(const TetRec &t, int64_t k, WRec &r) {
   r.w[5] = (((unsigned)dv[2] >> 8) & 0xfffu) | ((unsigned)dv[3] << 12);
 }
 
-PMX_HD int wrec_nb(unsigned w, int k) {
+// neighbour across face f: 0 boundary, -(f+1) far (tets[k].nb[f] holds it)
+PMX_HD int wrec_nb(unsigned w, int k, int f) {
   const int d = (int)(w << 8) >> 8;               // sign-extended 24 bits
-  return d == WREC_NONE ? 0 : k + d;
+  return d == WREC_NONE ? 0 : d == WREC_FAR ? -(f + 1) : k + d;
 }
 
-// tets[k] from its compact record r (escapes read the full record).  Decoded
-// before the escape test, so that a caller's record load is one load (a test
-// first would split off the flag word into a dependent load of its own).
+// a decoded neighbour with its far field resolved
+PMX_HD int wrec_resolve(int nb, const TetRec *__restrict__ tets, int k) {
+  return nb < 0 ? tets[k].nb[-nb - 1] : nb;
+}
+
+// tets[k] from its compact record r (a whole-tet escape reads the full record;
+// far neighbour fields stay -(f+1), see wrec_resolve).  Decoded before the
+// escape test, so that a caller's record load is one load (a test first would
+// split off the flag word into a dependent load of its own).
 PMX_HD TetRec wrec_decode(const WRec &r, const TetRec *__restrict__ tets, int k) {
   const int v0 = (int)r.w[0];
   const unsigned u1 = (r.w[1] >> 24) | ((r.w[2] >> 24) << 8) | (((r.w[3] >> 24) & 0xfu) << 16);
@@ -68,10 +81,10 @@ PMX_HD TetRec wrec_decode(const WRec &r, const TetRec *__restrict__ tets, int k)
   t.v[1] = v0 + ((int)(u1 << 12) >> 12);
   t.v[2] = v0 + ((int)(u2 << 12) >> 12);
   t.v[3] = v0 + ((int)r.w[5] >> 12);
-  t.nb[0] = wrec_nb(r.w[1], k);
-  t.nb[1] = wrec_nb(r.w[2], k);
-  t.nb[2] = wrec_nb(r.w[3], k);
-  t.nb[3] = wrec_nb(r.w[4], k);
+  t.nb[0] = wrec_nb(r.w[1], k, 0);
+  t.nb[1] = wrec_nb(r.w[2], k, 1);
+  t.nb[2] = wrec_nb(r.w[3], k, 2);
+  t.nb[3] = wrec_nb(r.w[4], k, 3);
   if ((r.w[3] >> 28) & WREC_ESC) t = tets[k];
   return t;
 }

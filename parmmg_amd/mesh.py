@@ -246,17 +246,26 @@ def numbering(m: Mesh, kind: str, seed: int = 7):
 
 
 def wrec_escapes(m: Mesh) -> int:
-    """Tets whose walk record does not fit the 24-B encoding (pmx_wrec.h): a
-    vertex delta from v[0] outside [-2^19, 2^19) or a neighbour delta from the
-    tet index outside (-2^23, 2^23); the walk reads those from the 32-B records."""
+    """Tets whose walk record escapes whole (pmx_wrec.h): a vertex delta from
+    v[0] outside [-2^19, 2^19); the walk reads those from the 32-B records."""
     t = m.tet[1:].astype(np.int64)
     valid = t[:, 0] > 0
     dv = t[:, 1:] - t[:, :1]
     esc = np.any((dv < -(1 << 19)) | (dv >= (1 << 19)), axis=1)
+    return int(np.count_nonzero(esc & valid))
+
+
+def wrec_far_fields(m: Mesh):
+    """Neighbour fields of the walk records that escape alone (pmx_wrec.h): a
+    delta from the tet index outside (-2^23 + 1, 2^23), the walk reading that
+    neighbour from the 32-B record when it crosses the face.  Returns (far
+    fields, tets with one or more)."""
+    t = m.tet[1:].astype(np.int64)
+    valid = t[:, 0] > 0
     nb = (m.adja[1:4 * m.ne + 1].reshape(m.ne, 4) >> 2).astype(np.int64)
     dn = nb - np.arange(1, m.ne + 1, dtype=np.int64)[:, None]
-    esc |= np.any((nb != 0) & ((dn <= -(1 << 23)) | (dn >= (1 << 23))), axis=1)
-    return int(np.count_nonzero(esc & valid))
+    far = (nb != 0) & ((dn <= -(1 << 23) + 1) | (dn >= (1 << 23))) & valid[:, None]
+    return int(np.count_nonzero(far)), int(np.count_nonzero(far.any(axis=1)))
 
 
 def iso_metric(x: np.ndarray) -> np.ndarray:

@@ -1,14 +1,15 @@
 // Round trip of the walk's compact tet records (parmmg_amd/csrc/pmx_wrec.h),
 // host-only (g++, ASan/UBSan): every valid tet decodes to its record, through
-// the packed fields or through the escape to the full record; deltas at the
-// field limits, boundary faces, deleted tets.
+// the packed fields, through a far neighbour field resolved from the full
+// record, or through the whole-tet escape; deltas at the field limits,
+// boundary faces, deleted tets.
 #include <cstdio>
 #include <cstdlib>
 #include <random>
 #include <vector>
 #include "pmx_wrec.h"
 
-static int check(const std::vector<TetRec> &tets, long long *nesc) {
+static int check(const std::vector<TetRec> &tets, long long *nesc, long long *nfar) {
   int bad = 0;
   for (size_t k = 1; k < tets.size(); k++) {
     WRec r;
@@ -19,7 +20,11 @@ static int check(const std::vector<TetRec> &tets, long long *nesc) {
       bad += t.v[0] != tets[k].v[0];
       continue;
     }
-    for (int i = 0; i < 4; i++) bad += (t.v[i] != tets[k].v[i]) + (t.nb[i] != tets[k].nb[i]);
+    for (int i = 0; i < 4; i++) {
+      *nfar += t.nb[i] < 0;
+      bad += t.nb[i] < 0 && t.nb[i] != -(i + 1);
+      bad += (t.v[i] != tets[k].v[i]) + (wrec_resolve(t.nb[i], tets.data(), (int)k) != tets[k].nb[i]);
+    }
   }
   return bad;
 }
@@ -50,10 +55,11 @@ int main() {
       t.nb[f] = (rng() % 6 == 0 || nb < 1 || nb > 2000000000LL) ? 0 : (int)nb;
     }
   }
-  long long nesc = 0;
-  const int bad = check(tets, &nesc);
-  printf("wrec roundtrip: %d tets, %lld escaped, %d mismatches\n", n, nesc, bad);
-  if (bad || nesc == 0 || nesc == n) return 1;
+  long long nesc = 0, nfar = 0;
+  const int bad = check(tets, &nesc, &nfar);
+  printf("wrec roundtrip: %d tets, %lld escaped, %lld far neighbour fields, %d mismatches\n", n, nesc, nfar,
+         bad);
+  if (bad || nesc == 0 || nesc == n || nfar == 0) return 1;
   printf("wrec roundtrip ok\n");
   return 0;
 }

@@ -70,3 +70,60 @@ def test_escaped_records(transfer):
     # went through the right vertices of the escaped records)
     ref = lin_field(x[vol])[:, 0]
     assert np.max(np.abs(a[2][1][vol, 0] - ref)) < 1e-12
+
+
+FAR_AS_WHOLE = 17 << 16           # exp 17: a record with a far field read whole (r04 rule, A/B)
+
+
+def _gapped(m, gap):
+    """m with its tets k > ne - ne // 10 moved up by `gap` indices (deleted
+    tets in between): every neighbour delta across the gap is far."""
+    ne = m.ne
+    k0 = ne - ne // 10
+    new = np.arange(ne + 1, dtype=np.int64)
+    new[k0 + 1:] += gap
+    tet = np.zeros((ne + gap + 1, 4), np.int32)
+    tet[new[1:]] = m.tet[1:]
+    old = m.adja[1:4 * ne + 1].reshape(ne, 4).astype(np.int64)
+    adja = np.zeros(4 * (ne + gap) + 1, np.int32)
+    rows = np.where(old > 0, 4 * new[old >> 2] + (old & 3), 0).astype(np.int32)
+    adja[1:].reshape(ne + gap, 4)[new[1:] - 1] = rows
+    return M.Mesh(m.xyz, tet, adja, m.tria, m.adjt, m.hausd), new
+
+
+def test_far_neighbour_fields(transfer):
+    """Mmg-appended numbering past the 24-bit neighbour field (r04 verdict
+    item 7): 10 % of the tets moved to the end, more than 2^23 indices away
+    (deleted tets in between).  Every face across the gap escapes alone
+    (pmx_wrec.h WREC_FAR) and is resolved when a walk crosses it.  The
+    compact walk, the 32-B walk and the whole-record rule of r04 (exp 17)
+    locate and interpolate bit for bit alike, and equal the same mesh without
+    the gap (tet indices shifted back)."""
+    n = 16
+    m0, _ = M.numbering(M.kuhn_cube(n), "appended")
+    m, new = _gapped(m0, (1 << 23) + 5)
+    nfar, ntf = M.wrec_far_fields(m)
+    assert M.wrec_escapes(m) == 0 and ntf > 0.3 * m0.ne, (nfar, ntf)
+    x, t = M.new_points(n, seed=9, surface=True)
+    sols = [M.on_vertices(m0, M.iso_metric), M.on_vertices(m0, lin_field)]
+    out = []
+    transfer.upload_background(m, sols, 0)
+    transfer.upload_points(x, t)
+    for flags in (0, FULL_RECORDS, FAR_AS_WHOLE):
+        transfer.run(flags=flags)
+        r = transfer.download()
+        out.append((r.elem.copy(), r.status.copy(), [s.copy() for s in r.sols]))
+    _assert_same(out[0], out[1])
+    _assert_same(out[0], out[2])
+    transfer.upload_background(m0, sols, 0)
+    transfer.upload_points(x, t)
+    transfer.run()
+    r = transfer.download()
+    e = r.elem.astype(np.int64)
+    vol = (t == 0) & (r.status == 1)
+    assert vol.sum() > 0.9 * (t == 0).sum()
+    assert np.array_equal(out[0][0][vol], new[e[vol]])
+    for u, v in zip(out[0][2], r.sols):
+        assert np.array_equal(u[vol].view(np.uint64), v[vol].view(np.uint64))
+    ref = lin_field(x[vol])[:, 0]
+    assert np.max(np.abs(out[0][2][1][vol, 0] - ref)) < 1e-12

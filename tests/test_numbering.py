@@ -51,3 +51,19 @@ def test_wrec_escape_rule():
     assert M.wrec_escapes(mm) == 1
     big[5, 3] = big[5, 0] + (1 << 19) - 1
     assert M.wrec_escapes(M.Mesh(m.xyz, big, m.adja, m.tria, m.adjt)) == 0
+
+
+def test_wrec_far_field_rule():
+    """A neighbour delta past the 24-bit field escapes that field only
+    (-2^23 is the boundary code, -2^23 + 1 the far code); an appended
+    numbering of more than 2^23 tets puts its moved tets' faces there."""
+    m = M.kuhn_cube(3)
+    assert M.wrec_far_fields(m) == (0, 0)
+    ad = m.adja.copy()
+    # tet 1's face 0 neighbour moved by > 2^23 (out of range on purpose:
+    # the rule is about the delta, not the mesh)
+    k, f = 1, int(np.nonzero(ad[1:5] > 0)[0][0])
+    for d, far in (((1 << 23) - 1, 0), (1 << 23, 1)):
+        ad[4 * (k - 1) + 1 + f] = (k + d) * 4
+        assert M.wrec_far_fields(M.Mesh(m.xyz, m.tet, ad, m.tria, m.adjt))[0] == far
+    assert M.wrec_escapes(M.Mesh(m.xyz, m.tet, ad, m.tria, m.adjt)) == 0

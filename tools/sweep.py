@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--opt", default="hint_stride=1,4")
     ap.add_argument("--n", type=int, default=0, help="override the config's cells per axis")
+    ap.add_argument("--numbering", default="lex", choices=["lex", "shuffle", "appended"],
+                    help="background tet numbering (bench.py --numbering)")
     ap.add_argument("--check", action="store_true",
                     help="compare every variant's results bit for bit with the first one's")
     args = ap.parse_args()
@@ -37,6 +39,9 @@ def main():
     if args.n:
         cfg["n"] = args.n
     m, x, t, sols, _ = bench.build_case(cfg, 0)
+    if args.numbering != "lex":
+        from parmmg_amd import mesh as M
+        m = M.numbering(m, args.numbering)[0]
     tr = Transfer(0)
     tr.upload_background(m, sols, 0)
     tr.upload_points(x, t)
@@ -77,6 +82,7 @@ def main():
         if v in mism:
             out[v]["mismatches"] = mism[v]
     print(json.dumps({"config": args.config, "n": cfg["n"], "npts": int(len(x)), "opt": key,
+                      "numbering": args.numbering,
                       "ms(median,min)": out}, indent=1))
 
 

@@ -460,9 +460,11 @@ def main():
     cfg = CONFIGS[args.config]
     ngrp = cfg.get("groups", 1)
     cases = [build_case(cfg, rank * ngrp + g) for g in range(ngrp)]
+    print(f"[bench] rank {rank}: {args.config} case built", file=sys.stderr, flush=True)
     if args.numbering != "lex":
         from parmmg_amd import mesh as M
         cases = [(M.numbering(c[0], args.numbering)[0],) + tuple(c[1:]) for c in cases]
+        print(f"[bench] rank {rank}: {args.numbering} numbering", file=sys.stderr, flush=True)
     # the CPU baseline first: its worker processes are forked before this
     # process touches the GPU
     cpu = None

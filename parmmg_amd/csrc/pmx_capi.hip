@@ -397,7 +397,7 @@ pmx_ctx *pmx_create(int device) {
       hipStreamCreateWithFlags(&ctx->up, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_topo, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_tets, hipEventDisableTiming) != hipSuccess ||
-      hipHostMalloc((void **)&ctx->h_nbad, 2 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void **)&ctx->h_nbad, 4 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess ||
       [&] {
         for (auto &e : ctx->ev_dl)
           if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return true;
@@ -567,7 +567,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     ~StreamGuard() { if (s) hipStreamSynchronize(s); }
   } topo_guard;
   if (!dgrow(ctx, ctx->d_xyz, (size_t)(np + 1) * 3) || !dgrow(ctx, ctx->d_tets, (size_t)(ne + 1)) ||
-      !dgrow(ctx, ctx->d_wrec, (size_t)(ne + 1)) ||
+      !dgrow(ctx, ctx->d_wrec, (size_t)(ne + 1)) || !dgrow(ctx, ctx->d_wfar, 2) ||
       !dgrow(ctx, ctx->d_tets_s, (size_t)std::max<int64_t>(ns, 1)) || !dgrow(ctx, ctx->d_sol, hs_n) ||
       !dgrow(ctx, ctx->d_tris, (size_t)(nt + 1)) || !dgrow(ctx, ctx->d_trn, (size_t)(nt + 1)) ||
       !dgrow(ctx, ctx->d_xyzq, (size_t)(np + 1)) ||
@@ -654,7 +654,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   }
   if (!dev_adja) {
     CK(hipMemcpyAsync(ctx->d_tets_s.p, hh, (size_t)ns * sizeof(int4), hipMemcpyHostToDevice, st));
-    launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, st);
+    launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, ctx->d_wfar.p, ctx->h_nbad + 2, st);
   }
   if (dev_adja) {
     // face matching on the device (pmx_topo.hip), then the tet records and
@@ -669,7 +669,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
       return 0;
     launch_build_tetrec(ctx->d_btv.p, ctx->d_adja.p, ne, PMX_HINT_STRIDE, ctx->d_tets.p, ctx->d_tets_s.p,
                         ctx->topo);
-    launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, ctx->topo);
+    launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, ctx->d_wfar.p, ctx->h_nbad + 2, ctx->topo);
     CK(hipEventRecord(ctx->ev_join, ctx->topo));
   }
   tr.mark("tets");
@@ -717,6 +717,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   // the node -> trias fans are the step's (pmx_run: PMMG_precompute_nodeTrias
   // runs inside the reference's call)
   if (dev_adja) CK(hipStreamWaitEvent(st, ctx->ev_join, 0));
+  if (!ctx->order_hint_samples(ne, st)) return 0;
   CK(hipGetLastError());
   tr.mark("trias + topology");
   CK(hipStreamSynchronize(ctx->stream));   // host staging vectors die here
@@ -934,14 +935,14 @@ bool pmx_ctx::pack_new_tets() {
   if (residency && ntet > 0) {
     const int64_t ns = (ntet + PMX_HINT_STRIDE - 1) / PMX_HINT_STRIDE;
     if (!dgrow(this, d_adja, (size_t)(4 * ntet + 5)) || !dgrow(this, d_tets_next, (size_t)(ntet + 1)) ||
-        !dgrow(this, d_wrec_next, (size_t)(ntet + 1)) ||
+        !dgrow(this, d_wrec_next, (size_t)(ntet + 1)) || !dgrow(this, d_wfar, 2) ||
         !dgrow(this, d_tets_s_next, (size_t)std::max<int64_t>(ns, 1)))
       return false;
     *h_nbad = 0;
     CK(hipStreamWaitEvent(topo, ev_tets, 0));
     if (!pmx_ctx_build_adja_device(this, d_ntetv.p, ntet, n, d_adja.p, topo, h_nbad)) return false;
     launch_build_tetrec(d_ntetv.p, d_adja.p, ntet, PMX_HINT_STRIDE, d_tets_next.p, d_tets_s_next.p, topo);
-    launch_build_wrec(d_tets_next.p, ntet, d_wrec_next.p, topo);
+    launch_build_wrec(d_tets_next.p, ntet, d_wrec_next.p, d_wfar.p + 1, h_nbad + 3, topo);
     CK(hipEventRecord(ev_topo, topo));
     next_topo = true;
   }
@@ -972,6 +973,31 @@ bool pmx_ctx::fix_orphans() {
   return true;
 }
 
+// the hint sample in cell order (k_sample_keys, pmx_kernels.hip), after the
+// grid of this background is set up and its coordinates are on the device.
+// PMX_HINT_SAMPLE_ORDER=0 keeps the tet order, =2 leaves each cell's run in
+// increasing tet order (A/Bs).
+bool pmx_ctx::order_hint_samples(int64_t ne, hipStream_t s) {
+  samples_sorted = false;
+  const char *e = getenv("PMX_HINT_SAMPLE_ORDER");
+  if (e && e[0] == '0') return true;
+  const int64_t n = (ne + PMX_HINT_STRIDE - 1) / PMX_HINT_STRIDE;
+  if (n < 1) return true;
+  const size_t tb = hint_sort_temp_bytes(n);
+  if (!dgrow(this, d_skey, (size_t)(2 * n)) || !dgrow(this, d_sidx, (size_t)(2 * n)) ||
+      !dgrow(this, d_salt, (size_t)n) || !dgrow(this, d_tets_sk, (size_t)n) ||
+      !dgrow(this, d_stmp, std::max<size_t>(tb, 1)))
+    return false;
+  if (!launch_hint_sort(d_tets_s.p, n, PMX_HINT_STRIDE, grid, d_xyz.p, d_skey.p, d_sidx.p, d_salt.p,
+                        d_tets_sk.p, d_stmp.p, tb, !(e && e[0] == '2'), s)) {
+    err = "hint sample: sort";
+    return false;
+  }
+  std::swap(d_tets_s, d_salt);
+  samples_sorted = true;
+  return true;
+}
+
 // ---- the step ---------------------------------------------------------------
 
 static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &opts, VolArgs &A) {
@@ -991,6 +1017,13 @@ static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &o
   A.ref_walk = (opts.flags & PMX_RUN_REFERENCE_WALK) ? 1 : 0;
   A.rec_start = (opts.flags & PMX_RUN_RECORD_STARTS) ? 1 : 0;
   A.exp = (opts.flags >> PMX_RUN_EXP_SHIFT) & 0xff;
+  // the compact records resolve a far neighbour field when a walk crosses it
+  // (a dependent read of the 32-B record); with many such tets the walk on
+  // the 32-B records is faster (r05, C3: lex 0 % of the tets, compact 2 %
+  // faster; 9 %, 32-B 1.5 % faster; appended 41 %, 32-B 5.5 % faster --
+  // DESIGN.md section 7).  exp 18: compact records always
+  if (A.exp != 18 && (uint64_t)ctx->h_nbad[2] * PMX_WREC_FAR_DIV > (uint64_t)std::max<int64_t>(ctx->ne, 1))
+    A.wrec = nullptr;
 }
 
 // pmx_run_opts.flags: the public PMX_RUN_* bits, plus the experiment switch
@@ -1009,7 +1042,7 @@ static bool run_flags_valid(int flags, std::string *err) {
   }
   const int e = (flags >> PMX_RUN_EXP_SHIFT) & 0xff;
   switch (e) {
-    case 0: case 6: case 9: case 10: case 11: case 12: case 13: case 15: case 16: case 17:
+    case 0: case 6: case 9: case 10: case 11: case 12: case 13: case 15: case 16: case 17: case 18:
       return true;
     case 4: case 5: case 14: {
       const char *v = getenv("PMX_EXPERIMENTS");
@@ -1123,7 +1156,8 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     const bool early = A.exp != 9;
     if (early && !fork_surface()) return 0;
     const int stride = opts.hint_stride > 0 ? opts.hint_stride : PMX_HINT_STRIDE;
-    launch_hint_build(stride == PMX_HINT_STRIDE ? ctx->d_tets_s.p : nullptr, ctx->d_tets.p, ctx->ne,
+    launch_hint_build(stride == PMX_HINT_STRIDE ? ctx->d_tets_s.p : nullptr,
+                      ctx->samples_sorted ? ctx->d_tets_sk.p : nullptr, ctx->d_tets.p, ctx->ne,
                       stride, ctx->d_grid.p, A.g, hint_xyz ? nullptr : ctx->d_xyzq.p, ctx->d_xyz.p, st,
                       exp == 16);
     if (exp == 13 && ctx->d_wrec.p) {
@@ -1753,6 +1787,7 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
     if (*ctx->h_nbad) { ctx->err = "pmx_promote_background: non-manifold tet faces"; return 0; }
     std::swap(ctx->d_tets, ctx->d_tets_next);
     std::swap(ctx->d_wrec, ctx->d_wrec_next);
+    ctx->h_nbad[2] = ctx->h_nbad[3];
     std::swap(ctx->d_tets_s, ctx->d_tets_s_next);
   } else {
     if (m->adja) {
@@ -1760,9 +1795,9 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
     } else if (!pmx_ctx_build_adja_device(ctx, ctx->d_ntetv.p, ne, n, ctx->d_adja.p, st, nullptr)) {
       return 0;
     }
-    if (!dgrow(ctx, ctx->d_wrec, (size_t)(ne + 1))) return 0;
+    if (!dgrow(ctx, ctx->d_wrec, (size_t)(ne + 1)) || !dgrow(ctx, ctx->d_wfar, 2)) return 0;
     launch_build_tetrec(ctx->d_ntetv.p, ctx->d_adja.p, ne, PMX_HINT_STRIDE, ctx->d_tets.p, ctx->d_tets_s.p, st);
-    launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, st);
+    launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, ctx->d_wfar.p, ctx->h_nbad + 2, st);
   }
   ctx->np = n;
   ctx->ne = ne;
@@ -1770,6 +1805,7 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
   ctx->hausd = m->hausd;
   tr.mark("tet records");
   if (!setup_grids(ctx, ctx->qlo, ctx->qhi, ne)) return 0;
+  if (!ctx->order_hint_samples(ne, st)) return 0;
   tr.mark("grids");
   CK(hipMemcpyAsync(ctx->d_tris.p, htr.data(), htr.size() * sizeof(TriRec), hipMemcpyHostToDevice, st));
   CK(hipGetLastError());
@@ -1815,7 +1851,7 @@ void pmx_ctx::free_all() {
   if (h_stage) hipHostFree(h_stage);
   h_stage = nullptr;
   h_stage_cap = 0;
-  dfree(d_xyz); dfree(d_tets); dfree(d_wrec); dfree(d_wrec_next); dfree(d_sol); dfree(d_tets_s); dfree(d_tris);
+  dfree(d_xyz); dfree(d_tets); dfree(d_wrec); dfree(d_wrec_next); dfree(d_wfar); dfree(d_skey); dfree(d_sidx); dfree(d_salt); dfree(d_stmp); dfree(d_tets_sk); dfree(d_sol); dfree(d_tets_s); dfree(d_tris);
   dfree(d_ntlist); dfree(d_ntval); dfree(d_ntkey); dfree(d_ntrange); dfree(d_nttmp); dfree(d_xyzq); dfree(d_trn); dfree(d_grid); dfree(d_tetv);
   dfree(d_kind); dfree(d_qmark); dfree(d_ctile); dfree(d_nsel); dfree(d_wmask); dfree(d_out); dfree(d_elem); dfree(d_status);
   dfree(d_steps); dfree(d_start); dfree(d_edge); dfree(d_vertex); dfree(d_list); dfree(d_found);

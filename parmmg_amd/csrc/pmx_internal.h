@@ -18,6 +18,9 @@ template <class T> struct DevBuf {
 #define PMX_HINT_STRIDE 4
 // pmx_run_opts.flags bits 16-23: the walk's measurement switch (VolArgs.exp; tools/walk_pmc.sh)
 #define PMX_RUN_EXP_SHIFT 16
+// the walk takes the 32-B tet records instead of the compact ones when more
+// than 1/PMX_WREC_FAR_DIV of the tets have a far neighbour field (pmx_wrec.h)
+#define PMX_WREC_FAR_DIV 16
 
 struct pmx_ctx {
   int device = 0;
@@ -49,8 +52,15 @@ struct pmx_ctx {
   DevBuf<double> d_xyz;                 // old vertices, x y z (24 B), slot 0 unused
   DevBuf<TetRec> d_tets;
   DevBuf<WRec> d_wrec;                  // the walk's compact copy of d_tets (built with it)
+  DevBuf<unsigned> d_wfar;              // [0] / [1]: far-field counters of d_wrec / d_wrec_next's builds
   DevBuf<double> d_sol;
-  DevBuf<int4> d_tets_s;                // host-packed hint sample: tets 1, 1+4, 1+8, ...
+  DevBuf<int4> d_tets_s;                // hint sample: tets 1, 1+4, 1+8, ... in the order of their cells
+  DevBuf<int> d_tets_sk;                // its tet indices (samples_sorted)
+  bool samples_sorted = false;
+  DevBuf<unsigned> d_skey;              // the sort (order_hint_samples): keys, indices, records, temp
+  DevBuf<int> d_sidx;
+  DevBuf<int4> d_salt;
+  DevBuf<char> d_stmp;
   DevBuf<TriRec> d_tris;
   // node -> trias fans (built on the device, in the step): ntlist = trias
   // sorted by (vertex, index), ntrange[3 k + l] = the run of vertex l of tria k
@@ -150,6 +160,7 @@ struct pmx_ctx {
   DevBuf<TetRec> d_tets_next;
   DevBuf<WRec> d_wrec_next;
   DevBuf<int4> d_tets_s_next;
+  // [2] / [3]: tets of d_wrec / d_wrec_next with a far neighbour field (pmx_wrec.h)
   unsigned *h_nbad = nullptr;           // pinned [2]: non-manifold faces of that build, [1] of a background upload's
   DevBuf<double> d_nqual;
   bool have_qtag = false;               // raw tags of the new points
@@ -187,6 +198,7 @@ struct pmx_ctx {
 
   hipEvent_t *next_event_slot();
   void free_all();
+  bool order_hint_samples(int64_t ne, hipStream_t s);
   bool build_node_trias(hipStream_t s);   // from d_tris, np, nt (pmx_bdy.hip)
   bool classify(hipStream_t s);           // the new points: kinds, lists, marks (pmx_capi.hip)
   bool launch_bdy(const VolArgs &a, hipStream_t s);

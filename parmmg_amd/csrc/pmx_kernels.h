@@ -56,7 +56,8 @@ struct VolArgs {
   int rec_start;                // write the start tet of every point (diagnostics)
   int exp;                      // measurement switch (tools/walk_pmc.sh): 0 production,
                                 // 4 no interpolation, 5 hint + hint record only,
-                                // 17 a record with a far neighbour field read whole
+                                // 17 a record with a far neighbour field read whole,
+                                // 18 compact records whatever their far fields
 };
 
 struct ExhArgs {
@@ -75,7 +76,7 @@ struct ExhArgs {
 // volume hint grid from every stride-th tet: `packed` = the host-packed
 // connectivity of tets 1, 1+stride, ... (stride == PMX_HINT_STRIDE), else the
 // tet records are read strided
-void launch_hint_build(const int4 *packed, const TetRec *tets, int64_t ne, int stride, int *grid,
+void launch_hint_build(const int4 *packed, const int *kidx, const TetRec *tets, int64_t ne, int stride, int *grid,
                        GridDesc g, const unsigned long long *xyzq, const double *xyz, hipStream_t s,
                        bool v0 = false);
 void launch_hint_inline(const int *grid, int64_t cells, const WRec *wr, uint4 *hrec, hipStream_t s);
@@ -124,7 +125,16 @@ void launch_classify(const uint16_t *tag, const uint8_t *mk, int64_t n, int2 *tc
 void launch_build_tetrec(const int4 *tv, const int *adja, int64_t ne, int stride, TetRec *tets, int4 *sample,
                          hipStream_t s);
 // the walk's compact records from the tet records (slots 0..ne)
-void launch_build_wrec(const TetRec *tets, int64_t ne, WRec *wr, hipStream_t s);
+// (*h_nfar, pinned, when stream s gets there: the tets with a far neighbour
+// field, pmx_wrec.h; d_nfar one device word)
+// the packed hint sample in the order of its cells (k_sample_keys): out[i]
+// = smp[t_i] and kidx[i] = 1 + stride * t_i; keys and idx 2n words each, tmp
+// hint_sort_temp_bytes(n) bytes
+size_t hint_sort_temp_bytes(int64_t n);
+bool launch_hint_sort(const int4 *smp, int64_t n, int stride, GridDesc g, const double *xyz, unsigned *keys,
+                      int *idx, int4 *out, int *kidx, void *tmp, size_t tmp_bytes, bool rev, hipStream_t s);
+void launch_build_wrec(const TetRec *tets, int64_t ne, WRec *wr, unsigned *d_nfar, unsigned *h_nfar,
+                       hipStream_t s);
 // workgroups of k_fallback that can be co-resident with `share` other
 // launches of it on this device (0 on error)
 int fallback_coresident_blocks(int device, int share);

@@ -224,13 +224,13 @@ def renumber(m: Mesh, tperm: np.ndarray, vperm: np.ndarray | None = None):
     return Mesh(xyz, tet, adja, tria, m.adjt.copy(), m.hausd), tinv
 
 
-def numbering(m: Mesh, kind: str, seed: int = 7):
+def numbering(m: Mesh, kind: str, seed: int = 7, frac: float = 0.1):
     """Background tet numberings of the bench: "lex" the
     generator's cell-lexicographic order (a Scotch-renumbered Mmg mesh);
     "shuffle" the tets in random order (seed 7, vertices kept); "appended" 10 %
     of the tets, chosen at random, moved to the end in their order (what Mmg's
-    insertions do to a numbering between renumberings).  Returns (mesh, tinv
-    or None)."""
+    insertions do to a numbering between renumberings; `frac` of them for
+    the record-format A/B).  Returns (mesh, tinv or None)."""
     if kind == "lex":
         return m, None
     rng = np.random.default_rng(seed)
@@ -238,7 +238,8 @@ def numbering(m: Mesh, kind: str, seed: int = 7):
         tp = rng.permutation(m.ne)
     elif kind == "appended":
         moved = np.zeros(m.ne, bool)
-        moved[rng.choice(m.ne, m.ne // 10, replace=False)] = True
+        nmov = m.ne // 10 if frac == 0.1 else int(m.ne * frac)
+        moved[rng.choice(m.ne, nmov, replace=False)] = True
         tp = np.concatenate([np.nonzero(~moved)[0], np.nonzero(moved)[0]])
     else:
         raise ValueError(f"unknown numbering {kind}")

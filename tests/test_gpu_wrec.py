@@ -127,3 +127,26 @@ def test_far_neighbour_fields(transfer):
         assert np.array_equal(u[vol].view(np.uint64), v[vol].view(np.uint64))
     ref = lin_field(x[vol])[:, 0]
     assert np.max(np.abs(out[0][2][1][vol, 0] - ref)) < 1e-12
+
+
+def test_hint_sample_order(transfer, monkeypatch):
+    """The hint sample sorted by cell at the upload (pmx_ctx::order_hint_samples)
+    carries its tet indices: on an appended numbering (sorted order != tet
+    order) the step locates and interpolates bit for bit as with the sample in
+    tet order, with walks as short."""
+    m, _ = M.numbering(M.kuhn_cube(16), "appended")
+    x, t = M.new_points(16, seed=3, surface=True)
+    sols = [M.on_vertices(m, M.iso_metric), M.on_vertices(m, lin_field)]
+    out = []
+    for order in ("0", "1"):
+        monkeypatch.setenv("PMX_HINT_SAMPLE_ORDER", order)
+        transfer.upload_background(m, sols, 0)
+        transfer.upload_points(x, t)
+        transfer.run(record_starts=True)
+        r = transfer.download()
+        out.append((r.elem.copy(), r.status.copy(), [s.copy() for s in r.sols],
+                    transfer.locate_stats()["stepav"], transfer.starts().copy()))
+    _assert_same(out[0], out[1])
+    assert out[1][3] < 1.2 * out[0][3], (out[0][3], out[1][3])
+    vol = (t == 0) & (out[1][1] == 1)
+    assert not np.array_equal(out[0][4][vol], out[1][4][vol])       # other start tets

@@ -25,8 +25,9 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--opt", default="hint_stride=1,4")
     ap.add_argument("--n", type=int, default=0, help="override the config's cells per axis")
-    ap.add_argument("--numbering", default="lex", choices=["lex", "shuffle", "appended"],
-                    help="background tet numbering (bench.py --numbering)")
+    ap.add_argument("--numbering", default="lex",
+                    help="background tet numbering (bench.py --numbering; appended:F moves "
+                         "a fraction F of the tets)")
     ap.add_argument("--check", action="store_true",
                     help="compare every variant's results bit for bit with the first one's")
     args = ap.parse_args()
@@ -41,7 +42,9 @@ def main():
     m, x, t, sols, _ = bench.build_case(cfg, 0)
     if args.numbering != "lex":
         from parmmg_amd import mesh as M
-        m = M.numbering(m, args.numbering)[0]
+        kind, _, frac = args.numbering.partition(":")
+        m = M.numbering(m, kind, frac=float(frac) if frac else 0.1)[0]
+        print("far fields, tets with one:", M.wrec_far_fields(m), "of", m.ne, flush=True)
     tr = Transfer(0)
     tr.upload_background(m, sols, 0)
     tr.upload_points(x, t)

@@ -173,8 +173,9 @@ void launch_hint_build(const int4 *packed, const int *kidx, const TetRec *tets, 
 // moved to the end) scatters a tenth of it, and each wave of those samples
 // gathers and writes 64 distinct lines -- C3 hint build 0.25 -> 0.42 ms
 // (r05).  Keys: the sample's cell.
-// (rev: entry i is sample n-1-i, so that the stable sort leaves each cell's
-// run in decreasing tet order and the cell's last store is its smallest tet)
+// (rev: entry i is sample n-1-i: the stable sort leaves each cell's run in
+// decreasing tet order, so the run's later stores -- the likelier survivors
+// of the plain stores -- are its smaller tets; any sample is a valid start)
 __global__ __launch_bounds__(256) void k_sample_keys(const int4 *__restrict__ smp, int64_t n, GridDesc g,
                                                      const double *__restrict__ xyz, unsigned *__restrict__ key,
                                                      int *__restrict__ idx, bool rev) {

@@ -1024,6 +1024,7 @@ static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &o
   // DESIGN.md section 7).  exp 18: compact records always
   if (A.exp != 18 && (uint64_t)ctx->h_nbad[2] * PMX_WREC_FAR_DIV > (uint64_t)std::max<int64_t>(ctx->ne, 1))
     A.wrec = nullptr;
+  A.far = ctx->h_nbad[2] > 0 ? 1 : 0;
 }
 
 // pmx_run_opts.flags: the public PMX_RUN_* bits, plus the experiment switch

@@ -54,6 +54,7 @@ struct VolArgs {
   int inline_ties;              // resolve face ties in place
   int ref_walk;                 // 1: k_walk (reference-order walk) instead of k_walks
   int rec_start;                // write the start tet of every point (diagnostics)
+  int far;                      // the compact records have far neighbour fields (pmx_wrec.h)
   int exp;                      // measurement switch (tools/walk_pmc.sh): 0 production,
                                 // 4 no interpolation, 5 hint + hint record only,
                                 // 17 a record with a far neighbour field read whole,

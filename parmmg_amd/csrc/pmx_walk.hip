@@ -448,7 +448,9 @@ __device__ __forceinline__ int hint_with_rec(const VolArgs &A, D3 p, TetRec &t) 
   return k;
 }
 
-template <int LAYOUT, int S, bool TIES, bool CW, bool HREC = false>
+// FAR: the compact records have far neighbour fields (VolArgs.far); without
+// them the walk compiles no resolution path
+template <int LAYOUT, int S, bool TIES, bool CW, bool HREC = false, bool FAR = true>
 __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
   const int64_t b = walk_xcd_remap(blockIdx.x, gridDim.x);
   const int64_t j = b * blockDim.x + threadIdx.x;
@@ -467,7 +469,7 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
       cur = hint_with_rec(A, p, t);
     } else {
       cur = walk_hint(A.grid, A.g, p);
-      t = walk_rec<CW>(A, cur, A.exp == 17);
+      t = walk_rec<CW>(A, cur, FAR && A.exp == 17);
     }
     if (A.rec_start) A.start[i] = cur;
     int ring[WALK_RING];
@@ -509,9 +511,8 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
         // smallest barycentric; a far field (< 0, pmx_wrec.h) counts as
         // admissible until it is chosen, then is resolved from the full record
         // and the choice made again (the same choice as on resolved fields)
-        int sb = -1;
-        for (int it = 0; it < 5; it++) {
-          sb = -1;
+        auto choose = [&]() {
+          int sb = -1;
           double wb = 0.0;
 #pragma unroll
           for (int k = 0; k < 4; k++) {
@@ -523,14 +524,20 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
             sb = take ? k : sb;
             wb = take ? w[k] : wb;
           }
-          if (sb < 0 || pick4(NB, sb) > 0) break;
-          const int r = wrec_resolve(pick4(NB, sb), A.tets, cur);
+          return sb;
+        };
+        int sb = choose();
+        if (FAR && sb >= 0 && pick4(NB, sb) < 0) {         // rare: a far field chosen
+          for (int it = 0; it < 4 && sb >= 0 && pick4(NB, sb) < 0; it++) {
+            const int r = wrec_resolve(pick4(NB, sb), A.tets, cur);
 #pragma unroll
-          for (int k = 0; k < 4; k++) NB[k] = (k == sb) ? r : NB[k];
+            for (int k = 0; k < 4; k++) NB[k] = (k == sb) ? r : NB[k];
+            sb = choose();
+          }
         }
         if (sb < 0) break;
         const int next = pick4(NB, sb);
-        const TetRec u = walk_rec<CW>(A, next, A.exp == 17);
+        const TetRec u = walk_rec<CW>(A, next, FAR && A.exp == 17);
         cur = next;
         t = u;
         if (u.v[0] <= 0) break;                            // !MG_EOK: let the scan decide
@@ -581,7 +588,7 @@ __global__ __launch_bounds__(256) void k_walks(VolArgs A) {
           const double lmin = fmin(fmin(lam[0], lam[1]), fmin(lam[2], lam[3]));
           if (lmin > -PMX_EPS) { found = true; break; }    // src/barycoord_pmmg.c:102-107
           if (step >= A.max_walk) break;
-          if ((t.nb[0] | t.nb[1] | t.nb[2] | t.nb[3]) < 0) t = A.tets[cur];   // far fields
+          if (FAR && (t.nb[0] | t.nb[1] | t.nb[2] | t.nb[3]) < 0) t = A.tets[cur];   // far fields
           const int next = exact_next(t, lam, ring, cur);
           if (!next) break;
           t = A.tets[next];
@@ -609,11 +616,20 @@ static void launch_walk_t(const VolArgs &a, int64_t nb, hipStream_t s) {
     const unsigned nbb = (unsigned)((a.nlist + bs - 1) / bs);
     if (a.exp == 13 && a.hrec && a.inline_ties)
       hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true, true>), dim3(nbb), dim3(bs), 0, s, a);
-    else if (a.inline_ties) hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true>), dim3(nbb), dim3(bs), 0, s, a);
-    else hipLaunchKernelGGL((k_walks<LAYOUT, S, false, true>), dim3(nbb), dim3(bs), 0, s, a);
+    else if (a.inline_ties && a.far)
+      hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true, false, true>), dim3(nbb), dim3(bs), 0, s, a);
+    else if (a.inline_ties)
+      hipLaunchKernelGGL((k_walks<LAYOUT, S, true, true, false, false>), dim3(nbb), dim3(bs), 0, s, a);
+    else if (a.far)
+      hipLaunchKernelGGL((k_walks<LAYOUT, S, false, true, false, true>), dim3(nbb), dim3(bs), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_walks<LAYOUT, S, false, true, false, false>), dim3(nbb), dim3(bs), 0, s, a);
   } else {
-    if (a.inline_ties) hipLaunchKernelGGL((k_walks<LAYOUT, S, true, false>), dim3((unsigned)nb), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_walks<LAYOUT, S, false, false>), dim3((unsigned)nb), dim3(256), 0, s, a);
+    // (the 32-B records have no far fields)
+    if (a.inline_ties)
+      hipLaunchKernelGGL((k_walks<LAYOUT, S, true, false, false, false>), dim3((unsigned)nb), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_walks<LAYOUT, S, false, false, false, false>), dim3((unsigned)nb), dim3(256), 0, s, a);
   }
 }
 

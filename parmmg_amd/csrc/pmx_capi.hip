@@ -975,8 +975,7 @@ bool pmx_ctx::fix_orphans() {
 
 // the hint sample in cell order (k_sample_keys, pmx_kernels.hip), after the
 // grid of this background is set up and its coordinates are on the device.
-// PMX_HINT_SAMPLE_ORDER=0 keeps the tet order, =2 leaves each cell's run in
-// increasing tet order (A/Bs).
+// PMX_HINT_SAMPLE_ORDER=0 keeps the tet order (A/B).
 bool pmx_ctx::order_hint_samples(int64_t ne, hipStream_t s) {
   samples_sorted = false;
   const char *e = getenv("PMX_HINT_SAMPLE_ORDER");
@@ -989,7 +988,7 @@ bool pmx_ctx::order_hint_samples(int64_t ne, hipStream_t s) {
       !dgrow(this, d_stmp, std::max<size_t>(tb, 1)))
     return false;
   if (!launch_hint_sort(d_tets_s.p, n, PMX_HINT_STRIDE, grid, d_xyz.p, d_skey.p, d_sidx.p, d_salt.p,
-                        d_tets_sk.p, d_stmp.p, tb, !(e && e[0] == '2'), s)) {
+                        d_tets_sk.p, d_stmp.p, tb, s)) {
     err = "hint sample: sort";
     return false;
   }

@@ -133,7 +133,7 @@ void launch_build_tetrec(const int4 *tv, const int *adja, int64_t ne, int stride
 // hint_sort_temp_bytes(n) bytes
 size_t hint_sort_temp_bytes(int64_t n);
 bool launch_hint_sort(const int4 *smp, int64_t n, int stride, GridDesc g, const double *xyz, unsigned *keys,
-                      int *idx, int4 *out, int *kidx, void *tmp, size_t tmp_bytes, bool rev, hipStream_t s);
+                      int *idx, int4 *out, int *kidx, void *tmp, size_t tmp_bytes, hipStream_t s);
 void launch_build_wrec(const TetRec *tets, int64_t ne, WRec *wr, unsigned *d_nfar, unsigned *h_nfar,
                        hipStream_t s);
 // workgroups of k_fallback that can be co-resident with `share` other

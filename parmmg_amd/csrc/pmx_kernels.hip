@@ -173,14 +173,14 @@ void launch_hint_build(const int4 *packed, const int *kidx, const TetRec *tets, 
 // moved to the end) scatters a tenth of it, and each wave of those samples
 // gathers and writes 64 distinct lines -- C3 hint build 0.25 -> 0.42 ms
 // (r05).  Keys: the sample's cell.
-// (rev: entry i is sample n-1-i: the stable sort leaves each cell's run in
-// decreasing tet order, so the run's later stores -- the likelier survivors
-// of the plain stores -- are its smaller tets; any sample is a valid start)
+// The stable sort leaves each cell's run in increasing tet order, the order
+// of the sample in tet order (r05 A/B: with the runs reversed the walk was
+// 1.7-2.3 % slower at C3, lex and appended; tools/ab_env.py).
 __global__ __launch_bounds__(256) void k_sample_keys(const int4 *__restrict__ smp, int64_t n, GridDesc g,
                                                      const double *__restrict__ xyz, unsigned *__restrict__ key,
-                                                     int *__restrict__ idx, bool rev) {
+                                                     int *__restrict__ idx) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t t = rev ? n - 1 - i : i;
+    const int64_t t = i;
     const int4 v = smp[t];
     unsigned kk = (unsigned)((int64_t)g.dim[0] * g.dim[1] * g.dim[2]);   // deleted tets last
     if (v.x > 0)
@@ -214,9 +214,9 @@ size_t hint_sort_temp_bytes(int64_t n) {
   return bytes;
 }
 bool launch_hint_sort(const int4 *smp, int64_t n, int stride, GridDesc g, const double *xyz, unsigned *keys,
-                      int *idx, int4 *out, int *kidx, void *tmp, size_t tmp_bytes, bool rev, hipStream_t s) {
+                      int *idx, int4 *out, int *kidx, void *tmp, size_t tmp_bytes, hipStream_t s) {
   const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 65536));
-  hipLaunchKernelGGL(k_sample_keys, dim3((unsigned)nb), dim3(256), 0, s, smp, n, g, xyz, keys, idx, rev);
+  hipLaunchKernelGGL(k_sample_keys, dim3((unsigned)nb), dim3(256), 0, s, smp, n, g, xyz, keys, idx);
   hipcub::DoubleBuffer<unsigned> k(keys, keys + n);
   hipcub::DoubleBuffer<int> v(idx, idx + n);
   if (hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, k, v, (int)n, 0, key_bits(g), s) != hipSuccess)

@@ -708,6 +708,106 @@ __global__ __launch_bounds__(256) void k_nt_runs(const unsigned *__restrict__ ke
 }
 
 
+// The fans by rotation (r05), for a closed manifold surface -- every
+// boundary of a ParMmg group's volume mesh, interfaces included: each
+// (tria, corner) slot walks its vertex's fan through the tria adjacency
+// (Mmg's adjt: edge i opposite vertex i) and writes its tria into the window
+// of the fan's owner (its smallest tria) at its rank: the fan's increasing
+// tria order of PMMG_precompute_nodeTrias.  One kernel, no atomics, no
+// np-sized arrays (the radix sort of C3's 2.3 M (vertex, tria) pairs took
+// ~0.26 ms alone on the GPU).  A fan that meets an
+// edge without a neighbour (open or non-manifold surface), a neighbour
+// without the vertex, or more than FAN_CAP trias counts in *bad: the upload
+// runs it once as a check, and a background with any such fan keeps the sort.
+#define FAN_CAP 32
+// one turn around v from tria k (corner l), the record of each tria in a
+// register (one dependent load per step); f(tria, corner of v) per tria, k
+// first; false if the fan does not close within FAN_CAP trias
+__device__ __forceinline__ int sel3(const int a[3], int i) { return i == 0 ? a[0] : i == 1 ? a[1] : a[2]; }
+template <class F>
+__device__ __forceinline__ bool fan_turn(const TriRec *__restrict__ tris, int k, int l, const TriRec &t0, F f) {
+  const int v = sel3(t0.v, l);
+  TriRec tc = t0;
+  int cx = (l + 1) % 3, w = sel3(t0.v, (l + 2) % 3);
+  f(k, l);
+  for (int n = 1;; n++) {
+    const int nxt = sel3(tc.nb, cx);               // across the edge {v, w}
+    if (nxt == k) return true;                     // closed
+    if (nxt <= 0 || n == FAN_CAP) return false;
+    tc = tris[nxt];
+    const int cv = tc.v[0] == v ? 0 : tc.v[1] == v ? 1 : tc.v[2] == v ? 2 : -1;
+    const int cw = tc.v[0] == w ? 0 : tc.v[1] == w ? 1 : tc.v[2] == w ? 2 : -1;
+    if (cv < 0 || cw < 0 || cv == cw || tc.v[0] <= 0) return false;
+    f(nxt, cv);
+    w = sel3(tc.v, 3 - cv - cw);                   // the other edge at v: {v, w'}
+    cx = cw;
+  }
+}
+// Every slot walks its fan once: the fan's window is its owner's (the
+// smallest tria), and the slot's tria goes to the window at its rank in the
+// fan (the number of smaller members) -- the sorted fan without a sort or
+// any dependent chain beyond the walk itself (r05: an owner writing the fan
+// and sorting it in place made a chain of ~35 dependent memory operations,
+// 0.19 ms per call beside the main stream's kernels).
+__global__ __launch_bounds__(256) void k_fan_rotate(const TriRec *__restrict__ tris, int64_t nt,
+                                                    int2 *__restrict__ range, int *__restrict__ list,
+                                                    unsigned *__restrict__ bad) {
+  unsigned nbad = 0;
+  for (int64_t i = 3 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 3 * (nt + 1);
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i / 3), l = (int)(i - 3 * (int64_t)k);
+    const TriRec t0 = tris[k];
+    if (t0.v[0] <= 0) { range[i] = make_int2(0, 0); continue; }
+    int n = 0, rank = 0, own = k, lown = l;
+    const bool ok = fan_turn(tris, k, l, t0, [&](int g, int c) {
+      n++;
+      rank += g < k ? 1 : 0;
+      if (g < own) { own = g; lown = c; }
+    });
+    if (!ok) { nbad++; range[i] = make_int2(0, 0); continue; }
+    const int base = (int)((3 * (int64_t)own + lown - 3) * FAN_CAP);
+    range[i] = make_int2(base, base + n);
+    list[base + rank] = k;
+  }
+  for (int o = 32; o > 0; o >>= 1) nbad += __shfl_xor(nbad, o);
+  if ((threadIdx.x & 63) == 0 && nbad) atomicAdd(bad, nbad);
+}
+
+bool pmx_ctx::fan_rotation(hipStream_t s, unsigned *d_bad) {
+  const int64_t m = 3 * nt;
+  if (!pmx_dgrow(this, d_ntrange, (size_t)(3 * (nt + 1))) || !pmx_dgrow(this, d_ntlist, (size_t)(m * FAN_CAP)))
+    return false;
+  const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>((m + 255) / 256, 16384));
+  hipLaunchKernelGGL(k_fan_rotate, dim3(nb), dim3(256), 0, s, d_tris.p, nt, d_ntrange.p, d_ntlist.p, d_bad);
+  if (hipGetLastError() != hipSuccess) {
+    err = "node trias: launch";
+    return false;
+  }
+  return true;
+}
+
+// the upload's check: the fans of this background by rotation, their
+// failures into h_nbad[4] (read after the upload's final sync).
+// PMX_FAN_ROTATION=0 keeps the sort (A/B, tests).
+bool pmx_ctx::check_fans(hipStream_t s) {
+  fan_rot = false;
+  h_nbad[4] = 1u;
+  if (nt < 1) return true;
+  const char *e = getenv("PMX_FAN_ROTATION");
+  if (e && e[0] == '0') return true;
+  if (!pmx_dgrow(this, d_wfar, 4)) return false;
+  if (hipMemsetAsync(d_wfar.p + 3, 0, sizeof(unsigned), s) != hipSuccess) {
+    err = "node trias: memset";
+    return false;
+  }
+  if (!fan_rotation(s, d_wfar.p + 3)) return false;
+  if (hipMemcpyAsync(h_nbad + 4, d_wfar.p + 3, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess) {
+    err = "node trias: check";
+    return false;
+  }
+  return true;
+}
+
 // the counting sort over the vertex ids
 static bool node_trias_counting(pmx_ctx *c, hipStream_t s) {
   const int64_t m = 3 * c->nt, np = c->np, nt = c->nt;
@@ -737,10 +837,11 @@ static bool node_trias_counting(pmx_ctx *c, hipStream_t s) {
   return true;
 }
 
-bool pmx_ctx::build_node_trias(hipStream_t s) {
+bool pmx_ctx::build_node_trias(hipStream_t s, int force) {
   const int64_t m = 3 * nt;
   if (m < 1) return true;
-  if (np <= 5 * m) {
+  if (fan_rot && force == 0) return fan_rotation(s, d_wfar.p + 2);
+  if (np <= 5 * m || force == 1) {
     if (!node_trias_counting(this, s)) return false;
     if (hipGetLastError() != hipSuccess) {
       err = "node trias: launch";

@@ -387,17 +387,33 @@ pmx_ctx *pmx_create(int device) {
   if (hipSetDevice(device) != hipSuccess) return nullptr;
   pmx_ctx *ctx = new pmx_ctx();
   ctx->device = device;
-  if (hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking) != hipSuccess) {
+  // PMX_SIDE_CUS=N (measurement): the side stream on CUs [0, N), the main
+  // stream on the rest (hipExtStreamCreateWithCUMask)
+  int side_cus = 0;
+  if (const char *e = getenv("PMX_SIDE_CUS")) side_cus = atoi(e);
+  int ncu = 0;
+  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+  std::vector<uint32_t> mside, mmain;
+  if (side_cus > 0 && side_cus < ncu) {
+    mside.assign((size_t)(ncu + 31) / 32, 0u);
+    mmain.assign((size_t)(ncu + 31) / 32, 0u);
+    for (int c = 0; c < ncu; c++) (c < side_cus ? mside : mmain)[c / 32] |= 1u << (c % 32);
+  }
+  if ((mmain.empty() ? hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking)
+                     : hipExtStreamCreateWithCUMask(&ctx->own, (uint32_t)mmain.size(), mmain.data())) !=
+      hipSuccess) {
     delete ctx;
     return nullptr;
   }
   ctx->stream = ctx->own;
-  if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess ||
+  if ((mside.empty() ? hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking)
+                     : hipExtStreamCreateWithCUMask(&ctx->side, (uint32_t)mside.size(), mside.data())) !=
+          hipSuccess ||
       hipStreamCreateWithFlags(&ctx->topo, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->up, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_topo, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_tets, hipEventDisableTiming) != hipSuccess ||
-      hipHostMalloc((void **)&ctx->h_nbad, 4 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void **)&ctx->h_nbad, 6 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess ||
       [&] {
         for (auto &e : ctx->ev_dl)
           if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return true;
@@ -526,7 +542,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   // with the device buffers)
   ctx->have_bg = ctx->ran = ctx->have_derived = ctx->have_tetv = ctx->have_qual = false;
   ctx->eager_nch = 0;
-  ctx->have_ptag = ctx->have_csr = ctx->have_surf = false;
+  ctx->have_ptag = ctx->have_csr = ctx->have_surf = ctx->fan_rot = false;
   ctx->stat_np = -1;
   if (!m) { ctx->err = "pmx_upload_background: null mesh"; return 0; }
   hipSetDevice(ctx->device);
@@ -567,7 +583,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     ~StreamGuard() { if (s) hipStreamSynchronize(s); }
   } topo_guard;
   if (!dgrow(ctx, ctx->d_xyz, (size_t)(np + 1) * 3) || !dgrow(ctx, ctx->d_tets, (size_t)(ne + 1)) ||
-      !dgrow(ctx, ctx->d_wrec, (size_t)(ne + 1)) || !dgrow(ctx, ctx->d_wfar, 2) ||
+      !dgrow(ctx, ctx->d_wrec, (size_t)(ne + 1)) || !dgrow(ctx, ctx->d_wfar, 4) ||
       !dgrow(ctx, ctx->d_tets_s, (size_t)std::max<int64_t>(ns, 1)) || !dgrow(ctx, ctx->d_sol, hs_n) ||
       !dgrow(ctx, ctx->d_tris, (size_t)(nt + 1)) || !dgrow(ctx, ctx->d_trn, (size_t)(nt + 1)) ||
       !dgrow(ctx, ctx->d_xyzq, (size_t)(np + 1)) ||
@@ -714,6 +730,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   ctx->sd = sd;
   if (!setup_grids(ctx, lo, hi, ne)) return 0;
   CK(hipMemcpyAsync(ctx->d_tris.p, htr.data(), htr.size() * sizeof(TriRec), hipMemcpyHostToDevice, st));
+  if (!ctx->check_fans(st)) return 0;
   // the node -> trias fans are the step's (pmx_run: PMMG_precompute_nodeTrias
   // runs inside the reference's call)
   if (dev_adja) CK(hipStreamWaitEvent(st, ctx->ev_join, 0));
@@ -726,6 +743,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     ctx->err = "pmx_upload_background: non-manifold tet faces";
     return 0;
   }
+  ctx->fan_rot = ctx->nt > 0 && ctx->h_nbad[4] == 0;
   ctx->have_bg = true;
   return 1;
 }
@@ -935,7 +953,7 @@ bool pmx_ctx::pack_new_tets() {
   if (residency && ntet > 0) {
     const int64_t ns = (ntet + PMX_HINT_STRIDE - 1) / PMX_HINT_STRIDE;
     if (!dgrow(this, d_adja, (size_t)(4 * ntet + 5)) || !dgrow(this, d_tets_next, (size_t)(ntet + 1)) ||
-        !dgrow(this, d_wrec_next, (size_t)(ntet + 1)) || !dgrow(this, d_wfar, 2) ||
+        !dgrow(this, d_wrec_next, (size_t)(ntet + 1)) || !dgrow(this, d_wfar, 4) ||
         !dgrow(this, d_tets_s_next, (size_t)std::max<int64_t>(ns, 1)))
       return false;
     *h_nbad = 0;
@@ -1042,7 +1060,7 @@ static bool run_flags_valid(int flags, std::string *err) {
   }
   const int e = (flags >> PMX_RUN_EXP_SHIFT) & 0xff;
   switch (e) {
-    case 0: case 6: case 9: case 10: case 11: case 12: case 13: case 15: case 16: case 17: case 18:
+    case 0: case 6: case 9: case 10: case 11: case 12: case 13: case 15: case 16: case 17: case 18: case 19: case 20:
       return true;
     case 4: case 5: case 14: {
       const char *v = getenv("PMX_EXPERIMENTS");
@@ -1105,8 +1123,12 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   // (on the side stream only once it has been forked from the main one: an
   // unforked side stream's event could precede ev[0])
   if (ev) CK(hipEventRecord(ev[3], bdy ? ss : st));
+  // exp 19 (A/B): the fans on the main stream ahead of the derived data (a
+  // few short kernels there, instead of passes starved on the side stream);
+  // exp 20: the same with the counting sort over the vertex ids
+  const int exp0 = (opts.flags >> PMX_RUN_EXP_SHIFT) & 0xff;
   if (bdy && csr) {
-    if (!ctx->build_node_trias(ss)) return 0;
+    if (!ctx->build_node_trias(exp0 == 19 || exp0 == 20 ? st : ss, exp0 == 20 ? 1 : 0)) return 0;
     ctx->have_csr = true;
   }
   // exp 15 (A/B): no fixed-point copy of the vertices -- the hint build
@@ -1118,9 +1140,15 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     if (hint_xyz)
       launch_bg_derive(ctx->d_xyz.p, 0, ctx->grid, ctx->d_xyzq.p, ctx->d_tris.p, ctx->nt, ctx->d_trn.p,
                        (bdy && !serial) ? side : st);
-    else
+    else if (bdy && !serial) {
+      // the tria normals only feed the surface path: on its stream (r05:
+      // the main stream's derived-data pass is the vertices alone)
+      launch_bg_derive(ctx->d_xyz.p, ctx->np, ctx->grid, ctx->d_xyzq.p, ctx->d_tris.p, 0, ctx->d_trn.p, st);
+      launch_bg_derive(ctx->d_xyz.p, 0, ctx->grid, ctx->d_xyzq.p, ctx->d_tris.p, ctx->nt, ctx->d_trn.p, side);
+    } else {
       launch_bg_derive(ctx->d_xyz.p, ctx->np, ctx->grid, ctx->d_xyzq.p, ctx->d_tris.p, ctx->nt,
                        ctx->d_trn.p, st);
+    }
     ctx->have_derived = !hint_xyz;
   }
   if (ev) CK(hipEventRecord(ev[7], st));
@@ -1795,7 +1823,7 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
     } else if (!pmx_ctx_build_adja_device(ctx, ctx->d_ntetv.p, ne, n, ctx->d_adja.p, st, nullptr)) {
       return 0;
     }
-    if (!dgrow(ctx, ctx->d_wrec, (size_t)(ne + 1)) || !dgrow(ctx, ctx->d_wfar, 2)) return 0;
+    if (!dgrow(ctx, ctx->d_wrec, (size_t)(ne + 1)) || !dgrow(ctx, ctx->d_wfar, 4)) return 0;
     launch_build_tetrec(ctx->d_ntetv.p, ctx->d_adja.p, ne, PMX_HINT_STRIDE, ctx->d_tets.p, ctx->d_tets_s.p, st);
     launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, ctx->d_wfar.p, ctx->h_nbad + 2, st);
   }
@@ -1808,8 +1836,10 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
   if (!ctx->order_hint_samples(ne, st)) return 0;
   tr.mark("grids");
   CK(hipMemcpyAsync(ctx->d_tris.p, htr.data(), htr.size() * sizeof(TriRec), hipMemcpyHostToDevice, st));
+  if (!ctx->check_fans(st)) return 0;
   CK(hipGetLastError());
   CK(hipStreamSynchronize(st));            // host vectors die here
+  ctx->fan_rot = ctx->nt > 0 && ctx->h_nbad[4] == 0;
   tr.mark("uploads + sync");
   ctx->have_ptag = tags;
   // the points and the results were consumed: the next step needs new points

@@ -52,7 +52,7 @@ struct pmx_ctx {
   DevBuf<double> d_xyz;                 // old vertices, x y z (24 B), slot 0 unused
   DevBuf<TetRec> d_tets;
   DevBuf<WRec> d_wrec;                  // the walk's compact copy of d_tets (built with it)
-  DevBuf<unsigned> d_wfar;              // [0] / [1]: far-field counters of d_wrec / d_wrec_next's builds
+  DevBuf<unsigned> d_wfar;              // [0] / [1]: far-field counters of d_wrec / d_wrec_next's builds, [2] / [3] bad fans
   DevBuf<double> d_sol;
   DevBuf<int4> d_tets_s;                // hint sample: tets 1, 1+4, 1+8, ... in the order of their cells
   DevBuf<int> d_tets_sk;                // its tet indices (samples_sorted)
@@ -160,7 +160,7 @@ struct pmx_ctx {
   DevBuf<TetRec> d_tets_next;
   DevBuf<WRec> d_wrec_next;
   DevBuf<int4> d_tets_s_next;
-  // [2] / [3]: tets of d_wrec / d_wrec_next with a far neighbour field (pmx_wrec.h)
+  // [2] / [3]: tets of d_wrec / d_wrec_next with a far neighbour field (pmx_wrec.h), [4]: bad fans
   unsigned *h_nbad = nullptr;           // pinned [2]: non-manifold faces of that build, [1] of a background upload's
   DevBuf<double> d_nqual;
   bool have_qtag = false;               // raw tags of the new points
@@ -199,7 +199,12 @@ struct pmx_ctx {
   hipEvent_t *next_event_slot();
   void free_all();
   bool order_hint_samples(int64_t ne, hipStream_t s);
-  bool build_node_trias(hipStream_t s);   // from d_tris, np, nt (pmx_bdy.hip)
+  // the fans by rotation (closed manifold surface, checked at the upload:
+  // fan_rot) or by a sort; force 1: the counting sort
+  bool fan_rot = false;
+  bool fan_rotation(hipStream_t s, unsigned *d_bad);
+  bool check_fans(hipStream_t s);
+  bool build_node_trias(hipStream_t s, int force = 0);   // from d_tris, np, nt (pmx_bdy.hip)
   bool classify(hipStream_t s);           // the new points: kinds, lists, marks (pmx_capi.hip)
   bool launch_bdy(const VolArgs &a, hipStream_t s);
   bool size_tria_grid();

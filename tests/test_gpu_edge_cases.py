@@ -382,3 +382,38 @@ def test_undersized_host_outputs_refused(transfer):
     refused(lib.pmx_tetra_qual(ctx, 0, dp(qb), m.ne), "pmx_tetra_qual")
     assert np.all(qb == -5.0)
     assert lib.pmx_tetra_qual(ctx, 0, dp(qb), m.ne + 1) == 1
+
+
+def _surface_run(tr, m, x, t, sols):
+    tr.upload_background(m, sols, 0)
+    tr.upload_points(x, t)
+    tr.run()
+    r = tr.download()
+    e, v = tr.border()
+    return r.elem.copy(), r.status.copy(), [s.copy() for s in r.sols], e.copy(), v.copy()
+
+
+@pytest.mark.parametrize("open_surface", [False, True])
+def test_fans_by_rotation_equal_sorted_fans(transfer, monkeypatch, open_surface):
+    """PMMG_precompute_nodeTrias two ways (pmx_bdy.hip): the fans walked
+    through the tria adjacency (closed manifold surface, checked at the
+    upload) and the sorted (vertex, tria) pairs (PMX_FAN_ROTATION=0, and
+    whatever the upload's check refuses: here an edge without its neighbour
+    opens the surface).  Same located trias, edges, vertices and fields, bit for bit."""
+    m, x, t, sols = cube_case(10, metric="iso")
+    if open_surface:                                 # one edge without its neighbour
+        adjt = m.adjt.copy()
+        k, i = 7, 0
+        a = adjt[3 * (k - 1) + 1 + i]
+        adjt[3 * (k - 1) + 1 + i] = 0
+        adjt[3 * (a // 3 - 1) + 1 + a % 3] = 0
+        m = M.Mesh(m.xyz, m.tet, m.adja, m.tria, adjt, m.hausd)
+    monkeypatch.setenv("PMX_FAN_ROTATION", "0")
+    a = _surface_run(transfer, m, x, t, sols)
+    monkeypatch.delenv("PMX_FAN_ROTATION")
+    b = _surface_run(transfer, m, x, t, sols)
+    for u, w in zip(a[:2] + a[3:], b[:2] + b[3:]):
+        assert np.array_equal(u, w)
+    for u, w in zip(a[2], b[2]):
+        assert np.array_equal(u.view(np.uint64), w.view(np.uint64))
+    assert np.count_nonzero((t != 0) & (b[1] == 1)) > 0.9 * np.count_nonzero(t != 0)

@@ -1,0 +1,3 @@
+tools/gpu_job.sh \
+ "r5w_sw_c3:400:python -u tools/sweep.py --config C3 --rounds 7 --reps 5 --check --opt flags=16,1245200,1310736" \
+ "r5w_tr:300:cd /tmp && export TMPDIR=/tmp && cd \$GRAFT_REPO_ROOT && rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/tr_w -o run -- python3 tools/sweep.py --config C3 --rounds 1 --reps 3 --opt flags=1310736"

@@ -792,7 +792,7 @@ bool pmx_ctx::fan_rotation(hipStream_t s, unsigned *d_bad) {
 bool pmx_ctx::check_fans(hipStream_t s) {
   fan_rot = false;
   h_nbad[4] = 1u;
-  if (nt < 1) return true;
+  if (nt < 1 || 3 * (nt + 1) * (int64_t)FAN_CAP > (int64_t)INT32_MAX) return true;   // int windows
   const char *e = getenv("PMX_FAN_ROTATION");
   if (e && e[0] == '0') return true;
   if (!pmx_dgrow(this, d_wfar, 4)) return false;

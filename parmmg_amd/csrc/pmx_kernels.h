@@ -58,7 +58,8 @@ struct VolArgs {
   int exp;                      // measurement switch (tools/walk_pmc.sh): 0 production,
                                 // 4 no interpolation, 5 hint + hint record only,
                                 // 17 a record with a far neighbour field read whole,
-                                // 18 compact records whatever their far fields
+                                // 18 compact records whatever their far fields,
+                                // (pmx_run) 19 / 20 fans on the main stream
 };
 
 struct ExhArgs {

@@ -137,8 +137,8 @@ __device__ __forceinline__ int64_t hint_cell(unsigned long long a, unsigned long
   return gcell(g, cq[0], cq[1], cq[2]);
 }
 
-template <bool PACKED, bool FROM_XYZ = false, bool V0 = false>
-__global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ packed, const int *__restrict__ kidx,
+template <bool PACKED, bool FROM_XYZ = false, bool V0 = false, int BS = 256>
+__global__ __launch_bounds__(BS) void k_hint_build(const int4 *__restrict__ packed, const int *__restrict__ kidx,
                                                     const TetRec *__restrict__ tets, int64_t ne,
                                                     int stride, int *__restrict__ grid, GridDesc g,
                                                     const unsigned long long *__restrict__ xyzq,
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256) void k_hint_build(const int4 *__restrict__ pac
 }
 void launch_hint_build(const int4 *packed, const int *kidx, const TetRec *tets, int64_t ne, int stride, int *grid,
                        GridDesc g, const unsigned long long *xyzq, const double *xyz, hipStream_t s,
-                       bool v0) {
+                       bool v0, int bs) {
   const int64_t n = (ne + stride - 1) / stride;
   const int64_t nb = std::max<int64_t>((n + 255) / 256, 1);
   if (v0 && xyzq && packed)
@@ -184,6 +184,12 @@ void launch_hint_build(const int4 *packed, const int *kidx, const TetRec *tets, 
   else if (packed && !xyzq)
     hipLaunchKernelGGL((k_hint_build<true, true>), dim3((unsigned)nb), dim3(256), 0, s, packed, kidx, tets, ne, stride,
                        grid, g, xyzq, xyz);
+  else if (packed && bs == 1024)
+    hipLaunchKernelGGL((k_hint_build<true, false, false, 1024>), dim3((unsigned)((n + 1023) / 1024)), dim3(1024), 0,
+                       s, packed, kidx, tets, ne, stride, grid, g, xyzq, xyz);
+  else if (packed && bs == 64)
+    hipLaunchKernelGGL((k_hint_build<true, false, false, 64>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s,
+                       packed, kidx, tets, ne, stride, grid, g, xyzq, xyz);
   else if (packed)
     hipLaunchKernelGGL((k_hint_build<true, false>), dim3((unsigned)nb), dim3(256), 0, s, packed, kidx, tets, ne, stride,
                        grid, g, xyzq, xyz);

@@ -711,9 +711,9 @@ __global__ __launch_bounds__(256) void k_nt_runs(const unsigned *__restrict__ ke
 // The fans by rotation (r05), for a closed manifold surface -- every
 // boundary of a ParMmg group's volume mesh, interfaces included: each
 // (tria, corner) slot walks its vertex's fan through the tria adjacency
-// (Mmg's adjt: edge i opposite vertex i); the fan's owner (its smallest
-// tria) writes it in increasing tria order (PMMG_precompute_nodeTrias's) into
-// its window, and every member's range.  One kernel, no atomics, no
+// (Mmg's adjt: edge i opposite vertex i) and writes its tria into the window
+// of the fan's owner (its smallest tria) at its rank: the fan's increasing
+// tria order of PMMG_precompute_nodeTrias.  One kernel, no atomics, no
 // np-sized arrays (the radix sort of C3's 2.3 M (vertex, tria) pairs took
 // ~0.26 ms alone on the GPU).  A fan that meets an
 // edge without a neighbour (open or non-manifold surface), a neighbour
@@ -743,72 +743,36 @@ __device__ __forceinline__ bool fan_turn(const TriRec *__restrict__ tris, int k,
     cx = cw;
   }
 }
-// Only the fan's owner (its smallest tria) writes it: a slot one of whose
-// two neighbours around v is smaller returns at once (no load); the other
-// local minima walk the fan and return unless they are the owner; the owner
-// walks it again, keeping the members (tria, corner) in its LDS row, sorts
-// them there and writes the fan and every member's range (r05: every slot
-// walking its fan and writing itself at its rank, 2.3 M walks at C3, ran
-// 0.12 ms beside the main stream; an owner sorting in global memory made a
-// ~35-deep dependent chain, 0.19 ms).
-#define FAN_ROW (FAN_CAP + 1)
+// Every slot walks its fan once: the fan's window is its owner's (the
+// smallest tria), and the slot's tria goes to the window at its rank in the
+// fan (the number of smaller members) -- the sorted fan without a sort and no
+// dependent chain beyond the walk itself.  r05 A/Bs at C3 (rocprof, beside
+// the main stream): this 0.12 ms; an owner sorting its fan in global memory
+// (a ~35-deep dependent chain) 0.19 ms; only the local minima walking and the
+// owner sorting in LDS (2.3 M walks -> 0.8 M, but serial chains in few
+// threads) 0.23 ms, step 2.061 vs 2.042 ms (profiles/r05_c3_sweep_fans_owner_lds.log).
 __global__ __launch_bounds__(256) void k_fan_rotate(const TriRec *__restrict__ tris, int64_t nt,
                                                     int2 *__restrict__ range, int *__restrict__ list,
                                                     unsigned *__restrict__ bad) {
-  __shared__ int mem[256 * FAN_ROW];              // per thread: its fan's members, g * 4 + corner
-  int *row = mem + threadIdx.x * FAN_ROW;
   unsigned nbad = 0;
   for (int64_t i = 3 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 3 * (nt + 1);
        i += (int64_t)gridDim.x * blockDim.x) {
     const int k = (int)(i / 3), l = (int)(i - 3 * (int64_t)k);
     const TriRec t0 = tris[k];
     if (t0.v[0] <= 0) { range[i] = make_int2(0, 0); continue; }
-    const int a = sel3(t0.nb, (l + 1) % 3), b = sel3(t0.nb, (l + 2) % 3);
-    if ((a > 0 && a < k) || (b > 0 && b < k)) continue;
-    int n = 0, own = k;
-    const bool ok = fan_turn(tris, k, l, t0, [&](int g, int) {
-      n++;
-      own = min(own, g);
-    });
-    if (!ok) { nbad++; continue; }
-    if (own != k) continue;
-    int j = 0;
-    fan_turn(tris, k, l, t0, [&](int g, int c) { row[j++] = g * 4 + c; });
-    for (int x0 = 1; x0 < n; x0++) {               // insertion sort by tria (in LDS)
-      const int x = row[x0];
-      int y = x0 - 1;
-      while (y >= 0 && row[y] > x) { row[y + 1] = row[y]; y--; }
-      row[y + 1] = x;
-    }
-    const int base = (int)((3 * (int64_t)k + l - 3) * FAN_CAP);
-    for (int r = 0; r < n; r++) {
-      const int g = row[r] >> 2, c = row[r] & 3;
-      list[base + r] = g;
-      range[3 * (int64_t)g + c] = make_int2(base, base + n);
-    }
-  }
-  for (int o = 32; o > 0; o >>= 1) nbad += __shfl_xor(nbad, o);
-  if ((threadIdx.x & 63) == 0 && nbad) atomicAdd(bad, nbad);
-}
-
-// (A/B, exp 23: every slot walks its fan and writes itself at its rank)
-__global__ __launch_bounds__(256) void k_fan_rank(const TriRec *__restrict__ tris, int64_t nt,
-                                                  int2 *__restrict__ range, int *__restrict__ list) {
-  for (int64_t i = 3 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 3 * (nt + 1);
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int k = (int)(i / 3), l = (int)(i - 3 * (int64_t)k);
-    const TriRec t0 = tris[k];
-    if (t0.v[0] <= 0) { range[i] = make_int2(0, 0); continue; }
     int n = 0, rank = 0, own = k, lown = l;
-    if (!fan_turn(tris, k, l, t0, [&](int g, int c) {
-          n++;
-          rank += g < k ? 1 : 0;
-          if (g < own) { own = g; lown = c; }
-        })) continue;
+    const bool ok = fan_turn(tris, k, l, t0, [&](int g, int c) {
+      n++;
+      rank += g < k ? 1 : 0;
+      if (g < own) { own = g; lown = c; }
+    });
+    if (!ok) { nbad++; range[i] = make_int2(0, 0); continue; }
     const int base = (int)((3 * (int64_t)own + lown - 3) * FAN_CAP);
     range[i] = make_int2(base, base + n);
     list[base + rank] = k;
   }
+  for (int o = 32; o > 0; o >>= 1) nbad += __shfl_xor(nbad, o);
+  if ((threadIdx.x & 63) == 0 && nbad) atomicAdd(bad, nbad);
 }
 
 bool pmx_ctx::fan_rotation(hipStream_t s, unsigned *d_bad) {
@@ -816,10 +780,7 @@ bool pmx_ctx::fan_rotation(hipStream_t s, unsigned *d_bad) {
   if (!pmx_dgrow(this, d_ntrange, (size_t)(3 * (nt + 1))) || !pmx_dgrow(this, d_ntlist, (size_t)(m * FAN_CAP)))
     return false;
   const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>((m + 255) / 256, 16384));
-  if (fan_rank)
-    hipLaunchKernelGGL(k_fan_rank, dim3(nb), dim3(256), 0, s, d_tris.p, nt, d_ntrange.p, d_ntlist.p);
-  else
-    hipLaunchKernelGGL(k_fan_rotate, dim3(nb), dim3(256), 0, s, d_tris.p, nt, d_ntrange.p, d_ntlist.p, d_bad);
+  hipLaunchKernelGGL(k_fan_rotate, dim3(nb), dim3(256), 0, s, d_tris.p, nt, d_ntrange.p, d_ntlist.p, d_bad);
   if (hipGetLastError() != hipSuccess) {
     err = "node trias: launch";
     return false;

@@ -1060,7 +1060,7 @@ static bool run_flags_valid(int flags, std::string *err) {
   }
   const int e = (flags >> PMX_RUN_EXP_SHIFT) & 0xff;
   switch (e) {
-    case 0: case 6: case 9: case 10: case 11: case 12: case 13: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 23:
+    case 0: case 6: case 9: case 10: case 11: case 12: case 13: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22:
       return true;
     case 4: case 5: case 14: {
       const char *v = getenv("PMX_EXPERIMENTS");
@@ -1128,7 +1128,6 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   // exp 20: the same with the counting sort over the vertex ids
   const int exp0 = (opts.flags >> PMX_RUN_EXP_SHIFT) & 0xff;
   if (bdy && csr) {
-    ctx->fan_rank = exp0 == 23;
     if (!ctx->build_node_trias(exp0 == 19 || exp0 == 20 ? st : ss, exp0 == 20 ? 1 : 0)) return 0;
     ctx->have_csr = true;
   }

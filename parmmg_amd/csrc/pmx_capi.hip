@@ -991,8 +991,8 @@ bool pmx_ctx::fix_orphans() {
   return true;
 }
 
-// the hint sample in cell order (k_sample_keys, pmx_kernels.hip), after the
-// grid of this background is set up and its coordinates are on the device.
+// the hint sample in the order of its tets' smallest vertex ids
+// (k_sample_keys, pmx_kernels.hip), once the sample is on the device and np set.
 // PMX_HINT_SAMPLE_ORDER=0 keeps the tet order (A/B).
 bool pmx_ctx::order_hint_samples(int64_t ne, hipStream_t s) {
   samples_sorted = false;
@@ -1005,8 +1005,8 @@ bool pmx_ctx::order_hint_samples(int64_t ne, hipStream_t s) {
       !dgrow(this, d_salt, (size_t)n) || !dgrow(this, d_tets_sk, (size_t)n) ||
       !dgrow(this, d_stmp, std::max<size_t>(tb, 1)))
     return false;
-  if (!launch_hint_sort(d_tets_s.p, n, PMX_HINT_STRIDE, grid, d_xyz.p, d_skey.p, d_sidx.p, d_salt.p,
-                        d_tets_sk.p, d_stmp.p, tb, s)) {
+  if (!launch_hint_sort(d_tets_s.p, n, PMX_HINT_STRIDE, np, d_skey.p, d_sidx.p, d_salt.p, d_tets_sk.p, d_stmp.p,
+                        tb, s)) {
     err = "hint sample: sort";
     return false;
   }

@@ -129,12 +129,12 @@ void launch_build_tetrec(const int4 *tv, const int *adja, int64_t ne, int stride
 // the walk's compact records from the tet records (slots 0..ne)
 // (*h_nfar, pinned, when stream s gets there: the tets with a far neighbour
 // field, pmx_wrec.h; d_nfar one device word)
-// the packed hint sample in the order of its cells (k_sample_keys): out[i]
-// = smp[t_i] and kidx[i] = 1 + stride * t_i; keys and idx 2n words each, tmp
-// hint_sort_temp_bytes(n) bytes
+// the packed hint sample in the order of its tets' smallest vertex ids
+// (k_sample_keys): out[i] = smp[t_i] and kidx[i] = 1 + stride * t_i; keys and
+// idx 2n words each, tmp hint_sort_temp_bytes(n) bytes
 size_t hint_sort_temp_bytes(int64_t n);
-bool launch_hint_sort(const int4 *smp, int64_t n, int stride, GridDesc g, const double *xyz, unsigned *keys,
-                      int *idx, int4 *out, int *kidx, void *tmp, size_t tmp_bytes, hipStream_t s);
+bool launch_hint_sort(const int4 *smp, int64_t n, int stride, int64_t np, unsigned *keys, int *idx, int4 *out,
+                      int *kidx, void *tmp, size_t tmp_bytes, hipStream_t s);
 void launch_build_wrec(const TetRec *tets, int64_t ne, WRec *wr, unsigned *d_nfar, unsigned *h_nfar,
                        hipStream_t s);
 // workgroups of k_fallback that can be co-resident with `share` other

@@ -198,27 +198,21 @@ void launch_hint_build(const int4 *packed, const int *kidx, const TetRec *tets, 
                        grid, g, xyzq, xyz);
 }
 
-// The packed hint sample in the order of the cells k_hint_build writes
-// (at every upload / promotion, not in the step).  In tet order the sample
-// is as coherent as the numbering: an Mmg-appended numbering (10 % of the tets
+// The packed hint sample in the order of its tets' smallest vertex ids (at
+// every upload / promotion, not in the step): a re-layout of connectivity
+// like the walk records, no geometry.  In tet order the sample is as
+// coherent as the tet numbering: an Mmg-appended numbering (10 % of the tets
 // moved to the end) scatters a tenth of it, and each wave of those samples
 // gathers and writes 64 distinct lines -- C3 hint build 0.25 -> 0.42 ms
-// (r05).  Keys: the sample's cell.
-// The stable sort leaves each cell's run in increasing tet order, the order
-// of the sample in tet order (r05 A/B: with the runs reversed the walk was
-// 1.7-2.3 % slower at C3, lex and appended; tools/ab_env.py).
-__global__ __launch_bounds__(256) void k_sample_keys(const int4 *__restrict__ smp, int64_t n, GridDesc g,
-                                                     const double *__restrict__ xyz, unsigned *__restrict__ key,
-                                                     int *__restrict__ idx) {
+// (r05).  The vertex numbering (Mmg keeps its vertices
+// in place, Scotch renumbers them spatially) orders it in space again.  The
+// stable sort leaves samples sharing a smallest vertex in tet order.
+__global__ __launch_bounds__(256) void k_sample_keys(const int4 *__restrict__ smp, int64_t n, unsigned nokey,
+                                                     unsigned *__restrict__ key, int *__restrict__ idx) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t t = i;
-    const int4 v = smp[t];
-    unsigned kk = (unsigned)((int64_t)g.dim[0] * g.dim[1] * g.dim[2]);   // deleted tets last
-    if (v.x > 0)
-      kk = (unsigned)hint_cell(quant_xyz(xyz + 3 * (int64_t)v.x, g), quant_xyz(xyz + 3 * (int64_t)v.y, g),
-                               quant_xyz(xyz + 3 * (int64_t)v.z, g), quant_xyz(xyz + 3 * (int64_t)v.w, g), g);
-    key[i] = kk;
-    idx[i] = (int)t;
+    const int4 v = smp[i];
+    key[i] = v.x > 0 ? (unsigned)min(min(v.x, v.y), min(v.z, v.w)) : nokey;   // deleted tets last
+    idx[i] = (int)i;
   }
 }
 // the sorted sample and the tet index of each entry (1 + stride * t)
@@ -231,10 +225,9 @@ __global__ __launch_bounds__(256) void k_sample_gather(const int4 *__restrict__ 
     kidx[i] = 1 + stride * t;
   }
 }
-static int key_bits(const GridDesc &g) {
-  const int64_t cells = (int64_t)g.dim[0] * g.dim[1] * g.dim[2];   // keys 0 .. cells
+static int key_bits(int64_t np) {
   int bits = 1;
-  while (bits < 32 && ((int64_t)1 << bits) <= cells) bits++;
+  while (bits < 32 && ((int64_t)1 << bits) <= np + 1) bits++;   // keys 1 .. np + 1
   return bits;
 }
 size_t hint_sort_temp_bytes(int64_t n) {
@@ -244,13 +237,13 @@ size_t hint_sort_temp_bytes(int64_t n) {
   hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, k, v, (int)n, 0, 32);
   return bytes;
 }
-bool launch_hint_sort(const int4 *smp, int64_t n, int stride, GridDesc g, const double *xyz, unsigned *keys,
-                      int *idx, int4 *out, int *kidx, void *tmp, size_t tmp_bytes, hipStream_t s) {
+bool launch_hint_sort(const int4 *smp, int64_t n, int stride, int64_t np, unsigned *keys, int *idx, int4 *out,
+                      int *kidx, void *tmp, size_t tmp_bytes, hipStream_t s) {
   const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 65536));
-  hipLaunchKernelGGL(k_sample_keys, dim3((unsigned)nb), dim3(256), 0, s, smp, n, g, xyz, keys, idx);
+  hipLaunchKernelGGL(k_sample_keys, dim3((unsigned)nb), dim3(256), 0, s, smp, n, (unsigned)(np + 1), keys, idx);
   hipcub::DoubleBuffer<unsigned> k(keys, keys + n);
   hipcub::DoubleBuffer<int> v(idx, idx + n);
-  if (hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, k, v, (int)n, 0, key_bits(g), s) != hipSuccess)
+  if (hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, k, v, (int)n, 0, key_bits(np), s) != hipSuccess)
     return false;
   hipLaunchKernelGGL(k_sample_gather, dim3((unsigned)nb), dim3(256), 0, s, smp, (const int *)v.Current(), n,
                      stride, out, kidx);

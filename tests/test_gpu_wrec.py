@@ -150,3 +150,35 @@ def test_hint_sample_order(transfer, monkeypatch):
     assert out[1][3] < 1.2 * out[0][3], (out[0][3], out[1][3])
     vol = (t == 0) & (out[1][1] == 1)
     assert not np.array_equal(out[0][4][vol], out[1][4][vol])       # other start tets
+
+
+COMPACT_FORCED = 18 << 16         # exp 18: compact records whatever their far fields
+
+
+def test_record_format_switch_at_size(transfer):
+    """An Mmg-appended numbering of 10.4 M tets (kuhn n = 120) with its moved
+    tenth 2^23 indices further up: a fifth of the 18.8 M tet slots have a far
+    neighbour field, above the 1/16 at which the walk takes the 32-B records
+    (pmx_capi.hip fill_vol_args).  The default step, the
+    compact records forced (exp 18: far fields resolved as crossed) and the
+    32-B walk forced (exp 6) agree bit for bit."""
+    n = 120
+    m0, _ = M.numbering(M.kuhn_cube(n), "appended")
+    m, _ = _gapped(m0, (1 << 23) + 5)
+    far, ntf = M.wrec_far_fields(m)
+    assert ntf * 16 > m.ne, (far, ntf, m.ne)
+    x, t = M.new_points(n, seed=4, surface=True)
+    x, t = x[::8].copy(), t[::8].copy()
+    sols = [M.on_vertices(m0, M.iso_metric), M.on_vertices(m0, lin_field)]
+    transfer.upload_background(m, sols, 0)
+    transfer.upload_points(x, t)
+    out = []
+    for flags in (0, COMPACT_FORCED, FULL_RECORDS):
+        transfer.run(flags=flags)
+        r = transfer.download()
+        out.append((r.elem.copy(), r.status.copy(), [s.copy() for s in r.sols]))
+    _assert_same(out[0], out[1])
+    _assert_same(out[0], out[2])
+    vol = (t == 0) & (out[0][1] == 1)
+    assert vol.sum() > 0.9 * (t == 0).sum()
+    assert np.max(np.abs(out[0][2][1][vol, 0] - lin_field(x[vol])[:, 0])) < 1e-12

@@ -95,10 +95,15 @@ __global__ __launch_bounds__(256) void k_bg_derive(const double *__restrict__ xy
     trn[k] = Pt4{n.x * dd, n.y * dd, n.z * dd, a};
   }
 }
+// PMX_DERIVE_BLOCKS (A/B): the vertex pass's block cap
+static int64_t derive_blocks() {
+  const char *e = getenv("PMX_DERIVE_BLOCKS");
+  return e ? std::max<int64_t>(1, atoll(e)) : 8192;
+}
 void launch_bg_derive(const double *xyz, int64_t np, GridDesc g, unsigned long long *xyzq,
                       const TriRec *tris, int64_t nt, Pt4 *trn, hipStream_t s) {
   const int64_t npair = np > 0 ? (np + 2) / 2 : 0;
-  const int nbv = (int)std::min<int64_t>((npair + 255) / 256, 8192);
+  const int nbv = (int)std::min<int64_t>((npair + 255) / 256, derive_blocks());
   const int nbt = (int)std::min<int64_t>((nt + 255) / 256, 4096);
   if (nbv + nbt < 1) return;
   hipLaunchKernelGGL(k_bg_derive, dim3((unsigned)(nbv + nbt)), dim3(256), 0, s, xyz, np, g, xyzq, tris, nt, trn,

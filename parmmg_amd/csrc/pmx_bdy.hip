@@ -751,9 +751,13 @@ __device__ __forceinline__ bool fan_turn(const TriRec *__restrict__ tris, int k,
 // (a ~35-deep dependent chain) 0.19 ms; only the local minima walking and the
 // owner sorting in LDS (2.3 M walks -> 0.8 M, but serial chains in few
 // threads) 0.23 ms, step 2.061 vs 2.042 ms (profiles/r05_c3_sweep_fans_owner_lds.log).
+// vcount (the upload's check only): every vertex's tria count; a fan that
+// closes without all of them (a vertex where two surface sheets touch: a
+// group pinched at a vertex) counts as bad
 __global__ __launch_bounds__(256) void k_fan_rotate(const TriRec *__restrict__ tris, int64_t nt,
                                                     int2 *__restrict__ range, int *__restrict__ list,
-                                                    unsigned *__restrict__ bad) {
+                                                    unsigned *__restrict__ bad,
+                                                    const unsigned *__restrict__ vcount) {
   unsigned nbad = 0;
   for (int64_t i = 3 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 3 * (nt + 1);
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -766,7 +770,7 @@ __global__ __launch_bounds__(256) void k_fan_rotate(const TriRec *__restrict__ t
       rank += g < k ? 1 : 0;
       if (g < own) { own = g; lown = c; }
     });
-    if (!ok) { nbad++; range[i] = make_int2(0, 0); continue; }
+    if (!ok || (vcount && vcount[sel3(t0.v, l)] != (unsigned)n)) { nbad++; range[i] = make_int2(0, 0); continue; }
     const int base = (int)((3 * (int64_t)own + lown - 3) * FAN_CAP);
     range[i] = make_int2(base, base + n);
     list[base + rank] = k;
@@ -775,12 +779,13 @@ __global__ __launch_bounds__(256) void k_fan_rotate(const TriRec *__restrict__ t
   if ((threadIdx.x & 63) == 0 && nbad) atomicAdd(bad, nbad);
 }
 
-bool pmx_ctx::fan_rotation(hipStream_t s, unsigned *d_bad) {
+bool pmx_ctx::fan_rotation(hipStream_t s, unsigned *d_bad, const unsigned *vcount) {
   const int64_t m = 3 * nt;
   if (!pmx_dgrow(this, d_ntrange, (size_t)(3 * (nt + 1))) || !pmx_dgrow(this, d_ntlist, (size_t)(m * FAN_CAP)))
     return false;
   const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>((m + 255) / 256, 16384));
-  hipLaunchKernelGGL(k_fan_rotate, dim3(nb), dim3(256), 0, s, d_tris.p, nt, d_ntrange.p, d_ntlist.p, d_bad);
+  hipLaunchKernelGGL(k_fan_rotate, dim3(nb), dim3(256), 0, s, d_tris.p, nt, d_ntrange.p, d_ntlist.p, d_bad,
+                     vcount);
   if (hipGetLastError() != hipSuccess) {
     err = "node trias: launch";
     return false;
@@ -789,7 +794,8 @@ bool pmx_ctx::fan_rotation(hipStream_t s, unsigned *d_bad) {
 }
 
 // the upload's check: the fans of this background by rotation, their
-// failures into h_nbad[4] (read after the upload's final sync).
+// failures (open, non-manifold, pinched, over FAN_CAP) into h_nbad[4] (read
+// after the upload's final sync).
 // PMX_FAN_ROTATION=0 keeps the sort (A/B, tests).
 bool pmx_ctx::check_fans(hipStream_t s) {
   fan_rot = false;
@@ -797,12 +803,17 @@ bool pmx_ctx::check_fans(hipStream_t s) {
   if (nt < 1 || 3 * (nt + 1) * (int64_t)FAN_CAP > (int64_t)INT32_MAX) return true;   // int windows
   const char *e = getenv("PMX_FAN_ROTATION");
   if (e && e[0] == '0') return true;
-  if (!pmx_dgrow(this, d_wfar, 4)) return false;
-  if (hipMemsetAsync(d_wfar.p + 3, 0, sizeof(unsigned), s) != hipSuccess) {
+  // every vertex's tria count (np-sized, at the upload only): a fan walked
+  // around one sheet of a vertex where several touch closes short of it
+  if (!pmx_dgrow(this, d_wfar, 4) || !pmx_dgrow(this, d_ntkey, (size_t)(np + 2))) return false;
+  if (hipMemsetAsync(d_wfar.p + 3, 0, sizeof(unsigned), s) != hipSuccess ||
+      hipMemsetAsync(d_ntkey.p, 0, (size_t)(np + 2) * sizeof(unsigned), s) != hipSuccess) {
     err = "node trias: memset";
     return false;
   }
-  if (!fan_rotation(s, d_wfar.p + 3)) return false;
+  const unsigned nbc = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nt + 255) / 256, 4096));
+  hipLaunchKernelGGL(k_nt_count, dim3(nbc), dim3(256), 0, s, d_tris.p, nt, d_ntkey.p);
+  if (!fan_rotation(s, d_wfar.p + 3, d_ntkey.p)) return false;
   if (hipMemcpyAsync(h_nbad + 4, d_wfar.p + 3, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess) {
     err = "node trias: check";
     return false;

@@ -202,7 +202,7 @@ struct pmx_ctx {
   // the fans by rotation (closed manifold surface, checked at the upload:
   // fan_rot) or by a sort; force 1: the counting sort
   bool fan_rot = false;
-  bool fan_rotation(hipStream_t s, unsigned *d_bad);
+  bool fan_rotation(hipStream_t s, unsigned *d_bad, const unsigned *vcount = nullptr);
   bool check_fans(hipStream_t s);
   bool build_node_trias(hipStream_t s, int force = 0);   // from d_tris, np, nt (pmx_bdy.hip)
   bool classify(hipStream_t s);           // the new points: kinds, lists, marks (pmx_capi.hip)

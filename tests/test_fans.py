@@ -3,8 +3,9 @@ the tria adjacency, the rule of k_fan_rotate (parmmg_amd/csrc/pmx_bdy.hip),
 restated on the CPU: every (tria, corner) slot turns around its vertex
 through Mmg's adjt (edge i opposite vertex i) and puts its tria at its rank
 in the window of the fan's smallest tria.  The lists equal the reference's
-construction (each vertex's trias in increasing index order) and a surface
-with an edge without its neighbour is refused."""
+construction (each vertex's trias in increasing index order); a surface with
+an edge without its neighbour, or a vertex whose fan does not hold all its
+trias (a pinched vertex), is refused."""
 import numpy as np
 
 from parmmg_amd import mesh as M
@@ -12,8 +13,30 @@ from parmmg_amd import mesh as M
 FAN_CAP = 32
 
 
+def pinched_cubes(n=3):
+    """Two Kuhn cubes touching at one vertex, (1, 1, 1): every edge of the
+    surface is manifold, the shared vertex has two separate fans."""
+    a = M.kuhn_cube(n, jitter=0.0)
+    xyz = np.vstack([a.xyz, a.xyz[1:] + 1.0])
+    ia = int(np.nonzero(np.all(np.abs(a.xyz[1:] - 1.0) < 1e-12, axis=1))[0][0]) + 1
+    ib = int(np.nonzero(np.all(np.abs(a.xyz[1:]) < 1e-12, axis=1))[0][0]) + 1
+    tb = a.tet[1:] + a.np
+    tb[tb == ib + a.np] = ia
+    tet = np.vstack([a.tet, tb]).astype(np.int32)
+    keep = np.ones(len(xyz), bool)
+    keep[ib + a.np] = False
+    newid = np.cumsum(keep) - 1
+    tet = newid[tet].astype(np.int32)
+    tet[0] = 0
+    return M.from_tets(xyz[keep], tet), ia
+
+
 def fans_by_rotation(tria, adjt):
     nt = len(tria) - 1
+    count = {}
+    for k in range(1, nt + 1):                  # the upload's check: trias per vertex
+        for v in tria[k]:
+            count[int(v)] = count.get(int(v), 0) + 1
     rng = {}
     lists = {}
     for k in range(1, nt + 1):
@@ -33,6 +56,8 @@ def fans_by_rotation(tria, adjt):
                 cv, cw = tn.index(v), tn.index(w)
                 members.append((nxt, cv))
                 cur, cx, w = nxt, cw, tn[3 - cv - cw]
+            if len(members) != count[v]:        # a fan of one sheet of a pinched vertex
+                return None
             own, lown = min(members)
             rank = sum(1 for g, _ in members if g < k)
             base = (3 * own + lown - 3) * FAN_CAP
@@ -65,3 +90,11 @@ def test_open_surface_refused():
     adjt[3 * (7 - 1) + 1] = 0
     adjt[3 * (a // 3 - 1) + 1 + a % 3] = 0
     assert fans_by_rotation(m.tria, adjt) is None
+
+
+def test_pinched_vertex_refused():
+    """Two surface sheets touching at a vertex: each fan walked around one
+    sheet closes short of the vertex's tria count -- the upload keeps the
+    sort (a ParMmg group pinched at a vertex by its partition)."""
+    m, _ = pinched_cubes()
+    assert fans_by_rotation(m.tria, m.adjt) is None

@@ -417,3 +417,33 @@ def test_fans_by_rotation_equal_sorted_fans(transfer, monkeypatch, open_surface)
     for u, w in zip(a[2], b[2]):
         assert np.array_equal(u.view(np.uint64), w.view(np.uint64))
     assert np.count_nonzero((t != 0) & (b[1] == 1)) > 0.9 * np.count_nonzero(t != 0)
+
+
+
+def test_fans_at_a_pinched_vertex(transfer, monkeypatch):
+    """Two cubes touching at one vertex (every surface edge manifold, two
+    fans at the shared vertex): the upload's check (each fan holds all the
+    vertex's trias) refuses the rotation, and surface points around the
+    pinch are located and interpolated as with the sorted fans."""
+    from test_fans import pinched_cubes
+    m, ip = pinched_cubes(3)
+    c = m.xyz[ip]
+    rng = np.random.default_rng(5)
+    pts = []
+    for sgn in (-1.0, 1.0):                      # the two sheets' faces through the pinch
+        for ax in range(3):
+            for _ in range(40):
+                p = c + sgn * rng.uniform(0.0, 0.15, 3)
+                p[ax] = c[ax]
+                pts.append(p)
+    x = np.array(pts)
+    t = np.full(len(x), 16, np.uint16)            # MG_BDY
+    sols = [M.on_vertices(m, M.iso_metric), M.on_vertices(m, lin_field)]
+    monkeypatch.setenv("PMX_FAN_ROTATION", "0")
+    a = _surface_run(transfer, m, x, t, sols)
+    monkeypatch.delenv("PMX_FAN_ROTATION")
+    b = _surface_run(transfer, m, x, t, sols)
+    for u, w in zip(a[:2] + a[3:], b[:2] + b[3:]):
+        assert np.array_equal(u, w)
+    for u, w in zip(a[2], b[2]):
+        assert np.array_equal(u.view(np.uint64), w.view(np.uint64))

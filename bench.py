@@ -524,6 +524,9 @@ def main():
     from parmmg_amd import mesh as M
     st["wrec_escapes"] = M.wrec_escapes(m)
     st["wrec_far_fields"], st["wrec_tets_with_far_fields"] = M.wrec_far_fields(m)
+    # the walk's record format (pmx_capi.hip fill_vol_args: 32-B records above
+    # 1/16 of the tets with a far neighbour field)
+    st["walk_records"] = "32-B" if st["wrec_tets_with_far_fields"] * 16 > m.ne else "24-B compact"
     # the same step on a background already prepared by an earlier step (what
     # repeated steps on one background cost; reported, never `value`)
     sync()
@@ -596,7 +599,10 @@ def main():
                      "alg_bytes_per_launch": b_vol, "avg_launch_ms": k_ms["vol"],
                      # >1: that many groups' walks run at once on separate
                      # streams, each launch's duration includes the others'
-                     "concurrent_launches": ngrp},
+                     "concurrent_launches": ngrp,
+                     # the whole step against the same peak (SURVEY 8(d)'s
+                     # algorithmic bytes of the step / ms_per_step)
+                     "step_frac": B_all / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
         "kernel_ms": k_ms,
         "per_iteration": {"ms": ms, "includes": (
             "every device pass of one PMMG_interpMetricsAndFields call on the raw uploaded arrays: "

@@ -805,7 +805,7 @@ bool pmx_ctx::check_fans(hipStream_t s) {
   if (e && e[0] == '0') return true;
   // every vertex's tria count (np-sized, at the upload only): a fan walked
   // around one sheet of a vertex where several touch closes short of it
-  if (!pmx_dgrow(this, d_wfar, 4) || !pmx_dgrow(this, d_ntkey, (size_t)(np + 2))) return false;
+  if (!pmx_dgrow(this, d_wfar, 8) || !pmx_dgrow(this, d_ntkey, (size_t)(np + 2))) return false;
   if (hipMemsetAsync(d_wfar.p + 3, 0, sizeof(unsigned), s) != hipSuccess ||
       hipMemsetAsync(d_ntkey.p, 0, (size_t)(np + 2) * sizeof(unsigned), s) != hipSuccess) {
     err = "node trias: memset";

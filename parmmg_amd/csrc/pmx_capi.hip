@@ -413,7 +413,7 @@ pmx_ctx *pmx_create(int device) {
       hipStreamCreateWithFlags(&ctx->up, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_topo, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_tets, hipEventDisableTiming) != hipSuccess ||
-      hipHostMalloc((void **)&ctx->h_nbad, 6 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void **)&ctx->h_nbad, 8 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess ||
       [&] {
         for (auto &e : ctx->ev_dl)
           if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return true;
@@ -583,7 +583,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     ~StreamGuard() { if (s) hipStreamSynchronize(s); }
   } topo_guard;
   if (!dgrow(ctx, ctx->d_xyz, (size_t)(np + 1) * 3) || !dgrow(ctx, ctx->d_tets, (size_t)(ne + 1)) ||
-      !dgrow(ctx, ctx->d_wrec, (size_t)(ne + 1)) || !dgrow(ctx, ctx->d_wfar, 4) ||
+      !dgrow(ctx, ctx->d_wrec, (size_t)(ne + 1)) || !dgrow(ctx, ctx->d_wfar, 8) ||
       !dgrow(ctx, ctx->d_tets_s, (size_t)std::max<int64_t>(ns, 1)) || !dgrow(ctx, ctx->d_sol, hs_n) ||
       !dgrow(ctx, ctx->d_tris, (size_t)(nt + 1)) || !dgrow(ctx, ctx->d_trn, (size_t)(nt + 1)) ||
       !dgrow(ctx, ctx->d_xyzq, (size_t)(np + 1)) ||
@@ -744,6 +744,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     return 0;
   }
   ctx->fan_rot = ctx->nt > 0 && ctx->h_nbad[4] == 0;
+  ctx->nsamp = ctx->samples_owner ? (int64_t)ctx->h_nbad[5] : 0;
   ctx->have_bg = true;
   return 1;
 }
@@ -953,7 +954,7 @@ bool pmx_ctx::pack_new_tets() {
   if (residency && ntet > 0) {
     const int64_t ns = (ntet + PMX_HINT_STRIDE - 1) / PMX_HINT_STRIDE;
     if (!dgrow(this, d_adja, (size_t)(4 * ntet + 5)) || !dgrow(this, d_tets_next, (size_t)(ntet + 1)) ||
-        !dgrow(this, d_wrec_next, (size_t)(ntet + 1)) || !dgrow(this, d_wfar, 4) ||
+        !dgrow(this, d_wrec_next, (size_t)(ntet + 1)) || !dgrow(this, d_wfar, 8) ||
         !dgrow(this, d_tets_s_next, (size_t)std::max<int64_t>(ns, 1)))
       return false;
     *h_nbad = 0;
@@ -991,13 +992,33 @@ bool pmx_ctx::fix_orphans() {
   return true;
 }
 
-// the hint sample in the order of its tets' smallest vertex ids
-// (k_sample_keys, pmx_kernels.hip), once the sample is on the device and np set.
-// PMX_HINT_SAMPLE_ORDER=0 keeps the tet order (A/B).
+// The hint sample, once the tets are on the device and np set.
+// PMX_HINT_SAMPLE_ORDER: 0 every 4th tet in tet order, 1 every 4th tet sorted
+// by its smallest vertex id (k_sample_keys), 2 (default) one tet per vertex,
+// in vertex order (k_vmin_owner; its count lands in h_nbad[5], nsamp after
+// the upload's sync) -- A/Bs in DESIGN.md section 7 r05.
 bool pmx_ctx::order_hint_samples(int64_t ne, hipStream_t s) {
-  samples_sorted = false;
+  samples_sorted = samples_owner = false;
+  nsamp = 0;
   const char *e = getenv("PMX_HINT_SAMPLE_ORDER");
-  if (e && e[0] == '0') return true;
+  const int mode = e ? atoi(e) : 2;
+  if (mode == 0) return true;
+  if (mode == 2) {
+    if (np < 1 || ne < 1) return true;
+    const size_t tb = owner_scan_temp_bytes(np);
+    if (!dgrow(this, d_skey, (size_t)(np + 2)) || !dgrow(this, d_sidx, (size_t)(2 * (np + 1))) ||
+        !dgrow(this, d_salt, (size_t)(np + 1)) || !dgrow(this, d_tets_sk, (size_t)(np + 1)) ||
+        !dgrow(this, d_stmp, std::max<size_t>(tb, 1)) || !dgrow(this, d_wfar, 8))
+      return false;
+    if (!launch_owner_sample(d_tets.p, ne, np, d_skey.p, d_sidx.p, d_sidx.p + (np + 1), d_salt.p, d_tets_sk.p,
+                             d_wfar.p + 4, h_nbad + 5, d_stmp.p, tb, s)) {
+      err = "hint sample: vertex owners";
+      return false;
+    }
+    std::swap(d_tets_s, d_salt);
+    samples_sorted = samples_owner = true;
+    return true;
+  }
   const int64_t n = (ne + PMX_HINT_STRIDE - 1) / PMX_HINT_STRIDE;
   if (n < 1) return true;
   const size_t tb = hint_sort_temp_bytes(n);
@@ -1184,10 +1205,11 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     const bool early = A.exp != 9;
     if (early && !fork_surface()) return 0;
     const int stride = opts.hint_stride > 0 ? opts.hint_stride : PMX_HINT_STRIDE;
-    launch_hint_build(stride == PMX_HINT_STRIDE ? ctx->d_tets_s.p : nullptr,
-                      ctx->samples_sorted ? ctx->d_tets_sk.p : nullptr, ctx->d_tets.p, ctx->ne,
+    const bool packed = stride == PMX_HINT_STRIDE;
+    launch_hint_build(packed ? ctx->d_tets_s.p : nullptr,
+                      packed && ctx->samples_sorted ? ctx->d_tets_sk.p : nullptr, ctx->d_tets.p, ctx->ne,
                       stride, ctx->d_grid.p, A.g, hint_xyz ? nullptr : ctx->d_xyzq.p, ctx->d_xyz.p, st,
-                      exp == 16, exp == 21 ? 1024 : exp == 22 ? 64 : 256);
+                      exp == 16, exp == 21 ? 1024 : exp == 22 ? 64 : 256, packed ? ctx->nsamp : 0);
     if (exp == 13 && ctx->d_wrec.p) {
       if (!dgrow(ctx, ctx->d_hrec, (size_t)(2 * ctx->gcells))) return 0;
       launch_hint_inline(ctx->d_grid.p, ctx->gcells, ctx->d_wrec.p, ctx->d_hrec.p, st);
@@ -1823,7 +1845,7 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
     } else if (!pmx_ctx_build_adja_device(ctx, ctx->d_ntetv.p, ne, n, ctx->d_adja.p, st, nullptr)) {
       return 0;
     }
-    if (!dgrow(ctx, ctx->d_wrec, (size_t)(ne + 1)) || !dgrow(ctx, ctx->d_wfar, 4)) return 0;
+    if (!dgrow(ctx, ctx->d_wrec, (size_t)(ne + 1)) || !dgrow(ctx, ctx->d_wfar, 8)) return 0;
     launch_build_tetrec(ctx->d_ntetv.p, ctx->d_adja.p, ne, PMX_HINT_STRIDE, ctx->d_tets.p, ctx->d_tets_s.p, st);
     launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, ctx->d_wfar.p, ctx->h_nbad + 2, st);
   }
@@ -1840,6 +1862,7 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
   CK(hipGetLastError());
   CK(hipStreamSynchronize(st));            // host vectors die here
   ctx->fan_rot = ctx->nt > 0 && ctx->h_nbad[4] == 0;
+  ctx->nsamp = ctx->samples_owner ? (int64_t)ctx->h_nbad[5] : 0;
   tr.mark("uploads + sync");
   ctx->have_ptag = tags;
   // the points and the results were consumed: the next step needs new points

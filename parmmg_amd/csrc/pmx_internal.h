@@ -57,6 +57,8 @@ struct pmx_ctx {
   DevBuf<int4> d_tets_s;                // hint sample: tets 1, 1+4, 1+8, ... in the order of their cells
   DevBuf<int> d_tets_sk;                // its tet indices (samples_sorted)
   bool samples_sorted = false;
+  bool samples_owner = false;           // the vertex-owner sample: nsamp entries
+  int64_t nsamp = 0;
   DevBuf<unsigned> d_skey;              // the sort (order_hint_samples): keys, indices, records, temp
   DevBuf<int> d_sidx;
   DevBuf<int4> d_salt;
@@ -160,7 +162,8 @@ struct pmx_ctx {
   DevBuf<TetRec> d_tets_next;
   DevBuf<WRec> d_wrec_next;
   DevBuf<int4> d_tets_s_next;
-  // [2] / [3]: tets of d_wrec / d_wrec_next with a far neighbour field (pmx_wrec.h), [4]: bad fans
+  // [2] / [3]: tets of d_wrec / d_wrec_next with a far neighbour field (pmx_wrec.h), [4]: bad fans,
+  // [5]: entries of the vertex-owner hint sample
   unsigned *h_nbad = nullptr;           // pinned [2]: non-manifold faces of that build, [1] of a background upload's
   DevBuf<double> d_nqual;
   bool have_qtag = false;               // raw tags of the new points

@@ -80,7 +80,7 @@ struct ExhArgs {
 // tet records are read strided
 void launch_hint_build(const int4 *packed, const int *kidx, const TetRec *tets, int64_t ne, int stride, int *grid,
                        GridDesc g, const unsigned long long *xyzq, const double *xyz, hipStream_t s,
-                       bool v0 = false, int bs = 256);
+                       bool v0 = false, int bs = 256, int64_t nsamp = 0);
 void launch_hint_inline(const int *grid, int64_t cells, const WRec *wr, uint4 *hrec, hipStream_t s);
 // per-background derived data: fixed-point grid coordinates of the vertices
 // (hint centroids) and the unit normals of the boundary trias
@@ -133,6 +133,13 @@ void launch_build_tetrec(const int4 *tv, const int *adja, int64_t ne, int stride
 // (k_sample_keys): out[i] = smp[t_i] and kidx[i] = 1 + stride * t_i; keys and
 // idx 2n words each, tmp hint_sort_temp_bytes(n) bytes
 size_t hint_sort_temp_bytes(int64_t n);
+// the vertex-owner sample (k_vmin_owner): out[i] / kidx[i] the i-th vertex's
+// owner tet in vertex order; owner np + 1 words, flag and pos np + 1 ints each,
+// tmp owner_scan_temp_bytes(np) bytes; the sample count into *h_count (pinned)
+size_t owner_scan_temp_bytes(int64_t np);
+bool launch_owner_sample(const TetRec *tets, int64_t ne, int64_t np, unsigned *owner, int *flag, int *pos,
+                         int4 *out, int *kidx, unsigned *d_count, unsigned *h_count, void *tmp, size_t tmp_bytes,
+                         hipStream_t s);
 bool launch_hint_sort(const int4 *smp, int64_t n, int stride, int64_t np, unsigned *keys, int *idx, int4 *out,
                       int *kidx, void *tmp, size_t tmp_bytes, hipStream_t s);
 void launch_build_wrec(const TetRec *tets, int64_t ne, WRec *wr, unsigned *d_nfar, unsigned *h_nfar,

@@ -144,11 +144,10 @@ __device__ __forceinline__ int64_t hint_cell(unsigned long long a, unsigned long
 
 template <bool PACKED, bool FROM_XYZ = false, bool V0 = false, int BS = 256>
 __global__ __launch_bounds__(BS) void k_hint_build(const int4 *__restrict__ packed, const int *__restrict__ kidx,
-                                                    const TetRec *__restrict__ tets, int64_t ne,
+                                                    const TetRec *__restrict__ tets, int64_t n,
                                                     int stride, int *__restrict__ grid, GridDesc g,
                                                     const unsigned long long *__restrict__ xyzq,
                                                     const double *__restrict__ xyz) {
-  const int64_t n = (ne + stride - 1) / stride;
   const int64_t t = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (t >= n) return;
   // the packed sample in cell order carries its tet indices (kidx)
@@ -177,29 +176,29 @@ __global__ __launch_bounds__(BS) void k_hint_build(const int4 *__restrict__ pack
 }
 void launch_hint_build(const int4 *packed, const int *kidx, const TetRec *tets, int64_t ne, int stride, int *grid,
                        GridDesc g, const unsigned long long *xyzq, const double *xyz, hipStream_t s,
-                       bool v0, int bs) {
-  const int64_t n = (ne + stride - 1) / stride;
+                       bool v0, int bs, int64_t nsamp) {
+  const int64_t n = nsamp > 0 ? nsamp : (ne + stride - 1) / stride;
   const int64_t nb = std::max<int64_t>((n + 255) / 256, 1);
   if (v0 && xyzq && packed)
-    hipLaunchKernelGGL((k_hint_build<true, false, true>), dim3((unsigned)nb), dim3(256), 0, s, packed, kidx, tets, ne,
+    hipLaunchKernelGGL((k_hint_build<true, false, true>), dim3((unsigned)nb), dim3(256), 0, s, packed, kidx, tets, n,
                        stride, grid, g, xyzq, xyz);
   else if (v0 && xyzq)
-    hipLaunchKernelGGL((k_hint_build<false, false, true>), dim3((unsigned)nb), dim3(256), 0, s, packed, kidx, tets, ne,
+    hipLaunchKernelGGL((k_hint_build<false, false, true>), dim3((unsigned)nb), dim3(256), 0, s, packed, kidx, tets, n,
                        stride, grid, g, xyzq, xyz);
   else if (packed && !xyzq)
-    hipLaunchKernelGGL((k_hint_build<true, true>), dim3((unsigned)nb), dim3(256), 0, s, packed, kidx, tets, ne, stride,
+    hipLaunchKernelGGL((k_hint_build<true, true>), dim3((unsigned)nb), dim3(256), 0, s, packed, kidx, tets, n, stride,
                        grid, g, xyzq, xyz);
   else if (packed && bs == 1024)
     hipLaunchKernelGGL((k_hint_build<true, false, false, 1024>), dim3((unsigned)((n + 1023) / 1024)), dim3(1024), 0,
-                       s, packed, kidx, tets, ne, stride, grid, g, xyzq, xyz);
+                       s, packed, kidx, tets, n, stride, grid, g, xyzq, xyz);
   else if (packed && bs == 64)
     hipLaunchKernelGGL((k_hint_build<true, false, false, 64>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s,
-                       packed, kidx, tets, ne, stride, grid, g, xyzq, xyz);
+                       packed, kidx, tets, n, stride, grid, g, xyzq, xyz);
   else if (packed)
-    hipLaunchKernelGGL((k_hint_build<true, false>), dim3((unsigned)nb), dim3(256), 0, s, packed, kidx, tets, ne, stride,
+    hipLaunchKernelGGL((k_hint_build<true, false>), dim3((unsigned)nb), dim3(256), 0, s, packed, kidx, tets, n, stride,
                        grid, g, xyzq, xyz);
   else
-    hipLaunchKernelGGL((k_hint_build<false, false>), dim3((unsigned)nb), dim3(256), 0, s, packed, kidx, tets, ne, stride,
+    hipLaunchKernelGGL((k_hint_build<false, false>), dim3((unsigned)nb), dim3(256), 0, s, packed, kidx, tets, n, stride,
                        grid, g, xyzq, xyz);
 }
 
@@ -220,6 +219,60 @@ __global__ __launch_bounds__(256) void k_sample_keys(const int4 *__restrict__ sm
     idx[i] = (int)i;
   }
 }
+// The vertex-owner sample (r05): one tet per vertex -- the smallest tet
+// among those whose smallest vertex it is -- in vertex order.  Like the
+// every-4th-tet sample it is connectivity only, but it covers space whatever
+// the tet numbering (a random numbering's every-4th-tet sample leaves a
+// Poisson share of the cells empty), and it has one entry per vertex instead
+// of ne / 4.
+__global__ __launch_bounds__(256) void k_vmin_owner(const TetRec *__restrict__ tets, int64_t ne,
+                                                    unsigned *__restrict__ owner) {
+  for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= ne;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int4 v = *reinterpret_cast<const int4 *>(tets + k);
+    if (v.x <= 0) continue;
+    atomicMin(owner + min(min(v.x, v.y), min(v.z, v.w)), (unsigned)k);
+  }
+}
+__global__ __launch_bounds__(256) void k_owner_flags(const unsigned *__restrict__ owner, int64_t np,
+                                                     int *__restrict__ flag) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v <= np; v += (int64_t)gridDim.x * blockDim.x)
+    flag[v] = (v >= 1 && owner[v] != 0xffffffffu) ? 1 : 0;
+}
+__global__ __launch_bounds__(256) void k_owner_gather(const unsigned *__restrict__ owner, const int *__restrict__ flag,
+                                                      const int *__restrict__ pos, int64_t np,
+                                                      const TetRec *__restrict__ tets, int4 *__restrict__ out,
+                                                      int *__restrict__ kidx, unsigned *__restrict__ count) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v <= np; v += (int64_t)gridDim.x * blockDim.x) {
+    if (flag[v]) {
+      const int k = (int)owner[v];
+      out[pos[v]] = *reinterpret_cast<const int4 *>(tets + k);
+      kidx[pos[v]] = k;
+    }
+    if (v == np) *count = (unsigned)(pos[v] + flag[v]);
+  }
+}
+size_t owner_scan_temp_bytes(int64_t np) {
+  size_t bytes = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const int *)nullptr, (int *)nullptr, (int)(np + 1));
+  return bytes;
+}
+bool launch_owner_sample(const TetRec *tets, int64_t ne, int64_t np, unsigned *owner, int *flag, int *pos,
+                         int4 *out, int *kidx, unsigned *d_count, unsigned *h_count, void *tmp, size_t tmp_bytes,
+                         hipStream_t s) {
+  if (hipMemsetAsync(owner, 0xff, (size_t)(np + 1) * sizeof(unsigned), s) != hipSuccess) return false;
+  const int64_t nbt = std::max<int64_t>(1, std::min<int64_t>((ne + 255) / 256, 65536));
+  const int64_t nbv = std::max<int64_t>(1, std::min<int64_t>((np + 256) / 256, 65536));
+  hipLaunchKernelGGL(k_vmin_owner, dim3((unsigned)nbt), dim3(256), 0, s, tets, ne, owner);
+  hipLaunchKernelGGL(k_owner_flags, dim3((unsigned)nbv), dim3(256), 0, s, (const unsigned *)owner, np, flag);
+  if (hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, (const int *)flag, pos, (int)(np + 1), s) != hipSuccess)
+    return false;
+  hipLaunchKernelGGL(k_owner_gather, dim3((unsigned)nbv), dim3(256), 0, s, (const unsigned *)owner,
+                     (const int *)flag, (const int *)pos, np, tets, out, kidx, d_count);
+  if (hipMemcpyAsync(h_count, d_count, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess) return false;
+  return hipGetLastError() == hipSuccess;
+}
+
 // the sorted sample and the tet index of each entry (1 + stride * t)
 __global__ __launch_bounds__(256) void k_sample_gather(const int4 *__restrict__ smp, const int *__restrict__ idx,
                                                        int64_t n, int stride, int4 *__restrict__ out,

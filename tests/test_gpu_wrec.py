@@ -130,15 +130,15 @@ def test_far_neighbour_fields(transfer):
 
 
 def test_hint_sample_order(transfer, monkeypatch):
-    """The hint sample sorted by cell at the upload (pmx_ctx::order_hint_samples)
-    carries its tet indices: on an appended numbering (sorted order != tet
-    order) the step locates and interpolates bit for bit as with the sample in
-    tet order, with walks as short."""
+    """The hint samples of pmx_ctx::order_hint_samples -- every 4th tet in tet
+    order (0), sorted by smallest vertex id (1), one owner tet per vertex (2,
+    the default) -- carry their tet indices: on an appended numbering the step
+    locates and interpolates bit for bit alike, with walks as short."""
     m, _ = M.numbering(M.kuhn_cube(16), "appended")
     x, t = M.new_points(16, seed=3, surface=True)
     sols = [M.on_vertices(m, M.iso_metric), M.on_vertices(m, lin_field)]
     out = []
-    for order in ("0", "1"):
+    for order in ("0", "1", "2"):
         monkeypatch.setenv("PMX_HINT_SAMPLE_ORDER", order)
         transfer.upload_background(m, sols, 0)
         transfer.upload_points(x, t)
@@ -147,9 +147,12 @@ def test_hint_sample_order(transfer, monkeypatch):
         out.append((r.elem.copy(), r.status.copy(), [s.copy() for s in r.sols],
                     transfer.locate_stats()["stepav"], transfer.starts().copy()))
     _assert_same(out[0], out[1])
+    _assert_same(out[0], out[2])
     assert out[1][3] < 1.2 * out[0][3], (out[0][3], out[1][3])
+    assert out[2][3] < 1.2 * out[0][3], (out[0][3], out[2][3])
     vol = (t == 0) & (out[1][1] == 1)
     assert not np.array_equal(out[0][4][vol], out[1][4][vol])       # other start tets
+    assert not np.array_equal(out[0][4][vol], out[2][4][vol])
 
 
 COMPACT_FORCED = 18 << 16         # exp 18: compact records whatever their far fields

@@ -671,6 +671,8 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   if (!dev_adja) {
     CK(hipMemcpyAsync(ctx->d_tets_s.p, hh, (size_t)ns * sizeof(int4), hipMemcpyHostToDevice, st));
     launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, ctx->d_wfar.p, ctx->h_nbad + 2, st);
+    // the hint sample while the host packs the solutions and trias
+    if (!ctx->order_hint_samples(ne, np, st)) return 0;
   }
   if (dev_adja) {
     // face matching on the device (pmx_topo.hip), then the tet records and
@@ -686,6 +688,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     launch_build_tetrec(ctx->d_btv.p, ctx->d_adja.p, ne, PMX_HINT_STRIDE, ctx->d_tets.p, ctx->d_tets_s.p,
                         ctx->topo);
     launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, ctx->d_wfar.p, ctx->h_nbad + 2, ctx->topo);
+    if (!ctx->order_hint_samples(ne, np, ctx->topo)) return 0;
     CK(hipEventRecord(ctx->ev_join, ctx->topo));
   }
   tr.mark("tets");
@@ -734,7 +737,6 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   // the node -> trias fans are the step's (pmx_run: PMMG_precompute_nodeTrias
   // runs inside the reference's call)
   if (dev_adja) CK(hipStreamWaitEvent(st, ctx->ev_join, 0));
-  if (!ctx->order_hint_samples(ne, st)) return 0;
   CK(hipGetLastError());
   tr.mark("trias + topology");
   CK(hipStreamSynchronize(ctx->stream));   // host staging vectors die here
@@ -997,7 +999,7 @@ bool pmx_ctx::fix_orphans() {
 // by its smallest vertex id (k_sample_keys), 2 (default) one tet per vertex,
 // in vertex order (k_vmin_owner; its count lands in h_nbad[5], nsamp after
 // the upload's sync) -- A/Bs in DESIGN.md section 7 r05.
-bool pmx_ctx::order_hint_samples(int64_t ne, hipStream_t s) {
+bool pmx_ctx::order_hint_samples(int64_t ne, int64_t np, hipStream_t s) {
   samples_sorted = samples_owner = false;
   nsamp = 0;
   const char *e = getenv("PMX_HINT_SAMPLE_ORDER");
@@ -1855,7 +1857,7 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
   ctx->hausd = m->hausd;
   tr.mark("tet records");
   if (!setup_grids(ctx, ctx->qlo, ctx->qhi, ne)) return 0;
-  if (!ctx->order_hint_samples(ne, st)) return 0;
+  if (!ctx->order_hint_samples(ne, ctx->np, st)) return 0;
   tr.mark("grids");
   CK(hipMemcpyAsync(ctx->d_tris.p, htr.data(), htr.size() * sizeof(TriRec), hipMemcpyHostToDevice, st));
   if (!ctx->check_fans(st)) return 0;

@@ -201,7 +201,7 @@ struct pmx_ctx {
 
   hipEvent_t *next_event_slot();
   void free_all();
-  bool order_hint_samples(int64_t ne, hipStream_t s);
+  bool order_hint_samples(int64_t ne, int64_t nverts, hipStream_t s);
   // the fans by rotation (closed manifold surface, checked at the upload:
   // fan_rot) or by a sort; force 1: the counting sort
   bool fan_rot = false;

@@ -225,13 +225,23 @@ __global__ __launch_bounds__(256) void k_sample_keys(const int4 *__restrict__ sm
 // the tet numbering (a random numbering's every-4th-tet sample leaves a
 // Poisson share of the cells empty), and it has one entry per vertex instead
 // of ne / 4.
+// (a lane whose left neighbour -- the previous tet -- has the same smallest
+// vertex skips its atomic: a coherent numbering puts a vertex's tets next to
+// each other, and same-address atomics serialise; r05: 3.6 -> see DESIGN)
 __global__ __launch_bounds__(256) void k_vmin_owner(const TetRec *__restrict__ tets, int64_t ne,
                                                     unsigned *__restrict__ owner) {
-  for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= ne;
-       k += (int64_t)gridDim.x * blockDim.x) {
-    const int4 v = *reinterpret_cast<const int4 *>(tets + k);
-    if (v.x <= 0) continue;
-    atomicMin(owner + min(min(v.x, v.y), min(v.z, v.w)), (unsigned)k);
+  const int64_t st = (int64_t)gridDim.x * blockDim.x;
+  const int64_t nit = (ne + st - 1) / st;           // uniform trip count (the shuffle below)
+  for (int64_t it = 0; it < nit; it++) {
+    const int64_t k = 1 + it * st + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int m = -1;
+    if (k <= ne) {
+      const int4 v = *reinterpret_cast<const int4 *>(tets + k);
+      if (v.x > 0) m = min(min(v.x, v.y), min(v.z, v.w));
+    }
+    const int ml = __shfl_up(m, 1, 64);
+    const bool first = (threadIdx.x & 63) == 0 || ml != m;
+    if (m > 0 && first) atomicMin(owner + m, (unsigned)k);
   }
 }
 __global__ __launch_bounds__(256) void k_owner_flags(const unsigned *__restrict__ owner, int64_t np,

@@ -54,12 +54,12 @@ struct pmx_ctx {
   DevBuf<WRec> d_wrec;                  // the walk's compact copy of d_tets (built with it)
   DevBuf<unsigned> d_wfar;              // [0] / [1]: far-field counters of d_wrec / d_wrec_next's builds, [2] / [3] bad fans
   DevBuf<double> d_sol;
-  DevBuf<int4> d_tets_s;                // hint sample: tets 1, 1+4, 1+8, ... in the order of their cells
+  DevBuf<int4> d_tets_s;                // hint sample: one owner tet per vertex (default) or every 4th tet (order_hint_samples)
   DevBuf<int> d_tets_sk;                // its tet indices (samples_sorted)
   bool samples_sorted = false;
   bool samples_owner = false;           // the vertex-owner sample: nsamp entries
   int64_t nsamp = 0;
-  DevBuf<unsigned> d_skey;              // the sort (order_hint_samples): keys, indices, records, temp
+  DevBuf<unsigned> d_skey;              // order_hint_samples scratch: keys / owners, indices / flags, records, temp
   DevBuf<int> d_sidx;
   DevBuf<int4> d_salt;
   DevBuf<char> d_stmp;

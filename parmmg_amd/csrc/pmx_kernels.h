@@ -80,7 +80,7 @@ struct ExhArgs {
 // tet records are read strided
 void launch_hint_build(const int4 *packed, const int *kidx, const TetRec *tets, int64_t ne, int stride, int *grid,
                        GridDesc g, const unsigned long long *xyzq, const double *xyz, hipStream_t s,
-                       bool v0 = false, int bs = 256, int64_t nsamp = 0);
+                       bool v0 = false, int bs = 256, int64_t nsamp = -1);
 void launch_hint_inline(const int *grid, int64_t cells, const WRec *wr, uint4 *hrec, hipStream_t s);
 // per-background derived data: fixed-point grid coordinates of the vertices
 // (hint centroids) and the unit normals of the boundary trias

@@ -177,8 +177,9 @@ __global__ __launch_bounds__(BS) void k_hint_build(const int4 *__restrict__ pack
 void launch_hint_build(const int4 *packed, const int *kidx, const TetRec *tets, int64_t ne, int stride, int *grid,
                        GridDesc g, const unsigned long long *xyzq, const double *xyz, hipStream_t s,
                        bool v0, int bs, int64_t nsamp) {
-  const int64_t n = nsamp > 0 ? nsamp : (ne + stride - 1) / stride;
-  const int64_t nb = std::max<int64_t>((n + 255) / 256, 1);
+  const int64_t n = nsamp >= 0 ? nsamp : (ne + stride - 1) / stride;   // nsamp < 0: every stride-th tet
+  if (n < 1) return;
+  const int64_t nb = (n + 255) / 256;
   if (v0 && xyzq && packed)
     hipLaunchKernelGGL((k_hint_build<true, false, true>), dim3((unsigned)nb), dim3(256), 0, s, packed, kidx, tets, n,
                        stride, grid, g, xyzq, xyz);

@@ -2,13 +2,22 @@
 """Benchmark of the MI355X transfer path (locate + interpolate new vertices).
 
 A step = one ParMmg iteration's PMMG_interpMetricsAndFields pass of one
-background group on one GPU, everything the device does per iteration: the
-background's derived data (fixed-point grid coordinates of its vertices, tria
-normals -- PMMG_precompute_triaNormals), the hint-grid build, adjacency-walk
-location of every new vertex (volume + surface), fused metric/field
-interpolation, exhaustive fallback.  Inputs (the raw background arrays and
-the new points) are resident in HBM, uploaded before the timed region; the
-host-staged (PCIe-inclusive) cycle is measured after it and reported apart.
+background group on one GPU: every device pass of that iteration on the
+uploaded raw arrays (PMX_RUN_FRESH_BACKGROUND, r06).  Per background: the
+fixed-point grid coordinates of its vertices, the tria normals
+(PMMG_precompute_triaNormals), the node -> trias fans with the upload's fan
+check (PMMG_precompute_nodeTrias), and whatever layout the upload derived on
+the device (none by default: the walk reads the 32-B tet records, the hint
+sample is packed by the host with them; the device face matching when the
+background came without Mmg's adjacency).  Per new mesh: the orphan marks
+from the new tets (the reference's vertex loop over the new tets), the tag
+dispatch and compaction of the new points.  Then the hint-grid build, the
+adjacency-walk location of every new vertex (volume + surface), the fused
+metric / field interpolation and the exhaustive fallback.  Inputs (the raw
+background arrays -- tet records {v, adja}, vertices, solutions, boundary
+trias -- and the new points and tets) are resident in HBM, uploaded before
+the timed region; the host-staged (PCIe-inclusive) cycles are measured after
+it and reported apart.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4]
 
@@ -451,7 +460,11 @@ def main():
         else:
             dist.init_process_group("gloo")
 
+    def phase(msg):
+        print(f"[bench {time.strftime('%H:%M:%S')}] rank {rank}: {msg}", file=sys.stderr, flush=True)
+
     from parmmg_amd import build
+    phase("build (libraries rebuilt only when stale)")
     build.build_meshgen()
     build.build_transfer()
     if rank == 0 and not args.no_cpu:
@@ -459,12 +472,14 @@ def main():
 
     cfg = CONFIGS[args.config]
     ngrp = cfg.get("groups", 1)
+    phase(f"build_case {args.config}")
     cases = [build_case(cfg, rank * ngrp + g) for g in range(ngrp)]
-    print(f"[bench] rank {rank}: {args.config} case built", file=sys.stderr, flush=True)
+    phase(f"{args.config} case built")
     if args.numbering != "lex":
         from parmmg_amd import mesh as M
+        phase(f"numbering {args.numbering}")
         cases = [(M.numbering(c[0], args.numbering)[0],) + tuple(c[1:]) for c in cases]
-        print(f"[bench] rank {rank}: {args.numbering} numbering", file=sys.stderr, flush=True)
+        phase(f"{args.numbering} numbering done")
     # the CPU baseline first: its worker processes are forked before this
     # process touches the GPU
     cpu = None
@@ -605,17 +620,17 @@ def main():
                      "step_frac": B_all / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
         "kernel_ms": k_ms,
         "per_iteration": {"ms": ms, "includes": (
-            "every device pass of one PMMG_interpMetricsAndFields call on the raw uploaded arrays: "
-            "derived background data (grid coordinates, tria normals = PMMG_precompute_triaNormals), "
-            "node -> trias fans (PMMG_precompute_nodeTrias), "
-            "tag dispatch + order-preserving compaction of the new points, hint grid, volume walk + "
+            "every device pass of one PMMG_interpMetricsAndFields call on the raw uploaded arrays "
+            "(PMX_RUN_FRESH_BACKGROUND): derived background data (grid coordinates, tria normals = "
+            "PMMG_precompute_triaNormals), node -> trias fans with the upload's fan check "
+            "(PMMG_precompute_nodeTrias), the layouts the upload derived on the device (none in the "
+            "default configuration), "
+            + ("orphan marks from the new tets (vertex loop over the new tets), " if not args.no_new_tets
+               else "")
+            + "tag dispatch + order-preserving compaction of the new points, hint grid, volume walk + "
             "interpolation, surface path, fallback"),
-            "per_upload_not_in_ms": (
-            "the step locates every point; the points in no valid new tet (orphans) are marked by a "
-            "kernel over the new tets once per points upload (k_mark_new_tets, ~0.5 ms at C3, on the "
-            "upload stream beside the first step) and their rows reset at the download -- like the "
-            "upload's connectivity layouts (walk records, hint sample), not repeated by the timed steps"
-            if not args.no_new_tets else "")},
+            "not_in_ms": "host packing and PCIe (pcie_inclusive); nothing the device runs per "
+                         "upload is outside the step"},
         "resident_background_ms_per_step": resident_ms,
         "step_alg_GBs": B_all / (ms * 1e-3) / 1e9,
         "locate": st,

@@ -75,13 +75,16 @@ static void nonunit_normal(const double *a, const double *b, const double *c, do
   n[2] = abx*acy - aby*acx;
 }
 
-/* MMG5_orvol -> MMG5_det4pt -> MMG5_det3pt1vec */
+/* MMG5_orvol -> MMG5_det4pt(c0,c1,c2,c3) -> MMG5_det3pt1vec(c0,c1,c2,v) with
+ * v = c3 - c0: the 3x3 determinant [c1-c0 | c2-c0 | v] expanded along v,
+ *   v0*(m10*m21 - m20*m11) - v1*(m00*m21 - m20*m01) + v2*(m00*m11 - m10*m01)
+ * (public Mmg source, src/common/tools.c; evaluated left to right) */
 static double orvol(const double *c0, const double *c1, const double *c2, const double *c3) {
-  double w0 = c3[0]-c0[0], w1 = c3[1]-c0[1], w2 = c3[2]-c0[2];
-  double m00 = c1[0]-c0[0], m01 = c2[0]-c0[0], m02 = w0;
-  double m10 = c1[1]-c0[1], m11 = c2[1]-c0[1], m12 = w1;
-  double m20 = c1[2]-c0[2], m21 = c2[2]-c0[2], m22 = w2;
-  return m00*(m11*m22 - m21*m12) - m10*(m01*m22 - m21*m02) + m20*(m01*m12 - m11*m02);
+  double m00 = c1[0]-c0[0], m01 = c2[0]-c0[0];
+  double m10 = c1[1]-c0[1], m11 = c2[1]-c0[1];
+  double m20 = c1[2]-c0[2], m21 = c2[2]-c0[2];
+  double v0 = c3[0]-c0[0], v1 = c3[1]-c0[1], v2 = c3[2]-c0[2];
+  return v0*(m10*m21 - m20*m11) - v1*(m00*m21 - m20*m01) + v2*(m00*m11 - m10*m01);
 }
 
 int orc_invmat(const double *m, double *mi) {

@@ -68,7 +68,17 @@ class _locked:
         return False
 
 
+def _log(msg: str) -> None:
+    """Timestamped progress on stderr: a rebuild (stale library on a fresh GPU
+    box) compiles for minutes, and a silent one reads as a hang."""
+    import time
+    sys.stderr.write(f"[build {time.strftime('%H:%M:%S')}] {msg}\n")
+    sys.stderr.flush()
+
+
 def _run(cmd: list[str]) -> None:
+    _log("run: " + " ".join(os.path.basename(c) if os.path.isabs(c) and c.endswith((".hip", ".c", ".so"))
+                            else c for c in cmd[:1] + [c for c in cmd if c.endswith((".hip", ".c"))]))
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)

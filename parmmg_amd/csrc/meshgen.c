@@ -25,6 +25,18 @@
 #include <omp.h>
 #endif
 
+/* Cap the OpenMP team (the Python loader passes the process's CPU share: a
+ * GPU box's affinity set is 256 CPUs under a 16-CPU cgroup quota, and 256
+ * spinning libgomp threads throttled by that quota can stall a parallel
+ * region for minutes). */
+void pmg_set_threads(int n) {
+#ifdef _OPENMP
+  if (n > 0) omp_set_num_threads(n);
+#else
+  (void)n;
+#endif
+}
+
 /* face f of a tet is opposite local vertex f; its vertices in MMG5_idir order */
 static const int FACEV[4][3] = {{1,2,3},{0,3,2},{0,1,3},{0,2,1}};
 /* triangle edge e is opposite local vertex e: (e+1)%3, (e+2)%3 */
@@ -371,7 +383,7 @@ int64_t pmg_new_points(int n, uint64_t seed, double jitter, int with_surface,
   return cnt;
 }
 
-/* Oriented volume check (6V), same operand order as the oracle's orvol. */
+/* Oriented volume check (6V): the sign only (the generator's own expansion). */
 int64_t pmg_count_inverted(int64_t ne, const double *xyz, const int *tet) {
   int64_t k, bad = 0;
 #pragma omp parallel for reduction(+:bad)

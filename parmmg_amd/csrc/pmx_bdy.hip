@@ -850,9 +850,21 @@ static bool node_trias_counting(pmx_ctx *c, hipStream_t s) {
   return true;
 }
 
-bool pmx_ctx::build_node_trias(hipStream_t s, int force) {
+bool pmx_ctx::build_node_trias(hipStream_t s, int force, bool check) {
   const int64_t m = 3 * nt;
   if (m < 1) return true;
+  if (fan_rot && force == 0 && check) {
+    // the upload's check again (a FRESH step: what a new background costs):
+    // every vertex's tria count beside the rotation
+    if (!pmx_dgrow(this, d_ntkey, (size_t)(np + 2))) return false;
+    if (hipMemsetAsync(d_ntkey.p, 0, (size_t)(np + 2) * sizeof(unsigned), s) != hipSuccess) {
+      err = "node trias: memset";
+      return false;
+    }
+    const unsigned nbc = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nt + 255) / 256, 4096));
+    hipLaunchKernelGGL(k_nt_count, dim3(nbc), dim3(256), 0, s, d_tris.p, nt, d_ntkey.p);
+    return fan_rotation(s, d_wfar.p + 2, d_ntkey.p);
+  }
   if (fan_rot && force == 0) return fan_rotation(s, d_wfar.p + 2);
   if (np <= 5 * m || force == 1) {
     if (!node_trias_counting(this, s)) return false;

@@ -377,6 +377,22 @@ static bool setup_grids(pmx_ctx *ctx, const double lo[3], const double hi[3], in
   return pmx_dgrow(ctx, ctx->d_grid, (size_t)cells);
 }
 
+// the background's derived layouts, decided per upload / promotion (A/B
+// switches): PMX_WALK_RECORDS=compact builds the
+// walk's 24-B records (a device pass per background: 1.26 ms at C3 for a walk
+// 2 % faster); PMX_HINT_SAMPLE_ORDER=2 the vertex-owner hint sample (three
+// device passes per background, 1.26 ms at C3, for a hint build 0.03 ms
+// faster on a lexicographic numbering).  Defaults: neither -- no device pass
+// per background beyond what every step does.
+static bool env_compact_records() {
+  const char *e = getenv("PMX_WALK_RECORDS");
+  return e && strcmp(e, "compact") == 0;
+}
+static int env_sample_mode() {
+  const char *e = getenv("PMX_HINT_SAMPLE_ORDER");
+  return (e && atoi(e) == 2) ? 2 : 0;
+}
+
 extern "C" {
 
 pmx_ctx *pmx_create(int device) {
@@ -549,6 +565,12 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   if (!check_background(ctx, m, nsol, sols, imet)) return 0;
   const int64_t np = m->np, ne = m->ne, nt = m->nt;
   const bool dev_adja = m->adja == nullptr;   // no MMG3D_hashTetra on the host: device face matching
+  ctx->compact_recs = env_compact_records();
+  ctx->sample_mode = env_sample_mode();
+  ctx->bg_btv = false;
+  // the host packs the every-4th-tet hint sample with the tet records (the
+  // device-adjacency path: k_build_tetrec writes it)
+  const bool host_sample = !dev_adja && ctx->sample_mode == 0;
   // a residency build of the next background's records shares the adjacency
   // scratch: let it finish (its result, in the *_next buffers, is kept)
   if (ctx->next_topo) CK(hipStreamSynchronize(ctx->topo));
@@ -571,7 +593,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   const size_t trec = dev_adja ? sizeof(int4) : sizeof(TetRec);
   const size_t o_p = 0, o_t = o_p + al256((size_t)(np + 1) * 24),
                o_h = o_t + al256((size_t)(ne + 1) * trec),
-               o_s = o_h + al256((size_t)ns * sizeof(int4)),
+               o_s = o_h + al256(host_sample ? (size_t)ns * sizeof(int4) : 0),
                total = o_s + al256(hs_n * sizeof(double));
   CK(hipStreamSynchronize(ctx->stream));   // the arena may still feed an earlier copy
   char *stg = hstage(ctx, total);
@@ -583,7 +605,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     ~StreamGuard() { if (s) hipStreamSynchronize(s); }
   } topo_guard;
   if (!dgrow(ctx, ctx->d_xyz, (size_t)(np + 1) * 3) || !dgrow(ctx, ctx->d_tets, (size_t)(ne + 1)) ||
-      !dgrow(ctx, ctx->d_wrec, (size_t)(ne + 1)) || !dgrow(ctx, ctx->d_wfar, 8) ||
+      (ctx->compact_recs && !dgrow(ctx, ctx->d_wrec, (size_t)(ne + 1))) || !dgrow(ctx, ctx->d_wfar, 8) ||
       !dgrow(ctx, ctx->d_tets_s, (size_t)std::max<int64_t>(ns, 1)) || !dgrow(ctx, ctx->d_sol, hs_n) ||
       !dgrow(ctx, ctx->d_tris, (size_t)(nt + 1)) || !dgrow(ctx, ctx->d_trn, (size_t)(nt + 1)) ||
       !dgrow(ctx, ctx->d_xyzq, (size_t)(np + 1)) ||
@@ -652,7 +674,8 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
             if (valid && (v[l] < 1 || v[l] > np || a < 0 || a / 4 > ne)) b = true;
           }
         }
-        if ((k - 1) % PMX_HINT_STRIDE == 0) hh[(k - 1) / PMX_HINT_STRIDE] = make_int4(v[0], v[1], v[2], v[3]);
+        if (host_sample && (k - 1) % PMX_HINT_STRIDE == 0)
+          hh[(k - 1) / PMX_HINT_STRIDE] = make_int4(v[0], v[1], v[2], v[3]);
       }
       if (b) __atomic_store_n(&bad, true, __ATOMIC_RELAXED);
       std::atomic_thread_fence(std::memory_order_seq_cst);
@@ -668,10 +691,12 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
     ctx->err = "pmx_upload_background: tet vertex or adjacency index out of range";
     return 0;
   }
+  ctx->h_nbad[2] = 0;                        // no far fields unless compact records are built
   if (!dev_adja) {
-    CK(hipMemcpyAsync(ctx->d_tets_s.p, hh, (size_t)ns * sizeof(int4), hipMemcpyHostToDevice, st));
-    launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, ctx->d_wfar.p, ctx->h_nbad + 2, st);
-    // the hint sample while the host packs the solutions and trias
+    if (host_sample)
+      CK(hipMemcpyAsync(ctx->d_tets_s.p, hh, (size_t)ns * sizeof(int4), hipMemcpyHostToDevice, st));
+    if (ctx->compact_recs) launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, ctx->d_wfar.p, ctx->h_nbad + 2, st);
+    // the owner sample (mode 2) while the host packs the solutions and trias
     if (!ctx->order_hint_samples(ne, np, st)) return 0;
   }
   if (dev_adja) {
@@ -687,7 +712,8 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
       return 0;
     launch_build_tetrec(ctx->d_btv.p, ctx->d_adja.p, ne, PMX_HINT_STRIDE, ctx->d_tets.p, ctx->d_tets_s.p,
                         ctx->topo);
-    launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, ctx->d_wfar.p, ctx->h_nbad + 2, ctx->topo);
+    if (ctx->compact_recs)
+      launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, ctx->d_wfar.p, ctx->h_nbad + 2, ctx->topo);
     if (!ctx->order_hint_samples(ne, np, ctx->topo)) return 0;
     CK(hipEventRecord(ctx->ev_join, ctx->topo));
   }
@@ -747,6 +773,7 @@ int pmx_upload_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol,
   }
   ctx->fan_rot = ctx->nt > 0 && ctx->h_nbad[4] == 0;
   ctx->nsamp = ctx->samples_owner ? (int64_t)ctx->h_nbad[5] : 0;
+  ctx->bg_btv = dev_adja;
   ctx->have_bg = true;
   return 1;
 }
@@ -864,6 +891,10 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   if (!dgrow(ctx, ctx->d_start, nn)) return 0;
   if (!dgrow(ctx, ctx->d_edge, nn)) return 0;
   if (!dgrow(ctx, ctx->d_vertex, nn)) return 0;
+  // start 0, edge / vertex unset (-1) for every point no step writes
+  CK(hipMemsetAsync(ctx->d_start.p, 0, nn * sizeof(int), ctx->stream));
+  CK(hipMemsetAsync(ctx->d_edge.p, 0xff, nn * sizeof(int), ctx->stream));
+  CK(hipMemsetAsync(ctx->d_vertex.p, 0xff, nn * sizeof(int), ctx->stream));
   if (!dgrow(ctx, ctx->d_list, nn)) return 0;
   if (!dgrow(ctx, ctx->d_found, nn)) return 0;
   if (!dgrow(ctx, ctx->d_bestk, nn)) return 0;
@@ -881,7 +912,6 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   // after the step: the step locates them too and fix_orphans resets their
   // rows before any consumer reads them (the reference never visits them,
   // src/interpmesh_pmmg.c:535-541)
-  ctx->pts_mark = false;
   ctx->have_pts = true;
   ctx->have_ntet = ntet > 0;
   ctx->n_ntet = ntet;
@@ -956,14 +986,15 @@ bool pmx_ctx::pack_new_tets() {
   if (residency && ntet > 0) {
     const int64_t ns = (ntet + PMX_HINT_STRIDE - 1) / PMX_HINT_STRIDE;
     if (!dgrow(this, d_adja, (size_t)(4 * ntet + 5)) || !dgrow(this, d_tets_next, (size_t)(ntet + 1)) ||
-        !dgrow(this, d_wrec_next, (size_t)(ntet + 1)) || !dgrow(this, d_wfar, 8) ||
+        (compact_recs && !dgrow(this, d_wrec_next, (size_t)(ntet + 1))) || !dgrow(this, d_wfar, 8) ||
         !dgrow(this, d_tets_s_next, (size_t)std::max<int64_t>(ns, 1)))
       return false;
     *h_nbad = 0;
     CK(hipStreamWaitEvent(topo, ev_tets, 0));
     if (!pmx_ctx_build_adja_device(this, d_ntetv.p, ntet, n, d_adja.p, topo, h_nbad)) return false;
     launch_build_tetrec(d_ntetv.p, d_adja.p, ntet, PMX_HINT_STRIDE, d_tets_next.p, d_tets_s_next.p, topo);
-    launch_build_wrec(d_tets_next.p, ntet, d_wrec_next.p, d_wfar.p + 1, h_nbad + 3, topo);
+    h_nbad[3] = 0;
+    if (compact_recs) launch_build_wrec(d_tets_next.p, ntet, d_wrec_next.p, d_wfar.p + 1, h_nbad + 3, topo);
     CK(hipEventRecord(ev_topo, topo));
     next_topo = true;
   }
@@ -994,47 +1025,56 @@ bool pmx_ctx::fix_orphans() {
   return true;
 }
 
-// The hint sample, once the tets are on the device and np set.
-// PMX_HINT_SAMPLE_ORDER: 0 every 4th tet in tet order, 1 every 4th tet sorted
-// by its smallest vertex id (k_sample_keys), 2 (default) one tet per vertex,
-// in vertex order (k_vmin_owner; its count lands in h_nbad[5], nsamp after
-// the upload's sync) -- A/Bs in DESIGN.md section 7 r05.
+// The hint sample, once the tets are on the device and np set
+// (sample_mode, PMX_HINT_SAMPLE_ORDER at the upload): 0 every 4th tet in tet
+// order, packed with the tet records (nothing to do here); 2 one tet per
+// vertex, in vertex order (k_vmin_owner; its count lands in h_nbad[5], nsamp
+// after the upload's sync) -- A/Bs in DESIGN.md section 7 r05 / r06.  (r05's
+// mode 1, the every-4th-tet sample sorted by smallest vertex, was dropped in
+// r06: its sort could not be redone by a FRESH step.)
 bool pmx_ctx::order_hint_samples(int64_t ne, int64_t np, hipStream_t s) {
   samples_sorted = samples_owner = false;
-  nsamp = 0;
-  const char *e = getenv("PMX_HINT_SAMPLE_ORDER");
-  const int mode = e ? atoi(e) : 2;
-  if (mode == 0) return true;
-  if (mode == 2) {
-    if (np < 1 || ne < 1) return true;
-    const size_t tb = owner_scan_temp_bytes(np);
-    if (!dgrow(this, d_skey, (size_t)(np + 2)) || !dgrow(this, d_sidx, (size_t)(2 * (np + 1))) ||
-        !dgrow(this, d_salt, (size_t)(np + 1)) || !dgrow(this, d_tets_sk, (size_t)(np + 1)) ||
-        !dgrow(this, d_stmp, std::max<size_t>(tb, 1)) || !dgrow(this, d_wfar, 8))
-      return false;
-    if (!launch_owner_sample(d_tets.p, ne, np, d_skey.p, d_sidx.p, d_sidx.p + (np + 1), d_salt.p, d_tets_sk.p,
-                             d_wfar.p + 4, h_nbad + 5, d_stmp.p, tb, s)) {
-      err = "hint sample: vertex owners";
-      return false;
-    }
-    std::swap(d_tets_s, d_salt);
-    samples_sorted = samples_owner = true;
-    return true;
-  }
-  const int64_t n = (ne + PMX_HINT_STRIDE - 1) / PMX_HINT_STRIDE;
-  if (n < 1) return true;
-  const size_t tb = hint_sort_temp_bytes(n);
-  if (!dgrow(this, d_skey, (size_t)(2 * n)) || !dgrow(this, d_sidx, (size_t)(2 * n)) ||
-      !dgrow(this, d_salt, (size_t)n) || !dgrow(this, d_tets_sk, (size_t)n) ||
-      !dgrow(this, d_stmp, std::max<size_t>(tb, 1)))
+  if (sample_mode != 2 || np < 1 || ne < 1) return true;
+  const size_t tb = owner_scan_temp_bytes(np);
+  if (!dgrow(this, d_skey, (size_t)(np + 2)) || !dgrow(this, d_sidx, (size_t)(2 * (np + 1))) ||
+      !dgrow(this, d_salt, (size_t)(np + 1)) || !dgrow(this, d_tets_sk, (size_t)(np + 1)) ||
+      !dgrow(this, d_stmp, std::max<size_t>(tb, 1)) || !dgrow(this, d_wfar, 8))
     return false;
-  if (!launch_hint_sort(d_tets_s.p, n, PMX_HINT_STRIDE, np, d_skey.p, d_sidx.p, d_salt.p, d_tets_sk.p, d_stmp.p,
-                        tb, s)) {
-    err = "hint sample: sort";
+  if (!launch_owner_sample(d_tets.p, ne, np, d_skey.p, d_sidx.p, d_sidx.p + (np + 1), d_salt.p, d_tets_sk.p,
+                           d_wfar.p + 4, h_nbad + 5, d_stmp.p, tb, s)) {
+    err = "hint sample: vertex owners";
     return false;
   }
   std::swap(d_tets_s, d_salt);
-  samples_sorted = true;
+  samples_sorted = samples_owner = true;
+  return true;
+}
+
+// PMX_RUN_FRESH_BACKGROUND: the device passes an upload runs on the raw
+// arrays, again, in stream order on s -- a ParMmg iteration brings a new
+// background (PMMG_update_oldGrps, src/libparmmg1.c:653) and the reference
+// recomputes its derived data inside the call (src/interpmesh_pmmg.c:514-518)
+bool pmx_ctx::rederive(hipStream_t s) {
+  pmx_ctx *ctx = this;                     // CK()
+  if (bg_btv) {
+    // face matching of the uploaded connectivity, then the tet records and
+    // the every-4th-tet sample (MMG3D_hashTetra's adjacency on the device)
+    if (!pmx_ctx_build_adja_device(this, d_btv.p, ne, np, d_adja.p, s, h_nbad + 1)) return false;
+    launch_build_tetrec(d_btv.p, d_adja.p, ne, PMX_HINT_STRIDE, d_tets.p, d_tets_s.p, s);
+  }
+  if (compact_recs) launch_build_wrec(d_tets.p, ne, d_wrec.p, d_wfar.p, h_nbad + 2, s);
+  if (sample_mode == 2 && !order_hint_samples(ne, np, s)) return false;
+  CK(hipGetLastError());
+  return true;
+}
+
+// the orphan marks from the device copy of the new tets (d_ntetv), on s
+bool pmx_ctx::mark_new_tets(hipStream_t s) {
+  pmx_ctx *ctx = this;
+  if (nq < 1) return true;
+  CK(hipMemsetAsync(d_qmark.p, 0, (size_t)nq, s));
+  launch_mark_new_tets(d_ntetv.p, n_ntet, d_qmark.p, s);
+  CK(hipGetLastError());
   return true;
 }
 
@@ -1062,7 +1102,8 @@ static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &o
   // the 32-B records is faster (r05, C3: lex 0 % of the tets, compact 2 %
   // faster; 9 %, 32-B 1.5 % faster; appended 41 %, 32-B 5.5 % faster --
   // DESIGN.md section 7).  exp 18: compact records always
-  if (A.exp != 18 && (uint64_t)ctx->h_nbad[2] * PMX_WREC_FAR_DIV > (uint64_t)std::max<int64_t>(ctx->ne, 1))
+  if (!ctx->compact_recs ||
+      (A.exp != 18 && (uint64_t)ctx->h_nbad[2] * PMX_WREC_FAR_DIV > (uint64_t)std::max<int64_t>(ctx->ne, 1)))
     A.wrec = nullptr;
   A.far = ctx->h_nbad[2] > 0 ? 1 : 0;
 }
@@ -1083,7 +1124,7 @@ static bool run_flags_valid(int flags, std::string *err) {
   }
   const int e = (flags >> PMX_RUN_EXP_SHIFT) & 0xff;
   switch (e) {
-    case 0: case 6: case 9: case 10: case 11: case 12: case 13: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22:
+    case 0: case 6: case 9: case 10: case 11: case 12: case 13: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 23:
       return true;
     case 4: case 5: case 14: {
       const char *v = getenv("PMX_EXPERIMENTS");
@@ -1120,9 +1161,17 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   // everything below is one iteration's device work on the uploaded raw
   // arrays: the per-background derived data (with PMX_RUN_FRESH_BACKGROUND,
   // or after an upload), the points' classification and compaction, the
-  // node -> trias CSR (surface points only), hint grids, walks, fallback
-  const bool derive = !ctx->have_derived || (opts.flags & PMX_RUN_FRESH_BACKGROUND);
-  const bool csr = ctx->nq_bdy_ub > 0 && (!ctx->have_csr || (opts.flags & PMX_RUN_FRESH_BACKGROUND));
+  // node -> trias CSR (surface points only), hint grids, walks, fallback.
+  // FRESH also redoes every device pass of the uploads (rederive: records,
+  // samples, face matching; the fan check; the orphan marks of the new
+  // tets): the step is then what a ParMmg iteration costs the device.
+  const bool fresh = (opts.flags & PMX_RUN_FRESH_BACKGROUND) != 0;
+  const bool derive = !ctx->have_derived || fresh;
+  const bool csr = ctx->nq_bdy_ub > 0 && (!ctx->have_csr || fresh);
+  // the orphan marks inside the step (FRESH with new tets): the new tets'
+  // DMA must have landed (a pending points view is packed now)
+  const bool marks = fresh && ctx->have_ntet && n > 0;
+  if (marks && !ctx->ensure_tets(st)) return 0;
   if (ev) CK(hipEventRecord(ev[0], st));
   // one prologue kernel zeroes the write masks, the counters and the hint grid
   ZeroRanges z{};
@@ -1151,8 +1200,17 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   // exp 20: the same with the counting sort over the vertex ids
   const int exp0 = (opts.flags >> PMX_RUN_EXP_SHIFT) & 0xff;
   if (bdy && csr) {
-    if (!ctx->build_node_trias(exp0 == 19 || exp0 == 20 ? st : ss, exp0 == 20 ? 1 : 0)) return 0;
+    if (!ctx->build_node_trias(exp0 == 19 || exp0 == 20 ? st : ss, exp0 == 20 ? 1 : 0, fresh)) return 0;
     ctx->have_csr = true;
+  }
+  // the orphan marks on `up`, beside the derived data and the hint build
+  // (the classification waits for them)
+  if (marks) {
+    CK(hipEventRecord(ctx->ev_fork, st));
+    CK(hipStreamWaitEvent(ctx->up, ctx->ev_fork, 0));
+    if (!ctx->mark_new_tets(ctx->up)) return 0;
+    CK(hipEventRecord(ctx->ev_tets, ctx->up));
+    ctx->tets_inflight = true;
   }
   // exp 15 (A/B): no fixed-point copy of the vertices -- the hint build
   // quantises the sampled tets' vertices itself -- and the tria normals on
@@ -1174,14 +1232,30 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     }
     ctx->have_derived = !hint_xyz;
   }
+  if (fresh && !ctx->rederive(st)) return 0;
   if (ev) CK(hipEventRecord(ev[7], st));
-  if (!ctx->classify(st)) return 0;
-  if (sd.metric_const)
-    launch_const_metric(ctx->d_kind.p, n, ctx->d_out.p, S, sd.off[sd.imet], sd.size[sd.imet],
-                        opts.hsiz, ctx->d_wmask.p, sd.imet, st);
+  // with the marks in the step, the hint build (which does not depend on the
+  // points) goes ahead of the classification, beside the marks
+  const int stride = opts.hint_stride > 0 ? opts.hint_stride : PMX_HINT_STRIDE;
+  const bool packed = stride == PMX_HINT_STRIDE;
   bool any_interp = false;
   for (int s = 0; s < sd.nsol; s++)
     if (!(s == sd.imet && sd.metric_const)) any_interp = true;
+  GridDesc g_hint = ctx->grid;
+  auto hint_build = [&]() {
+    launch_hint_build(packed ? ctx->d_tets_s.p : nullptr,
+                      packed && ctx->samples_sorted ? ctx->d_tets_sk.p : nullptr, ctx->d_tets.p, ctx->ne,
+                      stride, ctx->d_grid.p, g_hint, hint_xyz ? nullptr : ctx->d_xyzq.p, ctx->d_xyz.p, st,
+                      exp == 16, exp == 21 ? 1024 : exp == 22 ? 64 : 256,
+                      packed && ctx->samples_owner ? ctx->nsamp : -1);
+  };
+  const bool hint_first = marks && any_interp && exp != 23;   // exp 23 (A/B): the r05 order
+  if (hint_first) hint_build();
+  if (marks) CK(hipStreamWaitEvent(st, ctx->ev_tets, 0));
+  if (!ctx->classify(st, marks)) return 0;
+  if (sd.metric_const)
+    launch_const_metric(ctx->d_kind.p, n, ctx->d_out.p, S, sd.off[sd.imet], sd.size[sd.imet],
+                        opts.hsiz, ctx->d_wmask.p, sd.imet, st);
   // reference early exit (src/interpmesh_pmmg.c:508-512): nothing to locate
   if (!any_interp && bdy && !serial) {
     CK(hipEventRecord(ctx->ev_join, side));
@@ -1206,14 +1280,8 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     };
     const bool early = A.exp != 9;
     if (early && !fork_surface()) return 0;
-    const int stride = opts.hint_stride > 0 ? opts.hint_stride : PMX_HINT_STRIDE;
-    const bool packed = stride == PMX_HINT_STRIDE;
-    launch_hint_build(packed ? ctx->d_tets_s.p : nullptr,
-                      packed && ctx->samples_sorted ? ctx->d_tets_sk.p : nullptr, ctx->d_tets.p, ctx->ne,
-                      stride, ctx->d_grid.p, A.g, hint_xyz ? nullptr : ctx->d_xyzq.p, ctx->d_xyz.p, st,
-                      exp == 16, exp == 21 ? 1024 : exp == 22 ? 64 : 256,
-                      packed && ctx->samples_owner ? ctx->nsamp : -1);
-    if (exp == 13 && ctx->d_wrec.p) {
+    if (!hint_first) hint_build();
+    if (exp == 13 && A.wrec) {
       if (!dgrow(ctx, ctx->d_hrec, (size_t)(2 * ctx->gcells))) return 0;
       launch_hint_inline(ctx->d_grid.p, ctx->gcells, ctx->d_wrec.p, ctx->d_hrec.p, st);
       A.hrec = ctx->d_hrec.p;
@@ -1254,7 +1322,10 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   // first consumer of these results (fix_orphans); the new tets are packed
   // and sent now, while the device runs the step
   ctx->last_const_bit = sd.metric_const ? (1u << sd.imet) : 0u;
-  ctx->orph_fixed = false;
+  // with the marks in the step, the orphans were never located (KIND_ORPH):
+  // nothing to reset
+  ctx->orph_fixed = marks;
+  if (marks) ctx->orph_marks = true;
   ctx->out_S = S;
   ctx->out_n = n;
   if ((opts.flags & PMX_RUN_EAGER_DOWNLOAD) && !ctx->eager_download()) return 0;
@@ -1810,6 +1881,7 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
   tr.mark("trias");
   // the background invalid until this completes
   ctx->have_bg = ctx->have_derived = ctx->have_tetv = ctx->have_qual = ctx->have_ptag = ctx->have_csr = ctx->have_surf = false;
+  ctx->bg_btv = false;                     // records from the new tets (or the caller's adja), not d_btv
   ctx->stat_np = -1;
   const int64_t ns = (ne + PMX_HINT_STRIDE - 1) / PMX_HINT_STRIDE;
   if (!dgrow(ctx, ctx->d_xyz, (size_t)(n + 1) * 3) || !dgrow(ctx, ctx->d_sol, (size_t)(n + 1) * std::max(S, 1)) ||
@@ -1848,9 +1920,10 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
     } else if (!pmx_ctx_build_adja_device(ctx, ctx->d_ntetv.p, ne, n, ctx->d_adja.p, st, nullptr)) {
       return 0;
     }
-    if (!dgrow(ctx, ctx->d_wrec, (size_t)(ne + 1)) || !dgrow(ctx, ctx->d_wfar, 8)) return 0;
+    if ((ctx->compact_recs && !dgrow(ctx, ctx->d_wrec, (size_t)(ne + 1))) || !dgrow(ctx, ctx->d_wfar, 8)) return 0;
     launch_build_tetrec(ctx->d_ntetv.p, ctx->d_adja.p, ne, PMX_HINT_STRIDE, ctx->d_tets.p, ctx->d_tets_s.p, st);
-    launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, ctx->d_wfar.p, ctx->h_nbad + 2, st);
+    ctx->h_nbad[2] = 0;
+    if (ctx->compact_recs) launch_build_wrec(ctx->d_tets.p, ne, ctx->d_wrec.p, ctx->d_wfar.p, ctx->h_nbad + 2, st);
   }
   ctx->np = n;
   ctx->ne = ne;
@@ -1880,9 +1953,9 @@ int pmx_promote_background(pmx_ctx *ctx, const pmx_mesh_view *m, int nsol, const
 
 // the new points' classification and compaction on stream s (the marks, if
 // any, zeroed beforehand)
-bool pmx_ctx::classify(hipStream_t s) {
+bool pmx_ctx::classify(hipStream_t s, bool marks) {
   if (nq < 1) return true;
-  launch_classify(have_qtag ? d_qtag.p : nullptr, pts_mark ? d_qmark.p : nullptr, nq, d_ctile.p, d_kind.p, d_vollist.p, d_bdylist.p,
+  launch_classify(have_qtag ? d_qtag.p : nullptr, marks ? d_qmark.p : nullptr, nq, d_ctile.p, d_kind.p, d_vollist.p, d_bdylist.p,
                   d_nsel.p, s);
   if (hipGetLastError() != hipSuccess) {
     err = "classification: launch failed";

@@ -66,14 +66,15 @@ __device__ __forceinline__ D3 nonunit_normal(D3 a, D3 b, D3 c) {
   return n;
 }
 
-// MMG5_orvol -> MMG5_det4pt -> MMG5_det3pt1vec (restated)
+// MMG5_orvol -> MMG5_det4pt(c0,c1,c2,c3) -> MMG5_det3pt1vec(c0,c1,c2,v),
+// v = c3 - c0: [c1-c0 | c2-c0 | v] expanded along v, left to right (restated
+// from the public Mmg source; the same expression as oracle/pmx_oracle.c)
 __device__ __forceinline__ double orvol(D3 c0, D3 c1, D3 c2, D3 c3) {
-  double w0 = c3.x - c0.x, w1 = c3.y - c0.y, w2 = c3.z - c0.z;
-  double m00 = c1.x - c0.x, m01 = c2.x - c0.x, m02 = w0;
-  double m10 = c1.y - c0.y, m11 = c2.y - c0.y, m12 = w1;
-  double m20 = c1.z - c0.z, m21 = c2.z - c0.z, m22 = w2;
-  return m00 * (m11 * m22 - m21 * m12) - m10 * (m01 * m22 - m21 * m02) +
-         m20 * (m01 * m12 - m11 * m02);
+  double m00 = c1.x - c0.x, m01 = c2.x - c0.x;
+  double m10 = c1.y - c0.y, m11 = c2.y - c0.y;
+  double m20 = c1.z - c0.z, m21 = c2.z - c0.z;
+  double v0 = c3.x - c0.x, v1 = c3.y - c0.y, v2 = c3.z - c0.z;
+  return v0 * (m10 * m21 - m20 * m11) - v1 * (m00 * m21 - m20 * m01) + v2 * (m00 * m11 - m10 * m01);
 }
 
 // lambda_f = -((p - c_f) . n_f) / vol, c_f = first vertex of face f in

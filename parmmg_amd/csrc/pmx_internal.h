@@ -54,10 +54,20 @@ struct pmx_ctx {
   DevBuf<WRec> d_wrec;                  // the walk's compact copy of d_tets (built with it)
   DevBuf<unsigned> d_wfar;              // [0] / [1] far-field counters of d_wrec / d_wrec_next, [2] / [3] bad fans (step / upload check), [4] owner-sample count
   DevBuf<double> d_sol;
-  DevBuf<int4> d_tets_s;                // hint sample: one owner tet per vertex (default) or every 4th tet (order_hint_samples)
+  DevBuf<int4> d_tets_s;                // hint sample: every 4th tet (default, packed with the tets) or one owner tet per vertex (order_hint_samples)
   DevBuf<int> d_tets_sk;                // its tet indices (samples_sorted)
   bool samples_sorted = false;
   bool samples_owner = false;           // the vertex-owner sample: nsamp entries
+  // decided at each background upload / promotion (environment, A/B):
+  // compact_recs -- the walk's 24-B records d_wrec are built (PMX_WALK_RECORDS=compact;
+  //   default: the walk reads the 32-B records, no per-background pass);
+  // sample_mode -- PMX_HINT_SAMPLE_ORDER: 0 (default) every 4th tet, packed by the host
+  //   with the tet records (or by k_build_tetrec), 2 one owner tet per vertex (device passes)
+  bool compact_recs = false;
+  int sample_mode = 0;
+  // d_btv holds this background's raw connectivity and its adjacency was
+  // built on the device (an upload without Mmg's adja)
+  bool bg_btv = false;
   int64_t nsamp = 0;
   DevBuf<unsigned> d_skey;              // order_hint_samples scratch: keys / owners, indices / flags, records, temp
   DevBuf<int> d_sidx;
@@ -169,7 +179,6 @@ struct pmx_ctx {
   bool have_qtag = false;               // raw tags of the new points
   DevBuf<uint16_t> d_qtag;
   int64_t pts_first = 0;                // points view's first index
-  bool pts_mark = false;                // d_qmark holds the host's orphan marks (some point is in no valid new tet)
   // the new tets of the points view: packed (validated, orphan marks) and
   // sent by the first pmx_run after the upload, once its step is enqueued --
   // their DMA on `up` overlaps the step and the results' download (the step
@@ -202,13 +211,24 @@ struct pmx_ctx {
   hipEvent_t *next_event_slot();
   void free_all();
   bool order_hint_samples(int64_t ne, int64_t nverts, hipStream_t s);
+  // PMX_RUN_FRESH_BACKGROUND: the per-background device passes of an upload
+  // (face matching + records when the device built the adjacency, compact
+  // records, owner sample), again on stream s (pmx_capi.hip)
+  bool rederive(hipStream_t s);
+  // the orphan marks of the new tets on stream s: d_qmark[j] = 1 when a valid
+  // new tet holds point j (the reference's vertex loop, src/interpmesh_pmmg.c:535-541)
+  bool mark_new_tets(hipStream_t s);
   // the fans by rotation (closed manifold surface, checked at the upload:
   // fan_rot) or by a sort; force 1: the counting sort
   bool fan_rot = false;
   bool fan_rotation(hipStream_t s, unsigned *d_bad, const unsigned *vcount = nullptr);
   bool check_fans(hipStream_t s);
-  bool build_node_trias(hipStream_t s, int force = 0);   // from d_tris, np, nt (pmx_bdy.hip)
-  bool classify(hipStream_t s);           // the new points: kinds, lists, marks (pmx_capi.hip)
+  // from d_tris, np, nt (pmx_bdy.hip); check: the rotation also re-counts every
+  // vertex's trias, the upload's fan check (a FRESH step redoes it)
+  bool build_node_trias(hipStream_t s, int force = 0, bool check = false);
+  // the new points: kinds, lists (pmx_capi.hip); marks: the orphan marks
+  // (d_qmark) classify points in no valid new tet as KIND_ORPH
+  bool classify(hipStream_t s, bool marks = false);
   bool launch_bdy(const VolArgs &a, hipStream_t s);
   bool size_tria_grid();
   bool pack_new_tets();                   // the pending new tets: pack, send on `up`, residency build

@@ -116,8 +116,8 @@ struct OrphanRows {
 void launch_orphans(const uint8_t *mk, int64_t n, uint8_t keep, const OrphanRows &r, hipStream_t s);
 void launch_patch_rows(const int4 *ent, const double *vals, int64_t n, int S, double *sol, hipStream_t s);
 // new points, every step (the tag dispatch of the reference's vertex loop,
-// src/interpmesh_pmmg.c:541-560): kinds (mark != NULL: the host's orphan
-// marks, 0 = in no valid new tet) and the order-preserving compaction into
+// src/interpmesh_pmmg.c:541-560): kinds (mark != NULL: the orphan marks of
+// the new tets, 0 = in no valid new tet) and the order-preserving compaction into
 // the volume / surface lists; counts into nsel[0..1].  tcnt: scratch of cls_tiles(n) int2.
 #define CLS_TILE 16384               // 4 rounds of 256 threads x 16 points
 inline int64_t cls_tiles(int64_t n) { return (n + CLS_TILE - 1) / CLS_TILE; }
@@ -126,13 +126,6 @@ void launch_classify(const uint16_t *tag, const uint8_t *mk, int64_t n, int2 *tc
 
 void launch_build_tetrec(const int4 *tv, const int *adja, int64_t ne, int stride, TetRec *tets, int4 *sample,
                          hipStream_t s);
-// the walk's compact records from the tet records (slots 0..ne)
-// (*h_nfar, pinned, when stream s gets there: the tets with a far neighbour
-// field, pmx_wrec.h; d_nfar one device word)
-// the packed hint sample in the order of its tets' smallest vertex ids
-// (k_sample_keys): out[i] = smp[t_i] and kidx[i] = 1 + stride * t_i; keys and
-// idx 2n words each, tmp hint_sort_temp_bytes(n) bytes
-size_t hint_sort_temp_bytes(int64_t n);
 // the vertex-owner sample (k_vmin_owner): out[i] / kidx[i] the i-th vertex's
 // owner tet in vertex order; owner np + 1 words, flag and pos np + 1 ints each,
 // tmp owner_scan_temp_bytes(np) bytes; the sample count into *h_count (pinned)
@@ -140,8 +133,9 @@ size_t owner_scan_temp_bytes(int64_t np);
 bool launch_owner_sample(const TetRec *tets, int64_t ne, int64_t np, unsigned *owner, int *flag, int *pos,
                          int4 *out, int *kidx, unsigned *d_count, unsigned *h_count, void *tmp, size_t tmp_bytes,
                          hipStream_t s);
-bool launch_hint_sort(const int4 *smp, int64_t n, int stride, int64_t np, unsigned *keys, int *idx, int4 *out,
-                      int *kidx, void *tmp, size_t tmp_bytes, hipStream_t s);
+// the walk's compact records from the tet records (slots 0..ne)
+// (*h_nfar, pinned, when stream s gets there: the tets with a far neighbour
+// field, pmx_wrec.h; d_nfar one device word)
 void launch_build_wrec(const TetRec *tets, int64_t ne, WRec *wr, unsigned *d_nfar, unsigned *h_nfar,
                        hipStream_t s);
 // workgroups of k_fallback that can be co-resident with `share` other

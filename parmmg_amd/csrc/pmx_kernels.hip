@@ -203,23 +203,6 @@ void launch_hint_build(const int4 *packed, const int *kidx, const TetRec *tets, 
                        grid, g, xyzq, xyz);
 }
 
-// The packed hint sample in the order of its tets' smallest vertex ids (at
-// every upload / promotion, not in the step): a re-layout of connectivity
-// like the walk records, no geometry.  In tet order the sample is as
-// coherent as the tet numbering: an Mmg-appended numbering (10 % of the tets
-// moved to the end) scatters a tenth of it, and each wave of those samples
-// gathers and writes 64 distinct lines -- C3 hint build 0.25 -> 0.42 ms
-// (r05).  The vertex numbering (Mmg keeps its vertices
-// in place, Scotch renumbers them spatially) orders it in space again.  The
-// stable sort leaves samples sharing a smallest vertex in tet order.
-__global__ __launch_bounds__(256) void k_sample_keys(const int4 *__restrict__ smp, int64_t n, unsigned nokey,
-                                                     unsigned *__restrict__ key, int *__restrict__ idx) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int4 v = smp[i];
-    key[i] = v.x > 0 ? (unsigned)min(min(v.x, v.y), min(v.z, v.w)) : nokey;   // deleted tets last
-    idx[i] = (int)i;
-  }
-}
 // The vertex-owner sample (r05): one tet per vertex -- the smallest tet
 // among those whose smallest vertex it is -- in vertex order.  Like the
 // every-4th-tet sample it is connectivity only, but it covers space whatever
@@ -281,41 +264,6 @@ bool launch_owner_sample(const TetRec *tets, int64_t ne, int64_t np, unsigned *o
   hipLaunchKernelGGL(k_owner_gather, dim3((unsigned)nbv), dim3(256), 0, s, (const unsigned *)owner,
                      (const int *)flag, (const int *)pos, np, tets, out, kidx, d_count);
   if (hipMemcpyAsync(h_count, d_count, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess) return false;
-  return hipGetLastError() == hipSuccess;
-}
-
-// the sorted sample and the tet index of each entry (1 + stride * t)
-__global__ __launch_bounds__(256) void k_sample_gather(const int4 *__restrict__ smp, const int *__restrict__ idx,
-                                                       int64_t n, int stride, int4 *__restrict__ out,
-                                                       int *__restrict__ kidx) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int t = idx[i];
-    out[i] = smp[t];
-    kidx[i] = 1 + stride * t;
-  }
-}
-static int key_bits(int64_t np) {
-  int bits = 1;
-  while (bits < 32 && ((int64_t)1 << bits) <= np + 1) bits++;   // keys 1 .. np + 1
-  return bits;
-}
-size_t hint_sort_temp_bytes(int64_t n) {
-  size_t bytes = 0;
-  hipcub::DoubleBuffer<unsigned> k(nullptr, nullptr);
-  hipcub::DoubleBuffer<int> v(nullptr, nullptr);
-  hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, k, v, (int)n, 0, 32);
-  return bytes;
-}
-bool launch_hint_sort(const int4 *smp, int64_t n, int stride, int64_t np, unsigned *keys, int *idx, int4 *out,
-                      int *kidx, void *tmp, size_t tmp_bytes, hipStream_t s) {
-  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 65536));
-  hipLaunchKernelGGL(k_sample_keys, dim3((unsigned)nb), dim3(256), 0, s, smp, n, (unsigned)(np + 1), keys, idx);
-  hipcub::DoubleBuffer<unsigned> k(keys, keys + n);
-  hipcub::DoubleBuffer<int> v(idx, idx + n);
-  if (hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, k, v, (int)n, 0, key_bits(np), s) != hipSuccess)
-    return false;
-  hipLaunchKernelGGL(k_sample_gather, dim3((unsigned)nb), dim3(256), 0, s, smp, (const int *)v.Current(), n,
-                     stride, out, kidx);
   return hipGetLastError() == hipSuccess;
 }
 
@@ -730,19 +678,45 @@ void launch_orphans(const uint8_t *mk, int64_t n, uint8_t keep, const OrphanRows
 
 // the orphan marks from the new tets on the device: point j (0-based) is
 // marked when a valid new tet (1-based vertex j + 1) holds it -- the
-// reference's vertex loop over the new tets (src/interpmesh_pmmg.c:535-541)
+// reference's vertex loop over the new tets (src/interpmesh_pmmg.c:535-541).
+// HBM-bound on the 16-B tet reads; the byte stores are what costs beyond
+// them (r06: 0.50 ms at C3 with four stores per tet), so a lane skips the
+// vertices its left neighbour -- the previous tet, which in any coherent
+// numbering shares most of them -- also holds (that lane stores them), and
+// each lane takes two tets per round (two loads in flight).
 __global__ __launch_bounds__(256) void k_mark_new_tets(const int4 *__restrict__ tv, int64_t ne,
                                                        uint8_t *__restrict__ mk) {
-  for (int64_t k = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= ne;
-       k += (int64_t)gridDim.x * blockDim.x) {
-    const int4 v = tv[k];
-    if (v.x <= 0) continue;
-    mk[v.x - 1] = 1; mk[v.y - 1] = 1; mk[v.z - 1] = 1; mk[v.w - 1] = 1;
+  const int64_t st = (int64_t)gridDim.x * blockDim.x;
+  const int64_t nit = (ne + 2 * st - 1) / (2 * st);    // uniform trip count (the shuffles below)
+  const bool lane0 = (threadIdx.x & 63) == 0;
+  for (int64_t it = 0; it < nit; it++) {
+    const int64_t k0 = 1 + 2 * (it * st + (int64_t)blockIdx.x * blockDim.x) + threadIdx.x;
+    int4 v[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int64_t k = k0 + h * blockDim.x;
+      v[h] = k <= ne ? tv[k] : make_int4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int4 a = v[h];
+      int4 u;
+      u.x = __shfl_up(a.x, 1, 64); u.y = __shfl_up(a.y, 1, 64);
+      u.z = __shfl_up(a.z, 1, 64); u.w = __shfl_up(a.w, 1, 64);
+      if (lane0 || u.x <= 0) u = make_int4(0, 0, 0, 0);   // no valid left neighbour: store all
+      if (a.x <= 0) continue;                             // !MG_EOK
+      const int w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+      for (int l = 0; l < 4; l++) {
+        const int q = w[l];
+        if (q != u.x && q != u.y && q != u.z && q != u.w) mk[q - 1] = 1;
+      }
+    }
   }
 }
 void launch_mark_new_tets(const int4 *tv, int64_t ne, uint8_t *mk, hipStream_t s) {
   if (ne < 1) return;
-  const int64_t nb = std::min<int64_t>((ne + 255) / 256, 8192);
+  const int64_t nb = std::min<int64_t>((ne + 511) / 512, 8192);
   hipLaunchKernelGGL(k_mark_new_tets, dim3((unsigned)nb), dim3(256), 0, s, tv, ne, mk);
 }
 
@@ -866,11 +840,12 @@ __device__ __forceinline__ void kinds16(const uint16_t *__restrict__ tag, const 
     const unsigned t = (tw[i >> 1] >> (16 * (i & 1))) & 0xffffu;
     const bool in = j0 + i < n;
     // kind of a new point: PMMG_interpMetricsAndFields_mesh's dispatch
-    // (src/interpmesh_pmmg.c:541-560): !MG_VOK, in no valid new tet, MG_REQ,
-    // MG_BDY, volume
+    // (src/interpmesh_pmmg.c:541-560): !MG_VOK, MG_REQ (copied by
+    // PMMG_copyMetricsAndFields_point over every point, :311-446, whatever
+    // the tets), in no valid new tet (never visited), MG_BDY, volume
     unsigned k = (t >= PMX_TAG_NUL) ? KIND_NUL
-                 : (mark && !((mw[i >> 2] >> (8 * (i & 3))) & 0xffu)) ? KIND_ORPH
                  : (t & PMX_TAG_REQ) ? KIND_SKIP
+                 : (mark && !((mw[i >> 2] >> (8 * (i & 3))) & 0xffu)) ? KIND_ORPH
                  : (t & PMX_TAG_BDY) ? KIND_BDY : KIND_VOL;
     k = in ? k : 0xffu;
     cv += k == KIND_VOL;

@@ -32,6 +32,22 @@ MMG_TETRA = np.dtype([("qual", "f8"), ("v", "i4", 4), ("ref", "i4"), ("base", "i
 _mg = None
 
 
+def cpu_share() -> int:
+    """CPUs this process may use: its affinity set capped by the cgroup v2
+    quota (cpu.max; a GPU box: 16 of 256) -- the generator's OpenMP team."""
+    try:
+        k = len(os.sched_getaffinity(0))
+    except AttributeError:
+        k = os.cpu_count() or 1
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            k = min(k, max(1, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return max(1, k)
+
+
 def _meshgen() -> C.CDLL:
     global _mg
     if _mg is None:
@@ -55,6 +71,8 @@ def _meshgen() -> C.CDLL:
         lib.pmg_new_points.argtypes = [C.c_int, C.c_uint64, C.c_double, C.c_int, C.c_int, vp, vp]
         lib.pmg_count_inverted.restype = i64
         lib.pmg_count_inverted.argtypes = [i64, vp, vp]
+        lib.pmg_set_threads.argtypes = [C.c_int]
+        lib.pmg_set_threads(cpu_share())
         _mg = lib
     return _mg
 

@@ -447,3 +447,58 @@ def test_fans_at_a_pinched_vertex(transfer, monkeypatch):
         assert np.array_equal(u, w)
     for u, w in zip(a[2], b[2]):
         assert np.array_equal(u.view(np.uint64), w.view(np.uint64))
+
+
+@pytest.mark.parametrize("records,sample,adja", [("", "0", True), ("compact", "2", True), ("", "0", False),
+                                                 ("compact", "0", False)])
+def test_fresh_step_equals_upload_step(transfer, monkeypatch, records, sample, adja):
+    """PMX_RUN_FRESH_BACKGROUND redoes every device pass of the uploads inside
+    the step (r06): the compact walk records and the owner hint sample when the
+    upload built them, the device face matching of a background sent without
+    Mmg's adjacency, the fan check, and the orphan marks of the new tets --
+    the latter now BEFORE the classification, so orphans are never located
+    instead of located and reset.  Same bytes as the plain step whose orphan
+    rows fix_orphans resets: fields, write masks, elements, status, steps,
+    starts, border, locate statistics; twice in a row."""
+    if records:
+        monkeypatch.setenv("PMX_WALK_RECORDS", records)
+    monkeypatch.setenv("PMX_HINT_SAMPLE_ORDER", sample)
+    m, x, t, sols = cube_case(7, metric="ani", surface=True)
+    n = len(x)
+    x = x.copy()
+    t = t.copy()
+    t[3::53] |= M.TAG_REQ
+    rng = np.random.default_rng(5)
+    used = np.zeros(n, bool)
+    used[: int(0.8 * n)] = True
+    x[np.nonzero(~used)[0][:4]] = [1.5, -0.5, 0.5]      # orphans outside the domain
+    pool = np.nonzero(used)[0]
+    tets = np.zeros((len(pool) + 1, 4), np.int32)
+    tets[1:] = rng.choice(pool, size=(len(pool), 4))
+    tets[1:, 0] = pool
+    tets[0] = -1
+
+    def go(flags):
+        transfer.upload_background(m, sols, 0, adja=adja)
+        transfer.upload_points(x, t, tets)
+        res = []
+        for _ in range(2):
+            transfer.run(flags=flags, record_starts=True)
+            init = [np.full((n, s.shape[1]), -7.0) for s in sols]
+            r = transfer.download(init=init)
+            res.append((r, transfer.starts().copy(), transfer.border(), transfer.locate_stats()))
+        return res
+
+    a, b = go(0), go(N.RUN_FRESH_BACKGROUND)
+    for (ra, sa, ba, la), (rb, sb, bb, lb) in zip(a + a, b + b[::-1]):
+        assert np.array_equal(ra.elem, rb.elem) and np.array_equal(ra.status, rb.status)
+        assert np.array_equal(ra.steps, rb.steps)
+        for u, v in zip(ra.sols, rb.sols):
+            assert np.array_equal(u.view(np.uint64), v.view(np.uint64))
+        assert np.array_equal(sa, sb)
+        assert np.array_equal(ba[0], bb[0]) and np.array_equal(ba[1], bb[1])
+        assert la == lb
+    r = b[0][0]
+    assert np.all(r.elem[~used] == 0) and np.all(r.status[~used] == 0)
+    live = used & ((t & M.TAG_REQ) == 0)
+    assert np.all(r.status[live] != 0)

@@ -18,6 +18,14 @@ pytestmark = pytest.mark.gpu
 FULL_RECORDS = 6 << 16            # PMX_RUN_EXP_SHIFT: exp 6 = walk on the 32-B records
 
 
+@pytest.fixture(autouse=True)
+def _compact_records(monkeypatch):
+    """Since r06 the walk reads the 32-B records unless the upload builds the
+    compact ones (PMX_WALK_RECORDS=compact, read at every background upload):
+    these tests pin that path against the 32-B walk."""
+    monkeypatch.setenv("PMX_WALK_RECORDS", "compact")
+
+
 def _both(tr, m, x, t, sols):
     tr.upload_background(m, sols, 0)
     tr.upload_points(x, t)
@@ -131,28 +139,29 @@ def test_far_neighbour_fields(transfer):
 
 def test_hint_sample_order(transfer, monkeypatch):
     """The hint samples of pmx_ctx::order_hint_samples -- every 4th tet in tet
-    order (0), sorted by smallest vertex id (1), one owner tet per vertex (2,
-    the default) -- carry their tet indices: on an appended numbering the step
-    locates and interpolates bit for bit alike, with walks as short."""
+    order, packed with the tet records (0, the default since r06), one owner
+    tet per vertex (2) -- carry their tet indices: on an appended numbering the
+    step locates and interpolates bit for bit alike, with walks as short, and
+    a FRESH step (which rebuilds the owner sample) gives the same results."""
     m, _ = M.numbering(M.kuhn_cube(16), "appended")
     x, t = M.new_points(16, seed=3, surface=True)
     sols = [M.on_vertices(m, M.iso_metric), M.on_vertices(m, lin_field)]
     out = []
-    for order in ("0", "1", "2"):
+    for order in ("0", "2"):
         monkeypatch.setenv("PMX_HINT_SAMPLE_ORDER", order)
         transfer.upload_background(m, sols, 0)
         transfer.upload_points(x, t)
-        transfer.run(record_starts=True)
-        r = transfer.download()
-        out.append((r.elem.copy(), r.status.copy(), [s.copy() for s in r.sols],
-                    transfer.locate_stats()["stepav"], transfer.starts().copy()))
-    _assert_same(out[0], out[1])
-    _assert_same(out[0], out[2])
-    assert out[1][3] < 1.2 * out[0][3], (out[0][3], out[1][3])
+        for flags in (0, N.RUN_FRESH_BACKGROUND):
+            transfer.run(record_starts=True, flags=flags)
+            r = transfer.download()
+            out.append((r.elem.copy(), r.status.copy(), [s.copy() for s in r.sols],
+                        transfer.locate_stats()["stepav"], transfer.starts().copy()))
+    for o in out[1:]:
+        _assert_same(out[0], o)
     assert out[2][3] < 1.2 * out[0][3], (out[0][3], out[2][3])
-    vol = (t == 0) & (out[1][1] == 1)
-    assert not np.array_equal(out[0][4][vol], out[1][4][vol])       # other start tets
-    assert not np.array_equal(out[0][4][vol], out[2][4][vol])
+    vol = (t == 0) & (out[0][1] == 1)
+    assert not np.array_equal(out[0][4][vol], out[2][4][vol])       # other start tets
+    assert np.array_equal(out[2][4], out[3][4])                     # the FRESH rebuild: same sample
 
 
 COMPACT_FORCED = 18 << 16         # exp 18: compact records whatever their far fields

@@ -108,6 +108,17 @@ def _cpu_rank(r: int):
     return res["value"], res["sample"]
 
 
+def _physical_cores() -> int | None:
+    """Physical cores of the machine (lscpu's CORE,SOCKET pairs), or None."""
+    import subprocess
+    try:
+        out = subprocess.run(["lscpu", "-p=CORE,SOCKET"], capture_output=True, text=True, timeout=10).stdout
+    except (OSError, subprocess.SubprocessError):
+        return None
+    pairs = {ln.strip() for ln in out.splitlines() if ln and not ln.startswith("#")}
+    return len(pairs) or None
+
+
 def _cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -191,6 +202,7 @@ def cpu_baseline_node(m, x, t, sols, budget_s: float = 20.0) -> dict:
                                            f"{cpus[:K][0]}..{cpus[:K][-1]} of the affinity set",
             "memory_bound": K < share, "mem_budget_GB": budget / 1e9, "per_process_GB": per_proc / 1e9,
             "per_core": float(np.mean(rates)), "cpu_model": _cpu_model(),
+            "physical_cores": _physical_cores(),
             "sample": f"{K} concurrent processes, each: {res[0][1]}; node rate = sum of the "
                       f"{K} per-process rates (min {min(rates):.3g}, max {max(rates):.3g})"}
 
@@ -439,6 +451,12 @@ def main():
                     help="background tet numbering (SURVEY.md 8(d)): lex = the generator's "
                          "cell-lexicographic order (Scotch-like), shuffle = random order (seed 7), "
                          "appended = 10%% of the tets moved to the end (Mmg insertions)")
+    ap.add_argument("--no-seq", action="store_true",
+                    help="skip the sequential-surface leg (PMX_RUN_SEQUENTIAL_SURFACE, measured after "
+                         "the timed region)")
+    ap.add_argument("--run-exp", type=int, default=0,
+                    help="A/B measurement switch of the step (pmx_run flags bits 16-23, "
+                         "parmmg_amd/csrc/pmx_capi.hip run_flags_valid)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 process group backend (nccl = RCCL; gloo only to rehearse "
                          "the multi-rank path, e.g. several ranks on one GPU)")
@@ -488,8 +506,9 @@ def main():
         cpu = cpu_baseline_node(m, x, t, sols)
 
     from parmmg_amd import _native as N
+    from parmmg_amd import mesh as M
     from parmmg_amd.transfer import Transfer
-    FRESH = N.RUN_FRESH_BACKGROUND
+    FRESH = N.RUN_FRESH_BACKGROUND | (args.run_exp << 16)
     # every group of this rank in its own context (own stream): the groups'
     # steps are enqueued back to back and may overlap on the device
     trs = []
@@ -541,7 +560,10 @@ def main():
     st["wrec_far_fields"], st["wrec_tets_with_far_fields"] = M.wrec_far_fields(m)
     # the walk's record format (pmx_capi.hip fill_vol_args: 32-B records above
     # 1/16 of the tets with a far neighbour field)
-    st["walk_records"] = "32-B" if st["wrec_tets_with_far_fields"] * 16 > m.ne else "24-B compact"
+    # (r06: the compact records only when the upload builds them,
+    # PMX_WALK_RECORDS=compact; default the 32-B records, no per-background pass)
+    compact = os.environ.get("PMX_WALK_RECORDS") == "compact"
+    st["walk_records"] = "24-B compact" if compact and st["wrec_tets_with_far_fields"] * 16 <= m.ne else "32-B"
     # the same step on a background already prepared by an earlier step (what
     # repeated steps on one background cost; reported, never `value`)
     sync()
@@ -550,6 +572,32 @@ def main():
         step(flags=0)
     sync()
     resident_ms = (time.perf_counter() - t1) / args.steps * 1e3
+
+    # the reference's sequential surface semantics (PMX_RUN_SEQUENTIAL_SURFACE,
+    # bit-exact against the oracle's sequential run in tests/): its cost, and
+    # how many surface points the default (fresh-query) step answers
+    # differently -- another tria, edge or vertex
+    seq = None
+    if world == 1 and not args.no_seq and not args.no_new_tets:
+        sync()
+        tr.run(flags=N.RUN_FRESH_BACKGROUND)
+        r0 = tr.download()
+        e0, v0 = tr.border()
+        tr.synchronize()
+        t2 = time.perf_counter()
+        tr.run(flags=N.RUN_FRESH_BACKGROUND | N.RUN_SEQUENTIAL_SURFACE)
+        tr.synchronize()
+        seq_ms = (time.perf_counter() - t2) * 1e3
+        r1 = tr.download()
+        e1, v1 = tr.border()
+        ss = tr.seq_surface_stats()
+        b = (t & M.TAG_BDY) != 0
+        ndiff = int(((r0.elem != r1.elem) | (e0 != e1) | (v0 != v1))[b].sum())
+        seq = {"ms": seq_ms, "surface_points": ss["nseq"], "replayed": ss["nreplay"],
+               "default_mode_differs_on": ndiff,
+               "note": "one FRESH step with PMX_RUN_SEQUENTIAL_SURFACE, wall clock incl. host sync; "
+                       "the default step answers default_mode_differs_on surface points with another "
+                       "tria / edge / vertex than the reference's sequential run"}
 
     # host-staged rate (ParMmg's adapter path: host buffers in and out), measured
     # after the timed region and never reported as `value`
@@ -642,9 +690,22 @@ def main():
             b = pcie["binding_cycle"]["value"]
             cpu["binding_cycle"] = {"vertices_per_s": b, "speedup_vs_node": b / cpu["value"],
                                     "speedup_vs_core": b / cpu["per_core"]}
+        if cpu.get("physical_cores"):
+            # an ESTIMATE, not a measurement: the per-core rate of the K measured
+            # processes times the machine's physical cores (the reference run as
+            # one MPI rank per core on the whole node, memory bandwidth assumed
+            # to scale); what ParMmg gets from the GPU is binding_cycle
+            est = cpu["per_core"] * cpu["physical_cores"]
+            cpu["full_node_estimate"] = {
+                "value": est, "unit": "vertices/s", "cores": cpu["physical_cores"], "kind": "estimate",
+                "how": "per_core x physical cores (lscpu), not measured",
+                "device_step_vs_estimate": value / est,
+                "binding_cycle_vs_estimate": (pcie["binding_cycle"]["value"] / est) if pcie else None}
         out["cpu_baseline"] = cpu
     if pcie is not None:
         out["pcie_inclusive"] = pcie
+    if seq is not None:
+        out["sequential_surface"] = seq
     if dist is not None:
         out["qualhisto_allreduce"] = qs
         dist.destroy_process_group()

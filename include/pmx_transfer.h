@@ -84,8 +84,13 @@ typedef struct {
   int64_t nvol, nbdy;        /* located points by path            */
   int64_t nexhaust;          /* exhaustive searches               */
   int64_t nclosest;          /* not found -> closest element      */
-  int64_t stepmin, stepmax;  /* walk steps                        */
-  double  stepav;
+  int64_t stepmin, stepmax;  /* |steps| over every located point, */
+  double  stepav;            /* exhaustive ones included, as
+                                PMMG_locate_postprocessing (src/locate_pmmg.c:
+                                995-1028); an exhaustive point counts its walk
+                                steps + 1 (the reference adds every tet it
+                                scanned); no point: stepmin = the background's
+                                ne, stepav 0                          */
 } pmx_locate_stats;
 
 /* ---- context ---------------------------------------------------------- */
@@ -136,10 +141,23 @@ typedef struct {
 #define PMX_RUN_NO_INLINE_TIES   0x2  /* every near-face point to the tie BFS */
 #define PMX_RUN_RECORD_STARTS    0x4  /* keep each volume walk's start tet    */
 #define PMX_RUN_SERIAL_SURFACE   0x8  /* surface path on the main stream      */
-#define PMX_RUN_FRESH_BACKGROUND 0x10 /* rebuild the background's derived data
-                                         (grid coordinates, tria normals) as
-                                         the first step after an upload does:
-                                         one ParMmg iteration per step        */
+#define PMX_RUN_FRESH_BACKGROUND 0x10 /* redo every device pass the uploads
+                                         ran on the raw arrays (derived data,
+                                         fan check, device-built layouts, the
+                                         orphan marks of the new tets): one
+                                         ParMmg iteration per step            */
+#define PMX_RUN_SEQUENTIAL_SURFACE 0x40 /* the reference's SEQUENTIAL surface
+                                         semantics (src/interpmesh_pmmg.c:
+                                         528-599, src/locate_pmmg.c:209-334):
+                                         the boundary points in the vertex
+                                         loop's first-visit order through the
+                                         new tets, each query starting from the
+                                         previous one's tria, the point flags
+                                         of the shadow cone / wedge tests and
+                                         mesh->base carried over.  Needs the new
+                                         tets (points view or
+                                         pmx_upload_new_tets).  Default: every
+                                         query fresh from its hint tria        */
 #define PMX_RUN_DEBUG_BARRIER_TIMEOUT 0x100 /* test hook: the fallback's grid
                                          barriers do not wait (the step must
                                          then fail, never return silently)   */
@@ -178,6 +196,11 @@ int pmx_download_border(pmx_ctx *ctx, int *edge, int *vertex, int64_t cap);
  * interpolation had nothing to locate (src/interpmesh_pmmg.c:497-512). */
 int pmx_step_ready(pmx_ctx *ctx);
 int pmx_locate_stats_get(pmx_ctx *ctx, pmx_locate_stats *st);
+/* After a PMX_RUN_SEQUENTIAL_SURFACE step: the boundary points the reference
+ * would locate (*nseq) and how many of them the device replayed one by one on
+ * the reference's state (*nreplay; the others kept their speculative result:
+ * same start tria as the reference, no shadow-wedge test on the way). */
+int pmx_seq_surface_stats(pmx_ctx *ctx, int64_t *nseq, int64_t *nreplay);
 /* Lane utilisation of the last step's walks (path 0 volume, 1 surface): a
  * wave iterates until its longest walk ends, so step_sum / lane_steps is the
  * fraction of lane-steps that did work.  Over the walk's per-wave records:

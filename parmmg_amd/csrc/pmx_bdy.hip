@@ -46,6 +46,11 @@ struct BdyArgs {
   int64_t nlist;         // upper bound (launch size); the step's count is *nlist_dev
   const int *nlist_dev;
   uint4 *wstats;         // per-wave walk statistics
+  // PMX_RUN_SEQUENTIAL_SURFACE's speculative pass: per point its start tria
+  // and mesh->base (null: the hint tria, ordinal + 1), and whether the walk
+  // ran a shadow-wedge test (the only path to the point flags)
+  const int *seq_start, *seq_base;
+  uint8_t *seq_w;
 };
 
 // thread-private query state: visited trias + point-flag overrides
@@ -71,6 +76,31 @@ struct GlobState {
   __device__ int &OP(int i) { return ovp[i]; }
   __device__ int &OF(int i) { return ovf[i]; }
 };
+// the reference's own state, for the sequential replay (one lane): tria
+// flags tf[] compared with mesh->base, point flags pf[] kept across queries
+// (PF_INIT: still the incident-tria count PMMG_precompute_nodeTrias left)
+#define PF_INIT ((int)0x80808080)
+struct SeqState {
+  int *tf, *pf;
+  int base;
+  bool over = false;
+};
+// (agent-scope accesses: the replaying lane reads back what it wrote in
+// earlier queries, never a stale L1 line)
+__device__ __forceinline__ int ld_flag(const int *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_flag(int *p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool visited(SeqState &s, int t) { return ld_flag(s.tf + t) == s.base; }
+__device__ __forceinline__ void mark_visited(SeqState &s, int t) { st_flag(s.tf + t, s.base); }
+__device__ __forceinline__ int get_flag(SeqState &s, int p, int cnt) {
+  const int f = ld_flag(s.pf + p);
+  return f == PF_INIT ? cnt : f;
+}
+__device__ __forceinline__ void set_flag(SeqState &s, int p, int f) { st_flag(s.pf + p, f); }
+
 template <class St> __device__ __forceinline__ int st_cap(const St &s);
 template <int C> __device__ __forceinline__ int st_cap(const RegState<C> &) { return C; }
 template <> __device__ __forceinline__ int st_cap(const GlobState &s) { return s.capv; }
@@ -367,7 +397,8 @@ __device__ void interp_tria(const BdyArgs &A, int k, const Bary &b, int edge, in
 // returns 1 found, 2 stuck (needs exhaustive), 3 private-state overflow
 template <class St>
 __device__ int walk_bdy(const BdyArgs &A, St &s, D3 p, int start, int base, int &k, Bary &b,
-                        int &edge, int &vtx, int &step) {
+                        int &edge, int &vtx, int &step, bool &wedged) {
+  wedged = false;
   double cdist = 1.0e10;
   int ctria = 0;
   k = start;
@@ -395,6 +426,7 @@ __device__ int walk_bdy(const BdyArgs &A, St &s, D3 p, int start, int base, int 
       if (i == 2) nb = t.nb[2];
       if (!nb) continue;
       if (visited(s, nb)) {
+        wedged = true;
         int il = in_wedge(A, s, k, i, p, base, b);
         if (s.over) return 3;
         if (il == UNSET) continue;
@@ -433,12 +465,15 @@ __global__ __launch_bounds__(256) void k_locate_bdy(BdyArgs A) {
   if (j < *A.nlist_dev) {
     const int64_t i = A.list[j];
     const D3 p = ld3(A.q, (int)i);
-    int start = tria_hint(A, p);
+    const int start = A.seq_start ? A.seq_start[i] : tria_hint(A, p);
+    const int base = A.seq_base ? A.seq_base[i] : (int)(i + 1);
     A.start[i] = start;
     RegState<CAP> s;
     Bary b;
     int k, edge, vtx, step;
-    int r = walk_bdy(A, s, p, start, (int)(i + 1), k, b, edge, vtx, step);
+    bool wedged;
+    int r = walk_bdy(A, s, p, start, base, k, b, edge, vtx, step, wedged);
+    if (A.seq_w) A.seq_w[i] = wedged ? 1 : 0;
     if (r == 1) {
       finish_bdy(A, i, k, b, edge, vtx, 1, step);
       s_cnt = 1; s_sum = (unsigned)step; s_max = (unsigned)step; s_min = (unsigned)step;
@@ -474,7 +509,10 @@ __global__ __launch_bounds__(64) void k_locate_bdy_ovf(BdyArgs A, int *ws, int c
     s.init(ws + (size_t)tid * 3 * cap, cap);
     Bary b;
     int k, edge, vtx, step;
-    int r = walk_bdy(A, s, p, A.start[i], (int)(i + 1), k, b, edge, vtx, step);
+    bool wedged;
+    int r = walk_bdy(A, s, p, A.start[i], A.seq_base ? A.seq_base[i] : (int)(i + 1), k, b, edge, vtx, step,
+                     wedged);
+    if (A.seq_w) A.seq_w[i] = wedged ? 1 : 0;
     if (r == 1) {
       finish_bdy(A, i, k, b, edge, vtx, 1, step);
     } else {
@@ -805,7 +843,15 @@ bool pmx_ctx::check_fans(hipStream_t s) {
   if (e && e[0] == '0') return true;
   // every vertex's tria count (np-sized, at the upload only): a fan walked
   // around one sheet of a vertex where several touch closes short of it
-  if (!pmx_dgrow(this, d_wfar, 8) || !pmx_dgrow(this, d_ntkey, (size_t)(np + 2))) return false;
+  if (!pmx_dgrow(this, d_wfar, 8)) return false;
+  if (!pmx_dgrow(this, d_ntkey, (size_t)(np + 2)) ||
+      !pmx_dgrow(this, d_ntrange, (size_t)(3 * (nt + 1))) || !pmx_dgrow(this, d_ntlist, (size_t)(3 * nt * FAN_CAP))) {
+    // no room for the check or the fan windows (32 per tria corner): the
+    // surface keeps the sort-built fans, the upload goes on
+    (void)hipGetLastError();
+    err.clear();
+    return true;
+  }
   if (hipMemsetAsync(d_wfar.p + 3, 0, sizeof(unsigned), s) != hipSuccess ||
       hipMemsetAsync(d_ntkey.p, 0, (size_t)(np + 2) * sizeof(unsigned), s) != hipSuccess) {
     err = "node trias: memset";
@@ -933,6 +979,31 @@ bool pmx_ctx::size_tria_grid() {
   return true;
 }
 
+// the surface kernels' arguments for the step's points (tria hint grid tgd)
+static BdyArgs bdy_args(pmx_ctx *c, const VolArgs &a) {
+  BdyArgs B{};
+  B.xyz = c->d_xyz.p; B.tris = c->d_tris.p; B.trn = c->d_trn.p; B.ntrange = c->d_ntrange.p; B.ntlist = c->d_ntlist.p;
+  B.sol = c->d_sol.p; B.sd = a.sd; B.q = c->d_qxyz.p; B.kind = c->d_kind.p; B.nq = c->nq; B.nt = c->nt;
+  B.hausd = c->hausd; B.grid = c->d_tgrid; B.g = c->tgd;
+  B.out = c->d_out.p; B.wmask = c->d_wmask.p; B.elem = c->d_elem.p; B.status = c->d_status.p;
+  B.steps = c->d_steps.p; B.start = c->d_start.p; B.edge = c->d_edge.p; B.vertex = c->d_vertex.p;
+  B.stuck_list = c->d_blist.p; B.stuck_count = c->d_counts.p + 1;
+  B.ovf_list = c->d_olist.p; B.ovf_count = c->d_counts.p + 2;
+  B.list = c->d_bdylist.p; B.nlist = c->nq_bdy_ub; B.nlist_dev = c->d_nsel.p + 1; B.wstats = c->d_bstat.p;
+  return B;
+}
+
+// the walks, their private-list overflow pass and the exhaustive scan
+static void launch_bdy_walks(const BdyArgs &B, int *ows, int exp, hipStream_t s) {
+  const int64_t nb = (B.nlist + 255) / 256;
+  if (exp == 10)                         // A/B: the r01-r03 8-entry private lists
+    hipLaunchKernelGGL(k_locate_bdy<BDY_CAP / 2>, dim3((unsigned)nb), dim3(256), 0, s, B);
+  else
+    hipLaunchKernelGGL(k_locate_bdy<BDY_CAP>, dim3((unsigned)nb), dim3(256), 0, s, B);
+  hipLaunchKernelGGL(k_locate_bdy_ovf, dim3(OVF_THREADS / 64), dim3(64), 0, s, B, ows, OVF_CAP);
+  hipLaunchKernelGGL(k_exh_bdy, dim3(256), dim3(256), 0, s, B);
+}
+
 bool pmx_ctx::launch_bdy(const VolArgs &a, hipStream_t s) {
   if (nt < 1) { err = "surface points present but the background has no boundary trias"; return false; }
   if (!d_blist.p || d_blist.cap < (size_t)nq) {
@@ -948,9 +1019,8 @@ bool pmx_ctx::launch_bdy(const VolArgs &a, hipStream_t s) {
     d_ows.cap = (size_t)OVF_THREADS * 3 * OVF_CAP;
   }
   // tria hint grid: sized and allocated with the background
-  // (pmx_ctx::size_tria_grid), zeroed by the step's prologue kernel
-  const GridDesc tg = tgd;
-  // zeroed and built at the head of the surface path (off the main stream)
+  // (pmx_ctx::size_tria_grid), zeroed and built at the head of the surface
+  // path (off the main stream)
   if (hipMemsetAsync(d_tgrid, 0, sizeof(int) * (size_t)tcells, s) != hipSuccess) {
     err = "tria hint grid memset";
     return false;
@@ -959,23 +1029,273 @@ bool pmx_ctx::launch_bdy(const VolArgs &a, hipStream_t s) {
     int64_t nb = (nt + 255) / 256;
     if (nb > 4096) nb = 4096;
     hipLaunchKernelGGL(k_tria_hint_build, dim3((unsigned)std::max<int64_t>(nb, 1)), dim3(256), 0, s,
-                       d_tris.p, d_xyz.p, nt, d_tgrid, tg);
+                       d_tris.p, d_xyz.p, nt, d_tgrid, tgd);
   }
-  BdyArgs B{};
-  B.xyz = d_xyz.p; B.tris = d_tris.p; B.trn = d_trn.p; B.ntrange = d_ntrange.p; B.ntlist = d_ntlist.p;
-  B.sol = d_sol.p; B.sd = a.sd; B.q = d_qxyz.p; B.kind = d_kind.p; B.nq = nq; B.nt = nt;
-  B.hausd = hausd; B.grid = d_tgrid; B.g = tg;
-  B.out = d_out.p; B.wmask = d_wmask.p; B.elem = d_elem.p; B.status = d_status.p;
-  B.steps = d_steps.p; B.start = d_start.p; B.edge = d_edge.p; B.vertex = d_vertex.p;
-  B.stuck_list = d_blist.p; B.stuck_count = d_counts.p + 1;
-  B.ovf_list = d_olist.p; B.ovf_count = d_counts.p + 2;
-  B.list = d_bdylist.p; B.nlist = nq_bdy_ub; B.nlist_dev = d_nsel.p + 1; B.wstats = d_bstat.p;
-  int64_t nb = (nq_bdy_ub + 255) / 256;
-  if (a.exp == 10)                         // A/B: the r01-r03 8-entry private lists
-    hipLaunchKernelGGL(k_locate_bdy<BDY_CAP / 2>, dim3((unsigned)nb), dim3(256), 0, s, B);
-  else
-    hipLaunchKernelGGL(k_locate_bdy<BDY_CAP>, dim3((unsigned)nb), dim3(256), 0, s, B);
-  hipLaunchKernelGGL(k_locate_bdy_ovf, dim3(OVF_THREADS / 64), dim3(64), 0, s, B, d_ows.p, OVF_CAP);
-  hipLaunchKernelGGL(k_exh_bdy, dim3(256), dim3(256), 0, s, B);
+  launch_bdy_walks(bdy_args(this, a), d_ows.p, a.exp, s);
+  return hipGetLastError() == hipSuccess;
+}
+
+// ---- PMX_RUN_SEQUENTIAL_SURFACE ---------------------------------------------
+//
+// The reference runs the surface queries one after the other
+// (src/interpmesh_pmmg.c:535-599): in the vertex loop's first-visit order
+// through the new tets, each PMMG_locatePointBdy starting from the previous
+// one's tria (ifoundTria, :529/:556), with mesh->base counting every locate
+// (volume and surface, :521, src/locate_pmmg.c:607/805) and the point flags
+// of the shadow tests kept from query to query (PMMG_locatePointInCone marks
+// the apex with the base and its scanned neighbours with the apex index, and
+// skips a neighbour already marked with it, src/locate_pmmg.c:219,247-249;
+// PMMG_locatePointInWedge marks an edge end, :318-323).  A query reads those
+// flags only through a wedge test (a walk that meets an already visited
+// tria, :640-660).  On the device:
+//  1. first-visit keys 4 k + l of every point (k_seq_keys), sorted: the visit
+//     order; a scan gives each located point its mesh->base and each
+//     surface point its position in the surface sequence;
+//  2. a speculative pass of every surface query (the step's walks) starting
+//     from the device-semantics result of its predecessor, with its
+//     reference base; it records whether the walk ran a wedge test;
+//  3. one wavefront replays the sequence (k_seq_resolve): a query whose
+//     speculative start is the true one (the previous query's true tria) and
+//     whose walk never met the shadow tests keeps its speculative result --
+//     it read no carried state; any other is run again by one lane on the
+//     reference's own state (tria flags vs base, point flags kept across
+//     queries), in order.  A replayed walk that ends stuck hands its point to
+//     the exhaustive scan (k_exh_bdy, one launch from the host) and the
+//     replay resumes after it.
+
+// the first visit of every new point by the reference's vertex loop: key
+// 4 k + l over the valid tets that hold it (atomicMin).  A lane skips the
+// vertices its left neighbour (the previous tet) holds: that tet's keys are
+// smaller, so the run's leftmost lane gives the minimum (as k_mark_new_tets)
+__global__ __launch_bounds__(256) void k_seq_keys(const int4 *__restrict__ tv, int64_t ne,
+                                                  unsigned *__restrict__ key) {
+  const int64_t st = (int64_t)gridDim.x * blockDim.x;
+  const int64_t nit = (ne + st - 1) / st;
+  const bool lane0 = (threadIdx.x & 63) == 0;
+  for (int64_t it = 0; it < nit; it++) {
+    const int64_t k = 1 + it * st + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int4 a = k <= ne ? tv[k] : make_int4(0, 0, 0, 0);
+    int4 u;
+    u.x = __shfl_up(a.x, 1, 64); u.y = __shfl_up(a.y, 1, 64);
+    u.z = __shfl_up(a.z, 1, 64); u.w = __shfl_up(a.w, 1, 64);
+    if (lane0 || u.x <= 0) u = make_int4(0, 0, 0, 0);
+    if (a.x <= 0) continue;
+    const int w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int l = 0; l < 4; l++) {
+      const int q = w[l];
+      if (q != u.x && q != u.y && q != u.z && q != u.w) atomicMin(key + (q - 1), (unsigned)(4 * k + l));
+    }
+  }
+}
+// idx[i] = i; the speculative start (1) and base (0) of every point: a
+// surface point the loop never reaches (an orphan, located by a step without
+// the marks and reset afterwards) walks from tria 1
+__global__ __launch_bounds__(256) void k_seq_iota(int *__restrict__ idx, int *__restrict__ sstart,
+                                                  int *__restrict__ sbase, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    idx[i] = (int)i;
+    sstart[i] = 1;
+    sbase[i] = 0;
+  }
+}
+// per visit-order rank: located (a volume or surface point the loop reaches:
+// not NUL, not frozen) in the low word, surface in the high word
+__global__ __launch_bounds__(256) void k_seq_flags(const unsigned *__restrict__ skey, const int *__restrict__ sidx,
+                                                   const int8_t *__restrict__ kind, int64_t n,
+                                                   unsigned long long *__restrict__ val) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const int8_t kd = kind[sidx[r]];
+    const bool loc = skey[r] != 0xffffffffu && (kd == KIND_VOL || kd == KIND_BDY);
+    val[r] = (unsigned long long)(loc ? 1u : 0u) | ((unsigned long long)(loc && kd == KIND_BDY ? 1u : 0u) << 32);
+  }
+}
+// mesh->base of each located point (1 + the locates before it) and the
+// surface sequence; its length into *nseq
+__global__ __launch_bounds__(256) void k_seq_assign(const int *__restrict__ sidx,
+                                                    const unsigned long long *__restrict__ val,
+                                                    const unsigned long long *__restrict__ pre, int64_t n,
+                                                    int *__restrict__ base, int *__restrict__ seq,
+                                                    int *__restrict__ nseq) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long v = val[r], q = pre[r];
+    if (v & 1ull) {
+      const int i = sidx[r];
+      base[i] = (int)(q & 0xffffffffull) + 1;
+      if (v >> 32) seq[q >> 32] = i;
+    }
+    if (r == n - 1) *nseq = (int)((q + v) >> 32);
+  }
+}
+// the speculative start of every surface query: its predecessor's tria from
+// the step's (device-semantics) pass; the first query starts at tria 1 (:529)
+__global__ __launch_bounds__(256) void k_seq_starts(const int *__restrict__ seq, const int *__restrict__ nseq,
+                                                    const int *__restrict__ elem, int *__restrict__ sstart) {
+  const int n = *nseq;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x)
+    sstart[seq[j]] = j ? elem[seq[j - 1]] : 1;
+}
+
+// the replay: one wavefront.  ctl = {next position, start tria of it (-1: the
+// tria of the previous query, written by the exhaustive scan), state (0 done,
+// 1 stuck: the host scans), stuck point}.  Tria / point flags through
+// agent-scope accesses (the lane re-reads what it wrote in earlier queries).
+__global__ __launch_bounds__(64) void k_seq_resolve(BdyArgs A, const int *__restrict__ seq,
+                                                    const int *__restrict__ nseq_p, const int *__restrict__ sstart,
+                                                    const uint8_t *__restrict__ sw, const int *__restrict__ sbase,
+                                                    int *tf, int *pf, int *ctl, int *stk_list,
+                                                    unsigned *stk_count, unsigned *nreplay) {
+  const int lane = threadIdx.x;
+  const int nseq = *nseq_p;
+  int j = ctl[0];
+  int prev = ctl[1];
+  if (j >= nseq) return;
+  if (prev < 0) prev = A.elem[seq[j - 1]];
+  unsigned replays = 0;
+  while (j < nseq) {
+    const int jj = j + lane;
+    bool okk = false;
+    if (jj < nseq) {
+      const int i = seq[jj];
+      const int want = lane == 0 ? prev : A.elem[seq[jj - 1]];
+      okk = !sw[i] && sstart[i] == want;
+    }
+    const int nvalid = min(64, nseq - j);
+    const unsigned long long mask = nvalid == 64 ? ~0ull : ((1ull << nvalid) - 1ull);
+    const unsigned long long bad = ~__ballot(okk) & mask;
+    if (!bad) {                                  // the whole block keeps its speculative results
+      prev = A.elem[seq[j + nvalid - 1]];
+      j += nvalid;
+      continue;
+    }
+    const int f = __ffsll((long long)bad) - 1;
+    if (f > 0) prev = A.elem[seq[j + f - 1]];
+    j += f;
+    int r = 1, nk = 0;
+    if (lane == 0) {
+      const int i = seq[j];
+      const D3 p = ld3(A.q, i);
+      SeqState st{tf, pf, sbase[i]};
+      Bary b;
+      int k, edge, vtx, step;
+      bool wedged;
+      A.start[i] = prev;
+      r = walk_bdy(A, st, p, prev, sbase[i], k, b, edge, vtx, step, wedged);
+      replays++;
+      if (r == 1) {
+        finish_bdy(A, i, k, b, edge, vtx, 1, step);
+        nk = k;
+      } else {
+        A.steps[i] = -step;
+        stk_list[0] = i;
+        *stk_count = 1u;
+        ctl[0] = j;
+        ctl[2] = 1;
+        ctl[3] = i;
+      }
+    }
+    r = __shfl(r, 0, 64);
+    nk = __shfl(nk, 0, 64);
+    if (r != 1) {
+      if (lane == 0) atomicAdd(nreplay, replays);
+      return;
+    }
+    prev = nk;
+    j++;
+  }
+  if (lane == 0) {
+    ctl[0] = nseq;
+    ctl[2] = 0;
+    atomicAdd(nreplay, replays);
+  }
+}
+
+bool pmx_ctx::seq_surface(const VolArgs &a, hipStream_t s) {
+  pmx_ctx *ctx = this;
+  auto ck = [&](hipError_t e, const char *what) {
+    if (e == hipSuccess) return true;
+    ctx->err = std::string("sequential surface: ") + what + ": " + hipGetErrorString(e);
+    return false;
+  };
+  if (!have_ntet) {
+    err = "PMX_RUN_SEQUENTIAL_SURFACE: the first-visit order needs the new tets (points view or pmx_upload_new_tets)";
+    return false;
+  }
+  if (nq_bdy_ub < 1 || nq < 1) return true;
+  if (!ensure_tets(s)) return false;
+  const int64_t n = nq;
+  size_t sort_b = 0, scan_b = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, sort_b, (const unsigned *)nullptr, (unsigned *)nullptr,
+                                     (const int *)nullptr, (int *)nullptr, (int)n, 0, 32, s);
+  hipcub::DeviceScan::ExclusiveSum(nullptr, scan_b, (const unsigned long long *)nullptr,
+                                   (unsigned long long *)nullptr, (int)n, s);
+  if (!pmx_dgrow(this, d_sqkey, (size_t)(2 * n)) || !pmx_dgrow(this, d_sqidx, (size_t)(2 * n)) ||
+      !pmx_dgrow(this, d_sqval, (size_t)(2 * n)) || !pmx_dgrow(this, d_sqint, (size_t)(3 * n + 8)) ||
+      !pmx_dgrow(this, d_sqw, (size_t)n) || !pmx_dgrow(this, d_sqtmp, std::max(sort_b, scan_b)) ||
+      !pmx_dgrow(this, d_sqtf, (size_t)(nt + 1)) || !pmx_dgrow(this, d_sqpf, (size_t)(np + 1)))
+    return false;
+  unsigned *key = d_sqkey.p, *key2 = d_sqkey.p + n;
+  int *idx = d_sqidx.p, *idx2 = d_sqidx.p + n;
+  unsigned long long *val = d_sqval.p, *pre = d_sqval.p + n;
+  int *sbase = d_sqint.p, *seq = d_sqint.p + n, *sstart = d_sqint.p + 2 * n, *ctl = d_sqint.p + 3 * n;
+  int *nseq = ctl + 4;
+  unsigned *stk_count = (unsigned *)(ctl + 5), *nreplay = (unsigned *)(ctl + 6);
+  int *stk_list = ctl + 7;
+  const unsigned nbt = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n_ntet + 255) / 256, 8192));
+  const unsigned nbp = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
+  // 1. visit order, bases, sequence
+  if (!ck(hipMemsetAsync(key, 0xff, (size_t)n * sizeof(unsigned), s), "memset")) return false;
+  hipLaunchKernelGGL(k_seq_keys, dim3(nbt), dim3(256), 0, s, (const int4 *)d_ntetv.p, n_ntet, key);
+  hipLaunchKernelGGL(k_seq_iota, dim3(nbp), dim3(256), 0, s, idx, sstart, sbase, n);
+  if (!ck(hipcub::DeviceRadixSort::SortPairs(d_sqtmp.p, sort_b, (const unsigned *)key, key2, (const int *)idx, idx2,
+                                            (int)n, 0, 32, s), "sort"))
+    return false;
+  hipLaunchKernelGGL(k_seq_flags, dim3(nbp), dim3(256), 0, s, (const unsigned *)key2, (const int *)idx2,
+                     (const int8_t *)d_kind.p, n, val);
+  if (!ck(hipcub::DeviceScan::ExclusiveSum(d_sqtmp.p, scan_b, (const unsigned long long *)val, pre, (int)n, s),
+          "scan"))
+    return false;
+  hipLaunchKernelGGL(k_seq_assign, dim3(nbp), dim3(256), 0, s, (const int *)idx2, (const unsigned long long *)val,
+                     (const unsigned long long *)pre, n, sbase, seq, nseq);
+  // 2. the speculative pass
+  hipLaunchKernelGGL(k_seq_starts, dim3(nbp), dim3(256), 0, s, (const int *)seq, (const int *)nseq,
+                     (const int *)d_elem.p, sstart);
+  if (!ck(hipMemsetAsync(d_counts.p + 1, 0, 2 * sizeof(unsigned), s), "memset")) return false;
+  BdyArgs B = bdy_args(this, a);
+  B.seq_start = sstart;
+  B.seq_base = sbase;
+  B.seq_w = d_sqw.p;
+  launch_bdy_walks(B, d_ows.p, a.exp, s);
+  // 3. the replay, on the reference's state
+  if (!ck(hipMemsetAsync(d_sqtf.p, 0, (size_t)(nt + 1) * sizeof(int), s), "memset") ||
+      !ck(hipMemsetAsync(d_sqpf.p, 0x80, (size_t)(np + 1) * sizeof(int), s), "memset"))
+    return false;
+  int hctl[4] = {0, 1, 0, 0};
+  unsigned zero = 0;
+  if (!ck(hipMemcpyAsync(ctl, hctl, sizeof hctl, hipMemcpyHostToDevice, s), "ctl") ||
+      !ck(hipMemcpyAsync(nreplay, &zero, sizeof zero, hipMemcpyHostToDevice, s), "ctl"))
+    return false;
+  BdyArgs X = B;
+  X.stuck_list = stk_list;
+  X.stuck_count = stk_count;
+  for (int64_t round = 0;; round++) {
+    hipLaunchKernelGGL(k_seq_resolve, dim3(1), dim3(64), 0, s, B, (const int *)seq, (const int *)nseq,
+                       (const int *)sstart, (const uint8_t *)d_sqw.p, (const int *)sbase, d_sqtf.p, d_sqpf.p, ctl,
+                       stk_list, stk_count, nreplay);
+    if (!ck(hipMemcpyAsync(hctl, ctl, sizeof hctl, hipMemcpyDeviceToHost, s), "ctl") ||
+        !ck(hipStreamSynchronize(s), "sync"))
+      return false;
+    if (hctl[2] == 0) break;
+    // a replayed query ended stuck: the exhaustive scan of that one point
+    hipLaunchKernelGGL(k_exh_bdy, dim3(1), dim3(256), 0, s, X);
+    hctl[0] += 1;
+    hctl[1] = -1;
+    hctl[2] = 0;
+    if (!ck(hipMemcpyAsync(ctl, hctl, sizeof hctl, hipMemcpyHostToDevice, s), "ctl")) return false;
+  }
+  if (!ck(hipMemcpyAsync(&seq_stats[0], nreplay, sizeof(unsigned), hipMemcpyDeviceToHost, s), "stats") ||
+      !ck(hipMemcpyAsync(&seq_stats[1], nseq, sizeof(int), hipMemcpyDeviceToHost, s), "stats") ||
+      !ck(hipStreamSynchronize(s), "sync"))
+    return false;
   return hipGetLastError() == hipSuccess;
 }

@@ -1117,7 +1117,7 @@ static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &o
 static bool run_flags_valid(int flags, std::string *err) {
   const int pub = PMX_RUN_REFERENCE_WALK | PMX_RUN_NO_INLINE_TIES | PMX_RUN_RECORD_STARTS |
                   PMX_RUN_SERIAL_SURFACE | PMX_RUN_FRESH_BACKGROUND | PMX_RUN_DEBUG_BARRIER_TIMEOUT |
-                  PMX_RUN_EAGER_DOWNLOAD;
+                  PMX_RUN_EAGER_DOWNLOAD | PMX_RUN_SEQUENTIAL_SURFACE;
   if (flags & ~(pub | (0xff << PMX_RUN_EXP_SHIFT))) {
     *err = "pmx_run: unknown flag bits";
     return false;
@@ -1249,10 +1249,14 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
                       exp == 16, exp == 21 ? 1024 : exp == 22 ? 64 : 256,
                       packed && ctx->samples_owner ? ctx->nsamp : -1);
   };
-  const bool hint_first = marks && any_interp && exp != 23;   // exp 23 (A/B): the r05 order
+  // exp 23 (A/B): the marks beside the walk instead -- the points
+  // classified without them, the orphans located and their rows reset at the
+  // end of the step (k_orphans), the r05 order of the hint build
+  const bool marks_late = marks && exp == 23;
+  const bool hint_first = marks && !marks_late && any_interp;
   if (hint_first) hint_build();
-  if (marks) CK(hipStreamWaitEvent(st, ctx->ev_tets, 0));
-  if (!ctx->classify(st, marks)) return 0;
+  if (marks && !marks_late) CK(hipStreamWaitEvent(st, ctx->ev_tets, 0));
+  if (!ctx->classify(st, marks && !marks_late)) return 0;
   if (sd.metric_const)
     launch_const_metric(ctx->d_kind.p, n, ctx->d_out.p, S, sd.off[sd.imet], sd.size[sd.imet],
                         opts.hsiz, ctx->d_wmask.p, sd.imet, st);
@@ -1298,6 +1302,11 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     } else if (ev) {
       CK(hipEventRecord(ev[5], st));
     }
+    ctx->seq_stats_n = -1;
+    if (bdy && (opts.flags & PMX_RUN_SEQUENTIAL_SURFACE)) {
+      if (!ctx->seq_surface(A, st)) return 0;
+      ctx->seq_stats_n = 1;
+    }
     if (ev) CK(hipEventRecord(ev[6], st));
     ExhArgs E{};
     E.xyz = ctx->d_xyz.p; E.tets = ctx->d_tets.p; E.ne = ctx->ne; E.q = ctx->d_qxyz.p;
@@ -1312,6 +1321,12 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
       ctx->fallback_share = share;
     }
     if (ctx->nq_vol_ub) launch_exhaustive(E, A, ctx->fallback_blocks, st);
+    if (marks_late) {
+      CK(hipStreamWaitEvent(st, ctx->ev_tets, 0));
+      OrphanRows rr{ctx->d_wmask.p, ctx->d_elem.p, ctx->d_status.p, ctx->d_steps.p, ctx->d_start.p,
+                    ctx->d_edge.p, ctx->d_vertex.p, ctx->d_kind.p};
+      launch_orphans(ctx->d_qmark.p, n, (uint8_t)(sd.metric_const ? (1u << sd.imet) : 0u), rr, st);
+    }
     if (ev) CK(hipEventRecord(ev[4], st));
   } else if (ev) {
     for (int k = 1; k < PMX_EV_PER_RUN; k++)
@@ -1560,24 +1575,27 @@ int pmx_locate_stats_get(pmx_ctx *ctx, pmx_locate_stats *st) {
     CK(hipMemcpy(steps.data(), ctx->d_steps.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
     CK(hipMemcpy(kind.data(), ctx->d_kind.p, (size_t)n, hipMemcpyDeviceToHost));
   }
+  // PMMG_locate_postprocessing (src/locate_pmmg.c:995-1028): |steps| of every
+  // visited point, the exhaustive ones (steps < 0) included, min / max / mean
   memset(st, 0, sizeof *st);
-  int64_t located = 0, sum = 0, mx = 0, mn = INT64_MAX;
+  int64_t located = 0, sum = 0, mx = 0, mn = ctx->ne;
   for (int64_t i = 0; i < n; i++) {
     const int8_t k = kind[(size_t)i];
     if (k != KIND_VOL && k != KIND_BDY) continue;
     (k == KIND_VOL ? st->nvol : st->nbdy)++;
-    const int s = steps[(size_t)i];
-    if (s < 0) st->nexhaust++;
-    if (status[(size_t)i] == 0) st->nclosest++;
-    if (s > 0) {
-      located++;
-      sum += s;
-      mx = std::max<int64_t>(mx, s);
-      mn = std::min<int64_t>(mn, s);
+    int64_t s = steps[(size_t)i];
+    if (s < 0) {
+      st->nexhaust++;
+      s = -s;
     }
+    if (status[(size_t)i] == 0) st->nclosest++;
+    located++;
+    sum += s;
+    mx = std::max<int64_t>(mx, s);
+    mn = std::min<int64_t>(mn, s);
   }
   st->stepmax = mx;
-  st->stepmin = located ? mn : 0;
+  st->stepmin = mn;
   st->stepav = located ? (double)sum / (double)located : 0.0;
   return 1;
 }
@@ -1607,6 +1625,17 @@ int pmx_locate_wave_stats(pmx_ctx *ctx, int path, pmx_wave_stats *st) {
     st->lane_steps += 64 * (int64_t)r.z;
     st->wave_max_hist[std::min<unsigned>(r.z, 15u)]++;
   }
+  return 1;
+}
+
+int pmx_seq_surface_stats(pmx_ctx *ctx, int64_t *nseq, int64_t *nreplay) {
+  if (!ctx || !nseq || !nreplay) return 0;
+  if (ctx->seq_stats_n < 0 || !ctx->ran) {
+    ctx->err = "pmx_seq_surface_stats: the last step did not run PMX_RUN_SEQUENTIAL_SURFACE";
+    return 0;
+  }
+  *nseq = ctx->seq_stats[1];
+  *nreplay = ctx->seq_stats[0];
   return 1;
 }
 
@@ -1720,6 +1749,38 @@ int pmx_set_residency(pmx_ctx *ctx, int on) {
 
 int pmx_upload_new_tets(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, int64_t ne) {
   if (!ctx) return 0;
+  if (!ctx->have_pts) { ctx->err = "pmx_upload_new_tets: upload the new points first"; return 0; }
+  if (!tetra_v || ne < 1 || tetra_stride < 16 || 4 * ne >= (1LL << 31)) {
+    ctx->err = "pmx_upload_new_tets: bad new tets";
+    return 0;
+  }
+  hipSetDevice(ctx->device);
+  const int64_t first = ctx->pts_first, n = ctx->nq;
+  if (ctx->ran && ctx->view_tets) {
+    // the last step took its orphans from the points view's tets (never
+    // located, or located and reset): other tets would need another step.
+    // The same tets are accepted (their pinned copy, packed by that step, is
+    // compared row by row); nothing changes on a refusal.
+    if (ctx->tets_inflight) {
+      CK(hipEventSynchronize(ctx->ev_tets));
+      ctx->tets_inflight = false;
+    }
+    const int4 *old = (const int4 *)ctx->h_tets;
+    bool same = old && !ctx->tets_pending && ne == ctx->tview.ne;
+    const char *tc0 = (const char *)tetra_v;
+    for (int64_t k = 1; same && k <= ne; k++) {
+      const int *v = (const int *)(tc0 + k * tetra_stride);
+      const int4 o = old[k];
+      same = v[0] <= 0 ? o.x == 0
+                       : (o.x == (int)(v[0] - first + 1) && o.y == (int)(v[1] - first + 1) &&
+                          o.z == (int)(v[2] - first + 1) && o.w == (int)(v[3] - first + 1));
+    }
+    if (!same) {
+      ctx->err = "pmx_upload_new_tets: the last step took its orphans from the points view's new tets; "
+                 "other tets need another pmx_run";
+      return 0;
+    }
+  }
   ctx->have_ntet = false;
   if (ctx->next_topo) {                     // built from other tets: drop it
     CK(hipStreamSynchronize(ctx->topo));
@@ -1730,13 +1791,6 @@ int pmx_upload_new_tets(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, 
     CK(hipEventSynchronize(ctx->ev_tets));
     ctx->tets_inflight = false;
   }
-  if (!ctx->have_pts) { ctx->err = "pmx_upload_new_tets: upload the new points first"; return 0; }
-  if (!tetra_v || ne < 1 || tetra_stride < 16 || 4 * ne >= (1LL << 31)) {
-    ctx->err = "pmx_upload_new_tets: bad new tets";
-    return 0;
-  }
-  hipSetDevice(ctx->device);
-  const int64_t first = ctx->pts_first, n = ctx->nq;
   // packed into the pinned copy of the new tets (a strided quality output
   // reads their validity there)
   int4 *h = ctx->grow_htets(ne);
@@ -1986,6 +2040,8 @@ void pmx_ctx::free_all() {
   dfree(d_steps); dfree(d_start); dfree(d_edge); dfree(d_vertex); dfree(d_list); dfree(d_found);
   dfree(d_bestk); dfree(d_best); dfree(d_ties); dfree(d_counts); dfree(d_vollist); dfree(d_bdylist);
   dfree(d_vstat); dfree(d_bstat); dfree(d_hrec);
+  dfree(d_sqkey); dfree(d_sqidx); dfree(d_sqint); dfree(d_sqtf); dfree(d_sqpf); dfree(d_sqval); dfree(d_sqw);
+  dfree(d_sqtmp);
   dfree(d_qual); dfree(d_red); dfree(d_blist); dfree(d_olist); dfree(d_ows);
   dfree(d_ptag); dfree(d_touch); dfree(d_cidx); dfree(d_intv); dfree(d_pub); dfree(d_pkey);
   dfree(d_ppt); dfree(d_pedge); dfree(d_ntetv); dfree(d_nqual); dfree(d_qtag); dfree(d_gather);

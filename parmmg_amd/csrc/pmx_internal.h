@@ -115,6 +115,17 @@ struct pmx_ctx {
   DevBuf<uint4> d_vstat, d_bstat;       // per-wave walk statistics
   DevBuf<uint4> d_hrec;                 // exp 13: hint cells with their start record inline
   DevBuf<int> d_blist, d_olist, d_ows;
+  // PMX_RUN_SEQUENTIAL_SURFACE (pmx_bdy.hip seq_surface): visit keys / order,
+  // located / surface flags and their scan, bases | sequence | speculative
+  // starts | control words, wedge flags, cub scratch, the replay's tria and
+  // point flags; seq_stats = {replayed queries, surface sequence length}
+  DevBuf<unsigned> d_sqkey;
+  DevBuf<int> d_sqidx, d_sqint, d_sqtf, d_sqpf;
+  DevBuf<unsigned long long> d_sqval;
+  DevBuf<uint8_t> d_sqw;
+  DevBuf<char> d_sqtmp;
+  unsigned seq_stats[2] = {0, 0};
+  int64_t seq_stats_n = -1;             // -1: the last step was not sequential
   int *d_tgrid = nullptr;
   size_t d_tgrid_cap = 0;
   GridDesc tgd{};
@@ -230,6 +241,10 @@ struct pmx_ctx {
   // (d_qmark) classify points in no valid new tet as KIND_ORPH
   bool classify(hipStream_t s, bool marks = false);
   bool launch_bdy(const VolArgs &a, hipStream_t s);
+  // PMX_RUN_SEQUENTIAL_SURFACE after the step's surface pass, on stream s
+  // (synchronises the host: a replayed query that ends stuck is scanned by a
+  // launch of its own)
+  bool seq_surface(const VolArgs &a, hipStream_t s);
   bool size_tria_grid();
   bool pack_new_tets();                   // the pending new tets: pack, send on `up`, residency build
   bool ensure_tets(hipStream_t s);        // d_ntetv valid for work on stream s

@@ -228,6 +228,13 @@ class Transfer:
         self._chk(self.lib.pmx_locate_stats_get(self.ctx, C.byref(st)), "pmx_locate_stats_get")
         return {f: getattr(st, f) for f, _ in N.LocateStats._fields_}
 
+    def seq_surface_stats(self) -> dict:
+        """After a RUN_SEQUENTIAL_SURFACE step: the surface sequence length and
+        the queries replayed one by one on the reference's state."""
+        a, b = C.c_int64(), C.c_int64()
+        self._chk(self.lib.pmx_seq_surface_stats(self.ctx, C.byref(a), C.byref(b)), "pmx_seq_surface_stats")
+        return {"nseq": a.value, "nreplay": b.value}
+
     def wave_stats(self, path: int = 0) -> dict:
         """Lane utilisation of the last step's walks (path 0 volume, 1 surface):
         step_sum / lane_steps, lane_steps = sum over waves of 64 x the wave's

@@ -23,6 +23,7 @@ import pytest
 import bench
 from helpers import bits_equal, compare_exact, compare_volume, first_visit_order, lin_field
 from oracle import oracle as O
+from parmmg_amd import _native as N
 from parmmg_amd import mesh as M
 from parmmg_amd.transfer import Transfer
 
@@ -81,8 +82,18 @@ def test_full_size_parity(cfg):
     got = []
     for tr in trs:
         got.append((tr.download(), tr.starts(), tr.border(), tr.locate_stats()))
+    # the reference's sequential surface semantics (PMX_RUN_SEQUENTIAL_SURFACE)
+    seqr = []
+    for tr in trs:
+        import time
+        t0 = time.perf_counter()
+        tr.run(flags=N.RUN_SEQUENTIAL_SURFACE)
+        tr.synchronize()
+        dt = time.perf_counter() - t0
+        seqr.append((tr.download(), tr.border(), tr.seq_surface_stats(), dt))
         tr.close()
-    for g, ((m, x, t, sols, tv), s2, (r, starts, (edge, vert), st)) in enumerate(zip(cases, sols2, got)):
+    for g, ((m, x, t, sols, tv), s2, (r, starts, (edge, vert), st), (rq, (sqe, sqv), sst, sdt)) in enumerate(
+            zip(cases, sols2, got, seqr)):
         o = O.Oracle(m)
         vol = np.nonzero(t == 0)[0]
         bdy = np.nonzero(t == M.TAG_BDY)[0]
@@ -96,6 +107,12 @@ def test_full_size_parity(cfg):
               f"{c['ties']} ties")
         assert c["same"] >= c["nvol"] - max(3, c["nvol"] // 1000)
         assert np.all(r.status[vol] == 1)
+        # surface, the sequential mode: every surface point bit-exact against the
+        # reference's sequential run
+        compare_exact((rq.sols, rq.elem, rq.status, sqe, sqv), (qo, qe, qs, qed, qve), bdy, len(s2))
+        print(f"{cfg} group {g}: sequential surface mode: {len(bdy)} points bit-exact vs the sequential "
+              f"run, {sst['nreplay']} replayed on the reference's state, step {sdt * 1e3:.1f} ms")
+        assert sst["nseq"] == len(bdy)
         # surface, device semantics (each query from the device's start tria, the
         # point flags as PMMG_precompute_nodeTrias leaves them): every surface point
         sample = bdy

@@ -3,8 +3,8 @@
 oracle (the CPU restatement of the reference algorithm).
 
 These are regression vectors of the restatement, NOT pins against the
-reference: the reference ships no golden vectors for this path and cannot be
-built here (see DESIGN.md "Oracle").  Re-run after an intentional oracle
+reference: the reference ships no golden vectors for this path and compiles
+here only against stand-in Mmg headers (see DESIGN.md "Oracle").  Re-run after an intentional oracle
 change:  python tools/make_golden.py
 """
 import os

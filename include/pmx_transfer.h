@@ -158,6 +158,17 @@ typedef struct {
                                          tets (points view or
                                          pmx_upload_new_tets).  Default: every
                                          query fresh from its hint tria        */
+#define PMX_RUN_SEQUENTIAL_VOLUME 0x80 /* the reference's sequential volume
+                                         walk (src/locate_pmmg.c:786-883 from
+                                         the previous volume point's tet,
+                                         src/interpmesh_pmmg.c:529,606): ties
+                                         resolved by the reference's own path,
+                                         a walk into a deleted tet returning
+                                         the closest tet it visited.  Needs
+                                         the new tets.  Default: the canonical
+                                         (smallest-index) tet of a tie, and
+                                         the exhaustive scan after a deleted
+                                         tet                                  */
 #define PMX_RUN_DEBUG_BARRIER_TIMEOUT 0x100 /* test hook: the fallback's grid
                                          barriers do not wait (the step must
                                          then fail, never return silently)   */
@@ -201,6 +212,8 @@ int pmx_locate_stats_get(pmx_ctx *ctx, pmx_locate_stats *st);
  * the reference's state (*nreplay; the others kept their speculative result:
  * same start tria as the reference, no shadow-wedge test on the way). */
 int pmx_seq_surface_stats(pmx_ctx *ctx, int64_t *nseq, int64_t *nreplay);
+/* The same for the volume points of a PMX_RUN_SEQUENTIAL_VOLUME step. */
+int pmx_seq_volume_stats(pmx_ctx *ctx, int64_t *nseq, int64_t *nreplay);
 /* Lane utilisation of the last step's walks (path 0 volume, 1 surface): a
  * wave iterates until its longest walk ends, so step_sum / lane_steps is the
  * fraction of lane-steps that did work.  Over the walk's per-wave records:

@@ -69,6 +69,7 @@ RUN_FRESH_BACKGROUND = 0x10
 RUN_DEBUG_BARRIER_TIMEOUT = 0x100
 RUN_EAGER_DOWNLOAD = 0x20
 RUN_SEQUENTIAL_SURFACE = 0x40
+RUN_SEQUENTIAL_VOLUME = 0x80
 
 
 class Group(C.Structure):
@@ -158,6 +159,7 @@ SIGNATURES = {
     "pmx_locate_stats_get": (C.c_int, [C.c_void_p, C.POINTER(LocateStats)]),
     "pmx_locate_wave_stats": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(WaveStats)]),
     "pmx_seq_surface_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "pmx_seq_volume_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "pmx_device_buffer": (C.c_void_p, [C.c_void_p, C.c_int]),
     "pmx_device_alloc": (C.c_void_p, [C.c_void_p, C.c_size_t]),
     "pmx_device_free": (C.c_int, [C.c_void_p, C.c_void_p]),

@@ -1110,21 +1110,27 @@ __global__ __launch_bounds__(256) void k_seq_flags(const unsigned *__restrict__ 
     val[r] = (unsigned long long)(loc ? 1u : 0u) | ((unsigned long long)(loc && kd == KIND_BDY ? 1u : 0u) << 32);
   }
 }
-// mesh->base of each located point (1 + the locates before it) and the
-// surface sequence; its length into *nseq
+// mesh->base of each located point (1 + the locates before it), the surface
+// and the volume sequences; their lengths into nseq[0] / nseq[1]
 __global__ __launch_bounds__(256) void k_seq_assign(const int *__restrict__ sidx,
                                                     const unsigned long long *__restrict__ val,
                                                     const unsigned long long *__restrict__ pre, int64_t n,
                                                     int *__restrict__ base, int *__restrict__ seq,
-                                                    int *__restrict__ nseq) {
+                                                    int *__restrict__ vseq, int *__restrict__ nseq) {
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
     const unsigned long long v = val[r], q = pre[r];
+    const unsigned located = (unsigned)(q & 0xffffffffull), bdy = (unsigned)(q >> 32);
     if (v & 1ull) {
       const int i = sidx[r];
-      base[i] = (int)(q & 0xffffffffull) + 1;
-      if (v >> 32) seq[q >> 32] = i;
+      base[i] = (int)located + 1;
+      if (v >> 32) seq[bdy] = i;
+      else vseq[located - bdy] = i;
     }
-    if (r == n - 1) *nseq = (int)((q + v) >> 32);
+    if (r == n - 1) {
+      const unsigned long long e = q + v;
+      nseq[0] = (int)(e >> 32);
+      nseq[1] = (int)((e & 0xffffffffull) - (e >> 32));
+    }
   }
 }
 // the speculative start of every surface query: its predecessor's tria from
@@ -1210,18 +1216,20 @@ __global__ __launch_bounds__(64) void k_seq_resolve(BdyArgs A, const int *__rest
   }
 }
 
-bool pmx_ctx::seq_surface(const VolArgs &a, hipStream_t s) {
+bool pmx_ctx::seq_replay(const VolArgs &a, hipStream_t s, bool surf, bool vol) {
   pmx_ctx *ctx = this;
   auto ck = [&](hipError_t e, const char *what) {
     if (e == hipSuccess) return true;
-    ctx->err = std::string("sequential surface: ") + what + ": " + hipGetErrorString(e);
+    ctx->err = std::string("sequential replay: ") + what + ": " + hipGetErrorString(e);
     return false;
   };
+  seq_stats[0] = seq_stats[1] = seq_stats[2] = seq_stats[3] = 0;
+  if (!surf && !vol) return true;
   if (!have_ntet) {
-    err = "PMX_RUN_SEQUENTIAL_SURFACE: the first-visit order needs the new tets (points view or pmx_upload_new_tets)";
+    err = "PMX_RUN_SEQUENTIAL_*: the first-visit order needs the new tets (points view or pmx_upload_new_tets)";
     return false;
   }
-  if (nq_bdy_ub < 1 || nq < 1) return true;
+  if (nq < 1) return true;
   if (!ensure_tets(s)) return false;
   const int64_t n = nq;
   size_t sort_b = 0, scan_b = 0;
@@ -1230,21 +1238,27 @@ bool pmx_ctx::seq_surface(const VolArgs &a, hipStream_t s) {
   hipcub::DeviceScan::ExclusiveSum(nullptr, scan_b, (const unsigned long long *)nullptr,
                                    (unsigned long long *)nullptr, (int)n, s);
   if (!pmx_dgrow(this, d_sqkey, (size_t)(2 * n)) || !pmx_dgrow(this, d_sqidx, (size_t)(2 * n)) ||
-      !pmx_dgrow(this, d_sqval, (size_t)(2 * n)) || !pmx_dgrow(this, d_sqint, (size_t)(3 * n + 8)) ||
+      !pmx_dgrow(this, d_sqval, (size_t)(2 * n)) || !pmx_dgrow(this, d_sqint, (size_t)(4 * n + 128)) ||
       !pmx_dgrow(this, d_sqw, (size_t)n) || !pmx_dgrow(this, d_sqtmp, std::max(sort_b, scan_b)) ||
-      !pmx_dgrow(this, d_sqtf, (size_t)(nt + 1)) || !pmx_dgrow(this, d_sqpf, (size_t)(np + 1)))
+      (surf && (!pmx_dgrow(this, d_sqtf, (size_t)(nt + 1)) || !pmx_dgrow(this, d_sqpf, (size_t)(np + 1)))) ||
+      (vol && !pmx_dgrow(this, d_sqtv, (size_t)(ne + 1))))
     return false;
   unsigned *key = d_sqkey.p, *key2 = d_sqkey.p + n;
   int *idx = d_sqidx.p, *idx2 = d_sqidx.p + n;
   unsigned long long *val = d_sqval.p, *pre = d_sqval.p + n;
-  int *sbase = d_sqint.p, *seq = d_sqint.p + n, *sstart = d_sqint.p + 2 * n, *ctl = d_sqint.p + 3 * n;
-  int *nseq = ctl + 4;
-  unsigned *stk_count = (unsigned *)(ctl + 5), *nreplay = (unsigned *)(ctl + 6);
-  int *stk_list = ctl + 7;
+  int *sbase = d_sqint.p, *seq = d_sqint.p + n, *vseq = d_sqint.p + 2 * n, *sstart = d_sqint.p + 3 * n;
+  int *ctl = d_sqint.p + 4 * n;                  // [0..3] surface replay, [4..7] volume replay
+  int *nseq = ctl + 8;                           // [0] surface, [1] volume
+  unsigned *stk_count = (unsigned *)(ctl + 10), *nreplay = (unsigned *)(ctl + 11);   // [11] surface, [12] volume
+  int *stk_list = ctl + 13, *vstk_list = ctl + 14;
+  unsigned *vcounts = (unsigned *)(ctl + 32);   // the volume fallback's step counters (32 words)
+  int *vfound = ctl + 16, *vbestk = ctl + 17;
   const unsigned nbt = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n_ntet + 255) / 256, 8192));
   const unsigned nbp = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
-  // 1. visit order, bases, sequence
-  if (!ck(hipMemsetAsync(key, 0xff, (size_t)n * sizeof(unsigned), s), "memset")) return false;
+  // 1. visit order, bases, sequences
+  if (!ck(hipMemsetAsync(key, 0xff, (size_t)n * sizeof(unsigned), s), "memset") ||
+      !ck(hipMemsetAsync(ctl, 0, 64 * sizeof(int), s), "memset"))
+    return false;
   hipLaunchKernelGGL(k_seq_keys, dim3(nbt), dim3(256), 0, s, (const int4 *)d_ntetv.p, n_ntet, key);
   hipLaunchKernelGGL(k_seq_iota, dim3(nbp), dim3(256), 0, s, idx, sstart, sbase, n);
   if (!ck(hipcub::DeviceRadixSort::SortPairs(d_sqtmp.p, sort_b, (const unsigned *)key, key2, (const int *)idx, idx2,
@@ -1256,46 +1270,100 @@ bool pmx_ctx::seq_surface(const VolArgs &a, hipStream_t s) {
           "scan"))
     return false;
   hipLaunchKernelGGL(k_seq_assign, dim3(nbp), dim3(256), 0, s, (const int *)idx2, (const unsigned long long *)val,
-                     (const unsigned long long *)pre, n, sbase, seq, nseq);
-  // 2. the speculative pass
-  hipLaunchKernelGGL(k_seq_starts, dim3(nbp), dim3(256), 0, s, (const int *)seq, (const int *)nseq,
-                     (const int *)d_elem.p, sstart);
-  if (!ck(hipMemsetAsync(d_counts.p + 1, 0, 2 * sizeof(unsigned), s), "memset")) return false;
-  BdyArgs B = bdy_args(this, a);
-  B.seq_start = sstart;
-  B.seq_base = sbase;
-  B.seq_w = d_sqw.p;
-  launch_bdy_walks(B, d_ows.p, a.exp, s);
-  // 3. the replay, on the reference's state
-  if (!ck(hipMemsetAsync(d_sqtf.p, 0, (size_t)(nt + 1) * sizeof(int), s), "memset") ||
-      !ck(hipMemsetAsync(d_sqpf.p, 0x80, (size_t)(np + 1) * sizeof(int), s), "memset"))
-    return false;
-  int hctl[4] = {0, 1, 0, 0};
-  unsigned zero = 0;
-  if (!ck(hipMemcpyAsync(ctl, hctl, sizeof hctl, hipMemcpyHostToDevice, s), "ctl") ||
-      !ck(hipMemcpyAsync(nreplay, &zero, sizeof zero, hipMemcpyHostToDevice, s), "ctl"))
-    return false;
-  BdyArgs X = B;
-  X.stuck_list = stk_list;
-  X.stuck_count = stk_count;
-  for (int64_t round = 0;; round++) {
-    hipLaunchKernelGGL(k_seq_resolve, dim3(1), dim3(64), 0, s, B, (const int *)seq, (const int *)nseq,
-                       (const int *)sstart, (const uint8_t *)d_sqw.p, (const int *)sbase, d_sqtf.p, d_sqpf.p, ctl,
-                       stk_list, stk_count, nreplay);
-    if (!ck(hipMemcpyAsync(hctl, ctl, sizeof hctl, hipMemcpyDeviceToHost, s), "ctl") ||
-        !ck(hipStreamSynchronize(s), "sync"))
+                     (const unsigned long long *)pre, n, sbase, seq, vseq, nseq);
+  if (surf && nq_bdy_ub > 0) {
+    // 2. the speculative surface pass
+    hipLaunchKernelGGL(k_seq_starts, dim3(nbp), dim3(256), 0, s, (const int *)seq, (const int *)nseq,
+                       (const int *)d_elem.p, sstart);
+    if (!ck(hipMemsetAsync(d_counts.p + 1, 0, 2 * sizeof(unsigned), s), "memset")) return false;
+    BdyArgs B = bdy_args(this, a);
+    B.seq_start = sstart;
+    B.seq_base = sbase;
+    B.seq_w = d_sqw.p;
+    launch_bdy_walks(B, d_ows.p, a.exp, s);
+    // 3. the replay, on the reference's state
+    if (!ck(hipMemsetAsync(d_sqtf.p, 0, (size_t)(nt + 1) * sizeof(int), s), "memset") ||
+        !ck(hipMemsetAsync(d_sqpf.p, 0x80, (size_t)(np + 1) * sizeof(int), s), "memset"))
       return false;
-    if (hctl[2] == 0) break;
-    // a replayed query ended stuck: the exhaustive scan of that one point
-    hipLaunchKernelGGL(k_exh_bdy, dim3(1), dim3(256), 0, s, X);
-    hctl[0] += 1;
-    hctl[1] = -1;
-    hctl[2] = 0;
+    int hctl[4] = {0, 1, 0, 0};
     if (!ck(hipMemcpyAsync(ctl, hctl, sizeof hctl, hipMemcpyHostToDevice, s), "ctl")) return false;
+    BdyArgs X = B;
+    X.stuck_list = stk_list;
+    X.stuck_count = stk_count;
+    for (;;) {
+      hipLaunchKernelGGL(k_seq_resolve, dim3(1), dim3(64), 0, s, B, (const int *)seq, (const int *)nseq,
+                         (const int *)sstart, (const uint8_t *)d_sqw.p, (const int *)sbase, d_sqtf.p, d_sqpf.p, ctl,
+                         stk_list, stk_count, nreplay);
+      if (!ck(hipMemcpyAsync(hctl, ctl, sizeof hctl, hipMemcpyDeviceToHost, s), "ctl") ||
+          !ck(hipStreamSynchronize(s), "sync"))
+        return false;
+      if (hctl[2] == 0) break;
+      // a replayed query ended stuck: the exhaustive scan of that one point
+      hipLaunchKernelGGL(k_exh_bdy, dim3(1), dim3(256), 0, s, X);
+      hctl[0] += 1;
+      hctl[1] = -1;
+      hctl[2] = 0;
+      if (!ck(hipMemcpyAsync(ctl, hctl, sizeof hctl, hipMemcpyHostToDevice, s), "ctl")) return false;
+    }
   }
-  if (!ck(hipMemcpyAsync(&seq_stats[0], nreplay, sizeof(unsigned), hipMemcpyDeviceToHost, s), "stats") ||
-      !ck(hipMemcpyAsync(&seq_stats[1], nseq, sizeof(int), hipMemcpyDeviceToHost, s), "stats") ||
+  if (vol && nq_vol_ub > 0) {
+    // the volume: speculative pass from the predecessors' device results, then
+    // the replay on the reference's tet flags
+    hipLaunchKernelGGL(k_seq_starts, dim3(nbp), dim3(256), 0, s, (const int *)vseq, (const int *)(nseq + 1),
+                       (const int *)d_elem.p, sstart);
+    SeqVolArgs SV{vseq, nseq + 1, sstart, sbase, d_sqw.p, d_sqtv.p, ctl + 4, vstk_list, nreplay + 1};
+    launch_seqv_spec(a, SV, nq_vol_ub, s);
+    if (!ck(hipMemsetAsync(d_sqtv.p, 0, (size_t)(ne + 1) * sizeof(int), s), "memset")) return false;
+    int hctl[4] = {0, 1, 0, 0};
+    if (!ck(hipMemcpyAsync(ctl + 4, hctl, sizeof hctl, hipMemcpyHostToDevice, s), "ctl")) return false;
+    for (;;) {
+      launch_seqv_resolve(a, SV, s);
+      if (!ck(hipMemcpyAsync(hctl, ctl + 4, sizeof hctl, hipMemcpyDeviceToHost, s), "ctl") ||
+          !ck(hipStreamSynchronize(s), "sync"))
+        return false;
+      if (hctl[2] == 0) break;
+      // a replayed walk got stuck: k_fallback on that one point (its own
+      // counters: stuck count 1, no ties, barrier and error words zero)
+      const unsigned one = 1u;
+      const int imax = 0x7fffffff;
+      const unsigned long long umax = ~0ull;
+      if (!ck(hipMemsetAsync(vcounts, 0, 32 * sizeof(unsigned), s), "memset") ||
+          !ck(hipMemcpyAsync(vcounts, &one, sizeof one, hipMemcpyHostToDevice, s), "fallback") ||
+          !ck(hipMemcpyAsync(vfound, &imax, sizeof imax, hipMemcpyHostToDevice, s), "fallback") ||
+          !ck(hipMemcpyAsync(vbestk, &imax, sizeof imax, hipMemcpyHostToDevice, s), "fallback") ||
+          !ck(hipMemcpyAsync(val, &umax, sizeof umax, hipMemcpyHostToDevice, s), "fallback"))
+        return false;
+      VolArgs V = a;
+      V.stuck_list = vstk_list;
+      V.stuck_count = vcounts;
+      V.tie_count = vcounts + 3;
+      V.found = vfound;
+      V.bestk = vbestk;
+      V.best = val;
+      ExhArgs E{};
+      E.xyz = d_xyz.p; E.tets = d_tets.p; E.ne = ne; E.q = d_qxyz.p;
+      E.list = vstk_list; E.count = vcounts; E.found = vfound; E.best = val; E.bestk = vbestk;
+      E.spin_limit = 1L << 26;
+      launch_exhaustive(E, V, fallback_blocks, s);
+      if (!ck(hipStreamSynchronize(s), "sync")) return false;
+      unsigned derr = 0;
+      if (!ck(hipMemcpy(&derr, vcounts + PMX_CNT_ERR, sizeof derr, hipMemcpyDeviceToHost), "fallback")) return false;
+      if (derr) { err = "sequential replay: the one-point fallback's grid barrier timed out"; return false; }
+      hctl[0] += 1;
+      hctl[1] = -1;
+      hctl[2] = 0;
+      if (!ck(hipMemcpyAsync(ctl + 4, hctl, sizeof hctl, hipMemcpyHostToDevice, s), "ctl")) return false;
+    }
+  }
+  unsigned hr[2];
+  int hn[2];
+  if (!ck(hipMemcpyAsync(hr, nreplay, sizeof hr, hipMemcpyDeviceToHost, s), "stats") ||
+      !ck(hipMemcpyAsync(hn, nseq, sizeof hn, hipMemcpyDeviceToHost, s), "stats") ||
       !ck(hipStreamSynchronize(s), "sync"))
     return false;
+  seq_stats[0] = surf ? hr[0] : 0;
+  seq_stats[1] = surf ? (unsigned)hn[0] : 0;
+  seq_stats[2] = vol ? hr[1] : 0;
+  seq_stats[3] = vol ? (unsigned)hn[1] : 0;
   return hipGetLastError() == hipSuccess;
 }

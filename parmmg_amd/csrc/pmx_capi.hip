@@ -1117,7 +1117,7 @@ static void fill_vol_args(pmx_ctx *ctx, const SolDesc &sd, const pmx_run_opts &o
 static bool run_flags_valid(int flags, std::string *err) {
   const int pub = PMX_RUN_REFERENCE_WALK | PMX_RUN_NO_INLINE_TIES | PMX_RUN_RECORD_STARTS |
                   PMX_RUN_SERIAL_SURFACE | PMX_RUN_FRESH_BACKGROUND | PMX_RUN_DEBUG_BARRIER_TIMEOUT |
-                  PMX_RUN_EAGER_DOWNLOAD | PMX_RUN_SEQUENTIAL_SURFACE;
+                  PMX_RUN_EAGER_DOWNLOAD | PMX_RUN_SEQUENTIAL_SURFACE | PMX_RUN_SEQUENTIAL_VOLUME;
   if (flags & ~(pub | (0xff << PMX_RUN_EXP_SHIFT))) {
     *err = "pmx_run: unknown flag bits";
     return false;
@@ -1302,11 +1302,6 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     } else if (ev) {
       CK(hipEventRecord(ev[5], st));
     }
-    ctx->seq_stats_n = -1;
-    if (bdy && (opts.flags & PMX_RUN_SEQUENTIAL_SURFACE)) {
-      if (!ctx->seq_surface(A, st)) return 0;
-      ctx->seq_stats_n = 1;
-    }
     if (ev) CK(hipEventRecord(ev[6], st));
     ExhArgs E{};
     E.xyz = ctx->d_xyz.p; E.tets = ctx->d_tets.p; E.ne = ctx->ne; E.q = ctx->d_qxyz.p;
@@ -1321,6 +1316,14 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
       ctx->fallback_share = share;
     }
     if (ctx->nq_vol_ub) launch_exhaustive(E, A, ctx->fallback_blocks, st);
+    // the reference's sequential semantics, after every default result
+    ctx->seq_stats_n = -1;
+    const bool sq_s = bdy && (opts.flags & PMX_RUN_SEQUENTIAL_SURFACE);
+    const bool sq_v = ctx->nq_vol_ub > 0 && (opts.flags & PMX_RUN_SEQUENTIAL_VOLUME);
+    if (opts.flags & (PMX_RUN_SEQUENTIAL_SURFACE | PMX_RUN_SEQUENTIAL_VOLUME)) {
+      if (!ctx->seq_replay(A, st, sq_s, sq_v)) return 0;
+      ctx->seq_stats_n = 1;
+    }
     if (marks_late) {
       CK(hipStreamWaitEvent(st, ctx->ev_tets, 0));
       OrphanRows rr{ctx->d_wmask.p, ctx->d_elem.p, ctx->d_status.p, ctx->d_steps.p, ctx->d_start.p,
@@ -1631,11 +1634,22 @@ int pmx_locate_wave_stats(pmx_ctx *ctx, int path, pmx_wave_stats *st) {
 int pmx_seq_surface_stats(pmx_ctx *ctx, int64_t *nseq, int64_t *nreplay) {
   if (!ctx || !nseq || !nreplay) return 0;
   if (ctx->seq_stats_n < 0 || !ctx->ran) {
-    ctx->err = "pmx_seq_surface_stats: the last step did not run PMX_RUN_SEQUENTIAL_SURFACE";
+    ctx->err = "pmx_seq_surface_stats: the last step did not run PMX_RUN_SEQUENTIAL_SURFACE / _VOLUME";
     return 0;
   }
   *nseq = ctx->seq_stats[1];
   *nreplay = ctx->seq_stats[0];
+  return 1;
+}
+
+int pmx_seq_volume_stats(pmx_ctx *ctx, int64_t *nseq, int64_t *nreplay) {
+  if (!ctx || !nseq || !nreplay) return 0;
+  if (ctx->seq_stats_n < 0 || !ctx->ran) {
+    ctx->err = "pmx_seq_volume_stats: the last step did not run PMX_RUN_SEQUENTIAL_SURFACE / _VOLUME";
+    return 0;
+  }
+  *nseq = ctx->seq_stats[3];
+  *nreplay = ctx->seq_stats[2];
   return 1;
 }
 
@@ -2040,7 +2054,8 @@ void pmx_ctx::free_all() {
   dfree(d_steps); dfree(d_start); dfree(d_edge); dfree(d_vertex); dfree(d_list); dfree(d_found);
   dfree(d_bestk); dfree(d_best); dfree(d_ties); dfree(d_counts); dfree(d_vollist); dfree(d_bdylist);
   dfree(d_vstat); dfree(d_bstat); dfree(d_hrec);
-  dfree(d_sqkey); dfree(d_sqidx); dfree(d_sqint); dfree(d_sqtf); dfree(d_sqpf); dfree(d_sqval); dfree(d_sqw);
+  dfree(d_sqkey); dfree(d_sqidx); dfree(d_sqint); dfree(d_sqtf); dfree(d_sqpf); dfree(d_sqtv); dfree(d_sqval);
+  dfree(d_sqw);
   dfree(d_sqtmp);
   dfree(d_qual); dfree(d_red); dfree(d_blist); dfree(d_olist); dfree(d_ows);
   dfree(d_ptag); dfree(d_touch); dfree(d_cidx); dfree(d_intv); dfree(d_pub); dfree(d_pkey);

@@ -120,11 +120,11 @@ struct pmx_ctx {
   // starts | control words, wedge flags, cub scratch, the replay's tria and
   // point flags; seq_stats = {replayed queries, surface sequence length}
   DevBuf<unsigned> d_sqkey;
-  DevBuf<int> d_sqidx, d_sqint, d_sqtf, d_sqpf;
+  DevBuf<int> d_sqidx, d_sqint, d_sqtf, d_sqpf, d_sqtv;
   DevBuf<unsigned long long> d_sqval;
   DevBuf<uint8_t> d_sqw;
   DevBuf<char> d_sqtmp;
-  unsigned seq_stats[2] = {0, 0};
+  unsigned seq_stats[4] = {0, 0, 0, 0};   // surface replays / sequence, volume replays / sequence
   int64_t seq_stats_n = -1;             // -1: the last step was not sequential
   int *d_tgrid = nullptr;
   size_t d_tgrid_cap = 0;
@@ -241,10 +241,10 @@ struct pmx_ctx {
   // (d_qmark) classify points in no valid new tet as KIND_ORPH
   bool classify(hipStream_t s, bool marks = false);
   bool launch_bdy(const VolArgs &a, hipStream_t s);
-  // PMX_RUN_SEQUENTIAL_SURFACE after the step's surface pass, on stream s
+  // PMX_RUN_SEQUENTIAL_SURFACE / _VOLUME after the step's passes, on stream s
   // (synchronises the host: a replayed query that ends stuck is scanned by a
-  // launch of its own)
-  bool seq_surface(const VolArgs &a, hipStream_t s);
+  // launch of its own; pmx_bdy.hip)
+  bool seq_replay(const VolArgs &a, hipStream_t s, bool surf, bool vol);
   bool size_tria_grid();
   bool pack_new_tets();                   // the pending new tets: pack, send on `up`, residency build
   bool ensure_tets(hipStream_t s);        // d_ntetv valid for work on stream s

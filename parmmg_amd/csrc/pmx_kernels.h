@@ -138,6 +138,23 @@ bool launch_owner_sample(const TetRec *tets, int64_t ne, int64_t np, unsigned *o
 // field, pmx_wrec.h; d_nfar one device word)
 void launch_build_wrec(const TetRec *tets, int64_t ne, WRec *wr, unsigned *d_nfar, unsigned *h_nfar,
                        hipStream_t s);
+// PMX_RUN_SEQUENTIAL_VOLUME (pmx_walk.hip): the volume sequence (point
+// indices in the reference's visit order, its length on the device), each
+// point's speculative start and mesh->base, the speculation's "sure" flags,
+// the replay's tet flags (ne + 1, base compare), its control words and
+// one-point stuck list, the replay count
+struct SeqVolArgs {
+  const int *vseq;
+  const int *nvseq;
+  const int *sstart, *sbase;
+  uint8_t *sure;
+  int *tf;
+  int *ctl;
+  int *stk_list;
+  unsigned *nreplay;
+};
+void launch_seqv_spec(const VolArgs &a, const SeqVolArgs &s, int64_t nmax, hipStream_t st);
+void launch_seqv_resolve(const VolArgs &a, const SeqVolArgs &s, hipStream_t st);
 // workgroups of k_fallback that can be co-resident with `share` other
 // launches of it on this device (0 on error)
 int fallback_coresident_blocks(int device, int share);

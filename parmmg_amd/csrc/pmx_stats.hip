@@ -791,7 +791,10 @@ __device__ __forceinline__ bool owns_edge(const StatArgs &A, const TetRec (*srec
 #define LEN_QCAP 2048                 // > 255 left over + 6 * 256 queued
 // SURF (tensor metrics with surface data or ridge storage): every length by
 // len_tet_ani from the owner tet's xTetra edge tags and vertices.
-template <bool ANI, bool TAGS, bool PAR, int W = 1, bool L = false, bool SURF = false>
+// X (measurement only, PMX_PRILEN_EXP with PMX_EXPERIMENTS=1; wrong results):
+// bit 0 no length evaluation (1.0), bit 1 no shell rotation (every candidate
+// counts) -- the VALU breakdown of the r05 verdict's item 6.
+template <bool ANI, bool TAGS, bool PAR, int W = 1, bool L = false, bool SURF = false, int X = 0>
 __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
   __shared__ TetRec srec[2][256];
   __shared__ unsigned short q[LEN_QCAP];
@@ -917,16 +920,22 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
         const int c0 = sn[o0], c1 = sn[o1];
         // the first rotation step's records, issued with the points' loads
         TetRec r0{}, r1{};
-        if (c0) r0 = shell_rec<L>(A, srec, kb0, kb1, c0);
-        if (c1) r1 = shell_rec<L>(A, srec, kb0, kb1, c1);
+        if constexpr (!(X & 2)) {
+          if (c0) r0 = shell_rec<L>(A, srec, kb0, kb1, c0);
+          if (c1) r1 = shell_rec<L>(A, srec, kb0, kb1, c1);
+        }
         if constexpr (SURF) {
           const int vv[4] = {sv[0], sv[1], sv[2], sv[3]};
           len = len_tet_ani(A, vv, ia, a, b, A.etag ? (unsigned)A.etag[kk] : 0u);
+        } else if constexpr (X & 1) {
+          len = 1.0 + 1e-9 * (double)(a & 7);
         } else {
           len = edge_len_t<ANI>(A, a, b);
         }
-        on = owns_edge<TAGS, L>(A, srec, kb0, kb1, kk, a, b, c0, c1, keep0, keep1, r0, r1) &&
-             !(PAR && par_excluded(A, a, b));
+        if constexpr (X & 2) on = true;
+        else
+          on = owns_edge<TAGS, L>(A, srec, kb0, kb1, kk, a, b, c0, c1, keep0, keep1, r0, r1) &&
+               !(PAR && par_excluded(A, a, b));
         if constexpr (L) key = LEN_STEP2 + (long long)(6u * (unsigned)kk + (unsigned)ia);   // 6 ne < 2^32
         else key = LEN_STEP2 + 6 * kk + ia;
       }
@@ -1562,7 +1571,20 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
       k_prilen<true, false, false, 1, true, true>,  k_prilen<true, false, true, 1, true, true>,
       k_prilen<true, true, false, 1, true, true>,   k_prilen<true, true, true, 1, true, true>};
   const bool surf = ani && (ctx->have_surf || A.ridmet);
-  const KFn kern = surf ? kfs[(lean ? 4 : 0) | (sel & 3)] : kfn[sel];
+  KFn kern = surf ? kfs[(lean ? 4 : 0) | (sel & 3)] : kfn[sel];
+  // measurement variants of the default iso kernel (PMX_PRILEN_EXP=1..3 with
+  // PMX_EXPERIMENTS=1; results are wrong by design)
+  {
+    static const int xp = [] {
+      const char *e = getenv("PMX_PRILEN_EXP"), *x = getenv("PMX_EXPERIMENTS");
+      return (e && x && x[0] == '1') ? std::max(0, std::min(3, atoi(e))) : 0;
+    }();
+    static const KFn kx[4] = {k_prilen<false, false, false, 5, true>,
+                              k_prilen<false, false, false, 5, true, false, 1>,
+                              k_prilen<false, false, false, 5, true, false, 2>,
+                              k_prilen<false, false, false, 5, true, false, 3>};
+    if (xp && sel == 8 && !surf) kern = kx[xp];
+  }
   int nb = stat_blocks(ctx->ne);
   A.sched_chunk = 0;
   if (sched > 0) {

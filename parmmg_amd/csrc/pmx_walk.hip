@@ -653,3 +653,218 @@ void launch_walk(const VolArgs &a, hipStream_t s) {
   }
   launch_walk_t<LAYOUT_GEN, 0>(a, nb, s);
 }
+
+// ---- PMX_RUN_SEQUENTIAL_VOLUME: the reference's own walk, replayed in order --
+//
+// The reference's volume walk (PMMG_locatePointVol, src/locate_pmmg.c:786-883)
+// starts from the previous volume point's tet (src/interpmesh_pmmg.c:529,
+// :606-607) and marks every tet it visits with mesh->base.  Its answer depends
+// on that start only where several tets contain the point (ties), where the
+// walk gets stuck (status -1 instead of 1) or where it steps into a deleted
+// tet (it spins there until step > ne and returns the closest tet visited,
+// :809-811, :846-851).  pmx_bdy.hip's seq_replay sorts the points into the
+// vertex loop's order; here:
+//  * k_seqv_spec -- every volume point walks the reference's walk exactly
+//    (stable ascending-lambda order, first unvisited neighbour, closest
+//    tracking) from its predecessor's device-semantics tet; the visited set is
+//    a 16-entry lane list, and a walk that outgrows it, gets stuck or meets a
+//    deleted tet is left to the replay ("unsure");
+//  * k_seqv_resolve -- one wavefront keeps every speculative result whose
+//    start was the true one and that was sure, and walks the others again,
+//    in order, on the reference's tet flags (base compare); a stuck one goes
+//    to the exhaustive scan (k_fallback, one point, launched from the host).
+#define SEQV_CAP 16
+
+template <int CAP> struct SeqvRegVis {
+  int vis[CAP];
+  int nv = 0;
+  bool over = false;
+  __device__ bool visited(int t) const {
+    bool h = false;
+#pragma unroll
+    for (int i = 0; i < CAP; i++) h |= (i < nv) & (vis[i] == t);
+    return h;
+  }
+  __device__ void mark(int t) {
+    if (nv >= CAP) { over = true; return; }
+#pragma unroll
+    for (int i = 0; i < CAP; i++)
+      if (i == nv) vis[i] = t;
+    nv++;
+  }
+};
+struct SeqvGlobVis {
+  int *tf;
+  int base;
+  bool over = false;
+  __device__ bool visited(int t) const {
+    return __hip_atomic_load(tf + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == base;
+  }
+  __device__ void mark(int t) { __hip_atomic_store(tf + t, base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+};
+
+// returns 1 found (k, lam: its barycentrics in vertex order), 2 stuck (k the
+// last tet), 3 visited list overflow, 4 the deleted-tet spin (k = the closest
+// visited tet, 0 if none; step = ne + 1); ctet/lam of the closest for 4
+template <class VS>
+__device__ int ref_walk(const VolArgs &A, VS &vs, D3 p, int start, int &k, double lam[4], int &step) {
+  int cur = start > 0 ? start : 1;
+  double cdist = 1.0e10;
+  int ctet = 0;
+  step = 0;
+  while (step <= A.ne) {
+    step++;
+    const TetRec t = A.tets[cur];
+    if (t.v[0] <= 0) {                              // !MG_EOK: the reference spins here
+      step = (int)A.ne + 1;
+      k = ctet;
+      return 4;
+    }
+    vs.mark(cur);
+    if (vs.over) return 3;
+    const D3 P[4] = {ld3(A.xyz, t.v[0]), ld3(A.xyz, t.v[1]), ld3(A.xyz, t.v[2]), ld3(A.xyz, t.v[3])};
+    double l[4], vol;
+    tet_lambda(P, p, l, &vol);
+    double sv[4] = {l[0], l[1], l[2], l[3]};
+    int si[4] = {0, 1, 2, 3};
+    sort4(sv, si);
+    const double d = fabs(sv[0]) * vol;             // PMMG_locatePointInTetra :454-458
+    if (d < cdist) { cdist = d; ctet = cur; }
+    if (sv[0] > -PMX_EPS) {
+      k = cur;
+#pragma unroll
+      for (int f = 0; f < 4; f++) lam[f] = l[f];
+      return 1;
+    }
+    int next = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int nb = sel4(t.nb, si[r]);
+      if (!next && nb && !vs.visited(nb)) next = nb;
+    }
+    if (!next) { k = cur; return 2; }
+    cur = next;
+  }
+  k = ctet;
+  return 4;
+}
+
+// the closest tet's one-hot barycentrics (PMMG_barycoord3d_getClosest,
+// src/barycoord_pmmg.c:371-404): nearest vertex, first on ties
+__device__ void closest_vertex(const VolArgs &A, int k, D3 p, double lam[4]) {
+  const TetRec t = A.tets[k];
+  double best = 0.0;
+  int it = 0;
+  for (int l = 0; l < 4; l++) {
+    const D3 c = ld3(A.xyz, t.v[l]);
+    const double d0 = p.x - c.x, d1 = p.y - c.y, d2 = p.z - c.z;
+    const double d = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+    if (l == 0 || d < best) { best = d; it = l; }
+  }
+  for (int l = 0; l < 4; l++) lam[l] = (l == it) ? 1.0 : 0.0;
+}
+
+__device__ void seqv_finish(const VolArgs &A, int64_t i, int k, const double lam[4], int status, int steps) {
+  A.elem[i] = k;
+  A.status[i] = status;
+  A.steps[i] = steps;
+  if (k <= 0) return;                               // no tet at all: untouched
+  const TetRec t = A.tets[k];
+  const int v[4] = {t.v[0], t.v[1], t.v[2], t.v[3]};
+  const unsigned wm = interp_bar<4>(A.sol, A.sd, v, lam, A.out + i * A.sd.S);
+  A.wmask[i] = (uint8_t)(wm | A.const_bit);
+}
+
+__global__ __launch_bounds__(256) void k_seqv_spec(VolArgs A, SeqVolArgs S) {
+  const int n = *S.nvseq;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    const int i = S.vseq[j];
+    const D3 p{A.q[3 * (int64_t)i], A.q[3 * (int64_t)i + 1], A.q[3 * (int64_t)i + 2]};
+    SeqvRegVis<SEQV_CAP> vs;
+    int k, step;
+    double lam[4];
+    const int r = ref_walk(A, vs, p, S.sstart[i], k, lam, step);
+    A.start[i] = S.sstart[i];
+    S.sure[i] = r == 1 ? 1 : 0;
+    if (r == 1) seqv_finish(A, i, k, lam, 1, step);
+  }
+}
+
+// the replay: one wavefront; ctl = {next position, its start (-1: the tet of
+// the previous point), state (0 done, 1 stuck: the host scans), the point}
+__global__ __launch_bounds__(64) void k_seqv_resolve(VolArgs A, SeqVolArgs S) {
+  const int lane = threadIdx.x;
+  const int n = *S.nvseq;
+  int j = S.ctl[0];
+  int prev = S.ctl[1];
+  if (j >= n) return;
+  if (prev < 0) prev = A.elem[S.vseq[j - 1]];
+  unsigned replays = 0;
+  while (j < n) {
+    const int jj = j + lane;
+    bool okk = false;
+    if (jj < n) {
+      const int i = S.vseq[jj];
+      const int want = lane == 0 ? prev : A.elem[S.vseq[jj - 1]];
+      okk = S.sure[i] && S.sstart[i] == want;
+    }
+    const int nvalid = min(64, n - j);
+    const unsigned long long mask = nvalid == 64 ? ~0ull : ((1ull << nvalid) - 1ull);
+    const unsigned long long bad = ~__ballot(okk) & mask;
+    if (!bad) {
+      prev = A.elem[S.vseq[j + nvalid - 1]];
+      j += nvalid;
+      continue;
+    }
+    const int f = __ffsll((long long)bad) - 1;
+    if (f > 0) prev = A.elem[S.vseq[j + f - 1]];
+    j += f;
+    int r = 1, nk = 0;
+    if (lane == 0) {
+      const int i = S.vseq[j];
+      const D3 p{A.q[3 * (int64_t)i], A.q[3 * (int64_t)i + 1], A.q[3 * (int64_t)i + 2]};
+      SeqvGlobVis vs{S.tf, S.sbase[i]};
+      int k, step;
+      double lam[4];
+      A.start[i] = prev;
+      r = ref_walk(A, vs, p, prev, k, lam, step);
+      replays++;
+      if (r == 1) {
+        seqv_finish(A, i, k, lam, 1, step);
+        nk = k;
+      } else if (r == 4) {
+        if (k > 0) closest_vertex(A, k, p, lam);
+        seqv_finish(A, i, k, lam, 0, step);
+        nk = k;
+        r = 1;
+      } else {                                      // stuck: the exhaustive scan
+        A.steps[i] = -step;
+        S.stk_list[0] = i;
+        S.ctl[0] = j;
+        S.ctl[2] = 1;
+        S.ctl[3] = i;
+      }
+    }
+    r = __shfl(r, 0, 64);
+    nk = __shfl(nk, 0, 64);
+    if (r != 1) {
+      if (lane == 0) atomicAdd(S.nreplay, replays);
+      return;
+    }
+    prev = nk;
+    j++;
+  }
+  if (lane == 0) {
+    S.ctl[0] = n;
+    S.ctl[2] = 0;
+    atomicAdd(S.nreplay, replays);
+  }
+}
+
+void launch_seqv_spec(const VolArgs &a, const SeqVolArgs &s, int64_t nmax, hipStream_t st) {
+  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((nmax + 255) / 256, 65536));
+  hipLaunchKernelGGL(k_seqv_spec, dim3((unsigned)nb), dim3(256), 0, st, a, s);
+}
+void launch_seqv_resolve(const VolArgs &a, const SeqVolArgs &s, hipStream_t st) {
+  hipLaunchKernelGGL(k_seqv_resolve, dim3(1), dim3(64), 0, st, a, s);
+}

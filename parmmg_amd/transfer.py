@@ -235,6 +235,13 @@ class Transfer:
         self._chk(self.lib.pmx_seq_surface_stats(self.ctx, C.byref(a), C.byref(b)), "pmx_seq_surface_stats")
         return {"nseq": a.value, "nreplay": b.value}
 
+    def seq_volume_stats(self) -> dict:
+        """After a RUN_SEQUENTIAL_VOLUME step: the volume sequence length and
+        the walks replayed one by one on the reference's tet flags."""
+        a, b = C.c_int64(), C.c_int64()
+        self._chk(self.lib.pmx_seq_volume_stats(self.ctx, C.byref(a), C.byref(b)), "pmx_seq_volume_stats")
+        return {"nseq": a.value, "nreplay": b.value}
+
     def wave_stats(self, path: int = 0) -> dict:
         """Lane utilisation of the last step's walks (path 0 volume, 1 surface):
         step_sum / lane_steps, lane_steps = sum over waves of 64 x the wave's

@@ -87,10 +87,13 @@ def test_full_size_parity(cfg):
     for tr in trs:
         import time
         t0 = time.perf_counter()
-        tr.run(flags=N.RUN_SEQUENTIAL_SURFACE)
+        tr.run(flags=N.RUN_SEQUENTIAL_SURFACE | N.RUN_SEQUENTIAL_VOLUME)
         tr.synchronize()
         dt = time.perf_counter() - t0
-        seqr.append((tr.download(), tr.border(), tr.seq_surface_stats(), dt))
+        sst = tr.seq_surface_stats()
+        svt = tr.seq_volume_stats()
+        sst.update({"vol_nseq": svt["nseq"], "vol_nreplay": svt["nreplay"]})
+        seqr.append((tr.download(), tr.border(), sst, dt))
         tr.close()
     for g, ((m, x, t, sols, tv), s2, (r, starts, (edge, vert), st), (rq, (sqe, sqv), sst, sdt)) in enumerate(
             zip(cases, sols2, got, seqr)):
@@ -110,9 +113,14 @@ def test_full_size_parity(cfg):
         # surface, the sequential mode: every surface point bit-exact against the
         # reference's sequential run
         compare_exact((rq.sols, rq.elem, rq.status, sqe, sqv), (qo, qe, qs, qed, qve), bdy, len(s2))
-        print(f"{cfg} group {g}: sequential surface mode: {len(bdy)} points bit-exact vs the sequential "
-              f"run, {sst['nreplay']} replayed on the reference's state, step {sdt * 1e3:.1f} ms")
-        assert sst["nseq"] == len(bdy)
+        # ... and every volume point (ties included) in the sequential volume mode
+        assert np.array_equal(rq.elem[vol], qe[vol]) and np.array_equal(rq.status[vol], qs[vol])
+        for a, b in zip(rq.sols, qo):
+            assert bits_equal(a[vol], b[vol]).all()
+        print(f"{cfg} group {g}: sequential modes: {len(bdy)} surface + {len(vol)} volume points bit-exact vs "
+              f"the sequential run, {sst['nreplay']} + {sst['vol_nreplay']} replayed on the reference's state, "
+              f"step {sdt * 1e3:.1f} ms")
+        assert sst["nseq"] == len(bdy) and sst["vol_nseq"] == len(vol)
         # surface, device semantics (each query from the device's start tria, the
         # point flags as PMMG_precompute_nodeTrias leaves them): every surface point
         sample = bdy

@@ -26,7 +26,7 @@ from parmmg_amd import mesh as M
 pytestmark = pytest.mark.gpu
 
 REF_INPUTS = os.path.join(ROOT, "tests", "golden", "ref_inputs")
-SEQ = N.RUN_SEQUENTIAL_SURFACE
+SEQ = N.RUN_SEQUENTIAL_SURFACE | N.RUN_SEQUENTIAL_VOLUME
 
 
 def _run(tr, m, x, t, sols, tets, flags):
@@ -55,12 +55,18 @@ def check_seq(tr, m, x, t, sols, tets):
     vol = np.nonzero(live & ((tt & M.TAG_BDY) == 0))[0]
     assert st["nseq"] == len(bdy)
     compare_exact((rs.sols, rs.elem, rs.status, es, vs), (qo, qe, qs, qed, qve), bdy, len(sols))
-    # the volume points are the default step's
-    assert np.array_equal(rs.elem[vol], rd.elem[vol]) and np.array_equal(rs.status[vol], rd.status[vol])
-    for a, b in zip(rs.sols, rd.sols):
+    # the volume points too (PMX_RUN_SEQUENTIAL_VOLUME): the reference's own
+    # walk from the previous volume point's tet -- ties included
+    sv = tr.seq_volume_stats()
+    assert sv["nseq"] == len(vol)
+    assert np.array_equal(rs.elem[vol], qe[vol]), vol[rs.elem[vol] != qe[vol]][:10]
+    assert np.array_equal(rs.status[vol], qs[vol])
+    for a, b in zip(rs.sols, qo):
         assert bits_equal(a[vol], b[vol]).all()
+    st["vol_nseq"], st["vol_nreplay"] = sv["nseq"], sv["nreplay"]
     # how far the device semantics are from the sequential run on this case
     ndiff = int(((rd.elem[bdy] != qe[bdy]) | (ed[bdy] != qed[bdy]) | (vd[bdy] != qve[bdy])).sum())
+    st["vol_ndiff"] = int((rd.elem[vol] != qe[vol]).sum())
     return st, ndiff
 
 
@@ -70,7 +76,8 @@ def test_seq_surface_cube(transfer, n, metric):
     tets = M.new_point_tets(n, x, t)
     st, ndiff = check_seq(transfer, m, x, t, sols, tets)
     print(f"\nn={n}: {st['nseq']} surface points, {st['nreplay']} replayed, "
-          f"{ndiff} differ in device semantics")
+          f"{ndiff} differ in device semantics; volume {st['vol_nseq']} points, {st['vol_nreplay']} replayed, "
+          f"{st['vol_ndiff']} differ")
     assert st["nreplay"] <= st["nseq"]
 
 
@@ -134,3 +141,45 @@ def test_seq_surface_needs_new_tets(transfer):
     transfer.upload_points(x, t)
     with pytest.raises(RuntimeError, match="new tets"):
         transfer.run(flags=SEQ)
+
+
+def test_seq_volume_ties_on_old_vertices_edges_faces(transfer):
+    """Volume points ON the old mesh's vertices, edge midpoints and face
+    centroids (ties of 2 to ~20 tets): the default step returns the canonical
+    smallest-index tet, the sequential mode the tet the reference's own path
+    reaches first -- bit for bit against the oracle's sequential run."""
+    n = 7
+    m, x, t, sols = cube_case(n, metric="ani")
+    x = x.copy()
+    rng = np.random.default_rng(3)
+    vol = np.nonzero(t == 0)[0]
+    pick = rng.choice(vol, size=len(vol) // 3, replace=False)
+    inner = np.nonzero(np.all((m.xyz[1:] > 0.01) & (m.xyz[1:] < 0.99), axis=1))[0] + 1
+    third = len(pick) // 3
+    x[pick[:third]] = m.xyz[rng.choice(inner, third)]                    # old vertices
+    e = m.tet[rng.integers(1, m.ne + 1, third)]
+    x[pick[third:2 * third]] = 0.5 * (m.xyz[e[:, 0]] + m.xyz[e[:, 1]])   # edge midpoints
+    f = m.tet[rng.integers(1, m.ne + 1, len(pick) - 2 * third)]
+    x[pick[2 * third:]] = (m.xyz[f[:, 0]] + m.xyz[f[:, 1]] + m.xyz[f[:, 2]]) / 3.0   # face centroids
+    tets = M.new_point_tets(n, np.clip(x, 0, 1), t)
+    st, _ = check_seq(transfer, m, x, t, sols, tets)
+    print(f"\nties: volume {st['vol_nseq']} points, {st['vol_nreplay']} replayed, {st['vol_ndiff']} differ "
+          f"from the default step")
+    assert st["vol_ndiff"] > 0
+
+
+def test_seq_volume_walk_into_deleted_tets(transfer):
+    """Deleted background tets (v[0] = 0) whose neighbours still point at them:
+    the reference's walk that steps into one spins until step > ne and returns
+    the closest tet it visited (status 0, src/locate_pmmg.c:809-811,846-851);
+    the sequential mode does the same, bit for bit."""
+    n = 6
+    m, x, t, sols = cube_case(n, metric="iso")
+    c = m.centroids()
+    dead = np.nonzero(np.all(np.abs(c - 0.5) < 0.17, axis=1))[0] + 1
+    tet = m.tet.copy()
+    tet[dead, 0] = 0
+    md = M.Mesh(m.xyz, tet, m.adja, m.tria, m.adjt, m.hausd)
+    tets = M.new_point_tets(n, x, t)
+    st, _ = check_seq(transfer, md, x, t, sols, tets)
+    assert st["vol_nreplay"] > 0

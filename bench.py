@@ -573,10 +573,10 @@ def main():
     sync()
     resident_ms = (time.perf_counter() - t1) / args.steps * 1e3
 
-    # the reference's sequential surface semantics (PMX_RUN_SEQUENTIAL_SURFACE,
-    # bit-exact against the oracle's sequential run in tests/): its cost, and
-    # how many surface points the default (fresh-query) step answers
-    # differently -- another tria, edge or vertex
+    # the reference's sequential semantics (PMX_RUN_SEQUENTIAL_SURFACE |
+    # _VOLUME, bit-exact against the oracle's sequential run in tests/): their
+    # cost, and how many points the default step answers differently --
+    # another tria / edge / vertex on the surface, another tet in the volume
     seq = None
     if world == 1 and not args.no_seq and not args.no_new_tets:
         sync()
@@ -585,19 +585,22 @@ def main():
         e0, v0 = tr.border()
         tr.synchronize()
         t2 = time.perf_counter()
-        tr.run(flags=N.RUN_FRESH_BACKGROUND | N.RUN_SEQUENTIAL_SURFACE)
+        tr.run(flags=N.RUN_FRESH_BACKGROUND | N.RUN_SEQUENTIAL_SURFACE | N.RUN_SEQUENTIAL_VOLUME)
         tr.synchronize()
         seq_ms = (time.perf_counter() - t2) * 1e3
         r1 = tr.download()
         e1, v1 = tr.border()
-        ss = tr.seq_surface_stats()
+        ss, sv = tr.seq_surface_stats(), tr.seq_volume_stats()
         b = (t & M.TAG_BDY) != 0
         ndiff = int(((r0.elem != r1.elem) | (e0 != e1) | (v0 != v1))[b].sum())
-        seq = {"ms": seq_ms, "surface_points": ss["nseq"], "replayed": ss["nreplay"],
-               "default_mode_differs_on": ndiff,
-               "note": "one FRESH step with PMX_RUN_SEQUENTIAL_SURFACE, wall clock incl. host sync; "
-                       "the default step answers default_mode_differs_on surface points with another "
-                       "tria / edge / vertex than the reference's sequential run"}
+        vdiff = int((r0.elem != r1.elem)[~b].sum())
+        seq = {"ms": seq_ms, "surface_points": ss["nseq"], "surface_replayed": ss["nreplay"],
+               "default_mode_differs_on_surface": ndiff, "volume_points": sv["nseq"],
+               "volume_replayed": sv["nreplay"], "default_mode_differs_in_volume": vdiff,
+               "note": "one FRESH step with PMX_RUN_SEQUENTIAL_SURFACE | _VOLUME (the reference's sequential "
+                       "semantics), wall clock incl. host syncs; the default step answers the differing points "
+                       "with another tria / edge / vertex (surface) or tet (volume ties) than the reference's "
+                       "sequential run"}
 
     # host-staged rate (ParMmg's adapter path: host buffers in and out), measured
     # after the timed region and never reported as `value`

@@ -2054,7 +2054,7 @@ void pmx_ctx::free_all() {
   dfree(d_steps); dfree(d_start); dfree(d_edge); dfree(d_vertex); dfree(d_list); dfree(d_found);
   dfree(d_bestk); dfree(d_best); dfree(d_ties); dfree(d_counts); dfree(d_vollist); dfree(d_bdylist);
   dfree(d_vstat); dfree(d_bstat); dfree(d_hrec);
-  dfree(d_sqkey); dfree(d_sqidx); dfree(d_sqint); dfree(d_sqtf); dfree(d_sqpf); dfree(d_sqtv); dfree(d_sqval);
+  dfree(d_sqkey); dfree(d_sqidx); dfree(d_sqint); dfree(d_sqtf); dfree(d_sqpf); dfree(d_sqtv); dfree(d_sqows); dfree(d_sqval);
   dfree(d_sqw);
   dfree(d_sqtmp);
   dfree(d_qual); dfree(d_red); dfree(d_blist); dfree(d_olist); dfree(d_ows);

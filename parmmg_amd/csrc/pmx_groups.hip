@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "pmx_internal.h"
+#include <string>
 
 // MMG3D_Set_constantSize on the new points of the last pmx_upload_points,
 // without a background (the reference's -hsiz shortcut, :501-506, also when no
@@ -117,6 +118,16 @@ static int interp_groups(pmx_ctx *ectx, pmx_ctx *const *ctxs, int ngrp, pmx_grou
     // the background upload invalidated nothing of the points; run the step
     pmx_run_opts o{};
     o.flags = PMX_RUN_EAGER_DOWNLOAD;        // every group is downloaded below
+    // PMX_SEQUENTIAL=surface|volume|all: the reference's sequential
+    // semantics (PMX_RUN_SEQUENTIAL_*; the points view carries the new tets)
+    static const int seqf = [] {
+      const char *e = getenv("PMX_SEQUENTIAL");
+      if (!e) return 0;
+      const std::string v(e);
+      return (v == "surface" ? PMX_RUN_SEQUENTIAL_SURFACE : 0) | (v == "volume" ? PMX_RUN_SEQUENTIAL_VOLUME : 0) |
+             (v == "all" || v == "1" ? PMX_RUN_SEQUENTIAL_SURFACE | PMX_RUN_SEQUENTIAL_VOLUME : 0);
+    }();
+    o.flags |= seqf;
     if (!pmx_run(X, &o)) { fail(X); continue; }
     // outputs in Mmg layout start at point index `first`
     for (int k = 0; k < ns; k++)

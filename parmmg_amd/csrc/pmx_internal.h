@@ -120,7 +120,7 @@ struct pmx_ctx {
   // starts | control words, wedge flags, cub scratch, the replay's tria and
   // point flags; seq_stats = {replayed queries, surface sequence length}
   DevBuf<unsigned> d_sqkey;
-  DevBuf<int> d_sqidx, d_sqint, d_sqtf, d_sqpf, d_sqtv;
+  DevBuf<int> d_sqidx, d_sqint, d_sqtf, d_sqpf, d_sqtv, d_sqows;
   DevBuf<unsigned long long> d_sqval;
   DevBuf<uint8_t> d_sqw;
   DevBuf<char> d_sqtmp;

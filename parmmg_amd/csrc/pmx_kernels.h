@@ -153,7 +153,9 @@ struct SeqVolArgs {
   int *stk_list;
   unsigned *nreplay;
 };
-void launch_seqv_spec(const VolArgs &a, const SeqVolArgs &s, int64_t nmax, hipStream_t st);
+// the speculative pass and its overflow pass (workspace: seqv_ovf_ws_ints() ints)
+size_t seqv_ovf_ws_ints();
+void launch_seqv_spec(const VolArgs &a, const SeqVolArgs &s, int64_t nmax, int *ws, hipStream_t st);
 void launch_seqv_resolve(const VolArgs &a, const SeqVolArgs &s, hipStream_t st);
 // workgroups of k_fallback that can be co-resident with `share` other
 // launches of it on this device (0 on error)

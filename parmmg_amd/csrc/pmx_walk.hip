@@ -693,6 +693,21 @@ template <int CAP> struct SeqvRegVis {
     nv++;
   }
 };
+// a longer private list in a global workspace (the overflow pass)
+struct SeqvListVis {
+  int *vis;
+  int nv = 0, cap = 0;
+  bool over = false;
+  __device__ bool visited(int t) const {
+    for (int i = 0; i < nv; i++)
+      if (vis[i] == t) return true;
+    return false;
+  }
+  __device__ void mark(int t) {
+    if (nv >= cap) { over = true; return; }
+    vis[nv++] = t;
+  }
+};
 struct SeqvGlobVis {
   int *tf;
   int base;
@@ -785,6 +800,29 @@ __global__ __launch_bounds__(256) void k_seqv_spec(VolArgs A, SeqVolArgs S) {
     double lam[4];
     const int r = ref_walk(A, vs, p, S.sstart[i], k, lam, step);
     A.start[i] = S.sstart[i];
+    S.sure[i] = r == 1 ? 1 : r == 3 ? 2 : 0;       // 2: a longer walk, for the overflow pass
+    if (r == 1) seqv_finish(A, i, k, lam, 1, step);
+  }
+}
+
+// the walks that outgrew the lane list, again with a SEQV_OVF_CAP list in a
+// global workspace (walks from the previous point's tet are long where the
+// visit order jumps: ~2 % of C3's points walk more than 16 tets)
+#define SEQV_OVF_CAP 1024
+#define SEQV_OVF_THREADS (64 * 256)
+__global__ __launch_bounds__(256) void k_seqv_ovf(VolArgs A, SeqVolArgs S, int *ws) {
+  const int n = *S.nvseq;
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  for (int j = tid; j < n; j += gridDim.x * blockDim.x) {
+    const int i = S.vseq[j];
+    if (S.sure[i] != 2) continue;
+    const D3 p{A.q[3 * (int64_t)i], A.q[3 * (int64_t)i + 1], A.q[3 * (int64_t)i + 2]};
+    SeqvListVis vs;
+    vs.vis = ws + (size_t)tid * SEQV_OVF_CAP;
+    vs.cap = SEQV_OVF_CAP;
+    int k, step;
+    double lam[4];
+    const int r = ref_walk(A, vs, p, S.sstart[i], k, lam, step);
     S.sure[i] = r == 1 ? 1 : 0;
     if (r == 1) seqv_finish(A, i, k, lam, 1, step);
   }
@@ -861,9 +899,11 @@ __global__ __launch_bounds__(64) void k_seqv_resolve(VolArgs A, SeqVolArgs S) {
   }
 }
 
-void launch_seqv_spec(const VolArgs &a, const SeqVolArgs &s, int64_t nmax, hipStream_t st) {
+size_t seqv_ovf_ws_ints() { return (size_t)SEQV_OVF_THREADS * SEQV_OVF_CAP; }
+void launch_seqv_spec(const VolArgs &a, const SeqVolArgs &s, int64_t nmax, int *ws, hipStream_t st) {
   const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((nmax + 255) / 256, 65536));
   hipLaunchKernelGGL(k_seqv_spec, dim3((unsigned)nb), dim3(256), 0, st, a, s);
+  hipLaunchKernelGGL(k_seqv_ovf, dim3(SEQV_OVF_THREADS / 256), dim3(256), 0, st, a, s, ws);
 }
 void launch_seqv_resolve(const VolArgs &a, const SeqVolArgs &s, hipStream_t st) {
   hipLaunchKernelGGL(k_seqv_resolve, dim3(1), dim3(64), 0, st, a, s);

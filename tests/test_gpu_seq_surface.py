@@ -150,6 +150,7 @@ def test_seq_volume_ties_on_old_vertices_edges_faces(transfer):
     reaches first -- bit for bit against the oracle's sequential run."""
     n = 7
     m, x, t, sols = cube_case(n, metric="ani")
+    tets = M.new_point_tets(n, x, t)          # the vertex enumeration, before the points move
     x = x.copy()
     rng = np.random.default_rng(3)
     vol = np.nonzero(t == 0)[0]
@@ -161,7 +162,6 @@ def test_seq_volume_ties_on_old_vertices_edges_faces(transfer):
     x[pick[third:2 * third]] = 0.5 * (m.xyz[e[:, 0]] + m.xyz[e[:, 1]])   # edge midpoints
     f = m.tet[rng.integers(1, m.ne + 1, len(pick) - 2 * third)]
     x[pick[2 * third:]] = (m.xyz[f[:, 0]] + m.xyz[f[:, 1]] + m.xyz[f[:, 2]]) / 3.0   # face centroids
-    tets = M.new_point_tets(n, np.clip(x, 0, 1), t)
     st, _ = check_seq(transfer, m, x, t, sols, tets)
     print(f"\nties: volume {st['vol_nseq']} points, {st['vol_nreplay']} replayed, {st['vol_ndiff']} differ "
           f"from the default step")

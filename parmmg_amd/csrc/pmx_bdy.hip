@@ -1312,7 +1312,10 @@ bool pmx_ctx::seq_replay(const VolArgs &a, hipStream_t s, bool surf, bool vol) {
     hipLaunchKernelGGL(k_seq_starts, dim3(nbp), dim3(256), 0, s, (const int *)vseq, (const int *)(nseq + 1),
                        (const int *)d_elem.p, sstart);
     SeqVolArgs SV{vseq, nseq + 1, sstart, sbase, d_sqw.p, d_sqtv.p, ctl + 4, vstk_list, nreplay + 1};
-    if (!pmx_dgrow(this, d_sqows, seqv_ovf_ws_ints())) return false;
+    // the overflow pass's hash tables: generation 0 = empty (positions start at 1)
+    if (!pmx_dgrow(this, d_sqows, seqv_ovf_ws_ints()) ||
+        !ck(hipMemsetAsync(d_sqows.p, 0, seqv_ovf_ws_ints() * sizeof(int), s), "memset"))
+      return false;
     launch_seqv_spec(a, SV, nq_vol_ub, d_sqows.p, s);
     if (!ck(hipMemsetAsync(d_sqtv.p, 0, (size_t)(ne + 1) * sizeof(int), s), "memset")) return false;
     int hctl[4] = {0, 1, 0, 0};

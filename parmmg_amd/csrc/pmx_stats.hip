@@ -359,6 +359,73 @@ __device__ __forceinline__ int pick_nb(const TetRec &t, int l) {
 }
 
 
+// log1p as glibc computes it (sysdeps/ieee754/dbl-64/s_log1p.c: Sun's fdlibm
+// algorithm with its polynomial in the pairwise (Estrin) form glibc uses),
+// restated so that the lengths are the reference's bit for bit on a glibc
+// host -- ocml's log1p differs from it in the last ulp now and then.
+// Checked against glibc 2.35's log1p on 5e7 inputs over (-0.49, 20) and
+// tiny / huge ranges: no difference (tests/test_oracle.py pins the C twin of
+// this code against the host's log1p).  Needs -ffp-contract=off (the
+// library's flag): every product and sum rounded as in the C source.
+__device__ double pmx_log1p(double x) {
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const double Lp1 = 6.666666666666735130e-01, Lp2 = 3.999999999940941908e-01, Lp3 = 2.857142874366239149e-01,
+               Lp4 = 2.222219843214978396e-01, Lp5 = 1.818357216161805012e-01, Lp6 = 1.531383769920937332e-01,
+               Lp7 = 1.479819860511658591e-01;
+  double f = 0.0, c = 0.0, u;
+  int hx = __double2hiint(x), hu = 0, k = 1;
+  const int ax = hx & 0x7fffffff;
+  if (hx < 0x3FDA827A) {                          // x < 0.41422
+    if (ax >= 0x3ff00000) return x == -1.0 ? -__builtin_inf() : (x - x) / (x - x);   // x <= -1
+    if (ax < 0x3e200000) return ax < 0x3c900000 ? x : x - x * x * 0.5;                // |x| < 2^-29
+    if (hx > 0 || hx <= (int)0xbfd2bec3) { k = 0; f = x; hu = 1; }                     // -0.2929 < x < 0.41422
+  } else if (hx >= 0x7ff00000) {
+    return x + x;
+  }
+  if (k != 0) {
+    if (hx < 0x43400000) {
+      u = 1.0 + x;
+      hu = __double2hiint(u);
+      k = (hu >> 20) - 1023;
+      c = (k > 0) ? 1.0 - (u - x) : x - (u - 1.0);  // correction term
+      c /= u;
+    } else {
+      u = x;
+      hu = __double2hiint(u);
+      k = (hu >> 20) - 1023;
+      c = 0.0;
+    }
+    hu &= 0x000fffff;
+    if (hu < 0x6a09e) {
+      u = __hiloint2double(hu | 0x3ff00000, __double2loint(u));            // normalise u
+    } else {
+      k += 1;
+      u = __hiloint2double(hu | 0x3fe00000, __double2loint(u));            // normalise u / 2
+      hu = (0x00100000 - hu) >> 2;
+    }
+    f = u - 1.0;
+  }
+  const double hfsq = 0.5 * f * f;
+  const double dk = (double)k;
+  if (hu == 0) {                                   // |f| < 2^-20
+    if (f == 0.0) {
+      if (k == 0) return 0.0;
+      c += dk * ln2_lo;
+      return dk * ln2_hi + c;
+    }
+    const double R = hfsq * (1.0 - 0.66666666666666666 * f);
+    if (k == 0) return f - R;
+    return dk * ln2_hi - ((R - (dk * ln2_lo + c)) - f);
+  }
+  const double s = f / (2.0 + f);
+  const double z = s * s;
+  const double R1 = z * Lp1, z2 = z * z, R2 = Lp2 + z * Lp3, z4 = z2 * z2, R3 = Lp4 + z * Lp5, z6 = z4 * z2,
+               R4 = Lp6 + z * Lp7;
+  const double R = R1 + z2 * R2 + z4 * R3 + z6 * R4;
+  if (k == 0) return f - (hfsq - s * (hfsq + R));
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + (dk * ln2_lo + c))) - f);
+}
+
 // MMG5_lenEdg_iso / lenEdg33_ani (restated, unpinned; the surface lengths
 // MMG5_lenSurfEdg_iso / lenSurfEdg33_ani of the parallel edges take the same
 // formulas in classic metric storage)
@@ -378,7 +445,7 @@ __device__ __forceinline__ double edge_len_t(const StatArgs &A, int p1, int p2) 
   double l = ux * ux + uy * uy + uz * uz;
   l = sqrt(l);
   double r = h2 / h1 - 1.0;
-  return (fabs(r) < PMX_EPS) ? (l / h1) : (l / (h2 - h1) * log1p(r));
+  return (fabs(r) < PMX_EPS) ? (l / h1) : (l / (h2 - h1) * pmx_log1p(r));
 }
 __device__ double edge_len(const StatArgs &A, int p1, int p2) {
   return A.msize == 6 ? edge_len_t<true>(A, p1, p2) : edge_len_t<false>(A, p1, p2);
@@ -552,7 +619,7 @@ __device__ double len_iso_flat(const StatArgs &A, int p1, int p2) {
   double l = (c2.x - c1.x) * (c2.x - c1.x) + (c2.y - c1.y) * (c2.y - c1.y) + (c2.z - c1.z) * (c2.z - c1.z);
   l = sqrt(l);
   const double r = h2 / h1 - 1.0;
-  return (fabs(r) < PMX_EPS) ? (l / h1) : (l / (h2 - h1) * log1p(r));
+  return (fabs(r) < PMX_EPS) ? (l / h1) : (l / (h2 - h1) * pmx_log1p(r));
 }
 
 __device__ __forceinline__ void len_merge(LenPart &x, const LenPart &y) {

@@ -693,19 +693,29 @@ template <int CAP> struct SeqvRegVis {
     nv++;
   }
 };
-// a longer private list in a global workspace (the overflow pass)
-struct SeqvListVis {
-  int *vis;
-  int nv = 0, cap = 0;
+// a larger private set in a global workspace (the overflow pass): an
+// open-addressing hash of {tet, generation} entries -- the generation (the
+// point's sequence position + 1) makes a stale entry of an earlier point an
+// empty slot, so nothing is cleared between points; at most half full
+struct SeqvHashVis {
+  int2 *tab;
+  int mask = 0, nv = 0, gen = 0;
   bool over = false;
+  __device__ __forceinline__ unsigned slot0(int t) const { return ((unsigned)t * 2654435761u) & (unsigned)mask; }
   __device__ bool visited(int t) const {
-    for (int i = 0; i < nv; i++)
-      if (vis[i] == t) return true;
-    return false;
+    for (unsigned h = slot0(t);; h = (h + 1) & (unsigned)mask) {
+      const int2 e = tab[h];
+      if (e.y != gen) return false;
+      if (e.x == t) return true;
+    }
   }
   __device__ void mark(int t) {
-    if (nv >= cap) { over = true; return; }
-    vis[nv++] = t;
+    if (2 * (nv + 1) > mask + 1) { over = true; return; }
+    for (unsigned h = slot0(t);; h = (h + 1) & (unsigned)mask) {
+      const int2 e = tab[h];
+      if (e.y != gen) { tab[h] = make_int2(t, gen); nv++; return; }
+      if (e.x == t) return;
+    }
   }
 };
 struct SeqvGlobVis {
@@ -808,7 +818,7 @@ __global__ __launch_bounds__(256) void k_seqv_spec(VolArgs A, SeqVolArgs S) {
 // the walks that outgrew the lane list, again with a SEQV_OVF_CAP list in a
 // global workspace (walks from the previous point's tet are long where the
 // visit order jumps: ~2 % of C3's points walk more than 16 tets)
-#define SEQV_OVF_CAP 1024
+#define SEQV_OVF_CAP 4096            // hash slots per thread: walks of up to 2048 tets
 #define SEQV_OVF_THREADS (64 * 256)
 __global__ __launch_bounds__(256) void k_seqv_ovf(VolArgs A, SeqVolArgs S, int *ws) {
   const int n = *S.nvseq;
@@ -817,9 +827,10 @@ __global__ __launch_bounds__(256) void k_seqv_ovf(VolArgs A, SeqVolArgs S, int *
     const int i = S.vseq[j];
     if (S.sure[i] != 2) continue;
     const D3 p{A.q[3 * (int64_t)i], A.q[3 * (int64_t)i + 1], A.q[3 * (int64_t)i + 2]};
-    SeqvListVis vs;
-    vs.vis = ws + (size_t)tid * SEQV_OVF_CAP;
-    vs.cap = SEQV_OVF_CAP;
+    SeqvHashVis vs;
+    vs.tab = reinterpret_cast<int2 *>(ws) + (size_t)tid * SEQV_OVF_CAP;
+    vs.mask = SEQV_OVF_CAP - 1;
+    vs.gen = j + 1;
     int k, step;
     double lam[4];
     const int r = ref_walk(A, vs, p, S.sstart[i], k, lam, step);
@@ -899,7 +910,7 @@ __global__ __launch_bounds__(64) void k_seqv_resolve(VolArgs A, SeqVolArgs S) {
   }
 }
 
-size_t seqv_ovf_ws_ints() { return (size_t)SEQV_OVF_THREADS * SEQV_OVF_CAP; }
+size_t seqv_ovf_ws_ints() { return (size_t)SEQV_OVF_THREADS * SEQV_OVF_CAP * 2; }
 void launch_seqv_spec(const VolArgs &a, const SeqVolArgs &s, int64_t nmax, int *ws, hipStream_t st) {
   const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((nmax + 255) / 256, 65536));
   hipLaunchKernelGGL(k_seqv_spec, dim3((unsigned)nb), dim3(256), 0, st, a, s);

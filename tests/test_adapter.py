@@ -129,7 +129,7 @@ def test_adapter_reference_call_order(tmp_path):
     lo = O.prilen(mesh_new, met, tags=ntag)
     for p in pl:
         assert p["ned"] == lo["ned"] and p["nullEdge"] == lo["nullEdge"]
-        assert sum(abs(a - b) for a, b in zip(p["hl"], lo["hl"])) <= 2
+        assert p["hl"] == lo["hl"]                      # glibc's log1p restated on the device (r06)
         assert p["lmin"] == pytest.approx(lo["lmin"], rel=1e-15) and p["lmax"] == pytest.approx(lo["lmax"], rel=1e-15)
 
 

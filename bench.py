@@ -503,7 +503,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         m, x, t, sols, _ = cases[0]
+        phase("cpu baseline (forked oracle processes)")
         cpu = cpu_baseline_node(m, x, t, sols)
+        phase("cpu baseline done")
 
     from parmmg_amd import _native as N
     from parmmg_amd import mesh as M
@@ -511,6 +513,7 @@ def main():
     FRESH = N.RUN_FRESH_BACKGROUND | (args.run_exp << 16)
     # every group of this rank in its own context (own stream): the groups'
     # steps are enqueued back to back and may overlap on the device
+    phase("uploads")
     trs = []
     for g in range(ngrp):
         m, x, t, sols, tv = cases[g]
@@ -531,6 +534,7 @@ def main():
         for g in trs:
             g.synchronize()
 
+    phase("warmup + timed steps")
     for _ in range(args.warmup):
         step()
     sync()
@@ -579,6 +583,7 @@ def main():
     # another tria / edge / vertex on the surface, another tet in the volume
     seq = None
     if world == 1 and not args.no_seq and not args.no_new_tets:
+        phase("sequential-semantics step")
         sync()
         tr.run(flags=N.RUN_FRESH_BACKGROUND)
         r0 = tr.download()
@@ -606,6 +611,7 @@ def main():
     # after the timed region and never reported as `value`
     pcie = None
     if world == 1 and not args.no_pcie:
+        phase("host-staged cycles")
         pcie = pcie_inclusive(tr, m, x, t, sols)
         pcie["resident_cycle"] = resident_cycle(m, sols, cfg, local)
         pcie["binding_cycle"] = binding_cycle(m, x, t, tv, sols, local)
@@ -713,6 +719,7 @@ def main():
         out["qualhisto_allreduce"] = qs
         dist.destroy_process_group()
     if rank == 0:
+        phase("done")
         print(json.dumps(out), flush=True)
 
 

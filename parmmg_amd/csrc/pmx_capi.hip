@@ -1784,6 +1784,12 @@ int pmx_upload_new_tets(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, 
     const char *tc0 = (const char *)tetra_v;
     for (int64_t k = 1; same && k <= ne; k++) {
       const int *v = (const int *)(tc0 + k * tetra_stride);
+      if (v[0] > 0)
+        for (int l = 0; l < 4; l++)
+          if ((int64_t)v[l] - first < 0 || (int64_t)v[l] - first >= n) {
+            ctx->err = "pmx_upload_new_tets: tet vertex outside the uploaded points";
+            return 0;
+          }
       const int4 o = old[k];
       same = v[0] <= 0 ? o.x == 0
                        : (o.x == (int)(v[0] - first + 1) && o.y == (int)(v[1] - first + 1) &&

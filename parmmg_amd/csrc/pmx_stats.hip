@@ -432,8 +432,8 @@ __device__ double pmx_log1p(double x) {
 template <bool ANI>
 __device__ __forceinline__ double edge_len_t(const StatArgs &A, int p1, int p2) {
   D3 c1 = sld3(A, p1), c2 = sld3(A, p2);
-  double ux = c2.x - c1.x, uy = c2.y - c1.y, uz = c2.z - c1.z;
   if (ANI) {
+    double ux = c2.x - c1.x, uy = c2.y - c1.y, uz = c2.z - c1.z;
     const double *m1 = smet(A, p1), *m2 = smet(A, p2);
     double dd1 = mlen2(m1, ux, uy, uz);
     double dd2 = mlen2(m2, ux, uy, uz);
@@ -442,6 +442,10 @@ __device__ __forceinline__ double edge_len_t(const StatArgs &A, int p1, int p2) 
     return (sqrt(dd1) + sqrt(dd2) + 4.0 * sqrt(0.5 * (dd1 + dd2))) / 6.0;
   }
   double h1 = smet(A, p1)[0], h2 = smet(A, p2)[0];
+  // the sizes' loads issued with the coordinates' (the scheduler otherwise
+  // places them after the wait for the coordinates: a second round trip)
+  __builtin_amdgcn_sched_barrier(0);
+  double ux = c2.x - c1.x, uy = c2.y - c1.y, uz = c2.z - c1.z;
   double l = ux * ux + uy * uy + uz * uz;
   l = sqrt(l);
   double r = h2 / h1 - 1.0;
@@ -777,19 +781,21 @@ __device__ __forceinline__ TetRec shell_rec(const StatArgs &A, const TetRec (*sr
     const unsigned long long d1 = (unsigned long long)((long long)c - kb1);
     idx = d0 < 256ull ? (int)d0 : (d1 < 256ull ? 256 + (int)d1 : -1);
   }
-  // one LDS index into both batches (no select between LDS and global
-  // pointers: the loads stay in their own address spaces)
-  TetRec r;
-  if (idx >= 0) {
-    const int4 *l = reinterpret_cast<const int4 *>(&srec[0][0]) + 2 * idx;
-    const int4 lv = l[0], ln = l[1];
-    r = TetRec{{lv.x, lv.y, lv.z, lv.w}, {ln.x, ln.y, ln.z, ln.w}};
-  } else {
+  // one LDS index into both batches.  The LDS read is unconditional (slot 0
+  // for a miss) and only a miss loads from HBM: with both loads conditional
+  // the compiler merges them into one flat load through a selected pointer
+  // (r06 ISA: flat_load_dwordx4, which waits on both memory counters)
+  const int4 *l = reinterpret_cast<const int4 *>(&srec[0][0]) + 2 * (idx < 0 ? 0 : idx);
+  int4 lv = l[0], ln = l[1];
+  // (opaque to the optimiser: it would otherwise sink the LDS read into the
+  // hit branch and merge the two again)
+  asm volatile("" : "+v"(lv.x), "+v"(lv.y), "+v"(lv.z), "+v"(lv.w), "+v"(ln.x), "+v"(ln.y), "+v"(ln.z), "+v"(ln.w));
+  if (idx < 0) {
     const int4 *g = reinterpret_cast<const int4 *>(A.tets) + 2 * (int64_t)c;
-    const int4 gv = g[0], gn = g[1];
-    r = TetRec{{gv.x, gv.y, gv.z, gv.w}, {gn.x, gn.y, gn.z, gn.w}};
+    lv = g[0];
+    ln = g[1];
   }
-  return r;
+  return TetRec{{lv.x, lv.y, lv.z, lv.w}, {ln.x, ln.y, ln.z, ln.w}};
 }
 
 // True iff no admissible tet with index < k contains the edge (a, b) of tet
@@ -839,6 +845,45 @@ __device__ __forceinline__ bool owns_edge(const StatArgs &A, const TetRec (*srec
   return true;
 }
 
+// owns_edge without point tags, as straight-line selects for the first two
+// rotation steps (a Kuhn shell of 4 or 6 tets is decided there: the two
+// cursors meet), then owns_edge's loop for a longer shell.  The same
+// decisions in the same order as owns_edge<false, L>; the loop's early
+// returns become a "decided" mask, so the wave issues no branch per check.
+template <bool L>
+__device__ __forceinline__ bool owns_edge_flat(const StatArgs &A, const TetRec (*srec)[256], long long kb0,
+                                               long long kb1, int64_t k64, int a, int b, int c0, int c1, int keep0,
+                                               int keep1, TetRec r0, TetRec r1) {
+  using KT = typename std::conditional<L, int, int64_t>::type;
+  const KT k = (KT)k64;
+  bool done = false, own = true;
+#pragma unroll
+  for (int it = 0; it < 2; it++) {
+    c0 = (c0 == (int)k) ? 0 : c0;
+    c1 = (c1 == (int)k) ? 0 : c1;
+    // the checks of owns_edge's loop head, first decision wins
+    const bool d_end = !c0 && !c1;
+    const bool d_small = (c0 && c0 < k) || (c1 && c1 < k);
+    const bool d_meet = c0 && c0 == c1;
+    own = done ? own : (d_end ? true : (d_small ? false : true));
+    done = done || d_end || d_small || d_meet;
+    const int n0 = c0 ? rotate_step(r0, a, b, keep0) : 0;
+    const int n1 = c1 ? rotate_step(r1, a, b, keep1) : 0;
+    const bool d_closed = c0 && c1 && (n0 == c1 || n1 == c0);
+    done = done || d_closed;                       // own stays true
+    c0 = c0 ? n0 : 0;
+    c1 = c1 ? n1 : 0;
+    const bool need0 = c0 && c0 != (int)k, need1 = c1 && c1 != (int)k;
+    const bool d_small2 = (need0 && c0 < k) || (need1 && c1 < k);
+    own = done ? own : !d_small2;
+    done = done || d_small2 || (need0 && c0 == c1);
+    if (!done && need0) r0 = shell_rec<L>(A, srec, kb0, kb1, c0);
+    if (!done && need1) r1 = shell_rec<L>(A, srec, kb0, kb1, c1);
+  }
+  if (done) return own;
+  return owns_edge<false, L>(A, srec, kb0, kb1, k64, a, b, c0, c1, keep0, keep1, r0, r1);
+}
+
 // ---- prilen: unique edges by shell ownership, one pass ------------------------
 //
 // Each workgroup walks a contiguous range of tets, 256 records per batch:
@@ -858,9 +903,11 @@ __device__ __forceinline__ bool owns_edge(const StatArgs &A, const TetRec (*srec
 #define LEN_QCAP 2048                 // > 255 left over + 6 * 256 queued
 // SURF (tensor metrics with surface data or ridge storage): every length by
 // len_tet_ani from the owner tet's xTetra edge tags and vertices.
-// X (measurement only, PMX_PRILEN_EXP with PMX_EXPERIMENTS=1; wrong results):
-// bit 0 no length evaluation (1.0), bit 1 no shell rotation (every candidate
-// counts) -- the VALU breakdown of the r05 verdict's item 6.
+// X (measurement only, PMX_PRILEN_EXP): bits 0-1 with PMX_EXPERIMENTS=1 give
+// wrong results by design -- bit 0 no length evaluation (1.0), bit 1 no shell
+// rotation (every candidate counts), the VALU breakdown of the r05 verdict's
+// item 6; bit 2 (4: same results) the rotation as owns_edge's loop from the
+// first step instead of owns_edge_flat (r05's kernel, for the A/B).
 template <bool ANI, bool TAGS, bool PAR, int W = 1, bool L = false, bool SURF = false, int X = 0>
 __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
   __shared__ TetRec srec[2][256];
@@ -1000,6 +1047,9 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
           len = edge_len_t<ANI>(A, a, b);
         }
         if constexpr (X & 2) on = true;
+        else if constexpr (!(X & 4) && !TAGS)
+          on = owns_edge_flat<L>(A, srec, kb0, kb1, kk, a, b, c0, c1, keep0, keep1, r0, r1) &&
+               !(PAR && par_excluded(A, a, b));
         else
           on = owns_edge<TAGS, L>(A, srec, kb0, kb1, kk, a, b, c0, c1, keep0, keep1, r0, r1) &&
                !(PAR && par_excluded(A, a, b));
@@ -1640,16 +1690,20 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
   const bool surf = ani && (ctx->have_surf || A.ridmet);
   KFn kern = surf ? kfs[(lean ? 4 : 0) | (sel & 3)] : kfn[sel];
   // measurement variants of the default iso kernel (PMX_PRILEN_EXP=1..3 with
-  // PMX_EXPERIMENTS=1; results are wrong by design)
+  // PMX_EXPERIMENTS=1: results are wrong by design; 4: the r05 rotation loop)
   {
     static const int xp = [] {
       const char *e = getenv("PMX_PRILEN_EXP"), *x = getenv("PMX_EXPERIMENTS");
-      return (e && x && x[0] == '1') ? std::max(0, std::min(3, atoi(e))) : 0;
+      const int v = e ? atoi(e) : 0;
+      // 4: the rotation loop (same results, no PMX_EXPERIMENTS needed)
+      if (v == 4) return 4;
+      return (e && x && x[0] == '1') ? std::max(0, std::min(3, v)) : 0;
     }();
-    static const KFn kx[4] = {k_prilen<false, false, false, 5, true>,
+    static const KFn kx[5] = {k_prilen<false, false, false, 5, true>,
                               k_prilen<false, false, false, 5, true, false, 1>,
                               k_prilen<false, false, false, 5, true, false, 2>,
-                              k_prilen<false, false, false, 5, true, false, 3>};
+                              k_prilen<false, false, false, 5, true, false, 3>,
+                              k_prilen<false, false, false, 5, true, false, 4>};
     if (xp && sel == 8 && !surf) kern = kx[xp];
   }
   int nb = stat_blocks(ctx->ne);

@@ -426,13 +426,35 @@ __device__ double pmx_log1p(double x) {
   return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + (dk * ln2_lo + c))) - f);
 }
 
+// MMG5_lenEdg_iso in two halves: the loads (the sizes issued with the
+// coordinates -- the scheduler otherwise places them after the wait for the
+// coordinates, a second round trip) and the arithmetic, so that a caller can
+// put work between them
+struct IsoEdge { D3 c1, c2; double h1, h2; };
+__device__ __forceinline__ IsoEdge iso_edge_load(const StatArgs &A, int p1, int p2) {
+  IsoEdge e;
+  e.c1 = sld3(A, p1);
+  e.c2 = sld3(A, p2);
+  e.h1 = smet(A, p1)[0];
+  e.h2 = smet(A, p2)[0];
+  __builtin_amdgcn_sched_barrier(0);
+  return e;
+}
+__device__ __forceinline__ double iso_edge_len(const IsoEdge &e) {
+  double ux = e.c2.x - e.c1.x, uy = e.c2.y - e.c1.y, uz = e.c2.z - e.c1.z;
+  double l = ux * ux + uy * uy + uz * uz;
+  l = sqrt(l);
+  double r = e.h2 / e.h1 - 1.0;
+  return (fabs(r) < PMX_EPS) ? (l / e.h1) : (l / (e.h2 - e.h1) * pmx_log1p(r));
+}
+
 // MMG5_lenEdg_iso / lenEdg33_ani (restated, unpinned; the surface lengths
 // MMG5_lenSurfEdg_iso / lenSurfEdg33_ani of the parallel edges take the same
 // formulas in classic metric storage)
 template <bool ANI>
 __device__ __forceinline__ double edge_len_t(const StatArgs &A, int p1, int p2) {
-  D3 c1 = sld3(A, p1), c2 = sld3(A, p2);
   if (ANI) {
+    D3 c1 = sld3(A, p1), c2 = sld3(A, p2);
     double ux = c2.x - c1.x, uy = c2.y - c1.y, uz = c2.z - c1.z;
     const double *m1 = smet(A, p1), *m2 = smet(A, p2);
     double dd1 = mlen2(m1, ux, uy, uz);
@@ -441,15 +463,8 @@ __device__ __forceinline__ double edge_len_t(const StatArgs &A, int p1, int p2) 
     if (dd2 <= 0.0) dd2 = 0.0;
     return (sqrt(dd1) + sqrt(dd2) + 4.0 * sqrt(0.5 * (dd1 + dd2))) / 6.0;
   }
-  double h1 = smet(A, p1)[0], h2 = smet(A, p2)[0];
-  // the sizes' loads issued with the coordinates' (the scheduler otherwise
-  // places them after the wait for the coordinates: a second round trip)
-  __builtin_amdgcn_sched_barrier(0);
-  double ux = c2.x - c1.x, uy = c2.y - c1.y, uz = c2.z - c1.z;
-  double l = ux * ux + uy * uy + uz * uz;
-  l = sqrt(l);
-  double r = h2 / h1 - 1.0;
-  return (fabs(r) < PMX_EPS) ? (l / h1) : (l / (h2 - h1) * pmx_log1p(r));
+  const IsoEdge e = iso_edge_load(A, p1, p2);
+  return iso_edge_len(e);
 }
 __device__ double edge_len(const StatArgs &A, int p1, int p2) {
   return A.msize == 6 ? edge_len_t<true>(A, p1, p2) : edge_len_t<false>(A, p1, p2);
@@ -798,6 +813,19 @@ __device__ __forceinline__ TetRec shell_rec(const StatArgs &A, const TetRec (*sr
   return TetRec{{lv.x, lv.y, lv.z, lv.w}, {ln.x, ln.y, ln.z, ln.w}};
 }
 
+// A shell record from HBM / L2, unconditionally (index 0: the unused slot
+// 0).  No LDS path and no select on the loaded value: with either, the
+// compiler turns the load into a branch (a select of a single-use load
+// becomes a branch), and a conditional load makes it wait for every load in
+// flight at the next join -- here the number of loads in flight is the same
+// on every path, so the length's arithmetic overlaps the second step's
+// records.
+__device__ __forceinline__ TetRec shell_rec_g(const StatArgs &A, int c) {
+  const int4 *g = reinterpret_cast<const int4 *>(A.tets) + 2 * (int64_t)c;
+  const int4 gv = g[0], gn = g[1];
+  return TetRec{{gv.x, gv.y, gv.z, gv.w}, {gn.x, gn.y, gn.z, gn.w}};
+}
+
 // True iff no admissible tet with index < k contains the edge (a, b) of tet
 // k.  The shell is rotated from k through the two faces of k that contain the
 // edge (cursors c0, c1; keep0/keep1 = the vertex of the face just crossed),
@@ -850,15 +878,18 @@ __device__ __forceinline__ bool owns_edge(const StatArgs &A, const TetRec (*srec
 // cursors meet), then owns_edge's loop for a longer shell.  The same
 // decisions in the same order as owns_edge<false, L>; the loop's early
 // returns become a "decided" mask, so the wave issues no branch per check.
-template <bool L>
-__device__ __forceinline__ bool owns_edge_flat(const StatArgs &A, const TetRec (*srec)[256], long long kb0,
-                                               long long kb1, int64_t k64, int a, int b, int c0, int c1, int keep0,
-                                               int keep1, TetRec r0, TetRec r1) {
-  using KT = typename std::conditional<L, int, int64_t>::type;
-  const KT k = (KT)k64;
+// The steps are separate calls so that the caller can put work between them:
+// k_prilen evaluates the edge's length while the second step's records load.
+template <bool L, bool G>
+struct FlatRot {
+  int c0, c1, keep0, keep1;
+  TetRec r0, r1;
+  int i0, i1;                                      // where r0 / r1 were loaded from
   bool done = false, own = true;
-#pragma unroll
-  for (int it = 0; it < 2; it++) {
+  __device__ __forceinline__ void step(const StatArgs &A, const TetRec (*srec)[256], long long kb0, long long kb1,
+                                       int64_t k64, int a, int b) {
+    using KT = typename std::conditional<L, int, int64_t>::type;
+    const KT k = (KT)k64;
     c0 = (c0 == (int)k) ? 0 : c0;
     c1 = (c1 == (int)k) ? 0 : c1;
     // the checks of owns_edge's loop head, first decision wins
@@ -877,12 +908,23 @@ __device__ __forceinline__ bool owns_edge_flat(const StatArgs &A, const TetRec (
     const bool d_small2 = (need0 && c0 < k) || (need1 && c1 < k);
     own = done ? own : !d_small2;
     done = done || d_small2 || (need0 && c0 == c1);
-    if (!done && need0) r0 = shell_rec<L>(A, srec, kb0, kb1, c0);
-    if (!done && need1) r1 = shell_rec<L>(A, srec, kb0, kb1, c1);
+    if constexpr (G) {
+      // a record not needed is reloaded from where it came (same value)
+      i0 = (!done && need0) ? c0 : i0;
+      i1 = (!done && need1) ? c1 : i1;
+      r0 = shell_rec_g(A, i0);
+      r1 = shell_rec_g(A, i1);
+    } else {
+      if (!done && need0) r0 = shell_rec<L>(A, srec, kb0, kb1, c0);
+      if (!done && need1) r1 = shell_rec<L>(A, srec, kb0, kb1, c1);
+    }
   }
-  if (done) return own;
-  return owns_edge<false, L>(A, srec, kb0, kb1, k64, a, b, c0, c1, keep0, keep1, r0, r1);
-}
+  __device__ __forceinline__ bool finish(const StatArgs &A, const TetRec (*srec)[256], long long kb0, long long kb1,
+                                         int64_t k64, int a, int b) {
+    if (done) return own;
+    return owns_edge<false, L>(A, srec, kb0, kb1, k64, a, b, c0, c1, keep0, keep1, r0, r1);
+  }
+};
 
 // ---- prilen: unique edges by shell ownership, one pass ------------------------
 //
@@ -911,7 +953,7 @@ __device__ __forceinline__ bool owns_edge_flat(const StatArgs &A, const TetRec (
 template <bool ANI, bool TAGS, bool PAR, int W = 1, bool L = false, bool SURF = false, int X = 0>
 __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
   __shared__ TetRec srec[2][256];
-  __shared__ unsigned short q[LEN_QCAP];
+  __shared__ unsigned short q[LEN_QCAP + 2];     // + the spare entry of unset slots
   __shared__ unsigned wcnt[4];
   __shared__ long long kbase[2];                 // first tet of each LDS buffer
   __shared__ unsigned lcnt[10];
@@ -980,23 +1022,36 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
       if (k <= k1) {
         const int v[4] = {t.v[0], t.v[1], t.v[2], t.v[3]};
         if (t.v[0] > 0 && !(TAGS && tet_4ridge(A, v))) {
+          m = 0x3fu;
+          if constexpr (!TAGS) {
+            // a face neighbour with a smaller index disowns the face's three
+            // edges (those not through the opposite local vertex f):
+            // f = 0: edges 3,4,5; 1: 1,2,5; 2: 0,2,4; 3: 0,1,3 -- the same
+            // test as "n0 or n1 smaller" per edge, n0/n1 = the neighbours
+            // across the two faces that hold it
+            const unsigned emask[4] = {0x38u, 0x26u, 0x15u, 0x0bu};
 #pragma unroll
-          for (int ia = 0; ia < 6; ia++) {
-            const int n0 = pick_nb(t, oth0(ia)), n1 = pick_nb(t, oth1(ia));
-            if (!TAGS && ((n0 && n0 < k) || (n1 && n1 < k))) continue;   // disowned
-            m |= 1u << ia;
+            for (int f = 0; f < 4; f++) {
+              const int n = t.nb[f];
+              bool sm;
+              if constexpr (L) sm = (unsigned)n - 1u < (unsigned)k - 1u;   // 1 <= n < k
+              else sm = n && n < k;
+              m &= sm ? ~emask[f] : ~0u;
+            }
           }
         }
       }
-      // ring positions in (thread, ia) order: wave prefix + wave offsets
-      const unsigned c = __popc(m);
-      unsigned pre = c;
+      // ring positions in (thread, ia) order: the wave's exclusive prefix of
+      // the per-thread counts through one ballot per edge slot (mbcnt), the
+      // wave totals in LDS
+      unsigned pre = 0, wtot = 0;
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const unsigned y = __shfl_up(pre, o, 64);
-        if ((int)lane >= o) pre += y;
+      for (int ia = 0; ia < 6; ia++) {
+        const unsigned long long bb = __ballot((m >> ia) & 1u);
+        pre = __builtin_amdgcn_mbcnt_hi((unsigned)(bb >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bb, pre));
+        wtot += (unsigned)__popcll(bb);
       }
-      if (lane == 63) wcnt[wv] = pre;
+      if (lane == 0) wcnt[wv] = wtot;
       __syncthreads();
       unsigned base = 0, total = 0;
       for (unsigned w = 0; w < 4; w++) {
@@ -1004,10 +1059,14 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
         total += wcnt[w];
       }
       total = __builtin_amdgcn_readfirstlane(total);
-      unsigned pos = tail + base + pre - c;
+      unsigned pos = tail + base + pre;
+      // unconditional stores: an unset slot writes the spare entry q[LEN_QCAP]
 #pragma unroll
-      for (int ia = 0; ia < 6; ia++)
-        if ((m >> ia) & 1u) q[(pos++) & (LEN_QCAP - 1)] = (unsigned short)((buf << 11) | (tid << 3) | ia);
+      for (int ia = 0; ia < 6; ia++) {
+        const unsigned bit = (m >> ia) & 1u;
+        q[bit ? (pos & (LEN_QCAP - 1)) : LEN_QCAP] = (unsigned short)((buf << 11) | (tid << 3) | ia);
+        pos += bit;
+      }
       __syncthreads();
       tail += total;
     }
@@ -1034,11 +1093,27 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
         const int c0 = sn[o0], c1 = sn[o1];
         // the first rotation step's records, issued with the points' loads
         TetRec r0{}, r1{};
-        if constexpr (!(X & 2)) {
+        // FLAT: the rotation's first two steps as straight-line selects (no
+        // point tags); GREC (X bit 3): the flat steps' records always from
+        // HBM / L2, no LDS path; EARLY (X bit 4): the first step before the
+        // length (its records wanted first), the second step's loads in flight
+        // during the length's arithmetic
+        constexpr bool FLAT = !(X & 6) && !TAGS;
+        constexpr bool GREC = FLAT && (X & 8);
+        constexpr bool EARLY = FLAT && (X & 16) && !ANI && !SURF && !(X & 1);
+        if constexpr (GREC) {
+          r0 = shell_rec_g(A, c0);
+          r1 = shell_rec_g(A, c1);
+        } else if constexpr (!(X & 2)) {
           if (c0) r0 = shell_rec<L>(A, srec, kb0, kb1, c0);
           if (c1) r1 = shell_rec<L>(A, srec, kb0, kb1, c1);
         }
-        if constexpr (SURF) {
+        FlatRot<L, GREC> fr{c0, c1, keep0, keep1, r0, r1, c0, c1};
+        if constexpr (EARLY) {
+          const IsoEdge e = iso_edge_load(A, a, b);   // in flight during the step
+          fr.step(A, srec, kb0, kb1, kk, a, b);
+          len = iso_edge_len(e);
+        } else if constexpr (SURF) {
           const int vv[4] = {sv[0], sv[1], sv[2], sv[3]};
           len = len_tet_ani(A, vv, ia, a, b, A.etag ? (unsigned)A.etag[kk] : 0u);
         } else if constexpr (X & 1) {
@@ -1047,10 +1122,11 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
           len = edge_len_t<ANI>(A, a, b);
         }
         if constexpr (X & 2) on = true;
-        else if constexpr (!(X & 4) && !TAGS)
-          on = owns_edge_flat<L>(A, srec, kb0, kb1, kk, a, b, c0, c1, keep0, keep1, r0, r1) &&
-               !(PAR && par_excluded(A, a, b));
-        else
+        else if constexpr (FLAT) {
+          if constexpr (!EARLY) fr.step(A, srec, kb0, kb1, kk, a, b);
+          fr.step(A, srec, kb0, kb1, kk, a, b);
+          on = fr.finish(A, srec, kb0, kb1, kk, a, b) && !(PAR && par_excluded(A, a, b));
+        } else
           on = owns_edge<TAGS, L>(A, srec, kb0, kb1, kk, a, b, c0, c1, keep0, keep1, r0, r1) &&
                !(PAR && par_excluded(A, a, b));
         if constexpr (L) key = LEN_STEP2 + (long long)(6u * (unsigned)kk + (unsigned)ia);   // 6 ne < 2^32
@@ -1689,22 +1765,29 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
       k_prilen<true, true, false, 1, true, true>,   k_prilen<true, true, true, 1, true, true>};
   const bool surf = ani && (ctx->have_surf || A.ridmet);
   KFn kern = surf ? kfs[(lean ? 4 : 0) | (sel & 3)] : kfn[sel];
-  // measurement variants of the default iso kernel (PMX_PRILEN_EXP=1..3 with
-  // PMX_EXPERIMENTS=1: results are wrong by design; 4: the r05 rotation loop)
+  // measurement variants of the default iso kernel: PMX_PRILEN_EXP=1..3 with
+  // PMX_EXPERIMENTS=1 (results wrong by design: the VALU breakdown), 4 the r05
+  // rotation loop, 8 / 16 / 24 the flat rotation's record and order variants
+  // (same results)
   {
     static const int xp = [] {
       const char *e = getenv("PMX_PRILEN_EXP"), *x = getenv("PMX_EXPERIMENTS");
       const int v = e ? atoi(e) : 0;
-      // 4: the rotation loop (same results, no PMX_EXPERIMENTS needed)
-      if (v == 4) return 4;
+      if (v == 4 || v == 8 || v == 16 || v == 24) return v;
       return (e && x && x[0] == '1') ? std::max(0, std::min(3, v)) : 0;
     }();
-    static const KFn kx[5] = {k_prilen<false, false, false, 5, true>,
-                              k_prilen<false, false, false, 5, true, false, 1>,
-                              k_prilen<false, false, false, 5, true, false, 2>,
-                              k_prilen<false, false, false, 5, true, false, 3>,
-                              k_prilen<false, false, false, 5, true, false, 4>};
-    if (xp && sel == 8 && !surf) kern = kx[xp];
+    KFn kv = nullptr;
+    switch (xp) {
+      case 1: kv = k_prilen<false, false, false, 5, true, false, 1>; break;
+      case 2: kv = k_prilen<false, false, false, 5, true, false, 2>; break;
+      case 3: kv = k_prilen<false, false, false, 5, true, false, 3>; break;
+      case 4: kv = k_prilen<false, false, false, 5, true, false, 4>; break;
+      case 8: kv = k_prilen<false, false, false, 5, true, false, 8>; break;
+      case 16: kv = k_prilen<false, false, false, 5, true, false, 16>; break;
+      case 24: kv = k_prilen<false, false, false, 5, true, false, 24>; break;
+      default: break;
+    }
+    if (kv && sel == 8 && !surf) kern = kv;
   }
   int nb = stat_blocks(ctx->ne);
   A.sched_chunk = 0;

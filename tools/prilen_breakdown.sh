@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
 out=gpurun_out/prilen_$tag
 mkdir -p $out
-for x in 0 1 2 3 4; do
+for x in ${PRILEN_VARIANTS:-0 1 2 3 4}; do
   PMX_EXPERIMENTS=1 PMX_PRILEN_EXP=$x timeout -k 10 200 python3 tools/bench_stats.py --reps 5 $args \
     > $out/time_x$x.json 2> $out/time_x$x.err || { echo "time x$x failed"; exit 2; }
   PMX_EXPERIMENTS=1 PMX_PRILEN_EXP=$x timeout -s KILL 150 rocprofv3 --kernel-trace \

@@ -297,7 +297,9 @@ class Transfer:
         keys ``old_mesh`` (Mesh), ``old_met`` ((np+1,size) or None),
         ``old_fields`` (list), ``xyz`` (new points, (np+1,3) Mmg layout),
         ``tags`` (uint16, np+1), ``met`` / ``fields`` (output arrays in Mmg
-        layout, written in place), ``hsiz``."""
+        layout, written in place), ``hsiz``, optionally ``tets`` (the new
+        tets, (ne+1, 4) in Mmg's 1-based layout: the orphan rule and, with
+        PMX_SEQUENTIAL set, the reference's visit order)."""
         keep = []
         G = (N.Group * len(groups))()
         for g, d in zip(G, groups):
@@ -307,6 +309,10 @@ class Transfer:
             g.points.first, g.points.last = 1, xyz.shape[0] - 1
             g.points.c, g.points.stride = _dp(xyz), 24
             g.points.tag, g.points.tag_stride = tags.ctypes.data_as(N.u16ptr), 2
+            if d.get("tets") is not None:             # Mmg layout: (ne+1, 4), 1-based, v[0] = 0 deleted
+                tv = np.ascontiguousarray(d["tets"], np.int32)
+                keep.append(tv)
+                g.points.tetra_v, g.points.tetra_stride, g.points.ne = _ip(tv), 16, tv.shape[0] - 1
             g.hsiz = d.get("hsiz", 0.0)
             om = mesh_view(d["old_mesh"])
             keep.append(om)

@@ -415,18 +415,34 @@ pmx_ctx *pmx_create(int device) {
     mmain.assign((size_t)(ncu + 31) / 32, 0u);
     for (int c = 0; c < ncu; c++) (c < side_cus ? mside : mmain)[c / 32] |= 1u << (c % 32);
   }
-  if ((mmain.empty() ? hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking)
-                     : hipExtStreamCreateWithCUMask(&ctx->own, (uint32_t)mmain.size(), mmain.data())) !=
-      hipSuccess) {
-    delete ctx;
-    return nullptr;
-  }
+  // HIP maps a process's streams onto a few hardware queues (4 by default,
+  // GPU_MAX_HW_QUEUES) in creation order: a second context's streams share
+  // the first one's queues, and two streams on one queue run one after the
+  // other.  Contexts alternate their creation order so that the second one's
+  // main and surface streams land on the first one's idle residency (topo)
+  // and short-lived orphan-mark (up) queues instead of behind its walk
+  // (PMX_interpMetricsAndFields runs two groups' steps side by side).
+  static std::atomic<unsigned> n_created{0};
+  const bool odd = (n_created.fetch_add(1) & 1u) != 0;
+  auto mk_main = [&] {
+    return mmain.empty() ? hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking)
+                         : hipExtStreamCreateWithCUMask(&ctx->own, (uint32_t)mmain.size(), mmain.data());
+  };
+  auto mk_side = [&] {
+    return mside.empty() ? hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking)
+                         : hipExtStreamCreateWithCUMask(&ctx->side, (uint32_t)mside.size(), mside.data());
+  };
+  bool sok;
+  if (!odd)
+    sok = mk_main() == hipSuccess && mk_side() == hipSuccess &&
+          hipStreamCreateWithFlags(&ctx->up, hipStreamNonBlocking) == hipSuccess &&
+          hipStreamCreateWithFlags(&ctx->topo, hipStreamNonBlocking) == hipSuccess;
+  else
+    sok = hipStreamCreateWithFlags(&ctx->topo, hipStreamNonBlocking) == hipSuccess &&
+          hipStreamCreateWithFlags(&ctx->up, hipStreamNonBlocking) == hipSuccess && mk_main() == hipSuccess &&
+          mk_side() == hipSuccess;
   ctx->stream = ctx->own;
-  if ((mside.empty() ? hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking)
-                     : hipExtStreamCreateWithCUMask(&ctx->side, (uint32_t)mside.size(), mside.data())) !=
-          hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->topo, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->up, hipStreamNonBlocking) != hipSuccess ||
+  if (!sok ||
       hipEventCreateWithFlags(&ctx->ev_topo, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_tets, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc((void **)&ctx->h_nbad, 8 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess ||
@@ -465,7 +481,7 @@ void pmx_destroy(pmx_ctx *ctx) {
   if (ctx->peer) pmx_destroy(ctx->peer);
   ctx->peer = nullptr;
   hipSetDevice(ctx->device);
-  hipStreamSynchronize(ctx->stream);
+  if (ctx->stream) hipStreamSynchronize(ctx->stream);
   if (ctx->side) hipStreamSynchronize(ctx->side);
   if (ctx->topo) hipStreamSynchronize(ctx->topo);
   if (ctx->up) hipStreamSynchronize(ctx->up);

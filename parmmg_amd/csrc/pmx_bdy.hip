@@ -1311,12 +1311,31 @@ bool pmx_ctx::seq_replay(const VolArgs &a, hipStream_t s, bool surf, bool vol) {
     // the replay on the reference's tet flags
     hipLaunchKernelGGL(k_seq_starts, dim3(nbp), dim3(256), 0, s, (const int *)vseq, (const int *)(nseq + 1),
                        (const int *)d_elem.p, sstart);
-    SeqVolArgs SV{vseq, nseq + 1, sstart, sbase, d_sqw.p, d_sqtv.p, ctl + 4, vstk_list, nreplay + 1};
+    SeqVolArgs SV{vseq, nseq + 1, sstart, sbase, d_sqw.p, d_sqtv.p, ctl + 4, vstk_list, nreplay + 1, nullptr, nullptr};
     // the overflow pass's hash tables: generation 0 = empty (positions start at 1)
     if (!pmx_dgrow(this, d_sqows, seqv_ovf_ws_ints()) ||
         !ck(hipMemsetAsync(d_sqows.p, 0, seqv_ovf_ws_ints() * sizeof(int), s), "memset"))
       return false;
     launch_seqv_spec(a, SV, nq_vol_ub, d_sqows.p, s);
+    // the replay's candidates: positions whose speculative start may be wrong,
+    // in visit order (DeviceSelect keeps the order)
+    {
+      size_t sel_b = 0;
+      hipcub::CountingInputIterator<int> it(0);
+      if (!ck(hipcub::DeviceSelect::Flagged(nullptr, sel_b, it, (const uint8_t *)nullptr, (int *)nullptr,
+                                            (int *)nullptr, (int)nq_vol_ub, s),
+              "select") ||
+          !pmx_dgrow(this, d_sqflag, (size_t)nq_vol_ub) || !pmx_dgrow(this, d_sqcand, (size_t)nq_vol_ub + 1) ||
+          !pmx_dgrow(this, d_sqtmp, sel_b))
+        return false;
+      launch_seqv_flags(a, SV, nq_vol_ub, d_sqflag.p, s);
+      if (!ck(hipcub::DeviceSelect::Flagged(d_sqtmp.p, sel_b, it, (const uint8_t *)d_sqflag.p, d_sqcand.p + 1,
+                                            d_sqcand.p, (int)nq_vol_ub, s),
+              "select"))
+        return false;
+      SV.ncand = d_sqcand.p;
+      SV.cand = d_sqcand.p + 1;
+    }
     if (!ck(hipMemsetAsync(d_sqtv.p, 0, (size_t)(ne + 1) * sizeof(int), s), "memset")) return false;
     int hctl[4] = {0, 1, 0, 0};
     if (!ck(hipMemcpyAsync(ctl + 4, hctl, sizeof hctl, hipMemcpyHostToDevice, s), "ctl")) return false;

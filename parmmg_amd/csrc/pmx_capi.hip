@@ -2079,6 +2079,8 @@ void pmx_ctx::free_all() {
   dfree(d_sqkey); dfree(d_sqidx); dfree(d_sqint); dfree(d_sqtf); dfree(d_sqpf); dfree(d_sqtv); dfree(d_sqows); dfree(d_sqval);
   dfree(d_sqw);
   dfree(d_sqtmp);
+  dfree(d_sqflag);
+  dfree(d_sqcand);
   dfree(d_qual); dfree(d_red); dfree(d_blist); dfree(d_olist); dfree(d_ows);
   dfree(d_ptag); dfree(d_touch); dfree(d_cidx); dfree(d_intv); dfree(d_pub); dfree(d_pkey);
   dfree(d_ppt); dfree(d_pedge); dfree(d_ntetv); dfree(d_nqual); dfree(d_qtag); dfree(d_gather);

@@ -122,7 +122,8 @@ struct pmx_ctx {
   DevBuf<unsigned> d_sqkey;
   DevBuf<int> d_sqidx, d_sqint, d_sqtf, d_sqpf, d_sqtv, d_sqows;
   DevBuf<unsigned long long> d_sqval;
-  DevBuf<uint8_t> d_sqw;
+  DevBuf<uint8_t> d_sqw, d_sqflag;
+  DevBuf<int> d_sqcand;                 // [0] count, then the volume replay's candidate positions
   DevBuf<char> d_sqtmp;
   unsigned seq_stats[4] = {0, 0, 0, 0};   // surface replays / sequence, volume replays / sequence
   int64_t seq_stats_n = -1;             // -1: the last step was not sequential

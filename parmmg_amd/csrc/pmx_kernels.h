@@ -152,11 +152,15 @@ struct SeqVolArgs {
   int *ctl;
   int *stk_list;
   unsigned *nreplay;
+  const int *cand, *ncand;   // the positions whose speculative start may be wrong (sorted)
 };
 // the speculative pass and its overflow pass (workspace: seqv_ovf_ws_ints() ints)
 size_t seqv_ovf_ws_ints();
 void launch_seqv_spec(const VolArgs &a, const SeqVolArgs &s, int64_t nmax, int *ws, hipStream_t st);
 void launch_seqv_resolve(const VolArgs &a, const SeqVolArgs &s, hipStream_t st);
+// flags[j] (j < nmax) = position j of the volume sequence must be checked by
+// the replay: not sure, or its start is not its predecessor's speculative tet
+void launch_seqv_flags(const VolArgs &a, const SeqVolArgs &s, int64_t nmax, uint8_t *flags, hipStream_t st);
 // workgroups of k_fallback that can be co-resident with `share` other
 // launches of it on this device (0 on error)
 int fallback_coresident_blocks(int device, int share);

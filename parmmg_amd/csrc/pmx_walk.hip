@@ -839,75 +839,91 @@ __global__ __launch_bounds__(256) void k_seqv_ovf(VolArgs A, SeqVolArgs S, int *
   }
 }
 
-// the replay: one wavefront; ctl = {next position, its start (-1: the tet of
-// the previous point), state (0 done, 1 stuck: the host scans), the point}
+// the positions the replay must look at: a point whose speculative walk is
+// not sure, or started from another tet than its predecessor's speculative
+// result (ties, walks into deleted tets); position 0 starts from tet 1
+__global__ __launch_bounds__(256) void k_seqv_flags(VolArgs A, SeqVolArgs S, int64_t nmax, uint8_t *flags) {
+  const int n = *S.nvseq;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nmax; j += (int64_t)gridDim.x * blockDim.x) {
+    bool bad = false;
+    if (j < n) {
+      const int i = S.vseq[j];
+      const int want = j == 0 ? 1 : A.elem[S.vseq[j - 1]];
+      bad = !(S.sure[i] && S.sstart[i] == want);
+    }
+    flags[j] = bad ? 1 : 0;
+  }
+}
+
+// the replay: one lane, in visit order; ctl = {next position, its start (-1:
+// the tet of the previous point, after a stuck walk the host resolved),
+// state (0 done, 1 stuck: the host scans), the point}.  A position is looked
+// at when it is a candidate (S.cand) or when its predecessor was replayed
+// ("dirty"): every other point's speculative start is its predecessor's
+// final tet, so its speculative result stands.  (r06 first version scanned
+// all n positions with the wave: 0.40 s of C3's 0.65-s sequential step.)
 __global__ __launch_bounds__(64) void k_seqv_resolve(VolArgs A, SeqVolArgs S) {
-  const int lane = threadIdx.x;
+  if (threadIdx.x != 0) return;
   const int n = *S.nvseq;
   int j = S.ctl[0];
   int prev = S.ctl[1];
   if (j >= n) return;
+  bool dirty = prev < 0;                         // resumed after a stuck walk
   if (prev < 0) prev = A.elem[S.vseq[j - 1]];
+  const int nc = *S.ncand;
+  int lo = 0, hi = nc;                           // first candidate >= j
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (S.cand[mid] < j) lo = mid + 1;
+    else hi = mid;
+  }
+  int pos = lo;
   unsigned replays = 0;
   while (j < n) {
-    const int jj = j + lane;
-    bool okk = false;
-    if (jj < n) {
-      const int i = S.vseq[jj];
-      const int want = lane == 0 ? prev : A.elem[S.vseq[jj - 1]];
-      okk = S.sure[i] && S.sstart[i] == want;
-    }
-    const int nvalid = min(64, n - j);
-    const unsigned long long mask = nvalid == 64 ? ~0ull : ((1ull << nvalid) - 1ull);
-    const unsigned long long bad = ~__ballot(okk) & mask;
-    if (!bad) {
-      prev = A.elem[S.vseq[j + nvalid - 1]];
-      j += nvalid;
-      continue;
-    }
-    const int f = __ffsll((long long)bad) - 1;
-    if (f > 0) prev = A.elem[S.vseq[j + f - 1]];
-    j += f;
-    int r = 1, nk = 0;
-    if (lane == 0) {
-      const int i = S.vseq[j];
-      const D3 p{A.q[3 * (int64_t)i], A.q[3 * (int64_t)i + 1], A.q[3 * (int64_t)i + 2]};
-      SeqvGlobVis vs{S.tf, S.sbase[i]};
-      int k, step;
-      double lam[4];
-      A.start[i] = prev;
-      r = ref_walk(A, vs, p, prev, k, lam, step);
-      replays++;
-      if (r == 1) {
-        seqv_finish(A, i, k, lam, 1, step);
-        nk = k;
-      } else if (r == 4) {
-        if (k > 0) closest_vertex(A, k, p, lam);
-        seqv_finish(A, i, k, lam, 0, step);
-        nk = k;
-        r = 1;
-      } else {                                      // stuck: the exhaustive scan
-        A.steps[i] = -step;
-        S.stk_list[0] = i;
-        S.ctl[0] = j;
-        S.ctl[2] = 1;
-        S.ctl[3] = i;
+    if (!dirty) {
+      while (pos < nc && S.cand[pos] < j) pos++;
+      if (pos >= nc) break;                      // every later speculative result stands
+      const int c = S.cand[pos];
+      if (c > j) {
+        prev = A.elem[S.vseq[c - 1]];
+        j = c;
       }
     }
-    r = __shfl(r, 0, 64);
-    nk = __shfl(nk, 0, 64);
-    if (r != 1) {
-      if (lane == 0) atomicAdd(S.nreplay, replays);
+    const int i = S.vseq[j];
+    if (S.sure[i] && S.sstart[i] == prev) {      // the speculative walk started right
+      prev = A.elem[i];
+      dirty = false;
+      j++;
+      continue;
+    }
+    const D3 p{A.q[3 * (int64_t)i], A.q[3 * (int64_t)i + 1], A.q[3 * (int64_t)i + 2]};
+    SeqvGlobVis vs{S.tf, S.sbase[i]};
+    int k, step;
+    double lam[4];
+    A.start[i] = prev;
+    const int r = ref_walk(A, vs, p, prev, k, lam, step);
+    replays++;
+    if (r == 1) {
+      seqv_finish(A, i, k, lam, 1, step);
+    } else if (r == 4) {
+      if (k > 0) closest_vertex(A, k, p, lam);
+      seqv_finish(A, i, k, lam, 0, step);
+    } else {                                      // stuck: the exhaustive scan
+      A.steps[i] = -step;
+      S.stk_list[0] = i;
+      S.ctl[0] = j;
+      S.ctl[2] = 1;
+      S.ctl[3] = i;
+      atomicAdd(S.nreplay, replays);
       return;
     }
-    prev = nk;
+    prev = k;
+    dirty = true;
     j++;
   }
-  if (lane == 0) {
-    S.ctl[0] = n;
-    S.ctl[2] = 0;
-    atomicAdd(S.nreplay, replays);
-  }
+  S.ctl[0] = n;
+  S.ctl[2] = 0;
+  atomicAdd(S.nreplay, replays);
 }
 
 size_t seqv_ovf_ws_ints() { return (size_t)SEQV_OVF_THREADS * SEQV_OVF_CAP * 2; }
@@ -915,6 +931,10 @@ void launch_seqv_spec(const VolArgs &a, const SeqVolArgs &s, int64_t nmax, int *
   const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((nmax + 255) / 256, 65536));
   hipLaunchKernelGGL(k_seqv_spec, dim3((unsigned)nb), dim3(256), 0, st, a, s);
   hipLaunchKernelGGL(k_seqv_ovf, dim3(SEQV_OVF_THREADS / 256), dim3(256), 0, st, a, s, ws);
+}
+void launch_seqv_flags(const VolArgs &a, const SeqVolArgs &s, int64_t nmax, uint8_t *flags, hipStream_t st) {
+  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((nmax + 255) / 256, 65536));
+  hipLaunchKernelGGL(k_seqv_flags, dim3((unsigned)nb), dim3(256), 0, st, a, s, nmax, flags);
 }
 void launch_seqv_resolve(const VolArgs &a, const SeqVolArgs &s, hipStream_t st) {
   hipLaunchKernelGGL(k_seqv_resolve, dim3(1), dim3(64), 0, st, a, s);

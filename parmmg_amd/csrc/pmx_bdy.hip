@@ -789,13 +789,16 @@ __device__ __forceinline__ bool fan_turn(const TriRec *__restrict__ tris, int k,
 // (a ~35-deep dependent chain) 0.19 ms; only the local minima walking and the
 // owner sorting in LDS (2.3 M walks -> 0.8 M, but serial chains in few
 // threads) 0.23 ms, step 2.061 vs 2.042 ms (profiles/r05_c3_sweep_fans_owner_lds.log).
-// vcount (the upload's check only): every vertex's tria count; a fan that
-// closes without all of them (a vertex where two surface sheets touch: a
-// group pinched at a vertex) counts as bad
+// vown (the check only): each fan's owner slot writes its window base at
+// its vertex; k_fan_check then finds the vertices whose slots belong to more
+// than one fan (two surface sheets touching at a vertex: a group pinched
+// there), which the rotation alone cannot see.  No per-vertex counts, no
+// np-sized memset: every surface vertex has at least one fan owner, and no
+// other vertex is read.  (r06 first version: a per-vertex tria count by
+// atomics after an np-sized memset, 0.24 ms at C3 beside the step's prefix.)
 __global__ __launch_bounds__(256) void k_fan_rotate(const TriRec *__restrict__ tris, int64_t nt,
                                                     int2 *__restrict__ range, int *__restrict__ list,
-                                                    unsigned *__restrict__ bad,
-                                                    const unsigned *__restrict__ vcount) {
+                                                    unsigned *__restrict__ bad, int *__restrict__ vown) {
   unsigned nbad = 0;
   for (int64_t i = 3 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 3 * (nt + 1);
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -808,22 +811,43 @@ __global__ __launch_bounds__(256) void k_fan_rotate(const TriRec *__restrict__ t
       rank += g < k ? 1 : 0;
       if (g < own) { own = g; lown = c; }
     });
-    if (!ok || (vcount && vcount[sel3(t0.v, l)] != (unsigned)n)) { nbad++; range[i] = make_int2(0, 0); continue; }
+    if (!ok) { nbad++; range[i] = make_int2(0, 0); continue; }
     const int base = (int)((3 * (int64_t)own + lown - 3) * FAN_CAP);
     range[i] = make_int2(base, base + n);
     list[base + rank] = k;
+    if (vown && own == k && lown == l) vown[sel3(t0.v, l)] = base;
+  }
+  for (int o = 32; o > 0; o >>= 1) nbad += __shfl_xor(nbad, o);
+  if ((threadIdx.x & 63) == 0 && nbad) atomicAdd(bad, nbad);
+}
+__global__ __launch_bounds__(256) void k_fan_check(const TriRec *__restrict__ tris, int64_t nt,
+                                                   const int2 *__restrict__ range, const int *__restrict__ vown,
+                                                   unsigned *__restrict__ bad) {
+  unsigned nbad = 0;
+  for (int64_t i = 3 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 3 * (nt + 1);
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int2 r = range[i];
+    if (r.y <= r.x) continue;                      // deleted tria (a failed fan is counted already)
+    const int k = (int)(i / 3), l = (int)(i - 3 * (int64_t)k);
+    const int v = tris[k].v[l];
+    if (vown[v] != r.x) nbad++;
   }
   for (int o = 32; o > 0; o >>= 1) nbad += __shfl_xor(nbad, o);
   if ((threadIdx.x & 63) == 0 && nbad) atomicAdd(bad, nbad);
 }
 
-bool pmx_ctx::fan_rotation(hipStream_t s, unsigned *d_bad, const unsigned *vcount) {
+bool pmx_ctx::fan_rotation(hipStream_t s, unsigned *d_bad, bool check) {
   const int64_t m = 3 * nt;
   if (!pmx_dgrow(this, d_ntrange, (size_t)(3 * (nt + 1))) || !pmx_dgrow(this, d_ntlist, (size_t)(m * FAN_CAP)))
     return false;
+  if (check && !pmx_dgrow(this, d_ntkey, (size_t)(np + 2))) return false;
+  int *vown = check ? reinterpret_cast<int *>(d_ntkey.p) : nullptr;
   const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>((m + 255) / 256, 16384));
   hipLaunchKernelGGL(k_fan_rotate, dim3(nb), dim3(256), 0, s, d_tris.p, nt, d_ntrange.p, d_ntlist.p, d_bad,
-                     vcount);
+                     vown);
+  if (check)
+    hipLaunchKernelGGL(k_fan_check, dim3(nb), dim3(256), 0, s, d_tris.p, nt, (const int2 *)d_ntrange.p,
+                       (const int *)vown, d_bad);
   if (hipGetLastError() != hipSuccess) {
     err = "node trias: launch";
     return false;
@@ -841,8 +865,8 @@ bool pmx_ctx::check_fans(hipStream_t s) {
   if (nt < 1 || 3 * (nt + 1) * (int64_t)FAN_CAP > (int64_t)INT32_MAX) return true;   // int windows
   const char *e = getenv("PMX_FAN_ROTATION");
   if (e && e[0] == '0') return true;
-  // every vertex's tria count (np-sized, at the upload only): a fan walked
-  // around one sheet of a vertex where several touch closes short of it
+  // the vertices' fan owners (np-sized, no memset): a vertex where several
+  // surface sheets touch has more than one fan
   if (!pmx_dgrow(this, d_wfar, 8)) return false;
   if (!pmx_dgrow(this, d_ntkey, (size_t)(np + 2)) ||
       !pmx_dgrow(this, d_ntrange, (size_t)(3 * (nt + 1))) || !pmx_dgrow(this, d_ntlist, (size_t)(3 * nt * FAN_CAP))) {
@@ -852,14 +876,11 @@ bool pmx_ctx::check_fans(hipStream_t s) {
     err.clear();
     return true;
   }
-  if (hipMemsetAsync(d_wfar.p + 3, 0, sizeof(unsigned), s) != hipSuccess ||
-      hipMemsetAsync(d_ntkey.p, 0, (size_t)(np + 2) * sizeof(unsigned), s) != hipSuccess) {
+  if (hipMemsetAsync(d_wfar.p + 3, 0, sizeof(unsigned), s) != hipSuccess) {
     err = "node trias: memset";
     return false;
   }
-  const unsigned nbc = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nt + 255) / 256, 4096));
-  hipLaunchKernelGGL(k_nt_count, dim3(nbc), dim3(256), 0, s, d_tris.p, nt, d_ntkey.p);
-  if (!fan_rotation(s, d_wfar.p + 3, d_ntkey.p)) return false;
+  if (!fan_rotation(s, d_wfar.p + 3, true)) return false;
   if (hipMemcpyAsync(h_nbad + 4, d_wfar.p + 3, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess) {
     err = "node trias: check";
     return false;
@@ -901,17 +922,10 @@ bool pmx_ctx::build_node_trias(hipStream_t s, int force, bool check) {
   if (m < 1) return true;
   if (fan_rot && force == 0 && check) {
     // the upload's check again (a FRESH step: what a new background costs):
-    // every vertex's tria count beside the rotation
-    if (!pmx_dgrow(this, d_ntkey, (size_t)(np + 2))) return false;
-    if (hipMemsetAsync(d_ntkey.p, 0, (size_t)(np + 2) * sizeof(unsigned), s) != hipSuccess) {
-      err = "node trias: memset";
-      return false;
-    }
-    const unsigned nbc = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nt + 255) / 256, 4096));
-    hipLaunchKernelGGL(k_nt_count, dim3(nbc), dim3(256), 0, s, d_tris.p, nt, d_ntkey.p);
-    return fan_rotation(s, d_wfar.p + 2, d_ntkey.p);
+    // the vertices' fan owners beside the rotation
+    return fan_rotation(s, d_wfar.p + 2, true);
   }
-  if (fan_rot && force == 0) return fan_rotation(s, d_wfar.p + 2);
+  if (fan_rot && force == 0) return fan_rotation(s, d_wfar.p + 2, false);
   if (np <= 5 * m || force == 1) {
     if (!node_trias_counting(this, s)) return false;
     if (hipGetLastError() != hipSuccess) {

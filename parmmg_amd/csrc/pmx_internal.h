@@ -233,7 +233,7 @@ struct pmx_ctx {
   // the fans by rotation (closed manifold surface, checked at the upload:
   // fan_rot) or by a sort; force 1: the counting sort
   bool fan_rot = false;
-  bool fan_rotation(hipStream_t s, unsigned *d_bad, const unsigned *vcount = nullptr);
+  bool fan_rotation(hipStream_t s, unsigned *d_bad, bool check = false);
   bool check_fans(hipStream_t s);
   // from d_tris, np, nt (pmx_bdy.hip); check: the rotation also re-counts every
   // vertex's trias, the upload's fan check (a FRESH step redoes it)

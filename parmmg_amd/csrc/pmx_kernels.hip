@@ -686,6 +686,9 @@ void launch_orphans(const uint8_t *mk, int64_t n, uint8_t keep, const OrphanRows
 // each lane takes two tets per round (two loads in flight).
 __global__ __launch_bounds__(256) void k_mark_new_tets(const int4 *__restrict__ tv, int64_t ne,
                                                        uint8_t *__restrict__ mk) {
+  // (r06: an XCD-aware split -- each XCD one contiguous eighth of the tets,
+  // so its byte stores stay in its own L2 -- measured 0.565 vs 0.549 ms
+  // beside the step's prefix: not kept)
   const int64_t st = (int64_t)gridDim.x * blockDim.x;
   const int64_t nit = (ne + 2 * st - 1) / (2 * st);    // uniform trip count (the shuffles below)
   const bool lane0 = (threadIdx.x & 63) == 0;

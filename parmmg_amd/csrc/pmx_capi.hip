@@ -424,9 +424,23 @@ pmx_ctx *pmx_create(int device) {
   // (PMX_interpMetricsAndFields runs two groups' steps side by side).
   static std::atomic<unsigned> n_created{0};
   const bool odd = (n_created.fetch_add(1) & 1u) != 0;
+  // PMX_STREAM_PRIO=1 (A/B): the main stream at the device's greatest
+  // priority, the orphan-mark stream at its least, so that the walk's
+  // critical prefix (derived data, hint build) is dispatched first
+  static const bool prio = [] {
+    const char *e = getenv("PMX_STREAM_PRIO");
+    return e && e[0] == '1';
+  }();
+  int p_least = 0, p_greatest = 0;
+  if (prio) hipDeviceGetStreamPriorityRange(&p_least, &p_greatest);
   auto mk_main = [&] {
+    if (mmain.empty() && prio) return hipStreamCreateWithPriority(&ctx->own, hipStreamNonBlocking, p_greatest);
     return mmain.empty() ? hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking)
                          : hipExtStreamCreateWithCUMask(&ctx->own, (uint32_t)mmain.size(), mmain.data());
+  };
+  auto mk_up = [&] {
+    return prio ? hipStreamCreateWithPriority(&ctx->up, hipStreamNonBlocking, p_least)
+                : hipStreamCreateWithFlags(&ctx->up, hipStreamNonBlocking);
   };
   auto mk_side = [&] {
     return mside.empty() ? hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking)
@@ -434,13 +448,11 @@ pmx_ctx *pmx_create(int device) {
   };
   bool sok;
   if (!odd)
-    sok = mk_main() == hipSuccess && mk_side() == hipSuccess &&
-          hipStreamCreateWithFlags(&ctx->up, hipStreamNonBlocking) == hipSuccess &&
+    sok = mk_main() == hipSuccess && mk_side() == hipSuccess && mk_up() == hipSuccess &&
           hipStreamCreateWithFlags(&ctx->topo, hipStreamNonBlocking) == hipSuccess;
   else
-    sok = hipStreamCreateWithFlags(&ctx->topo, hipStreamNonBlocking) == hipSuccess &&
-          hipStreamCreateWithFlags(&ctx->up, hipStreamNonBlocking) == hipSuccess && mk_main() == hipSuccess &&
-          mk_side() == hipSuccess;
+    sok = hipStreamCreateWithFlags(&ctx->topo, hipStreamNonBlocking) == hipSuccess && mk_up() == hipSuccess &&
+          mk_main() == hipSuccess && mk_side() == hipSuccess;
   ctx->stream = ctx->own;
   if (!sok ||
       hipEventCreateWithFlags(&ctx->ev_topo, hipEventDisableTiming) != hipSuccess ||

@@ -1767,13 +1767,13 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
   KFn kern = surf ? kfs[(lean ? 4 : 0) | (sel & 3)] : kfn[sel];
   // measurement variants of the default iso kernel: PMX_PRILEN_EXP=1..3 with
   // PMX_EXPERIMENTS=1 (results wrong by design: the VALU breakdown), 4 the r05
-  // rotation loop, 8 / 16 / 24 the flat rotation's record and order variants
-  // (same results)
+  // rotation loop, 8 / 16 / 24 the flat rotation's record and order variants,
+  // 32 / 33 the default at 6 / 4 waves per SIMD (same results)
   {
     static const int xp = [] {
       const char *e = getenv("PMX_PRILEN_EXP"), *x = getenv("PMX_EXPERIMENTS");
       const int v = e ? atoi(e) : 0;
-      if (v == 4 || v == 8 || v == 16 || v == 24) return v;
+      if (v == 4 || v == 8 || v == 16 || v == 24 || v == 32 || v == 33) return v;
       return (e && x && x[0] == '1') ? std::max(0, std::min(3, v)) : 0;
     }();
     KFn kv = nullptr;
@@ -1785,6 +1785,8 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
       case 8: kv = k_prilen<false, false, false, 5, true, false, 8>; break;
       case 16: kv = k_prilen<false, false, false, 5, true, false, 16>; break;
       case 24: kv = k_prilen<false, false, false, 5, true, false, 24>; break;
+      case 32: kv = k_prilen<false, false, false, 6, true, false, 0>; break;    // 6 waves / SIMD
+      case 33: kv = k_prilen<false, false, false, 4, true, false, 0>; break;    // 4 waves / SIMD
       default: break;
     }
     if (kv && sel == 8 && !surf) kern = kv;

@@ -215,18 +215,64 @@ __global__ __launch_bounds__(256) void k_qual(StatArgs A, double *qual, QualPart
   const int64_t k0 = 1 + lb * per, k1 = min(A.ne, k0 + per - 1), kstep = blockDim.x;
   // 16-B connectivity stream: the neighbours are not needed here
   int4 cv = (k0 + (int64_t)threadIdx.x <= k1) ? A.tetv[k0 + threadIdx.x] : make_int4(0, 0, 0, 0);
+  // the vertex rows are loaded for every lane (an invalid tet reads row 0 and
+  // discards the result), then the next connectivity: loads return in
+  // order, so a prefetch issued before the gathers (r05) made every gather
+  // wait for it -- the prefetch hid nothing.  The ridge-storage mean
+  // (OUTQUA with a tensor metric) keeps the tag-dependent loads.
+  const bool pre = !(ANI && A.ridmet);
   for (int64_t kb = k0; kb <= k1; kb += kstep) {   // uniform over the block
     const int64_t k = kb + threadIdx.x;
     const bool in = k <= k1;
     const int v[4] = {cv.x, cv.y, cv.z, cv.w};
-    const int64_t kn = k + kstep;
-    if (kn <= k1) cv = A.tetv[kn];
     const bool valid = in && v[0] > 0;
+    const int64_t kn = k + kstep;
+    double q = 0.0;
+    bool rid4 = false;
+    if (use_stored || pre) {
+      const int vb = A.vbase;
+      const int w[4] = {valid ? v[0] : vb, valid ? v[1] : vb, valid ? v[2] : vb, valid ? v[3] : vb};
+      unsigned tg[4] = {0u, 0u, 0u, 0u};
+      if (OUT && A.ptag) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) tg[i] = stag(A, w[i]);
+      }
+      double qs = 0.0;
+      D3 P[4];
+      double mv[ANI ? 4 : 1][6];
+      if constexpr (use_stored) {
+        qs = qual[in ? k : k1];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++) P[i] = sld3(A, w[i]);
+        if constexpr (ANI) {
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const double *m = smet(A, w[i]);
+#pragma unroll
+            for (int j = 0; j < 6; j++) mv[i][j] = m[j];
+          }
+        }
+      }
+      cv = A.tetv[kn <= k1 ? kn : k1];
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (use_stored) {
+        q = qs;
+      } else if constexpr (ANI) {
+        q = caltet_ani(P[0], P[1], P[2], P[3], mv[0], mv[1], mv[2], mv[3]);
+      } else {
+        q = caltet_iso(P[0], P[1], P[2], P[3]);
+      }
+      if (OUT && A.ptag) rid4 = ridge_pt(tg[0]) && ridge_pt(tg[1]) && ridge_pt(tg[2]) && ridge_pt(tg[3]);
+    } else {
+      if (kn <= k1) cv = A.tetv[kn];
+      if (valid) q = tet_quality<ANI>(A, v);
+      if (OUT && valid) rid4 = tet_4ridge(A, v);
+    }
     // !MG_EOK: no quality (0, not a stale value)
     if (MODE == QM_STORE && in && !valid) qual[k] = 0.0;
     double rap = 0.0;
     if (valid) {
-      const double q = use_stored ? qual[k] : tet_quality<ANI>(A, v);
       if (MODE == QM_STORE) qual[k] = q;
       rap = ALPHAD * q;
       if (MODE != QM_STORE) {
@@ -239,7 +285,7 @@ __global__ __launch_bounds__(256) void k_qual(StatArgs A, double *qual, QualPart
     cne += (unsigned)__popcll(__ballot(valid));
     cgood += (unsigned)__popcll(__ballot(valid && rap > 0.12));
     cmed += (unsigned)__popcll(__ballot(valid && rap > 0.5));
-    if (OUT) cnrid += (unsigned)__popcll(__ballot(valid && tet_4ridge(A, v)));
+    if (OUT) cnrid += (unsigned)__popcll(__ballot(valid && rid4));
     int ir = (int)(5.0 * rap);
     ir = ir < 4 ? ir : 4;
     // the bin from three bit ballots (scalar mask algebra) instead of five

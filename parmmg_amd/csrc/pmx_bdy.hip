@@ -1008,13 +1008,16 @@ static BdyArgs bdy_args(pmx_ctx *c, const VolArgs &a) {
 }
 
 // the walks, their private-list overflow pass and the exhaustive scan
-static void launch_bdy_walks(const BdyArgs &B, int *ows, int exp, hipStream_t s) {
+// ovf_threads: the overflow pass's threads, OVF_THREADS unless the caller
+// sized the workspace for more (the sequential mode's speculative pass, whose
+// walks from the predecessors' trias overflow by the thousand)
+static void launch_bdy_walks(const BdyArgs &B, int *ows, int exp, hipStream_t s, int ovf_threads = OVF_THREADS) {
   const int64_t nb = (B.nlist + 255) / 256;
   if (exp == 10)                         // A/B: the r01-r03 8-entry private lists
     hipLaunchKernelGGL(k_locate_bdy<BDY_CAP / 2>, dim3((unsigned)nb), dim3(256), 0, s, B);
   else
     hipLaunchKernelGGL(k_locate_bdy<BDY_CAP>, dim3((unsigned)nb), dim3(256), 0, s, B);
-  hipLaunchKernelGGL(k_locate_bdy_ovf, dim3(OVF_THREADS / 64), dim3(64), 0, s, B, ows, OVF_CAP);
+  hipLaunchKernelGGL(k_locate_bdy_ovf, dim3(ovf_threads / 64), dim3(64), 0, s, B, ows, OVF_CAP);
   hipLaunchKernelGGL(k_exh_bdy, dim3(256), dim3(256), 0, s, B);
 }
 
@@ -1294,7 +1297,10 @@ bool pmx_ctx::seq_replay(const VolArgs &a, hipStream_t s, bool surf, bool vol) {
     B.seq_start = sstart;
     B.seq_base = sbase;
     B.seq_w = d_sqw.p;
-    launch_bdy_walks(B, d_ows.p, a.exp, s);
+    // 4x the overflow threads (C3: 96 ms of long speculative walks on 4096)
+    const int seq_ovf = 4 * OVF_THREADS;
+    if (!pmx_dgrow(this, d_ows, (size_t)seq_ovf * 3 * OVF_CAP)) return false;
+    launch_bdy_walks(B, d_ows.p, a.exp, s, seq_ovf);
     // 3. the replay, on the reference's state
     if (!ck(hipMemsetAsync(d_sqtf.p, 0, (size_t)(nt + 1) * sizeof(int), s), "memset") ||
         !ck(hipMemsetAsync(d_sqpf.p, 0x80, (size_t)(np + 1) * sizeof(int), s), "memset"))

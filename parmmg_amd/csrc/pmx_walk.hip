@@ -819,7 +819,7 @@ __global__ __launch_bounds__(256) void k_seqv_spec(VolArgs A, SeqVolArgs S) {
 // global workspace (walks from the previous point's tet are long where the
 // visit order jumps: ~2 % of C3's points walk more than 16 tets)
 #define SEQV_OVF_CAP 4096            // hash slots per thread: walks of up to 2048 tets
-#define SEQV_OVF_THREADS (64 * 256)
+#define SEQV_OVF_THREADS (4 * 64 * 256)    // 2 GB of hash tables (r06: 4x, C3 78 ms on 16384 threads)
 __global__ __launch_bounds__(256) void k_seqv_ovf(VolArgs A, SeqVolArgs S, int *ws) {
   const int n = *S.nvseq;
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;

@@ -76,6 +76,57 @@ struct GlobState {
   __device__ int &OP(int i) { return ovp[i]; }
   __device__ int &OF(int i) { return ovf[i]; }
 };
+// GlobState with hashed lists (the sequential mode's overflow pass: walks
+// from the predecessors' trias run hundreds of steps, and the linear lists
+// make each of them quadratic -- C3: 82-96 ms, a few walks long).  Open
+// addressing in per-thread tables tagged with the walk's generation (its
+// overflow-list position + 1; the caller zeroes the tables before the pass):
+// the same set and map as the lists
+struct GlobHashState {
+  int2 *vt;                      // visited trias: (tria, gen)
+  int4 *ft;                      // point flags: (point, gen, flag, -)
+  int mask = 0, gen = 0, nv = 0, no = 0, capv = 0;
+  bool over = false;
+};
+#define GHS_SLOTS 4096           // per table and thread; at most half of them used
+__device__ __forceinline__ unsigned ghs_hash(int x) { return (unsigned)x * 2654435761u; }
+__device__ bool visited(GlobHashState &s, int t) {
+  for (unsigned h = ghs_hash(t) & s.mask;; h = (h + 1) & s.mask) {
+    const int2 e = s.vt[h];
+    if (e.y != s.gen) return false;
+    if (e.x == t) return true;
+  }
+}
+__device__ void mark_visited(GlobHashState &s, int t) {
+  unsigned h = ghs_hash(t) & s.mask;
+  for (;; h = (h + 1) & s.mask) {
+    const int2 e = s.vt[h];
+    if (e.y != s.gen) break;
+    if (e.x == t) return;
+  }
+  if (s.nv >= s.capv) { s.over = true; return; }
+  s.vt[h] = make_int2(t, s.gen);
+  s.nv++;
+}
+__device__ int get_flag(GlobHashState &s, int p, int cnt) {
+  for (unsigned h = ghs_hash(p) & s.mask;; h = (h + 1) & s.mask) {
+    const int4 e = s.ft[h];
+    if (e.y != s.gen) return cnt;
+    if (e.x == p) return e.z;
+  }
+}
+__device__ void set_flag(GlobHashState &s, int p, int f) {
+  unsigned h = ghs_hash(p) & s.mask;
+  for (;; h = (h + 1) & s.mask) {
+    const int4 e = s.ft[h];
+    if (e.y != s.gen) break;
+    if (e.x == p) { s.ft[h].z = f; return; }
+  }
+  if (s.no >= s.capv) { s.over = true; return; }
+  s.ft[h] = make_int4(p, s.gen, f, 0);
+  s.no++;
+}
+
 // the reference's own state, for the sequential replay (one lane): tria
 // flags tf[] compared with mesh->base, point flags pf[] kept across queries
 // (PF_INIT: still the incident-tria count PMMG_precompute_nodeTrias left)
@@ -507,6 +558,38 @@ __global__ __launch_bounds__(64) void k_locate_bdy_ovf(BdyArgs A, int *ws, int c
     const D3 p = ld3(A.q, (int)i);
     GlobState s;
     s.init(ws + (size_t)tid * 3 * cap, cap);
+    Bary b;
+    int k, edge, vtx, step;
+    bool wedged;
+    int r = walk_bdy(A, s, p, A.start[i], A.seq_base ? A.seq_base[i] : (int)(i + 1), k, b, edge, vtx, step,
+                     wedged);
+    if (A.seq_w) A.seq_w[i] = wedged ? 1 : 0;
+    if (r == 1) {
+      finish_bdy(A, i, k, b, edge, vtx, 1, step);
+    } else {
+      unsigned slot = atomicAdd(A.stuck_count, 1u);
+      A.stuck_list[slot] = (int)i;
+      A.steps[i] = -step;
+    }
+  }
+}
+
+// the sequential mode's overflow pass, on hashed lists (workspace:
+// ghs_ws_ints() ints per thread, zeroed by the caller)
+__global__ __launch_bounds__(64) void k_locate_bdy_ovf_hash(BdyArgs A, int *ws) {
+  const unsigned n = *A.ovf_count;
+  const unsigned nthr = gridDim.x * blockDim.x;
+  const unsigned tid = blockIdx.x * blockDim.x + threadIdx.x;
+  int *w = ws + (size_t)tid * (GHS_SLOTS * 6);
+  for (unsigned j = tid; j < n; j += nthr) {
+    int64_t i = A.ovf_list[j];
+    const D3 p = ld3(A.q, (int)i);
+    GlobHashState s;
+    s.vt = reinterpret_cast<int2 *>(w);
+    s.ft = reinterpret_cast<int4 *>(w + 2 * GHS_SLOTS);
+    s.mask = GHS_SLOTS - 1;
+    s.capv = GHS_SLOTS / 2;
+    s.gen = (int)j + 1;
     Bary b;
     int k, edge, vtx, step;
     bool wedged;
@@ -1011,13 +1094,17 @@ static BdyArgs bdy_args(pmx_ctx *c, const VolArgs &a) {
 // ovf_threads: the overflow pass's threads, OVF_THREADS unless the caller
 // sized the workspace for more (the sequential mode's speculative pass, whose
 // walks from the predecessors' trias overflow by the thousand)
-static void launch_bdy_walks(const BdyArgs &B, int *ows, int exp, hipStream_t s, int ovf_threads = OVF_THREADS) {
+static void launch_bdy_walks(const BdyArgs &B, int *ows, int exp, hipStream_t s, int ovf_threads = OVF_THREADS,
+                             bool hashed = false) {
   const int64_t nb = (B.nlist + 255) / 256;
   if (exp == 10)                         // A/B: the r01-r03 8-entry private lists
     hipLaunchKernelGGL(k_locate_bdy<BDY_CAP / 2>, dim3((unsigned)nb), dim3(256), 0, s, B);
   else
     hipLaunchKernelGGL(k_locate_bdy<BDY_CAP>, dim3((unsigned)nb), dim3(256), 0, s, B);
-  hipLaunchKernelGGL(k_locate_bdy_ovf, dim3(ovf_threads / 64), dim3(64), 0, s, B, ows, OVF_CAP);
+  if (hashed)
+    hipLaunchKernelGGL(k_locate_bdy_ovf_hash, dim3(ovf_threads / 64), dim3(64), 0, s, B, ows);
+  else
+    hipLaunchKernelGGL(k_locate_bdy_ovf, dim3(ovf_threads / 64), dim3(64), 0, s, B, ows, OVF_CAP);
   hipLaunchKernelGGL(k_exh_bdy, dim3(256), dim3(256), 0, s, B);
 }
 
@@ -1163,74 +1250,95 @@ __global__ __launch_bounds__(256) void k_seq_starts(const int *__restrict__ seq,
 // tria of the previous query, written by the exhaustive scan), state (0 done,
 // 1 stuck: the host scans), stuck point}.  Tria / point flags through
 // agent-scope accesses (the lane re-reads what it wrote in earlier queries).
+// flags[j] (j < nmax) = surface position j must be looked at by the replay:
+// its speculative walk read carried state (a wedge / cone test) or started
+// from another tria than its predecessor's speculative result
+__global__ __launch_bounds__(256) void k_seq_sflags(const int *__restrict__ seq, const int *__restrict__ nseq_p,
+                                                    const int *__restrict__ sstart, const uint8_t *__restrict__ sw,
+                                                    const int *__restrict__ elem, int64_t nmax,
+                                                    uint8_t *__restrict__ flags) {
+  const int n = *nseq_p;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nmax; j += (int64_t)gridDim.x * blockDim.x) {
+    bool bad = false;
+    if (j < n) {
+      const int i = seq[j];
+      const int want = j == 0 ? 1 : elem[seq[j - 1]];
+      bad = sw[i] || sstart[i] != want;
+    }
+    flags[j] = bad ? 1 : 0;
+  }
+}
+
+// the replay, one lane, in visit order over the candidate positions (cand,
+// sorted) and the successor of every replayed query; ctl = {next position,
+// its start (-1: the tria of the previous point, after a stuck walk the host
+// resolved), state (0 done, 1 stuck), the point}.  (r06 first version: the
+// wave scanned all positions, 64 at a time.)
 __global__ __launch_bounds__(64) void k_seq_resolve(BdyArgs A, const int *__restrict__ seq,
                                                     const int *__restrict__ nseq_p, const int *__restrict__ sstart,
                                                     const uint8_t *__restrict__ sw, const int *__restrict__ sbase,
                                                     int *tf, int *pf, int *ctl, int *stk_list,
-                                                    unsigned *stk_count, unsigned *nreplay) {
-  const int lane = threadIdx.x;
+                                                    unsigned *stk_count, unsigned *nreplay,
+                                                    const int *__restrict__ cand, const int *__restrict__ ncand) {
+  if (threadIdx.x != 0) return;
   const int nseq = *nseq_p;
   int j = ctl[0];
   int prev = ctl[1];
   if (j >= nseq) return;
+  bool dirty = prev < 0;
   if (prev < 0) prev = A.elem[seq[j - 1]];
+  const int nc = *ncand;
+  int lo = 0, hi = nc;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (cand[mid] < j) lo = mid + 1;
+    else hi = mid;
+  }
+  int pos = lo;
   unsigned replays = 0;
   while (j < nseq) {
-    const int jj = j + lane;
-    bool okk = false;
-    if (jj < nseq) {
-      const int i = seq[jj];
-      const int want = lane == 0 ? prev : A.elem[seq[jj - 1]];
-      okk = !sw[i] && sstart[i] == want;
-    }
-    const int nvalid = min(64, nseq - j);
-    const unsigned long long mask = nvalid == 64 ? ~0ull : ((1ull << nvalid) - 1ull);
-    const unsigned long long bad = ~__ballot(okk) & mask;
-    if (!bad) {                                  // the whole block keeps its speculative results
-      prev = A.elem[seq[j + nvalid - 1]];
-      j += nvalid;
-      continue;
-    }
-    const int f = __ffsll((long long)bad) - 1;
-    if (f > 0) prev = A.elem[seq[j + f - 1]];
-    j += f;
-    int r = 1, nk = 0;
-    if (lane == 0) {
-      const int i = seq[j];
-      const D3 p = ld3(A.q, i);
-      SeqState st{tf, pf, sbase[i]};
-      Bary b;
-      int k, edge, vtx, step;
-      bool wedged;
-      A.start[i] = prev;
-      r = walk_bdy(A, st, p, prev, sbase[i], k, b, edge, vtx, step, wedged);
-      replays++;
-      if (r == 1) {
-        finish_bdy(A, i, k, b, edge, vtx, 1, step);
-        nk = k;
-      } else {
-        A.steps[i] = -step;
-        stk_list[0] = i;
-        *stk_count = 1u;
-        ctl[0] = j;
-        ctl[2] = 1;
-        ctl[3] = i;
+    if (!dirty) {
+      while (pos < nc && cand[pos] < j) pos++;
+      if (pos >= nc) break;
+      const int c = cand[pos];
+      if (c > j) {
+        prev = A.elem[seq[c - 1]];
+        j = c;
       }
     }
-    r = __shfl(r, 0, 64);
-    nk = __shfl(nk, 0, 64);
+    const int i = seq[j];
+    if (!sw[i] && sstart[i] == prev) {
+      prev = A.elem[i];
+      dirty = false;
+      j++;
+      continue;
+    }
+    const D3 p = ld3(A.q, i);
+    SeqState st{tf, pf, sbase[i]};
+    Bary b;
+    int k, edge, vtx, step;
+    bool wedged;
+    A.start[i] = prev;
+    const int r = walk_bdy(A, st, p, prev, sbase[i], k, b, edge, vtx, step, wedged);
+    replays++;
     if (r != 1) {
-      if (lane == 0) atomicAdd(nreplay, replays);
+      A.steps[i] = -step;
+      stk_list[0] = i;
+      *stk_count = 1u;
+      ctl[0] = j;
+      ctl[2] = 1;
+      ctl[3] = i;
+      atomicAdd(nreplay, replays);
       return;
     }
-    prev = nk;
+    finish_bdy(A, i, k, b, edge, vtx, 1, step);
+    prev = k;
+    dirty = true;
     j++;
   }
-  if (lane == 0) {
-    ctl[0] = nseq;
-    ctl[2] = 0;
-    atomicAdd(nreplay, replays);
-  }
+  ctl[0] = nseq;
+  ctl[2] = 0;
+  atomicAdd(nreplay, replays);
 }
 
 bool pmx_ctx::seq_replay(const VolArgs &a, hipStream_t s, bool surf, bool vol) {
@@ -1297,23 +1405,46 @@ bool pmx_ctx::seq_replay(const VolArgs &a, hipStream_t s, bool surf, bool vol) {
     B.seq_start = sstart;
     B.seq_base = sbase;
     B.seq_w = d_sqw.p;
-    // 4x the overflow threads (C3: 96 ms of long speculative walks on 4096)
-    const int seq_ovf = 4 * OVF_THREADS;
-    if (!pmx_dgrow(this, d_ows, (size_t)seq_ovf * 3 * OVF_CAP)) return false;
-    launch_bdy_walks(B, d_ows.p, a.exp, s, seq_ovf);
+    // the overflow pass on hashed lists and 2x the threads (C3: 82-96 ms of
+    // long speculative walks on linear lists)
+    const int seq_ovf = 2 * OVF_THREADS;
+    const size_t ws_ints = (size_t)seq_ovf * GHS_SLOTS * 6;
+    if (!pmx_dgrow(this, d_ows, ws_ints) ||
+        !ck(hipMemsetAsync(d_ows.p, 0, ws_ints * sizeof(int), s), "memset"))
+      return false;
+    launch_bdy_walks(B, d_ows.p, a.exp, s, seq_ovf, true);
     // 3. the replay, on the reference's state
     if (!ck(hipMemsetAsync(d_sqtf.p, 0, (size_t)(nt + 1) * sizeof(int), s), "memset") ||
         !ck(hipMemsetAsync(d_sqpf.p, 0x80, (size_t)(np + 1) * sizeof(int), s), "memset"))
       return false;
     int hctl[4] = {0, 1, 0, 0};
     if (!ck(hipMemcpyAsync(ctl, hctl, sizeof hctl, hipMemcpyHostToDevice, s), "ctl")) return false;
+    // the replay's candidates, in visit order
+    {
+      size_t sel_b = 0;
+      hipcub::CountingInputIterator<int> it(0);
+      if (!ck(hipcub::DeviceSelect::Flagged(nullptr, sel_b, it, (const uint8_t *)nullptr, (int *)nullptr,
+                                            (int *)nullptr, (int)nq_bdy_ub, s),
+              "select") ||
+          !pmx_dgrow(this, d_sqflag, (size_t)nq_bdy_ub) || !pmx_dgrow(this, d_sqcand, (size_t)nq_bdy_ub + 1) ||
+          !pmx_dgrow(this, d_sqtmp, sel_b))
+        return false;
+      const unsigned nbs = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nq_bdy_ub + 255) / 256, 8192));
+      hipLaunchKernelGGL(k_seq_sflags, dim3(nbs), dim3(256), 0, s, (const int *)seq, (const int *)nseq,
+                         (const int *)sstart, (const uint8_t *)d_sqw.p, (const int *)d_elem.p, (int64_t)nq_bdy_ub,
+                         d_sqflag.p);
+      if (!ck(hipcub::DeviceSelect::Flagged(d_sqtmp.p, sel_b, it, (const uint8_t *)d_sqflag.p, d_sqcand.p + 1,
+                                            d_sqcand.p, (int)nq_bdy_ub, s),
+              "select"))
+        return false;
+    }
     BdyArgs X = B;
     X.stuck_list = stk_list;
     X.stuck_count = stk_count;
     for (;;) {
       hipLaunchKernelGGL(k_seq_resolve, dim3(1), dim3(64), 0, s, B, (const int *)seq, (const int *)nseq,
                          (const int *)sstart, (const uint8_t *)d_sqw.p, (const int *)sbase, d_sqtf.p, d_sqpf.p, ctl,
-                         stk_list, stk_count, nreplay);
+                         stk_list, stk_count, nreplay, (const int *)(d_sqcand.p + 1), (const int *)d_sqcand.p);
       if (!ck(hipMemcpyAsync(hctl, ctl, sizeof hctl, hipMemcpyDeviceToHost, s), "ctl") ||
           !ck(hipStreamSynchronize(s), "sync"))
         return false;

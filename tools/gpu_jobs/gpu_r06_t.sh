@@ -1,0 +1,4 @@
+tools/gpu_job.sh \
+ "r6t_seq:600:python -u -m pytest tests/test_gpu_seq_surface.py tests/test_gpu_seq_seam.py tests/test_gpu_configs.py::test_full_size_parity -x -q -s --timeout 500 --timeout-method thread" \
+ "r6t_b:300:python -u bench.py --no-cpu --no-pcie --steps 10" \
+ "r6t_tr:300:bash tools/profile_trace.sh r6t --steps 3 --warmup 1"

@@ -1,0 +1,4 @@
+tools/gpu_job.sh \
+ "r6u_seq:600:python -u -m pytest tests/test_gpu_seq_surface.py tests/test_gpu_seq_seam.py tests/test_gpu_configs.py::test_full_size_parity -x -q -s --timeout 500 --timeout-method thread" \
+ "r6u_b:300:python -u bench.py --no-cpu --no-pcie --steps 10" \
+ "r6u_tr:300:bash tools/profile_trace.sh r6u --steps 3 --warmup 1"

@@ -607,6 +607,28 @@ def main():
                        "with another tria / edge / vertex (surface) or tet (volume ties) than the reference's "
                        "sequential run"}
 
+    # the shipped binding's configuration (integration/pmmg_pmx.c sends no
+    # adjacency: 16 B/tet less over PCIe), where every FRESH step also runs the
+    # device face matching of the background -- reported beside ms_per_step,
+    # never `value`
+    devadj = None
+    if world == 1 and not args.no_pcie:
+        phase("FRESH steps with device face matching")
+        sync()
+        tr.upload_background(m, sols, 0, adja=False)
+        tr.run(flags=FRESH)
+        tr.synchronize()
+        t3 = time.perf_counter()
+        nda = max(3, min(args.steps, 10))
+        for _ in range(nda):
+            tr.run(flags=FRESH)
+        tr.synchronize()
+        devadj = {"ms": (time.perf_counter() - t3) / nda * 1e3, "steps": nda,
+                  "note": "group 0, background uploaded without Mmg's adjacency (the shipped binding's "
+                          "choice): each FRESH step also rebuilds the face adjacency and the tet records "
+                          "on the device (pmx_topo.hip face matching)"}
+        tr.upload_background(m, sols, 0)
+
     # host-staged rate (ParMmg's adapter path: host buffers in and out), measured
     # after the timed region and never reported as `value`
     pcie = None
@@ -687,7 +709,8 @@ def main():
             + "tag dispatch + order-preserving compaction of the new points, hint grid, volume walk + "
             "interpolation, surface path, fallback"),
             "not_in_ms": "host packing and PCIe (pcie_inclusive); nothing the device runs per "
-                         "upload is outside the step"},
+                         "upload is outside the step",
+            "binding_configuration": devadj},
         "resident_background_ms_per_step": resident_ms,
         "step_alg_GBs": B_all / (ms * 1e-3) / 1e9,
         "locate": st,

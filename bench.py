@@ -628,6 +628,8 @@ def main():
                           "choice): each FRESH step also rebuilds the face adjacency and the tet records "
                           "on the device (pmx_topo.hip face matching)"}
         tr.upload_background(m, sols, 0)
+        tr.run(flags=FRESH)                    # the legs below read the last step's results
+        tr.synchronize()
 
     # host-staged rate (ParMmg's adapter path: host buffers in and out), measured
     # after the timed region and never reported as `value`

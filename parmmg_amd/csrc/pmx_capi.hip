@@ -1152,7 +1152,7 @@ static bool run_flags_valid(int flags, std::string *err) {
   }
   const int e = (flags >> PMX_RUN_EXP_SHIFT) & 0xff;
   switch (e) {
-    case 0: case 6: case 9: case 10: case 11: case 12: case 13: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 23:
+    case 0: case 6: case 9: case 10: case 11: case 12: case 13: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 23: case 24:
       return true;
     case 4: case 5: case 14: {
       const char *v = getenv("PMX_EXPERIMENTS");

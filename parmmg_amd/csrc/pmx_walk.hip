@@ -253,6 +253,25 @@ __device__ __forceinline__ void walk_finish(const VolArgs &A, int64_t i, D3 p, b
       // one 4-B word -- two stores fewer per point (not decoded downstream)
       const unsigned wm = interp_layout<LAYOUT, S>(A.sol, A.sd, v, lam, A.out + i * A.sd.S);
       A.status[i] = (int)(1u | ((wm | A.const_bit) << 2) | ((unsigned)step << 10));
+    } else if (A.exp == 24) {
+      // A/B (r06): the results stored non-temporally (streamed past L2, which
+      // keeps the records and vertex rows other walks reuse)
+      __builtin_nontemporal_store(cur, A.elem + i);
+      __builtin_nontemporal_store(1, A.status + i);
+      __builtin_nontemporal_store(step, A.steps + i);
+      unsigned wm;
+      if constexpr (LAYOUT == LAYOUT_ISO || LAYOUT == LAYOUT_ANI) {
+        constexpr int NO = LAYOUT == LAYOUT_ANI ? 6 : (S > 0 ? S : 1);
+        double o[NO];
+        wm = interp_layout<LAYOUT, S>(A.sol, A.sd, v, lam, o);
+        if (wm) {                                  // (a failed inversion leaves the row untouched)
+#pragma unroll
+          for (int j = 0; j < NO; j++) __builtin_nontemporal_store(o[j], A.out + i * A.sd.S + j);
+        }
+      } else {
+        wm = interp_layout<LAYOUT, S>(A.sol, A.sd, v, lam, A.out + i * A.sd.S);
+      }
+      __builtin_nontemporal_store((uint8_t)(wm | A.const_bit), A.wmask + i);
     } else {
       A.status[i] = 1;
       A.steps[i] = step;

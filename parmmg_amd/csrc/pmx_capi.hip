@@ -1152,7 +1152,7 @@ static bool run_flags_valid(int flags, std::string *err) {
   }
   const int e = (flags >> PMX_RUN_EXP_SHIFT) & 0xff;
   switch (e) {
-    case 0: case 6: case 9: case 10: case 11: case 12: case 13: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 23: case 24:
+    case 0: case 6: case 9: case 10: case 11: case 12: case 13: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 23: case 24: case 25:
       return true;
     case 4: case 5: case 14: {
       const char *v = getenv("PMX_EXPERIMENTS");
@@ -1227,7 +1227,10 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   // few short kernels there, instead of passes starved on the side stream);
   // exp 20: the same with the counting sort over the vertex ids
   const int exp0 = (opts.flags >> PMX_RUN_EXP_SHIFT) & 0xff;
-  if (bdy && csr) {
+  // exp 25 (A/B, r06): the fans (and a FRESH step's fan check) on the side
+  // stream after the classification, beside the walk instead of the prefix
+  const bool fans_late = exp0 == 25 && bdy && !serial;
+  if (bdy && csr && !fans_late) {
     if (!ctx->build_node_trias(exp0 == 19 || exp0 == 20 ? st : ss, exp0 == 20 ? 1 : 0, fresh)) return 0;
     ctx->have_csr = true;
   }
@@ -1305,6 +1308,10 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
       if (!bdy || serial) return true;
       CK(hipEventRecord(ctx->ev_fork2, st));
       CK(hipStreamWaitEvent(side, ctx->ev_fork2, 0));
+      if (fans_late && csr) {
+        if (!ctx->build_node_trias(side, 0, fresh)) return false;
+        ctx->have_csr = true;
+      }
       if (!ctx->launch_bdy(A, side)) return false;
       if (ev) CK(hipEventRecord(ev[5], side));
       CK(hipEventRecord(ctx->ev_join, side));

@@ -684,24 +684,26 @@ void launch_orphans(const uint8_t *mk, int64_t n, uint8_t keep, const OrphanRows
 // vertices its left neighbour -- the previous tet, which in any coherent
 // numbering shares most of them -- also holds (that lane stores them), and
 // each lane takes two tets per round (two loads in flight).
+// H tets per thread and iteration (loads in flight); PMX_MARK_TPT=4 (A/B)
+template <int H>
 __global__ __launch_bounds__(256) void k_mark_new_tets(const int4 *__restrict__ tv, int64_t ne,
                                                        uint8_t *__restrict__ mk) {
   // (r06: an XCD-aware split -- each XCD one contiguous eighth of the tets,
   // so its byte stores stay in its own L2 -- measured 0.565 vs 0.549 ms
   // beside the step's prefix: not kept)
   const int64_t st = (int64_t)gridDim.x * blockDim.x;
-  const int64_t nit = (ne + 2 * st - 1) / (2 * st);    // uniform trip count (the shuffles below)
+  const int64_t nit = (ne + H * st - 1) / (H * st);    // uniform trip count (the shuffles below)
   const bool lane0 = (threadIdx.x & 63) == 0;
   for (int64_t it = 0; it < nit; it++) {
-    const int64_t k0 = 1 + 2 * (it * st + (int64_t)blockIdx.x * blockDim.x) + threadIdx.x;
-    int4 v[2];
+    const int64_t k0 = 1 + H * (it * st + (int64_t)blockIdx.x * blockDim.x) + threadIdx.x;
+    int4 v[H];
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
+    for (int h = 0; h < H; h++) {
       const int64_t k = k0 + h * blockDim.x;
       v[h] = k <= ne ? tv[k] : make_int4(0, 0, 0, 0);
     }
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
+    for (int h = 0; h < H; h++) {
       const int4 a = v[h];
       int4 u;
       u.x = __shfl_up(a.x, 1, 64); u.y = __shfl_up(a.y, 1, 64);
@@ -719,8 +721,15 @@ __global__ __launch_bounds__(256) void k_mark_new_tets(const int4 *__restrict__ 
 }
 void launch_mark_new_tets(const int4 *tv, int64_t ne, uint8_t *mk, hipStream_t s) {
   if (ne < 1) return;
-  const int64_t nb = std::min<int64_t>((ne + 511) / 512, 8192);
-  hipLaunchKernelGGL(k_mark_new_tets, dim3((unsigned)nb), dim3(256), 0, s, tv, ne, mk);
+  static const int tpt = [] {
+    const char *e = getenv("PMX_MARK_TPT");
+    return e && e[0] == '4' ? 4 : 2;
+  }();
+  const int64_t nb = std::min<int64_t>((ne + 256 * tpt - 1) / (256 * tpt), 8192);
+  if (tpt == 4)
+    hipLaunchKernelGGL(k_mark_new_tets<4>, dim3((unsigned)nb), dim3(256), 0, s, tv, ne, mk);
+  else
+    hipLaunchKernelGGL(k_mark_new_tets<2>, dim3((unsigned)nb), dim3(256), 0, s, tv, ne, mk);
 }
 
 // ---- device residency across iterations (pmx_promote_background) ----------------

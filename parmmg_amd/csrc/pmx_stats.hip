@@ -486,18 +486,25 @@ __device__ __forceinline__ IsoEdge iso_edge_load(const StatArgs &A, int p1, int 
   __builtin_amdgcn_sched_barrier(0);
   return e;
 }
+template <bool TWO = false>   // TWO (A/B): the two-branch form, two divisions in a mixed wave
 __device__ __forceinline__ double iso_edge_len(const IsoEdge &e) {
   double ux = e.c2.x - e.c1.x, uy = e.c2.y - e.c1.y, uz = e.c2.z - e.c1.z;
   double l = ux * ux + uy * uy + uz * uz;
   l = sqrt(l);
   double r = e.h2 / e.h1 - 1.0;
-  return (fabs(r) < PMX_EPS) ? (l / e.h1) : (l / (e.h2 - e.h1) * pmx_log1p(r));
+  if constexpr (TWO) return (fabs(r) < PMX_EPS) ? (l / e.h1) : (l / (e.h2 - e.h1) * pmx_log1p(r));
+  // one division for both branches (l / h1 or l / (h2 - h1): the same
+  // correctly rounded quotients as the two-branch form, one instead of two
+  // in a wave whose lanes take both)
+  const bool flat = fabs(r) < PMX_EPS;
+  const double q = l / (flat ? e.h1 : (e.h2 - e.h1));
+  return flat ? q : q * pmx_log1p(r);
 }
 
 // MMG5_lenEdg_iso / lenEdg33_ani (restated, unpinned; the surface lengths
 // MMG5_lenSurfEdg_iso / lenSurfEdg33_ani of the parallel edges take the same
 // formulas in classic metric storage)
-template <bool ANI>
+template <bool ANI, bool TWO = false>
 __device__ __forceinline__ double edge_len_t(const StatArgs &A, int p1, int p2) {
   if (ANI) {
     D3 c1 = sld3(A, p1), c2 = sld3(A, p2);
@@ -510,7 +517,7 @@ __device__ __forceinline__ double edge_len_t(const StatArgs &A, int p1, int p2) 
     return (sqrt(dd1) + sqrt(dd2) + 4.0 * sqrt(0.5 * (dd1 + dd2))) / 6.0;
   }
   const IsoEdge e = iso_edge_load(A, p1, p2);
-  return iso_edge_len(e);
+  return iso_edge_len<TWO>(e);
 }
 __device__ double edge_len(const StatArgs &A, int p1, int p2) {
   return A.msize == 6 ? edge_len_t<true>(A, p1, p2) : edge_len_t<false>(A, p1, p2);
@@ -684,7 +691,9 @@ __device__ double len_iso_flat(const StatArgs &A, int p1, int p2) {
   double l = (c2.x - c1.x) * (c2.x - c1.x) + (c2.y - c1.y) * (c2.y - c1.y) + (c2.z - c1.z) * (c2.z - c1.z);
   l = sqrt(l);
   const double r = h2 / h1 - 1.0;
-  return (fabs(r) < PMX_EPS) ? (l / h1) : (l / (h2 - h1) * pmx_log1p(r));
+  const bool flat = fabs(r) < PMX_EPS;
+  const double q = l / (flat ? h1 : (h2 - h1));
+  return flat ? q : q * pmx_log1p(r);
 }
 
 __device__ __forceinline__ void len_merge(LenPart &x, const LenPart &y) {
@@ -1165,7 +1174,7 @@ __global__ __launch_bounds__(256, W) void k_prilen(StatArgs A, LenPart *parts) {
         } else if constexpr (X & 1) {
           len = 1.0 + 1e-9 * (double)(a & 7);
         } else {
-          len = edge_len_t<ANI>(A, a, b);
+          len = edge_len_t<ANI, (X & 128) != 0>(A, a, b);
         }
         if constexpr (X & 2) on = true;
         else if constexpr (FLAT) {
@@ -1819,7 +1828,7 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
     static const int xp = [] {
       const char *e = getenv("PMX_PRILEN_EXP"), *x = getenv("PMX_EXPERIMENTS");
       const int v = e ? atoi(e) : 0;
-      if (v == 4 || v == 8 || v == 16 || v == 24 || v == 32 || v == 33) return v;
+      if (v == 4 || v == 8 || v == 16 || v == 24 || v == 32 || v == 33 || v == 128) return v;
       return (e && x && x[0] == '1') ? std::max(0, std::min(3, v)) : 0;
     }();
     KFn kv = nullptr;
@@ -1833,6 +1842,7 @@ int pmx_prilen_device(pmx_ctx *ctx, int metRidTyp, const pmx_par_edges *par, voi
       case 24: kv = k_prilen<false, false, false, 5, true, false, 24>; break;
       case 32: kv = k_prilen<false, false, false, 6, true, false, 0>; break;    // 6 waves / SIMD
       case 33: kv = k_prilen<false, false, false, 4, true, false, 0>; break;    // 4 waves / SIMD
+      case 128: kv = k_prilen<false, false, false, 5, true, false, 128>; break; // two-division length
       default: break;
     }
     if (kv && sel == 8 && !surf) kern = kv;

@@ -853,7 +853,7 @@ int pmx_upload_points(pmx_ctx *ctx, const pmx_points_view *pv) {
   uint16_t *htg = (uint16_t *)(st + o_tg);
   const char *pc = (const char *)pv->c;
   const char *tg = (const char *)pv->tag;
-  if (!dgrow(ctx, ctx->d_qxyz, nn * 3) || !dgrow(ctx, ctx->d_kind, nn) || !dgrow(ctx, ctx->d_qmark, nn) ||
+  if (!dgrow(ctx, ctx->d_qxyz, nn * 3) || !dgrow(ctx, ctx->d_kind, nn) || !dgrow(ctx, ctx->d_qmark, nn + 64) ||   // + 64: the marks' word-wide flush
       !dgrow(ctx, ctx->d_nsel, 2) || !dgrow(ctx, ctx->d_vollist, nn) || !dgrow(ctx, ctx->d_bdylist, nn) ||
       !dgrow(ctx, ctx->d_ctile, (size_t)std::max<int64_t>(cls_tiles(n), 1)) ||
       (tg && !dgrow(ctx, ctx->d_qtag, nn)) || (ntet && !dgrow(ctx, ctx->d_ntetv, (size_t)(ntet + 1))))
@@ -996,7 +996,7 @@ bool pmx_ctx::pack_new_tets() {
     // the orphan marks, on the device once the tets are there (the host's
     // byte stores into a point-sized array cost as much as the packing)
     CK(hipMemsetAsync(d_qmark.p, 0, (size_t)n, up));
-    launch_mark_new_tets(d_ntetv.p, ntet, d_qmark.p, up);
+    launch_mark_new_tets(d_ntetv.p, ntet, d_qmark.p, n, up);
     CK(hipGetLastError());
     orph_marks = true;
   }
@@ -1101,7 +1101,7 @@ bool pmx_ctx::mark_new_tets(hipStream_t s) {
   pmx_ctx *ctx = this;
   if (nq < 1) return true;
   CK(hipMemsetAsync(d_qmark.p, 0, (size_t)nq, s));
-  launch_mark_new_tets(d_ntetv.p, n_ntet, d_qmark.p, s);
+  launch_mark_new_tets(d_ntetv.p, n_ntet, d_qmark.p, nq, s);
   CK(hipGetLastError());
   return true;
 }
@@ -1152,7 +1152,7 @@ static bool run_flags_valid(int flags, std::string *err) {
   }
   const int e = (flags >> PMX_RUN_EXP_SHIFT) & 0xff;
   switch (e) {
-    case 0: case 6: case 9: case 10: case 11: case 12: case 13: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 23: case 24: case 25:
+    case 0: case 6: case 9: case 10: case 11: case 12: case 13: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 23: case 24: case 25: case 26:
       return true;
     case 4: case 5: case 14: {
       const char *v = getenv("PMX_EXPERIMENTS");
@@ -1236,13 +1236,18 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
   }
   // the orphan marks on `up`, beside the derived data and the hint build
   // (the classification waits for them)
-  if (marks) {
+  // exp 26 (A/B): the marks start after the derived data (which they slow
+  // by sharing the memory system), beside the latency-bound hint build only
+  const bool marks_after_derive = marks && exp0 == 26;
+  auto launch_marks = [&]() -> bool {
     CK(hipEventRecord(ctx->ev_fork, st));
     CK(hipStreamWaitEvent(ctx->up, ctx->ev_fork, 0));
-    if (!ctx->mark_new_tets(ctx->up)) return 0;
+    if (!ctx->mark_new_tets(ctx->up)) return false;
     CK(hipEventRecord(ctx->ev_tets, ctx->up));
     ctx->tets_inflight = true;
-  }
+    return true;
+  };
+  if (marks && !marks_after_derive && !launch_marks()) return 0;
   // exp 15 (A/B): no fixed-point copy of the vertices -- the hint build
   // quantises the sampled tets' vertices itself -- and the tria normals on
   // the surface stream
@@ -1264,6 +1269,7 @@ int pmx_run(pmx_ctx *ctx, const pmx_run_opts *o) {
     ctx->have_derived = !hint_xyz;
   }
   if (fresh && !ctx->rederive(st)) return 0;
+  if (marks_after_derive && !launch_marks()) return 0;
   if (ev) CK(hipEventRecord(ev[7], st));
   // with the marks in the step, the hint build (which does not depend on the
   // points) goes ahead of the classification, beside the marks
@@ -1881,7 +1887,7 @@ int pmx_upload_new_tets(pmx_ctx *ctx, const int *tetra_v, int64_t tetra_stride, 
     // marks come from them (a step already run has its orphan rows reset
     // from these marks by the next consumer of its results)
     CK(hipMemsetAsync(ctx->d_qmark.p, 0, (size_t)n, ctx->stream));
-    launch_mark_new_tets(ctx->d_ntetv.p, ne, ctx->d_qmark.p, ctx->stream);
+    launch_mark_new_tets(ctx->d_ntetv.p, ne, ctx->d_qmark.p, n, ctx->stream);
     CK(hipGetLastError());
     ctx->orph_marks = true;
     if (ctx->ran) ctx->orph_fixed = false;

@@ -107,7 +107,7 @@ void launch_tet_conn(const TetRec *src, int64_t n, int4 *dst, hipStream_t s);
 void launch_promote(const double *qxyz, const double *out, const uint16_t *qtag, int64_t n, int S, double *xyz,
                     double *sol, uint16_t *ptag, hipStream_t s);
 // points in no valid new tet (mk == 0) after a step: rows back to untouched
-void launch_mark_new_tets(const int4 *tv, int64_t ne, uint8_t *mk, hipStream_t s);
+void launch_mark_new_tets(const int4 *tv, int64_t ne, uint8_t *mk, int64_t nmk, hipStream_t s);
 struct OrphanRows {
   uint8_t *wmask;
   int *elem, *status, *steps, *start, *edge, *vertex;

@@ -719,13 +719,166 @@ __global__ __launch_bounds__(256) void k_mark_new_tets(const int4 *__restrict__ 
     }
   }
 }
-void launch_mark_new_tets(const int4 *tv, int64_t ne, uint8_t *mk, hipStream_t s) {
+// r06 (late): the same marks with the next round's tets loaded BEFORE this
+// round's byte stores, and every store issued (a buffer store whose offset is
+// out of the descriptor's range when it is filtered out: the hardware drops
+// it, no branch).  vmcnt counts loads and stores in one in-order counter on
+// gfx950, so k_mark_new_tets' loads, issued after the previous round's
+// stores, waited for those stores too (`s_waitcnt vmcnt(0)` at the loop
+// head); here the head waits vmcnt(4H): the stores stay in flight.
+template <int H>
+__global__ __launch_bounds__(256) void k_mark_new_tets_pipe(const int4 *__restrict__ tv, int64_t ne,
+                                                            uint8_t *__restrict__ mk, int nmk) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(mk, (short)0, nmk, 0x00020000);
+  const int64_t st = (int64_t)gridDim.x * blockDim.x;
+  const int64_t nit = (ne + H * st - 1) / (H * st);    // uniform trip count (the shuffles below)
+  const bool lane0 = (threadIdx.x & 63) == 0;
+  const int64_t kb = 1 + H * (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int4 v[H];
+#pragma unroll
+  for (int h = 0; h < H; h++) v[h] = tv[min(kb + h * (int64_t)blockDim.x, ne)];
+  // 4H dropped stores (offset out of range): the loop is entered with the
+  // same VMEM pattern as its back edge (loads, then 4H stores), so the
+  // compiler's wait at the loop head is vmcnt(4H) on both paths, not 0
+#pragma unroll
+  for (int l = 0; l < 4 * H; l++) __builtin_amdgcn_raw_buffer_store_b8((unsigned char)1, rs, nmk + l * 64, 0, 0);
+  for (int64_t it = 0; it < nit; it++) {
+    const int64_t k0 = kb + H * it * st;
+    int4 a[H];
+#pragma unroll
+    for (int h = 0; h < H; h++) {
+      a[h] = v[h];
+      if (!(k0 + h * (int64_t)blockDim.x <= ne && a[h].x > 0)) a[h] = make_int4(0, 0, 0, 0);   // !MG_EOK / tail
+    }
+    // the next round's tets (clamped: the last round reloads row ne, unused)
+#pragma unroll
+    for (int h = 0; h < H; h++) v[h] = tv[min(k0 + H * st + h * (int64_t)blockDim.x, ne)];
+#pragma unroll
+    for (int h = 0; h < H; h++) {
+      const int4 q4 = a[h];
+      int4 u;
+      u.x = __shfl_up(q4.x, 1, 64); u.y = __shfl_up(q4.y, 1, 64);
+      u.z = __shfl_up(q4.z, 1, 64); u.w = __shfl_up(q4.w, 1, 64);
+      if (lane0) u = make_int4(0, 0, 0, 0);             // no left neighbour: store all
+      const int w[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+      for (int l = 0; l < 4; l++) {
+        const int q = w[l];
+        const bool keep = q > 0 && q != u.x && q != u.y && q != u.z && q != u.w;
+        __builtin_amdgcn_raw_buffer_store_b8((unsigned char)1, rs, keep ? q - 1 : nmk, 0, 0);
+      }
+    }
+  }
+}
+
+// r06 (late): the marks deduplicated in LDS.  What bounds k_mark_new_tets is
+// not its 16-B tet stream but its byte stores: one L2 write request per lane
+// and vertex (≈ 1.5-2 per tet after the left-neighbour filter, a vertex is in
+// ≈ 24 tets).  Here a workgroup takes 256 H consecutive tets at a time and
+// marks their vertices in an LDS byte window [wb, wb + MW_WIN) anchored at
+// the chunk's first valid tet (a coherent numbering -- Morton or Scotch --
+// keeps a chunk's vertices together); the window is flushed as 32-bit words,
+// one global atomicOr per word that holds a mark (the bytes of the marks
+// array ORed: marks are only ever set, so concurrent chunks and the plain
+// byte stores of out-of-window vertices compose).  Any numbering stays
+// correct: a vertex outside the window is stored directly, as before.
+#define MW_WIN 16384
+template <int H>
+__global__ __launch_bounds__(256) void k_mark_new_tets_win(const int4 *__restrict__ tv, int64_t ne,
+                                                           uint8_t *__restrict__ mk, int64_t nmk) {
+  __shared__ unsigned win[MW_WIN / 4];
+  __shared__ int s_base;
+  unsigned *mk32 = reinterpret_cast<unsigned *>(mk);
+  uint8_t *wb8 = reinterpret_cast<uint8_t *>(win);
+  for (int i = threadIdx.x; i < MW_WIN / 4; i += 256) win[i] = 0u;
+  const int64_t C = 256 * H;
+  const int64_t nch = (ne + C - 1) / C;
+  const bool lane0 = (threadIdx.x & 63) == 0;
+  for (int64_t c = blockIdx.x; c < nch; c += gridDim.x) {        // uniform over the workgroup
+    const int64_t k0 = 1 + c * C + threadIdx.x;
+    int4 v[H];
+#pragma unroll
+    for (int h = 0; h < H; h++) {
+      const int64_t k = k0 + h * 256;
+      v[h] = k <= ne ? tv[k] : make_int4(0, 0, 0, 0);
+    }
+    // window anchor: the first valid tet's smallest vertex, less a quarter
+    // window (vertices of a chunk's later cells may precede it), 4-aligned
+    if (threadIdx.x == 0) {
+      const int4 a = v[0];
+      const int m = a.x > 0 ? min(min(a.x, a.y), min(a.z, a.w)) - 1 : 0;
+      s_base = max(0, m - MW_WIN / 4) & ~3;
+    }
+    __syncthreads();
+    const int wb = s_base;
+#pragma unroll
+    for (int h = 0; h < H; h++) {
+      const int4 a = v[h];
+      int4 u;
+      u.x = __shfl_up(a.x, 1, 64); u.y = __shfl_up(a.y, 1, 64);
+      u.z = __shfl_up(a.z, 1, 64); u.w = __shfl_up(a.w, 1, 64);
+      if (lane0 || u.x <= 0) u = make_int4(0, 0, 0, 0);
+      if (a.x <= 0) continue;                             // !MG_EOK
+      const int w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+      for (int l = 0; l < 4; l++) {
+        const int q = w[l];
+        if (q == u.x || q == u.y || q == u.z || q == u.w) continue;
+        const unsigned off = (unsigned)(q - 1 - wb);
+        if (off < (unsigned)MW_WIN) wb8[off] = 1;
+        else mk[q - 1] = 1;
+      }
+    }
+    __syncthreads();
+    // flush: one atomicOr per word holding a mark, then clear it
+    const int64_t w0 = wb >> 2;
+    for (int i = threadIdx.x; i < MW_WIN / 4; i += 256) {
+      const unsigned x = win[i];
+      if (x) {
+        if (w0 + i < (nmk + 3) / 4) atomicOr(mk32 + w0 + i, x);
+        win[i] = 0u;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+void launch_mark_new_tets(const int4 *tv, int64_t ne, uint8_t *mk, int64_t nmk, hipStream_t s) {
+  // PMX_MARK_WIN=0 (A/B): the marks without the LDS window
+  static const bool winm = [] {
+    const char *e = getenv("PMX_MARK_WIN");
+    return !(e && e[0] == '0');
+  }();
+  if (winm && ne >= 1 && nmk > 0 && nmk < INT32_MAX - MW_WIN) {
+    const int64_t nb = std::min<int64_t>((ne + 1023) / 1024, 4096);
+    hipLaunchKernelGGL(k_mark_new_tets_win<4>, dim3((unsigned)nb), dim3(256), 0, s, tv, ne, mk, nmk);
+    return;
+  }
   if (ne < 1) return;
   static const int tpt = [] {
     const char *e = getenv("PMX_MARK_TPT");
     return e && e[0] == '4' ? 4 : 2;
   }();
-  const int64_t nb = std::min<int64_t>((ne + 256 * tpt - 1) / (256 * tpt), 8192);
+  // PMX_MARK_PIPE=1 (A/B): k_mark_new_tets_pipe (beside the derived data it
+  // takes memory bandwidth from them: C3 step 2.481-2.500 vs 2.470-2.488 ms)
+  static const bool pipe = [] {
+    const char *e = getenv("PMX_MARK_PIPE");
+    return e && e[0] == '1';
+  }();
+  // PMX_MARK_BLOCKS (A/B): the block cap -- the marks run beside the derived
+  // data and the hint build, which they slow by sharing the memory system
+  static const int64_t cap = [] {
+    const char *e = getenv("PMX_MARK_BLOCKS");
+    return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)8192;
+  }();
+  const int64_t nb = std::min<int64_t>((ne + 256 * tpt - 1) / (256 * tpt), cap);
+  if (pipe && nmk > 0 && nmk < INT32_MAX - 4096) {
+    if (tpt == 4)
+      hipLaunchKernelGGL(k_mark_new_tets_pipe<4>, dim3((unsigned)nb), dim3(256), 0, s, tv, ne, mk, (int)nmk);
+    else
+      hipLaunchKernelGGL(k_mark_new_tets_pipe<2>, dim3((unsigned)nb), dim3(256), 0, s, tv, ne, mk, (int)nmk);
+    return;
+  }
   if (tpt == 4)
     hipLaunchKernelGGL(k_mark_new_tets<4>, dim3((unsigned)nb), dim3(256), 0, s, tv, ne, mk);
   else

@@ -537,3 +537,48 @@ def test_new_tets_after_a_step_must_match_the_view(transfer):
         transfer.upload_new_tets(tets)               # the same tets: accepted
         r2 = transfer.download()
         assert np.array_equal(r.elem, r2.elem) and np.all(r2.elem[~used] == 0)
+
+
+@pytest.mark.parametrize("order", ["coherent", "scattered"])
+def test_orphan_marks_window_and_far_vertices(transfer, order):
+    """The orphan marks (k_mark_new_tets_win: an LDS byte window per chunk of
+    new tets, flushed as word-wide atomicOr, vertices outside the window
+    stored directly) at a size where the vertex ids span far more than one
+    window: every point of a valid new tet is visited, every other one is an
+    orphan -- at the upload (marks with the points) and inside a FRESH step
+    (marks redone by the step), with deleted tets (v[0] <= 0) among them."""
+    m, x, t, sols = cube_case(48, metric="iso", surface=False, fields=False)
+    n = len(x)
+    assert n > 4 * 16384
+    rng = np.random.default_rng(7)
+    used = rng.random(n) < 0.8
+    pool = np.nonzero(used)[0] + 1                   # 1-based
+    if order == "coherent":
+        # tets over consecutive used points (each used point in >= 1 tet)
+        tv = np.concatenate([pool, pool[: (-len(pool)) % 4]]).reshape(-1, 4)
+        tv = np.concatenate([tv, np.sort(rng.choice(pool, size=(len(pool) // 2, 4)), axis=0)])
+    else:
+        tv = rng.choice(pool, size=(len(pool), 4))
+        tv[: len(pool), 0] = rng.permutation(pool)
+    tets = np.zeros((len(tv) + 1, 4), np.int32)
+    tets[1:] = tv
+    tets[0] = -1
+    # deleted tets whose vertices are orphans: they must not mark them
+    dead = rng.choice(len(tv), size=len(tv) // 50, replace=False) + 1
+    orph = np.nonzero(~used)[0] + 1
+    tets[dead, 1:] = rng.choice(orph, size=(len(dead), 3))
+    tets[dead, 0] = 0
+    covered = np.zeros(n + 1, bool)
+    ok = tets[1:, 0] > 0
+    covered[tets[1:][ok].ravel()] = True
+    covered = covered[1:]
+    assert (~covered).sum() > 1000 and covered.sum() > 4 * 16384
+    transfer.upload_background(m, sols, 0)
+    for flags in (0, N.RUN_FRESH_BACKGROUND):
+        transfer.upload_points(x, t, tets)
+        transfer.run(flags=flags)
+        r = transfer.download()
+        assert np.all(r.status[~covered] == 0) and np.all(r.elem[~covered] == 0), flags
+        assert np.all(r.status[covered] != 0), flags
+        st = transfer.locate_stats()
+        assert st["nvol"] == int(covered.sum()), flags

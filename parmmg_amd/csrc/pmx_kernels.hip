@@ -849,9 +849,17 @@ void launch_mark_new_tets(const int4 *tv, int64_t ne, uint8_t *mk, int64_t nmk, 
     const char *e = getenv("PMX_MARK_WIN");
     return !(e && e[0] == '0');
   }();
+  // PMX_MARK_H=8 (A/B): 2048 tets per chunk instead of 1024
+  static const int wh = [] {
+    const char *e = getenv("PMX_MARK_H");
+    return e && e[0] == '8' ? 8 : 4;
+  }();
   if (winm && ne >= 1 && nmk > 0 && nmk < INT32_MAX - MW_WIN) {
-    const int64_t nb = std::min<int64_t>((ne + 1023) / 1024, 4096);
-    hipLaunchKernelGGL(k_mark_new_tets_win<4>, dim3((unsigned)nb), dim3(256), 0, s, tv, ne, mk, nmk);
+    const int64_t nb = std::min<int64_t>((ne + 256 * wh - 1) / (256 * wh), 4096);
+    if (wh == 8)
+      hipLaunchKernelGGL(k_mark_new_tets_win<8>, dim3((unsigned)nb), dim3(256), 0, s, tv, ne, mk, nmk);
+    else
+      hipLaunchKernelGGL(k_mark_new_tets_win<4>, dim3((unsigned)nb), dim3(256), 0, s, tv, ne, mk, nmk);
     return;
   }
   if (ne < 1) return;

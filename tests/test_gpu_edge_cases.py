@@ -562,7 +562,7 @@ def test_orphan_marks_window_and_far_vertices(transfer, order):
         tv[: len(pool), 0] = rng.permutation(pool)
     tets = np.zeros((len(tv) + 1, 4), np.int32)
     tets[1:] = tv
-    tets[0] = -1
+    tets[0] = 0
     # deleted tets whose vertices are orphans: they must not mark them
     dead = rng.choice(len(tv), size=len(tv) // 50, replace=False) + 1
     orph = np.nonzero(~used)[0] + 1
@@ -575,7 +575,7 @@ def test_orphan_marks_window_and_far_vertices(transfer, order):
     assert (~covered).sum() > 1000 and covered.sum() > 4 * 16384
     transfer.upload_background(m, sols, 0)
     for flags in (0, N.RUN_FRESH_BACKGROUND):
-        transfer.upload_points(x, t, tets)
+        transfer.upload_points(x, t, tets_mmg=tets)      # 1-based, v[0] = 0 deleted
         transfer.run(flags=flags)
         r = transfer.download()
         assert np.all(r.status[~covered] == 0) and np.all(r.elem[~covered] == 0), flags

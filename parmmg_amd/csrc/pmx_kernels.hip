@@ -174,12 +174,36 @@ __global__ __launch_bounds__(BS) void k_hint_build(const int4 *__restrict__ pack
   }
   grid[hint_cell(a, b, c, d, g)] = (int)k;
 }
+// PMX_HINT_FILT=1 (A/B, late r06): the same build with one grid store per
+// run of samples in one cell -- a lane whose left neighbour's sample falls in
+// its cell leaves the store to it (consecutive samples of a coherent
+// numbering share cells; any sample of the cell is a valid start, and the
+// left one is as good as the racy last writer)
+__global__ __launch_bounds__(256) void k_hint_build_filt(const int4 *__restrict__ packed, int64_t n, int stride,
+                                                         int *__restrict__ grid, GridDesc g,
+                                                         const unsigned long long *__restrict__ xyzq) {
+  const int64_t t = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  const int64_t k = 1 + t * stride;
+  const int4 v = packed[t < n ? t : n - 1];
+  int64_t c = -1;
+  if (t < n && v.x > 0) c = hint_cell(xyzq[v.x], xyzq[v.y], xyzq[v.z], xyzq[v.w], g);
+  const long long cl = __shfl_up((long long)c, 1, 64);
+  if (c >= 0 && ((threadIdx.x & 63) == 0 || cl != (long long)c)) grid[c] = (int)k;
+}
 void launch_hint_build(const int4 *packed, const int *kidx, const TetRec *tets, int64_t ne, int stride, int *grid,
                        GridDesc g, const unsigned long long *xyzq, const double *xyz, hipStream_t s,
                        bool v0, int bs, int64_t nsamp) {
   const int64_t n = nsamp >= 0 ? nsamp : (ne + stride - 1) / stride;   // nsamp < 0: every stride-th tet
   if (n < 1) return;
   const int64_t nb = (n + 255) / 256;
+  static const bool filt = [] {
+    const char *e = getenv("PMX_HINT_FILT");
+    return e && e[0] == '1';
+  }();
+  if (filt && packed && !kidx && xyzq && !v0 && bs == 256 && nsamp < 0 && n < INT32_MAX) {
+    hipLaunchKernelGGL(k_hint_build_filt, dim3((unsigned)nb), dim3(256), 0, s, packed, n, stride, grid, g, xyzq);
+    return;
+  }
   if (v0 && xyzq && packed)
     hipLaunchKernelGGL((k_hint_build<true, false, true>), dim3((unsigned)nb), dim3(256), 0, s, packed, kidx, tets, n,
                        stride, grid, g, xyzq, xyz);
